@@ -1,0 +1,196 @@
+/*
+ * boxfusion_hip.h — C-ABI of libboxfusion_hip.so, the MI355X (gfx950) hot path of
+ * BoxFusion's per-frame detect + multi-view 3D box fusion.
+ *
+ * Conventions (every entry point):
+ *   - All data pointers are CALLER-OWNED DEVICE pointers (e.g. torch tensors' data_ptr()),
+ *     contiguous, with the dtype named in the signature.  Nothing here allocates device memory.
+ *   - `stream` is a hipStream_t passed as void* (NULL = the legacy default stream).
+ *   - Every call is asynchronous on `stream` and returns a bf_status (0 = ok, < 0 = error).
+ *     Device-side capacity problems are reported through an int32 device status word where the
+ *     signature has one (BF_DEV_* flags); the caller reads it after synchronising.
+ *   - Functions are stateless and reentrant; concurrent calls on different streams are safe.
+ *
+ * Each function cites the reference interface it replaces (paths relative to the reference
+ * repository pliam1105/BoxFusion).
+ */
+#ifndef BOXFUSION_HIP_H
+#define BOXFUSION_HIP_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    BF_OK = 0,
+    BF_ERR_ARG = -1,       /* bad size / null pointer */
+    BF_ERR_LAUNCH = -2,    /* hipLaunchKernel / hipGetLastError failure */
+    BF_ERR_CAPACITY = -3,  /* host-detectable capacity overflow (e.g. n > BF_MAX_BOXES) */
+    BF_ERR_UNSUPPORTED = -4
+} bf_status;
+
+/* device status word flags (OR-ed) */
+#define BF_DEV_OK 0
+#define BF_DEV_FUSION_LIST_OVERFLOW 1   /* a fusion_list row exceeded its capacity */
+#define BF_DEV_HULL_OVERFLOW 2          /* a 2-D hull / clip buffer exceeded its capacity */
+
+#define BF_MAX_BOXES 4096               /* NMS / association scan limit per call */
+
+/* ------------------------------------------------------------------------------------------
+ * Library identity
+ * ------------------------------------------------------------------------------------------ */
+const char* bf_version(void);
+/* returns the number of HIP devices visible (>= 0) or a negative bf_status */
+int bf_device_count(void);
+
+/* ------------------------------------------------------------------------------------------
+ * 3-D box geometry  (boxfusion/boxes.py, boxfusion/instances.py)
+ * ------------------------------------------------------------------------------------------ */
+
+/* GeneralInstance3DBoxes.corners (boxes.py:725-778).
+ * xyzlhw f32[n,6], R f32[n,3,3] -> corners f32[n,8,3] in the reference's v0..v7 order. */
+int bf_box_corners(const float* xyzlhw, const float* R, int n, float* corners, void* stream);
+
+/* GeneralInstance3DBoxes.transform2world (boxes.py:825-833), in place.
+ * xyz <- Rc*xyz + tc, R <- Rc*R with cam_pose f32[n,4,4] (camera->world). */
+int bf_box_transform2world(float* xyzlhw, float* R, const float* cam_pose, int n, void* stream);
+
+/* Instances3D.project_3d_boxes (instances.py:333-369):
+ * corners f32[n,8,3], cam_pose f32[n,4,4], K f32[3,3] -> uv f32[n,8,2], clamped to [0,W]x[0,H]
+ * (no Z>0 guard, as in the reference). */
+int bf_project_boxes(const float* corners, const float* cam_pose, const float* K, int n,
+                     float W, float H, float* uv, void* stream);
+
+/* Sampled 3-D OBB IoU of every pair (instances.py:493-613, Instances3D.obb_iou):
+ * vertex/edge-midpoint gate against the 12 hull facets (eps 1e-6), then a 25^3 linspace grid over
+ * the union AABB.  corners f32[n,8,3] -> iou f64[n,n] (symmetric, diagonal = 1).
+ * `workspace` must hold bf_obb_iou_workspace_size(n) bytes. */
+size_t bf_obb_iou_workspace_size(int n);
+int bf_obb_iou_matrix(const float* corners, int n, double* iou, void* workspace, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Spatial association: greedy 3-D NMS with fusion-list bookkeeping
+ *   nms_3d (instances.py:22-101) + BoxManager.record (box_manager.py:40-88)
+ *   + compute_pose_center_disparity (box_manager.py:188-215)
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+    float iou_threshold;     /* cfg box_fusion.nms_threshold */
+    float translation_gap;   /* cfg association.translation_gap (metres) */
+    float rotation_gap;      /* cfg association.rotation_gap (degrees) */
+    float center_gap;        /* 0.5 m (box_manager.py:55) */
+    int   max_list;          /* 5: a fusion list only grows while shorter than this */
+    int   list_capacity;     /* row stride (capacity) of fl_items */
+} bf_nms_cfg;
+
+/* One greedy scan over n boxes of all_pred_box.
+ *   iou        f64[n,n]  from bf_obb_iou_matrix
+ *   corners    f32[n,8,3] (box centres = mean of the 8 corners, as nms_3d:49)
+ *   scores     f32[n];  init_id i32[n];  cam_poses f32[M,4,4] indexed by init_id
+ *   fl_items   i32[n,cap] / fl_len i32[n]: BoxManager.fusion_list rows (in/out)
+ *   valid_num  f32[n] (in/out, +1 for every box that suppressed something)
+ * outputs (device): keep i32[n] sorted ascending, n_keep i32[1], success i32[n] sorted, n_success
+ *   i32[1], events i32[n,3] = (cur, idx, branch) in scan order, n_events i32[1],
+ *   status i32[1] (BF_DEV_* flags). */
+int bf_nms_scan(const double* iou, const float* corners, const float* scores,
+                const int32_t* init_id, const float* cam_poses, int n,
+                int32_t* fl_items, int32_t* fl_len, float* valid_num,
+                int32_t* keep, int32_t* n_keep, int32_t* success, int32_t* n_success,
+                int32_t* events, int32_t* n_events, int32_t* status,
+                const bf_nms_cfg* cfg, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Cross-view correspondence association for small boxes
+ *   Instances3D.correspondence_association (instances.py:411-490) + project_3d_to_2d_box
+ *   (:670-717) + IoU_2D_box (:643-668) + BoxManager.record_corr (box_manager.py:90-129)
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+    float small_size;        /* cfg box_fusion.small_size */
+    float threshold;         /* cfg association.small_threshold */
+    float translation_gap;
+    float rotation_gap;
+    float W, H;              /* image size used for the 2-D projection */
+    int   max_list;
+    int   list_capacity;
+} bf_corr_cfg;
+
+/*   n_all boxes = n_glo global boxes followed by the new keyframe's boxes.
+ *   corners f32[n_all,8,3], dims f32[n_all,3], scores f32[n_all], boxes2d f32[n_all,4] (xyxy),
+ *   init_id i32[n_all], cam_poses f32[M,4,4], cur_pose f32[4,4] (camera->world of this keyframe),
+ *   K f32[3,3]; mask i32[n_mask] = sorted NMS keep; success i32[n_success] = sorted success_nms.
+ *   In/out: fl_items/fl_len (fusion lists), valid_num f32[n_all].
+ *   Out: keep_out i32[n_mask] sorted, n_keep_out i32[1], events i32[n_all,3], n_events,
+ *        status i32[1]. */
+int bf_corr_assoc(const float* corners, const float* dims, const float* scores,
+                  const float* boxes2d, const int32_t* init_id, const float* cam_poses,
+                  const float* cur_pose, const float* K, int n_all, int n_glo,
+                  const int32_t* mask, int n_mask, const int32_t* success, int n_success,
+                  int32_t* fl_items, int32_t* fl_len, float* valid_num,
+                  int32_t* keep_out, int32_t* n_keep_out, int32_t* events, int32_t* n_events,
+                  int32_t* status, const bf_corr_cfg* cfg, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Multi-view box fusion: particle-swarm refinement
+ *   BoxFusion.boxfusion (box_fusion.py:622-724), init_opt_params (:566-600),
+ *   compute_iou_value CUDA kernel (:264-405), evaluate_iou (:413-461), cal_transform (:475-535),
+ *   update_PST (:537-563), init_searchsize (:468-472).  One launch refines every job, all
+ *   iterations on the device.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+    int   iters;             /* box_fusion.iters (20) */
+    int   pst_size;          /* particles, multiple of 64, <= 1024 */
+    int   max_accept;        /* 200 (cal_transform early stop) */
+    int   legacy_promotion;  /* 1: numpy<2 value-based promotion (pinned numpy 1.26.4, f64 host
+                                scalars); 0: NEP 50 promotion (numpy>=2, f32 host scalars) */
+    /* host-side Python floats of the reference, kept in f64 so both promotion modes are exact */
+    double center_init, shape_init;  /* random_opt.center_init_size / shape_init_size */
+    double center_coef, shape_coef;  /* random_opt.*_scaling_coefficient */
+    double beta;             /* momentum 0.9 (box_fusion.py:622) */
+    double min_scale;        /* 1e-3 (update_PST default) */
+    float img_h, img_w;      /* BoxFusion.H / .W */
+    float K[16];             /* BoxFusion.K (4x4 row-major) */
+} bf_fuse_cfg;
+
+/*   job j fuses views [view_off[j], view_off[j]+n_views[j]) of the view table:
+ *   view_box f32[V,6] (xyzlhw, per_frame_box.pred_boxes_3d.tensor rows),
+ *   view_R f32[V,3,3], view_score f32[V], view_pose f32[V,4,4], view_tc f32[V,8,2]
+ *   (per_frame_box.projected_boxes rows).  pst f32[pst_size,6] (row 0 must be zeros).
+ *   out_box f32[n_jobs,6]: refined xyzlhw (lhw >= 0.01), only meaningful where out_updated==1.
+ *   out_iters i32[n_jobs]: iterations executed.  trace (nullable) f32[n_jobs, iters, pst_size]
+ *   receives every iteration's fitness vector. */
+int bf_fusion_fit(const int32_t* view_off, const int32_t* n_views, int n_jobs,
+                  const float* view_box, const float* view_R, const float* view_score,
+                  const float* view_pose, const float* view_tc, const float* pst,
+                  const bf_fuse_cfg* cfg, float* out_box, int32_t* out_updated,
+                  int32_t* out_iters, float* trace, int32_t* status, void* stream);
+
+/* Single evaluation of the reference fitness kernel (compute_iou_value + evaluate_iou):
+ *   box f32[6], R f32[9], views as above (n_views), search_size f32[6] -> fitness f32[pst_size]
+ *   = (sum over views in order of |1 - IoU2D|) / (n_views + 1e-6f). */
+int bf_fusion_fitness(const float* box, const float* R, int n_views, const float* view_pose,
+                      const float* view_tc, const float* pst, int pst_size,
+                      const float* search_size, const bf_fuse_cfg* cfg, float* fitness,
+                      void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Per-frame depth work
+ * ------------------------------------------------------------------------------------------ */
+/* Preprocessor.standardize_depth_map (preprocessor.py:97-129) for a batch of b frames:
+ *   depth f32[b,h,w] -> out f32[b,h,w] standardised (invalid -> mean), params f32[b,2] =
+ *   (trunc_mean, trunc_std).  Trimmed order statistics by radix select, no sort. */
+size_t bf_depth_standardize_workspace_size(int b, int h, int w);
+int bf_depth_standardize(const float* depth, int b, int h, int w, float* out, float* params,
+                         void* workspace, void* stream);
+
+/* tools/utils.py unproject + get_camera_coords (:232-287):
+ *   depth f32[h,w], K f32[3,3], RT f32[4,4] -> xyz f32[h,w,3], valid u8[h,w]
+ *   (valid = d > 0 && d < max_depth; max_depth <= 0 disables the upper bound). */
+int bf_backproject(const float* depth, const float* K, const float* RT, int h, int w,
+                   float max_depth, float* xyz, uint8_t* valid, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BOXFUSION_HIP_H */

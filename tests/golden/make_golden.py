@@ -1,0 +1,413 @@
+"""Generate the committed golden fixtures by running the REFERENCE code (pliam1105/BoxFusion at
+/root/reference) in this container.  Run:  python tests/golden/make_golden.py
+
+Only absent third-party modules are replaced, never reference logic:
+  * torchvision  — instances.py:11-19 builds an unused Normalize at import;
+  * cv2.imread   — box_fusion.py:32 reads data/pst_1024_0.tiff (read here with PIL, mode 'F');
+  * pycuda       — box_fusion.py:8-19,63-452 compiles compute_iou_value at run time.  The kernel
+                   text cannot be built here (it needs curand/CUDA headers), so the stand-in
+                   `SourceModule` returns the ORACLE's restatement of that kernel (or_fitness_raw);
+                   everything around it (evaluate_iou, cal_transform, update_PST, momentum,
+                   init_opt_params, boxfusion control flow) is the reference's own Python.
+  * numpy.linspace — wrapped to float64 bounds: the pinned numpy 1.26 promotes the float32 bounds
+                   of instances.py:588-590 to float64; numpy 2.x here would not.
+The numpy here is 2.x, so the fusion trace follows NEP 50 scalar promotion (legacy_promotion=0).
+
+Fixtures written to tests/golden/*.npz (data only, no pickles).
+"""
+from __future__ import annotations
+
+import contextlib
+import io
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = os.environ.get("BOXFUSION_REFERENCE", "/root/reference")
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, REF)
+
+from oracle import oracle as OR  # noqa: E402
+from boxfusion_amd.synthetic import Scene, SCANNET_K  # noqa: E402
+
+
+# ------------------------------------------------------------------------------------------
+# stand-ins for absent third-party modules
+# ------------------------------------------------------------------------------------------
+def _install_stubs():
+    tv = types.ModuleType("torchvision")
+    tvt = types.ModuleType("torchvision.transforms")
+    tvt.Normalize = lambda *a, **k: None
+    tvt.Compose = lambda x: x
+    tv.transforms = tvt
+    sys.modules["torchvision"] = tv
+    sys.modules["torchvision.transforms"] = tvt
+
+    cv2 = types.ModuleType("cv2")
+
+    def imread(path, flag=None):
+        from PIL import Image
+        return np.array(Image.open(path))
+
+    cv2.imread = imread
+    sys.modules["cv2"] = cv2
+
+    pycuda = types.ModuleType("pycuda")
+    drv = types.ModuleType("pycuda.driver")
+
+    class PointerHolderBase:
+        pass
+
+    class _Arg:
+        def __init__(self, a):
+            self.a = a
+
+    drv.PointerHolderBase = PointerHolderBase
+    drv.In = _Arg
+    drv.InOut = _Arg
+    comp = types.ModuleType("pycuda.compiler")
+    STATE = {}
+
+    class SourceModule:
+        def __init__(self, src, no_extern_c=False):
+            pass
+
+        def get_function(self, name):
+            assert name == "compute_iou_value"
+
+            def kernel(box, tc, scores, pst, rot, poses, K, ss, value, count, other, block, grid):
+                h, w, npart, nv = other.a
+                cfg = STATE["cfg"]
+                cfg.img_h, cfg.img_w = float(h), float(w)
+                kk = np.asarray(K.a, np.float32)
+                for i in range(16):
+                    cfg.K[i] = float(kk[i])
+                vbuf = np.zeros(int(npart), np.float32)
+                cbuf = np.zeros(int(npart), np.float32)
+                OR.lib().or_fitness_raw(
+                    OR._p(OR._f32(box.a)), OR._p(OR._f32(rot.a)), int(nv), OR._p(OR._f32(poses.a)),
+                    OR._p(OR._f32(tc.a)), OR._p(OR._f32(pst.a)), int(npart),
+                    OR._p(OR._f32(ss.a)), __import__("ctypes").byref(cfg), OR._p(vbuf),
+                    OR._p(cbuf))
+                value.a += vbuf
+                count.a += cbuf
+
+            return kernel
+
+    comp.SourceModule = SourceModule
+    pycuda.driver = drv
+    pycuda.compiler = comp
+    sys.modules["pycuda"] = pycuda
+    sys.modules["pycuda.driver"] = drv
+    sys.modules["pycuda.autoprimaryctx"] = types.ModuleType("pycuda.autoprimaryctx")
+    sys.modules["pycuda.compiler"] = comp
+    sys.modules["pycuda.gpuarray"] = types.ModuleType("pycuda.gpuarray")
+
+    _lin = np.linspace
+
+    def linspace(start, stop, num=50, *a, **k):
+        if isinstance(start, np.floating) and isinstance(stop, np.floating):
+            start, stop = np.float64(start), np.float64(stop)
+        return _lin(start, stop, num, *a, **k)
+
+    np.linspace = linspace
+    return STATE
+
+
+STUB_STATE = _install_stubs()
+
+from boxfusion.boxes import GeneralInstance3DBoxes  # noqa: E402
+from boxfusion.instances import Instances3D  # noqa: E402
+from boxfusion.box_manager import BoxManager  # noqa: E402
+from boxfusion.box_fusion import BoxFusion  # noqa: E402
+from boxfusion.preprocessor import Preprocessor  # noqa: E402
+
+
+def quiet():
+    return contextlib.redirect_stdout(io.StringIO())
+
+
+def ragged(lists):
+    flat = np.array([v for row in lists for v in row], np.int32)
+    off = np.zeros(len(lists) + 1, np.int32)
+    off[1:] = np.cumsum([len(r) for r in lists])
+    return flat, off
+
+
+SCANNET_CFG = dict(
+    dataset="scannet",
+    data=dict(datadir="/synthetic/scannet", gap=1),
+    cam=dict(H=480, W=640, fx=574.540771, fy=577.583740, cx=322.522827, cy=238.558853),
+    detection=dict(score_thresh=0.5, uv_bound=True, uv_bound_value=0.9, floor_mask=True,
+                   floor_ratio=15, scale_box=1.5),
+    association=dict(small_threshold=0.1, rotation_gap=30, translation_gap=0.8),
+    box_fusion=dict(use=True, iters=20, pst_path=os.path.join(REF, "data/pst_1024_0.tiff"),
+                    pst_size=1024, check_valid=False, nms_threshold=0.1, small_size=0.35,
+                    random_opt=dict(center_init_size=0.1, center_scaling_coefficient=0.1,
+                                    shape_init_size=0.5, shape_scaling_coefficient=0.5)),
+)
+
+
+# ------------------------------------------------------------------------------------------
+# 1. OBB IoU pairs
+# ------------------------------------------------------------------------------------------
+def gen_obb_pairs(n=400, seed=0):
+    from scipy.spatial.transform import Rotation as Rot
+    rng = np.random.default_rng(seed)
+    C = np.zeros((n, 2, 8, 3), np.float32)
+    for t in range(n):
+        xyz = rng.uniform(-3, 3, (2, 3)).astype(np.float32)
+        lhw = rng.uniform(0.15, 1.2, (2, 3)).astype(np.float32)
+        yaw = rng.uniform(-np.pi, np.pi, 2)
+        if t % 4 == 0:
+            yaw = np.round(yaw / (np.pi / 2)) * (np.pi / 2)
+        R = np.stack([np.array([[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]])
+                      for a in yaw]).astype(np.float32)
+        if t % 5 == 1:
+            Rw = Rot.random(random_state=t).as_matrix().astype(np.float32)
+            R = (Rw @ R).astype(np.float32)
+        kind = t % 6
+        if kind in (0, 1, 2):      # overlapping
+            xyz[1] = xyz[0] + rng.normal(0, 0.15, 3)
+        elif kind == 3:            # nested
+            xyz[1] = xyz[0]
+            lhw[1] = lhw[0] * 0.5
+            R[1] = R[0]
+        elif kind == 4:            # touching faces (axis aligned, shared face)
+            R[:] = np.eye(3, dtype=np.float32)
+            xyz[1] = xyz[0]
+            xyz[1][0] = xyz[0][0] + (lhw[0][0] + lhw[1][0]) / 2
+        b = GeneralInstance3DBoxes(torch.from_numpy(np.concatenate([xyz, lhw], 1)),
+                                   torch.from_numpy(R))
+        C[t] = b.corners.numpy()
+    iou = np.array([Instances3D.obb_iou(C[t, 0], C[t, 1]) for t in range(n)], np.float64)
+    return dict(corners=C, iou=iou)
+
+
+# ------------------------------------------------------------------------------------------
+# 2. box geometry
+# ------------------------------------------------------------------------------------------
+def gen_geometry(n=64, seed=1):
+    rng = np.random.default_rng(seed)
+    scene = Scene(seed=seed)
+    xyzlhw = np.concatenate([rng.uniform(-2, 2, (n, 2)), rng.uniform(0.5, 5, (n, 1)),
+                             rng.uniform(0.1, 2.0, (n, 3))], 1).astype(np.float32)
+    yaw = rng.uniform(-np.pi, np.pi, n)
+    R = np.stack([[[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]]
+                  for a in yaw]).astype(np.float32)
+    poses = np.stack([scene.pose(int(f)) for f in rng.integers(0, 1000, n)]).astype(np.float32)
+    b = GeneralInstance3DBoxes(torch.from_numpy(xyzlhw), torch.from_numpy(R))
+    corners_cam = b.corners.numpy().copy()
+    ins = Instances3D((480, 640))
+    ins.pred_boxes_3d = b
+    ins.cam_pose = torch.from_numpy(poses)
+    b.transform2world(ins.cam_pose)
+    ins.project_3d_boxes(SCANNET_K, H=480, W=640)
+    return dict(xyzlhw=xyzlhw, R=R, poses=poses, corners_cam=corners_cam,
+                world_tensor=b.tensor.numpy(), world_R=b.R.numpy(),
+                corners_world=b.corners.numpy(), projected=ins.projected_boxes.numpy())
+
+
+# ------------------------------------------------------------------------------------------
+# 3. depth
+# ------------------------------------------------------------------------------------------
+def gen_depth(seed=2):
+    rng = np.random.default_rng(seed)
+    cases = []
+    d = rng.uniform(0.5, 4.5, (48, 64)).astype(np.float32)
+    d[rng.uniform(size=d.shape) < 0.05] = 0
+    cases.append(d)
+    d = np.round(rng.uniform(0.5, 4.5, (48, 64)), 1).astype(np.float32)  # heavy ties
+    d[rng.uniform(size=d.shape) < 0.2] = -1.0
+    cases.append(d)
+    d = np.zeros((48, 64), np.float32)  # no valid value
+    d[3, 4] = 2.0
+    cases.append(d)
+    d = rng.uniform(0.5, 4.5, (48, 64)).astype(np.float32)
+    d[rng.uniform(size=d.shape) < 0.1] = np.nan
+    cases.append(d)
+    D = np.stack(cases)
+    outs, params = [], []
+    for c in cases:
+        o, p = Preprocessor.standardize_depth_map(torch.from_numpy(c.copy()))
+        outs.append(o.numpy())
+        params.append(p.numpy())
+    return dict(depth=D, out=np.stack(outs), params=np.stack(params))
+
+
+# ------------------------------------------------------------------------------------------
+# 4. full fusion-chain trace (demo.py:200-305 order) on the synthetic scene
+# ------------------------------------------------------------------------------------------
+def make_instances(det, H=480, W=640):
+    p = Instances3D((H, W))
+    p.scores = torch.from_numpy(det["scores"].copy())
+    p.pred_boxes = torch.from_numpy(det["pred_boxes"].copy())
+    p.pred_boxes_3d = GeneralInstance3DBoxes(torch.from_numpy(det["xyzlhw"].copy()),
+                                             torch.from_numpy(det["R"].copy()))
+    p.pred_proj_xy = torch.from_numpy(det["proj_xy"].copy())
+    return p
+
+
+def gen_trace(n_keyframes=14, frame_step=25, seed=3, period=400, **scene_kw):
+    cfg = SCANNET_CFG
+    scene = Scene(seed=seed, period=period, **scene_kw)
+    STUB_STATE["cfg"] = OR.fuse_cfg(cfg, np.eye(4), 480, 640, legacy=False)
+    with quiet():
+        box_manager = BoxManager(cfg)
+        fuser = BoxFusion(cfg)
+    fuser.update_intrinsics((640, 480), SCANNET_K)
+    H, W = 480, 640
+    all_pred_box = None
+    all_poses = None
+    per_frame_ins = None
+    all_kf_pose = {}
+    box_count = 0
+    rec = {k: [] for k in ["frame", "pose", "n_det", "pre_n", "pre_tensor", "pre_R", "pre_scores",
+                           "pre_init_id", "pre_valid_num", "pre_boxes2d", "nms_keep", "nms_success",
+                           "nms_valid_num", "corr_keep", "corr_valid_num", "post_tensor",
+                           "post_valid_num"]}
+    fl = {k: [] for k in ["pre_fl", "nms_fl", "corr_fl", "post_fl", "fused"]}
+    dets = []
+    for k in range(n_keyframes):
+        frame = k * frame_step
+        det = scene.detections(frame)
+        pose = scene.pose(frame)
+        dets.append(det)
+        pred = make_instances(det)
+        n = len(pred)
+        all_kf_pose[frame] = pose
+        pose_np = np.repeat(pose[None], n, 0)
+        pred.cam_pose = torch.from_numpy(pose_np)
+        pred.frame_id = torch.tensor([frame]).repeat(n)
+        pred.init_id = box_count + torch.arange(n)
+        pred.valid_num = torch.zeros(n)
+        pred.pred_boxes_3d.transform2world(pred.cam_pose)
+        pred.project_3d_boxes(SCANNET_K, H=H, W=W)
+        box_count += n
+        rec["frame"].append(frame)
+        rec["pose"].append(pose)
+        rec["n_det"].append(n)
+        if all_pred_box is None:
+            all_pred_box = pred
+            all_poses = pose_np
+            per_frame_ins = pred
+            box_manager.init_new_predictions(n, 0)
+            for key in ["pre_n"]:
+                rec[key].append(0)
+            for key in ["pre_tensor", "pre_R", "pre_scores", "pre_init_id", "pre_valid_num",
+                        "pre_boxes2d", "nms_keep", "nms_success", "nms_valid_num", "corr_keep",
+                        "corr_valid_num"]:
+                rec[key].append(None)
+            for key in ["pre_fl", "nms_fl", "corr_fl"]:
+                fl[key].append([])
+            rec["post_tensor"].append(all_pred_box.pred_boxes_3d.tensor.numpy().copy())
+            rec["post_valid_num"].append(all_pred_box.valid_num.numpy().copy())
+            fl["post_fl"].append([list(map(int, r)) for r in box_manager.fusion_list])
+            fl["fused"].append([list(map(int, r)) for r in box_manager.already_fusion])
+            continue
+        rec["pre_n"].append(len(all_pred_box))
+        rec["pre_tensor"].append(all_pred_box.pred_boxes_3d.tensor.numpy().copy())
+        rec["pre_R"].append(all_pred_box.pred_boxes_3d.R.numpy().copy())
+        rec["pre_scores"].append(all_pred_box.scores.numpy().copy())
+        rec["pre_init_id"].append(all_pred_box.init_id.numpy().copy())
+        rec["pre_valid_num"].append(all_pred_box.valid_num.numpy().copy())
+        rec["pre_boxes2d"].append(all_pred_box.pred_boxes.numpy().copy())
+        fl["pre_fl"].append([list(map(int, r)) for r in box_manager.fusion_list])
+        with quiet():
+            box_manager.init_new_predictions(n, len(per_frame_ins))
+            num_before_cat = len(all_pred_box)
+            cur_global = all_pred_box
+            all_pred_box = Instances3D.cat([all_pred_box, pred])
+            per_frame_ins = Instances3D.cat([per_frame_ins, pred])
+            all_poses = np.concatenate((all_poses, pose_np), 0)
+            mask, success = Instances3D.spatial_association(
+                all_pred_box, cfg["box_fusion"]["nms_threshold"], box_manager,
+                per_frame_ins.cam_pose)
+        rec["nms_keep"].append(np.asarray(mask, np.int32))
+        rec["nms_success"].append(np.asarray(success, np.int32))
+        rec["nms_valid_num"].append(all_pred_box.valid_num.numpy().copy())
+        fl["nms_fl"].append([list(map(int, r)) for r in box_manager.fusion_list])
+        cur_keep_idx = [i - num_before_cat for i in mask if i >= num_before_cat]
+        cur_success = [i - num_before_cat for i in success if i >= num_before_cat]
+        keep_idx = np.asarray(mask)
+        if len(cur_keep_idx) > 0:
+            with quiet():
+                all_pred_box, all_poses, keep_idx = Instances3D.correspondence_association(
+                    cfg, box_manager, cur_keep_idx, cur_success, pred, cur_global, all_pred_box,
+                    all_poses, per_frame_ins.cam_pose, frame, mask, torch.from_numpy(SCANNET_K),
+                    all_kf_pose, threshold=cfg["association"]["small_threshold"], H=H, W=W)
+            rec["corr_keep"].append(np.asarray(keep_idx, np.int32))
+            rec["corr_valid_num"].append(None)
+            fl["corr_fl"].append([list(map(int, r)) for r in box_manager.fusion_list])
+            box_manager.update(keep_idx)
+            with quiet():
+                fuser.boxfusion(all_pred_box, per_frame_ins, box_manager)
+        else:
+            rec["corr_keep"].append(np.asarray(mask, np.int32))
+            rec["corr_valid_num"].append(None)
+            fl["corr_fl"].append([list(map(int, r)) for r in box_manager.fusion_list])
+            all_pred_box = all_pred_box[mask]
+            all_poses = all_poses[mask]
+            box_manager.update(keep_idx)
+        rec["post_tensor"].append(all_pred_box.pred_boxes_3d.tensor.numpy().copy())
+        rec["post_valid_num"].append(all_pred_box.valid_num.numpy().copy())
+        fl["post_fl"].append([list(map(int, r)) for r in box_manager.fusion_list])
+        fl["fused"].append([list(map(int, r)) for r in box_manager.already_fusion])
+
+    out = {}
+    # per-frame (cumulative) arrays as the reference left them
+    out["pf_tensor"] = per_frame_ins.pred_boxes_3d.tensor.numpy()
+    out["pf_R"] = per_frame_ins.pred_boxes_3d.R.numpy()
+    out["pf_scores"] = per_frame_ins.scores.numpy()
+    out["pf_pose"] = per_frame_ins.cam_pose.numpy()
+    out["pf_proj"] = per_frame_ins.projected_boxes.numpy()
+    out["pf_boxes2d"] = per_frame_ins.pred_boxes.numpy()
+    out["frame"] = np.asarray(rec["frame"], np.int32)
+    out["pose"] = np.stack(rec["pose"])
+    out["n_det"] = np.asarray(rec["n_det"], np.int32)
+    out["pre_n"] = np.asarray(rec["pre_n"], np.int32)
+    for key in ["scores", "pred_boxes", "xyzlhw", "R", "proj_xy"]:
+        out["det_" + key] = np.concatenate([d[key] for d in dets], 0)
+    spec = dict(pre_tensor=((6,), np.float32), pre_R=((3, 3), np.float32),
+                pre_scores=((), np.float32), pre_init_id=((), np.int64),
+                pre_valid_num=((), np.float32), pre_boxes2d=((4,), np.float32),
+                nms_keep=((), np.int32), nms_success=((), np.int32),
+                nms_valid_num=((), np.float32), corr_keep=((), np.int32),
+                post_tensor=((6,), np.float32), post_valid_num=((), np.float32))
+    for key, (tail, dt) in spec.items():
+        rows = [np.asarray(r, dt) if r is not None else np.zeros((0,) + tail, dt)
+                for r in rec[key]]
+        out[key] = np.concatenate(rows, 0)
+        out[key + "_off"] = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int32)
+    for key, lists in fl.items():
+        lens = np.array([len(ls) for ls in lists], np.int32)
+        flat_rows = [row for ls in lists for row in ls]
+        f, o = ragged(flat_rows)
+        out[key + "_flat"], out[key + "_rowoff"] = f, o
+        out[key + "_nrows"] = lens
+    return out
+
+
+def main():
+    torch.set_num_threads(8)
+    np.savez_compressed(os.path.join(HERE, "obb_pairs.npz"), **gen_obb_pairs())
+    print("obb_pairs done")
+    np.savez_compressed(os.path.join(HERE, "geometry.npz"), **gen_geometry())
+    print("geometry done")
+    np.savez_compressed(os.path.join(HERE, "depth.npz"), **gen_depth())
+    print("depth done")
+    np.savez_compressed(os.path.join(HERE, "fusion_trace.npz"), **gen_trace())
+    print("trace done")
+    np.savez_compressed(os.path.join(HERE, "fusion_trace_small.npz"),
+                        **gen_trace(n_keyframes=16, frame_step=10, seed=5, period=300, noise=3.0,
+                                    dim_lo=0.08, dim_hi=0.6, n_objects=40))
+    print("small-object trace done")
+
+
+if __name__ == "__main__":
+    main()
