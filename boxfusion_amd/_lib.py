@@ -1,0 +1,223 @@
+"""ctypes binding of libboxfusion_hip.so (the C-ABI in include/boxfusion_hip.h).
+
+Every wrapper takes/returns torch tensors that live on the HIP device and launches on the current
+torch stream.  There is deliberately no CPU fallback: if the shared library is missing or the
+tensors are not on the GPU, the call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libboxfusion_hip.so")
+_LIB = None
+
+c_int, c_float, c_double, c_void_p, c_size_t = (ctypes.c_int, ctypes.c_float, ctypes.c_double,
+                                                ctypes.c_void_p, ctypes.c_size_t)
+
+BF_DEV_FUSION_LIST_OVERFLOW = 1
+BF_DEV_HULL_OVERFLOW = 2
+BF_DEV_VIEW_OVERFLOW = 4
+
+
+class NmsCfg(ctypes.Structure):
+    _fields_ = [("iou_threshold", c_double), ("translation_gap", c_float),
+                ("rotation_gap", c_float), ("center_gap", c_double),
+                ("max_list", c_int), ("list_capacity", c_int)]
+
+
+class CorrCfg(ctypes.Structure):
+    _fields_ = [("small_size", c_double), ("threshold", c_double),
+                ("translation_gap", c_float), ("rotation_gap", c_float),
+                ("W", c_float), ("H", c_float), ("max_list", c_int), ("list_capacity", c_int)]
+
+
+class FuseCfg(ctypes.Structure):
+    _fields_ = [("iters", c_int), ("pst_size", c_int), ("max_accept", c_int),
+                ("legacy_promotion", c_int),
+                ("center_init", c_double), ("shape_init", c_double),
+                ("center_coef", c_double), ("shape_coef", c_double),
+                ("beta", c_double), ("min_scale", c_double),
+                ("img_h", c_float), ("img_w", c_float), ("K", c_float * 16)]
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise HipError(f"{LIB_PATH} is missing: build it with `python -m boxfusion_amd.build`")
+        _LIB = ctypes.CDLL(LIB_PATH)
+        _LIB.bf_version.restype = ctypes.c_char_p
+        _LIB.bf_obb_iou_workspace_size.restype = c_size_t
+        _LIB.bf_obb_iou_workspace_size.argtypes = [c_int]
+    return _LIB
+
+
+def _ptr(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise HipError("boxfusion_amd kernels need device tensors (no CPU fallback)")
+    if not t.is_contiguous():
+        raise HipError("tensor must be contiguous")
+    return c_void_p(t.data_ptr())
+
+
+def _stream():
+    return c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _check(rc, name):
+    if rc != 0:
+        raise HipError(f"{name} failed with bf_status {rc}")
+
+
+def _need(t, dtype, name):
+    if t.dtype != dtype:
+        raise HipError(f"{name}: expected {dtype}, got {t.dtype}")
+    return t
+
+
+def version():
+    return lib().bf_version().decode()
+
+
+# ------------------------------------------------------------------------------------------
+# geometry
+# ------------------------------------------------------------------------------------------
+def box_corners(xyzlhw, R):
+    xyzlhw = _need(xyzlhw.contiguous(), torch.float32, "xyzlhw")
+    R = _need(R.contiguous(), torch.float32, "R")
+    n = xyzlhw.shape[0]
+    out = torch.empty((n, 8, 3), dtype=torch.float32, device=xyzlhw.device)
+    _check(lib().bf_box_corners(_ptr(xyzlhw), _ptr(R), c_int(n), _ptr(out), _stream()),
+           "bf_box_corners")
+    return out
+
+
+def box_transform2world(xyzlhw, R, cam_pose):
+    """in place on xyzlhw / R (both contiguous f32 device tensors)"""
+    n = xyzlhw.shape[0]
+    _check(lib().bf_box_transform2world(_ptr(xyzlhw), _ptr(R), _ptr(cam_pose.contiguous()),
+                                        c_int(n), _stream()), "bf_box_transform2world")
+
+
+def project_boxes(corners, cam_pose, K, W, H):
+    n = corners.shape[0]
+    uv = torch.empty((n, 8, 2), dtype=torch.float32, device=corners.device)
+    _check(lib().bf_project_boxes(_ptr(corners.contiguous()), _ptr(cam_pose.contiguous()),
+                                  _ptr(K.contiguous()), c_int(n), c_float(W), c_float(H), _ptr(uv),
+                                  _stream()), "bf_project_boxes")
+    return uv
+
+
+def obb_iou_matrix(corners):
+    corners = _need(corners.contiguous(), torch.float32, "corners")
+    n = corners.shape[0]
+    iou = torch.empty((n, n), dtype=torch.float64, device=corners.device)
+    ws = torch.empty(max(1, int(lib().bf_obb_iou_workspace_size(n))), dtype=torch.uint8,
+                     device=corners.device)
+    _check(lib().bf_obb_iou_matrix(_ptr(corners), c_int(n), _ptr(iou), _ptr(ws), _stream()),
+           "bf_obb_iou_matrix")
+    return iou
+
+
+# ------------------------------------------------------------------------------------------
+# association
+# ------------------------------------------------------------------------------------------
+def nms_scan(iou, corners, scores, init_id, cam_poses, fl_items, fl_len, valid_num, cfg: NmsCfg):
+    """returns device tensors: keep, n_keep, success, n_success, events, n_events, status"""
+    dev = iou.device
+    n = scores.shape[0]
+    i32 = dict(dtype=torch.int32, device=dev)
+    keep = torch.empty(n + 1, **i32)
+    succ = torch.empty(n + 1, **i32)
+    events = torch.empty((n + 1, 3), **i32)
+    counts = torch.zeros(4, **i32)  # n_keep, n_success, n_events, status
+    _check(lib().bf_nms_scan(_ptr(iou), _ptr(corners), _ptr(scores), _ptr(init_id),
+                             _ptr(cam_poses), c_int(n), _ptr(fl_items), _ptr(fl_len),
+                             _ptr(valid_num), _ptr(keep), _ptr(counts[0:1]), _ptr(succ),
+                             _ptr(counts[1:2]), _ptr(events), _ptr(counts[2:3]),
+                             _ptr(counts[3:4]), ctypes.byref(cfg), _stream()), "bf_nms_scan")
+    return keep, succ, events, counts
+
+
+def corr_assoc(corners, dims, scores, boxes2d, init_id, cam_poses, cur_pose, K, n_glo, mask,
+               success, fl_items, fl_len, valid_num, cfg: CorrCfg):
+    dev = corners.device
+    n_all = scores.shape[0]
+    i32 = dict(dtype=torch.int32, device=dev)
+    keep = torch.empty(max(1, mask.shape[0]), **i32)
+    events = torch.empty((n_all + 1, 3), **i32)
+    counts = torch.zeros(3, **i32)  # n_keep, n_events, status
+    succ = success if success.numel() else torch.zeros(1, **i32)
+    _check(lib().bf_corr_assoc(_ptr(corners), _ptr(dims), _ptr(scores), _ptr(boxes2d),
+                               _ptr(init_id), _ptr(cam_poses), _ptr(cur_pose), _ptr(K),
+                               c_int(n_all), c_int(n_glo), _ptr(mask), c_int(mask.shape[0]),
+                               _ptr(succ), c_int(success.numel()), _ptr(fl_items), _ptr(fl_len),
+                               _ptr(valid_num), _ptr(keep), _ptr(counts[0:1]), _ptr(events),
+                               _ptr(counts[1:2]), _ptr(counts[2:3]), ctypes.byref(cfg),
+                               _stream()), "bf_corr_assoc")
+    return keep, events, counts
+
+
+# ------------------------------------------------------------------------------------------
+# fusion
+# ------------------------------------------------------------------------------------------
+def fusion_fit(view_off, n_views, view_box, view_R, view_score, view_pose, view_tc, pst,
+               cfg: FuseCfg, trace=False):
+    dev = view_box.device
+    n_jobs = view_off.shape[0]
+    out_box = torch.empty((n_jobs, 6), dtype=torch.float32, device=dev)
+    out_upd = torch.empty(n_jobs, dtype=torch.int32, device=dev)
+    out_it = torch.empty(n_jobs, dtype=torch.int32, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    tr = (torch.empty((n_jobs, cfg.iters, cfg.pst_size), dtype=torch.float32, device=dev)
+          if trace else None)
+    _check(lib().bf_fusion_fit(_ptr(view_off), _ptr(n_views), c_int(n_jobs), _ptr(view_box),
+                               _ptr(view_R), _ptr(view_score), _ptr(view_pose), _ptr(view_tc),
+                               _ptr(pst), ctypes.byref(cfg), _ptr(out_box), _ptr(out_upd),
+                               _ptr(out_it), _ptr(tr), _ptr(status), _stream()), "bf_fusion_fit")
+    return out_box, out_upd, out_it, status, tr
+
+
+def fusion_fitness(box, R, view_pose, view_tc, pst, search_size, cfg: FuseCfg):
+    nv = view_pose.shape[0]
+    out = torch.empty(pst.shape[0], dtype=torch.float32, device=box.device)
+    _check(lib().bf_fusion_fitness(_ptr(box), _ptr(R), c_int(nv), _ptr(view_pose),
+                                   _ptr(view_tc), _ptr(pst), c_int(pst.shape[0]),
+                                   _ptr(search_size), ctypes.byref(cfg), _ptr(out), _stream()),
+           "bf_fusion_fitness")
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# per-frame depth
+# ------------------------------------------------------------------------------------------
+def depth_standardize(depth):
+    """depth f32[b,h,w] -> (standardised f32[b,h,w], params f32[b,2])"""
+    depth = _need(depth.contiguous(), torch.float32, "depth")
+    b, h, w = depth.shape
+    out = torch.empty_like(depth)
+    params = torch.empty((b, 2), dtype=torch.float32, device=depth.device)
+    _check(lib().bf_depth_standardize(_ptr(depth), c_int(b), c_int(h), c_int(w), _ptr(out),
+                                      _ptr(params), None, _stream()), "bf_depth_standardize")
+    return out, params
+
+
+def backproject(depth, K, RT, max_depth=10.0):
+    h, w = depth.shape
+    xyz = torch.empty((h, w, 3), dtype=torch.float32, device=depth.device)
+    valid = torch.empty((h, w), dtype=torch.uint8, device=depth.device)
+    _check(lib().bf_backproject(_ptr(depth.contiguous()), _ptr(K.contiguous()),
+                                _ptr(RT.contiguous()), c_int(h), c_int(w),
+                                c_float(max_depth if max_depth is not None else 0.0), _ptr(xyz),
+                                _ptr(valid), _stream()), "bf_backproject")
+    return xyz, valid.bool()

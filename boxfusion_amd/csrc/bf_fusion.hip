@@ -1,0 +1,455 @@
+// bf_fusion.hip — multi-view box fusion (particle-swarm refinement) on gfx950.
+//
+// Reference: BoxFusion.boxfusion (box_fusion.py:622-724).  The reference launches its CUDA
+// kernel compute_iou_value (:264-405) once per iteration per box, with a host round trip, a
+// Python loop over 1023 particles (cal_transform :475-535) and host scalar updates (update_PST
+// :537-563, momentum :685-706).  Here ONE launch refines every job: workgroup = one fused box,
+// lane = one particle (pst_size <= 1024 lanes = 16 wave64), and all iterations run on the device:
+//
+//   per iteration:  fitness[p] = sum_v |1 - IoU2D(hull(proj_v(box (+) PST[p]*s)), hull(tc_v))|
+//                                / (V + 1e-6)            (views summed in order: deterministic,
+//                                                         unlike the reference's atomicAdd)
+//                   accepted = first `max_accept` particles j >= 1 with fitness[j] < fitness[0]
+//                              (block ballot prefix, order-preserving)
+//                   weighted sums in reference order on 8 lanes (f64 or f32 per promotion mode)
+//                   lane 0: cal_transform / update_PST / momentum / accept, exactly as the host
+//
+// Arithmetic follows the reference kernel's float32 (+ f64 line intersection) expression by
+// expression; compiled with -ffp-contract=off.  Hull buffers have fixed capacity; inputs that
+// would overflow the reference's own fixed buffers (corners_i[36], convex_inter[8]) set
+// BF_DEV_HULL_OVERFLOW (the result is still the mathematically intended one).
+#include "bf_common.h"
+
+#define FUSE_MAX_VIEWS 32
+#define FUSE_MAX_PST 1024
+#define CAND_CAP 64
+
+struct P2 {
+    float x, y;
+};
+
+__device__ __forceinline__ float cross2(P2 o, P2 a, P2 b) {
+    return (a.x - o.x) * (b.y - o.y) - (a.y - o.y) * (b.x - o.x);
+}
+
+// convex_hull (box_fusion.py:95-145): exchange sort by (x, y), monotone chain, pop on cross <= 0
+template <int CAP>
+__device__ int convex_hull(P2* in, int n, P2* out) {
+    if (n == 0) return 0;
+    for (int i = 0; i < n - 1; ++i)
+        for (int j = i + 1; j < n; ++j)
+            if (in[i].x > in[j].x || (in[i].x == in[j].x && in[i].y > in[j].y)) {
+                P2 tt = in[i]; in[i] = in[j]; in[j] = tt;
+            }
+    P2 lower[CAP], upper[CAP];
+    int nl = 0, nu = 0;
+    for (int i = 0; i < n; ++i) {
+        while (nl >= 2 && cross2(lower[nl - 2], lower[nl - 1], in[i]) <= 0) nl--;
+        lower[nl++] = in[i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        while (nu >= 2 && cross2(upper[nu - 2], upper[nu - 1], in[i]) <= 0) nu--;
+        upper[nu++] = in[i];
+    }
+    nl--; nu--;
+    for (int i = 0; i < nl; ++i) out[i] = lower[i];
+    for (int i = 0; i < nu; ++i) out[nl + i] = upper[i];
+    return nl + nu;
+}
+
+__device__ __forceinline__ float polygon_area(const P2* p, int n) {
+    float a = 0.0f;
+    for (int i = 0; i < n; ++i) {
+        P2 p1 = p[i], p2 = p[(i + 1) % n];
+        a += p1.x * p2.y - p2.x * p1.y;
+    }
+    return (float)(fabs((double)a) / 2.0);
+}
+
+__device__ __forceinline__ bool line_intersection(P2 a1, P2 a2, P2 b1, P2 b2, P2* out) {
+    double dx1 = a2.x - a1.x, dy1 = a2.y - a1.y, dx2 = b2.x - b1.x, dy2 = b2.y - b1.y;
+    double den = dx1 * dy2 - dy1 * dx2;
+    if (fabs(den) < 1e-8) return false;
+    double tt = (dx2 * (a1.y - b1.y) + dy2 * (b1.x - a1.x)) / den;
+    double s = (dx1 * (a1.y - b1.y) + dy1 * (b1.x - a1.x)) / den;
+    if (tt >= -1e-8 && tt <= 1.00000001 && s >= -1e-8 && s <= 1.00000001) {
+        out->x = (float)(a1.x + tt * dx1);
+        out->y = (float)(a1.y + tt * dy1);
+        return true;
+    }
+    return false;
+}
+
+__device__ __forceinline__ bool point_in_polygon(P2 p, const P2* poly, int n) {
+    bool in = false;
+    for (int i = 0; i < n; ++i) {
+        P2 p1 = poly[i], p2 = poly[(i + 1) % n];
+        if ((p1.y > p.y) != (p2.y > p.y)) {
+            float xi = ((p.y - p1.y) * (p2.x - p1.x) / (p2.y - p1.y)) + p1.x;
+            if (p.x < xi) in = !in;
+        }
+    }
+    return in;
+}
+
+// IoU of the hulls of two 8-point sets (polygon_intersection :202-261 + :374-396)
+__device__ float iou_hulls(P2* c0, P2* ct, int* flags) {
+    P2 h0[8], ht[8];
+    int n0 = convex_hull<8>(c0, 8, h0);
+    int nt = convex_hull<8>(ct, 8, ht);
+    P2 cand[CAND_CAP];
+    int nc = 0;
+    for (int i = 0; i < n0; ++i)
+        if (point_in_polygon(h0[i], ht, nt) && nc < CAND_CAP) cand[nc++] = h0[i];
+    for (int i = 0; i < nt; ++i)
+        if (point_in_polygon(ht[i], h0, n0) && nc < CAND_CAP) cand[nc++] = ht[i];
+    for (int i = 0; i < n0; ++i)
+        for (int j = 0; j < nt; ++j) {
+            P2 pt;
+            if (line_intersection(h0[i], h0[(i + 1) % n0], ht[j], ht[(j + 1) % nt], &pt)) {
+                if (nc < CAND_CAP) cand[nc++] = pt;
+                else *flags |= BF_DEV_HULL_OVERFLOW;
+            }
+        }
+    if (nc > 36) *flags |= BF_DEV_HULL_OVERFLOW;
+    P2 hi[CAND_CAP];
+    int ni = convex_hull<CAND_CAP>(cand, nc, hi);
+    if (ni > 8) *flags |= BF_DEV_HULL_OVERFLOW;
+    float inter = polygon_area(hi, ni);
+    float a0 = polygon_area(h0, n0);
+    float at = polygon_area(ht, nt);
+    float uni = a0 + at - inter;
+    float iou = 0;
+    if (uni > 0) iou = (float)((double)inter / ((double)uni + 0.00001));
+    return iou;
+}
+
+struct FuseViews {
+    float pose[FUSE_MAX_VIEWS][16];
+    float tc[FUSE_MAX_VIEWS][16];
+};
+
+// fitness of one particle (box already perturbed into its 8 corners) over all views
+__device__ float particle_fitness(const float* corners, const FuseViews& V, int nv,
+                                  const bf_fuse_cfg& cfg, int* flags) {
+    float val = 0.0f, cnt = 0.0f;
+    for (int v = 0; v < nv; ++v) {
+        const float* P = V.pose[v];
+        P2 c0[8], ct[8];
+        for (int j = 0; j < 8; ++j) {
+            float vx = corners[3 * j] - P[3], vy = corners[3 * j + 1] - P[7], vz = corners[3 * j + 2] - P[11];
+            float cx = P[0] * vx + P[4] * vy + P[8] * vz;
+            float cy = P[1] * vx + P[5] * vy + P[9] * vz;
+            float cz = P[2] * vx + P[6] * vy + P[10] * vz;
+            float px = ((cx * cfg.K[0]) / cz + cfg.K[2]);
+            float py = ((cy * cfg.K[5]) / cz + cfg.K[6]);
+            c0[j].x = (px > cfg.img_w) ? cfg.img_w : (px < 0) ? 0 : px;
+            c0[j].y = (py > cfg.img_h) ? cfg.img_h : (py < 0) ? 0 : py;
+            ct[j].x = V.tc[v][2 * j];
+            ct[j].y = V.tc[v][2 * j + 1];
+        }
+        float iou = iou_hulls(c0, ct, flags);
+        val += fabsf(1 - iou);
+        cnt += 1.0f;
+    }
+    return val / (cnt + 1e-6f);
+}
+
+// compute_iou_value's box perturbation + corners (box_fusion.py:289-331)
+__device__ __forceinline__ void particle_corners(const float* box, const float* R, const float* prow,
+                                                 const float* ss, float* corners) {
+    float x = box[0] + prow[0] * ss[0];
+    float y = box[1] + prow[1] * ss[1];
+    float z = box[2] + prow[2] * ss[2];
+    float w = box[5] + prow[5] * ss[5];
+    float h = box[4] + prow[4] * ss[4];
+    float l = box[3] + prow[3] * ss[3];
+    w = fmaxf(w, 0.01f);
+    h = fmaxf(h, 0.01f);
+    l = fmaxf(l, 0.01f);
+    const float xyz[3] = {x, y, z};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const float v[3] = {bf_vsign_x(c) > 0 ? l / 2 : -l / 2, bf_vsign_y(c) > 0 ? h / 2 : -h / 2,
+                            bf_vsign_z(c) > 0 ? w / 2 : -w / 2};
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            float s = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) s += R[j * 3 + k] * v[k];
+            s += xyz[j];
+            corners[3 * c + j] = s;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// single evaluation (evaluate_iou) — used by tests and by callers that drive their own loop
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) k_fitness(const float* __restrict__ box,
+                                                  const float* __restrict__ R, int nv,
+                                                  const float* __restrict__ vpose,
+                                                  const float* __restrict__ vtc,
+                                                  const float* __restrict__ pst, int np_,
+                                                  const float* __restrict__ ss, bf_fuse_cfg cfg,
+                                                  float* __restrict__ fitness) {
+    __shared__ FuseViews V;
+    for (int q = threadIdx.x; q < nv * 16; q += blockDim.x) {
+        V.pose[q / 16][q % 16] = vpose[q];
+        V.tc[q / 16][q % 16] = vtc[q];
+    }
+    __syncthreads();
+    int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= np_) return;
+    float b[6], r[9], s[6], corners[24];
+    for (int k = 0; k < 6; ++k) { b[k] = box[k]; s[k] = ss[k]; }
+    for (int k = 0; k < 9; ++k) r[k] = R[k];
+    particle_corners(b, r, pst + 6 * p, s, corners);
+    int flags = 0;
+    fitness[p] = particle_fitness(corners, V, nv, cfg, &flags);
+}
+
+BF_API int bf_fusion_fitness(const float* box, const float* R, int n_views, const float* view_pose,
+                             const float* view_tc, const float* pst, int pst_size,
+                             const float* search_size, const bf_fuse_cfg* cfg, float* fitness,
+                             void* stream) {
+    if (!cfg || !box || !R || !view_pose || !view_tc || !pst || !search_size || !fitness)
+        return BF_ERR_ARG;
+    if (n_views <= 0 || n_views > FUSE_MAX_VIEWS || pst_size <= 0) return BF_ERR_CAPACITY;
+    hipLaunchKernelGGL(k_fitness, dim3(bf_cdiv(pst_size, 256)), dim3(256), 0, bf_stream(stream), box,
+                       R, n_views, view_pose, view_tc, pst, pst_size, search_size, *cfg, fitness);
+    return bf_check_launch();
+}
+
+// ------------------------------------------------------------------------------------------
+// full refinement: one workgroup per job
+// ------------------------------------------------------------------------------------------
+struct FuseState {
+    double x[6];        // global_xyzlwh (f64, box_fusion.py:655)
+    float ss[6];        // search_size (f32)
+    float prev[6];      // previous_search_size (f32)
+    float R[9];         // mean_rot
+    float box32[6];     // x cast to f32 for the kernel
+    double dsum[8];     // cal_transform sums (legacy promotion)
+    float fsum[8];      // cal_transform sums (NEP 50 promotion)
+    int n_acc;
+    int prev_success, fails, need_update, stop, iters_done;
+};
+
+__global__ void __launch_bounds__(1024) k_fuse(const int32_t* __restrict__ view_off,
+                                               const int32_t* __restrict__ n_views,
+                                               const float* __restrict__ vbox,
+                                               const float* __restrict__ vR,
+                                               const float* __restrict__ vscore,
+                                               const float* __restrict__ vpose,
+                                               const float* __restrict__ vtc,
+                                               const float* __restrict__ pst, bf_fuse_cfg cfg,
+                                               float* __restrict__ out_box,
+                                               int32_t* __restrict__ out_updated,
+                                               int32_t* __restrict__ out_iters,
+                                               float* __restrict__ trace,
+                                               int32_t* __restrict__ status) {
+    const int job = blockIdx.x;
+    const int t = threadIdx.x;
+    const int P = cfg.pst_size;
+    const int nv = n_views[job];
+    const int off = view_off[job];
+    __shared__ FuseViews V;
+    __shared__ float s_pst[FUSE_MAX_PST][6];
+    __shared__ float s_fit[FUSE_MAX_PST];
+    __shared__ int s_acc[FUSE_MAX_PST];
+    __shared__ int s_wave[FUSE_MAX_PST / 64];
+    __shared__ FuseState S;
+    __shared__ int s_flags;
+    if (nv <= 0 || nv > FUSE_MAX_VIEWS) {  // uniform per workgroup
+        if (t == 0) {
+            out_updated[job] = 0;
+            out_iters[job] = 0;
+            atomicOr(status, BF_DEV_VIEW_OVERFLOW);
+        }
+        return;
+    }
+
+    for (int q = t; q < nv * 16; q += blockDim.x) {
+        V.pose[q / 16][q % 16] = vpose[(size_t)off * 16 + q];
+        V.tc[q / 16][q % 16] = vtc[(size_t)off * 16 + q];
+    }
+    for (int q = t; q < P * 6; q += blockDim.x) s_pst[q / 6][q % 6] = pst[q];
+    if (t == 0) {
+        s_flags = 0;
+        // init_opt_params (box_fusion.py:566-600)
+        const float* vb = vbox + (size_t)off * 6;
+        const float* vs = vscore + off;
+        int best = 0;
+        for (int v = 1; v < nv; ++v)
+            if (vs[v] > vs[best]) best = v;
+        for (int k = 0; k < 3; ++k) {
+            float s = vb[k];
+            for (int v = 1; v < nv; ++v) s = s + vb[6 * v + k];
+            S.x[k] = (double)(s / (float)nv);
+        }
+        const float* bd = vb + 6 * best + 3;
+        int si[3] = {0, 1, 2};
+        for (int i = 1; i < 3; ++i) {
+            int tt = si[i], j = i - 1;
+            while (j >= 0 && bd[si[j]] > bd[tt]) { si[j + 1] = si[j]; --j; }
+            si[j + 1] = tt;
+        }
+        int rank[3];
+        for (int r = 0; r < 3; ++r) rank[si[r]] = r;
+        float acc[3] = {0, 0, 0};
+        for (int v = 0; v < nv; ++v) {
+            float d[3] = {vb[6 * v + 3], vb[6 * v + 4], vb[6 * v + 5]};
+            for (int i = 1; i < 3; ++i) {
+                float tt = d[i];
+                int j = i - 1;
+                while (j >= 0 && d[j] > tt) { d[j + 1] = d[j]; --j; }
+                d[j + 1] = tt;
+            }
+            for (int k = 0; k < 3; ++k) acc[k] = (v == 0) ? d[rank[k]] : acc[k] + d[rank[k]];
+        }
+        for (int k = 0; k < 3; ++k) S.x[3 + k] = (double)(acc[k] / (float)nv);
+        for (int k = 0; k < 9; ++k) S.R[k] = vR[(size_t)(off + best) * 9 + k];
+        for (int k = 0; k < 3; ++k) {
+            S.ss[k] = (float)cfg.center_init;
+            S.ss[3 + k] = (float)cfg.shape_init;
+            S.prev[k] = 0.f;
+            S.prev[3 + k] = 0.f;
+        }
+        S.prev_success = 0; S.fails = 0; S.need_update = 0; S.stop = 0; S.iters_done = 0;
+    }
+    __syncthreads();
+
+    for (int it = 0; it < cfg.iters; ++it) {
+        if (t == 0)
+            for (int k = 0; k < 6; ++k) S.box32[k] = (float)S.x[k];
+        __syncthreads();
+        // ---- fitness of particle t ---------------------------------------------------------
+        if (t < P) {
+            float corners[24];
+            float b[6], r[9], ss[6];
+            for (int k = 0; k < 6; ++k) { b[k] = S.box32[k]; ss[k] = S.ss[k]; }
+            for (int k = 0; k < 9; ++k) r[k] = S.R[k];
+            particle_corners(b, r, s_pst[t], ss, corners);
+            int flags = 0;
+            float f = particle_fitness(corners, V, nv, cfg, &flags);
+            s_fit[t] = f;
+            if (flags) atomicOr(&s_flags, flags);
+            if (trace) trace[((size_t)job * cfg.iters + it) * P + t] = f;
+        }
+        __syncthreads();
+        // ---- accepted particles: j >= 1, fit[j] < fit[0], first max_accept in index order ----
+        const float f0 = s_fit[0];
+        bool flag = (t >= 1) && (t < P) && (s_fit[t] < f0);
+        unsigned long long m = __ballot(flag);
+        if (bf_lane() == 0) s_wave[t >> 6] = __popcll(m);
+        __syncthreads();
+        int before = 0, total = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+            if (w < (t >> 6)) before += s_wave[w];
+            total += s_wave[w];
+        }
+        int rnk = before + bf_lanes_below(m);
+        if (flag && rnk < cfg.max_accept) s_acc[rnk] = t;
+        const int n_acc = total < cfg.max_accept ? total : cfg.max_accept;
+        __syncthreads();
+        // ---- cal_transform sums in reference order (8 independent sequential sums) ---------
+        if (t < 8) {
+            double ds = 0.0;
+            float fs = 0.0f;
+            for (int k = 0; k < n_acc; ++k) {
+                int j = s_acc[k];
+                float w = f0 - s_fit[j];
+                float prod = (t < 6) ? s_pst[j][t] * w : (t == 6 ? w : s_fit[j] * w);
+                if (cfg.legacy_promotion) ds += (double)prod;
+                else fs = fs + prod;
+            }
+            S.dsum[t] = ds;
+            S.fsum[t] = fs;
+        }
+        __syncthreads();
+        // ---- lane 0: cal_transform tail, update_PST, momentum, accept ----------------------
+        if (t == 0) {
+            const bool success = n_acc > 0;
+            float mt[6] = {0, 0, 0, 0, 0, 0};
+            double iou_d = 0;
+            float iou_f = 0;
+            if (!success) {
+                iou_d = f0;
+                iou_f = f0;
+            } else if (cfg.legacy_promotion) {
+                iou_d = S.dsum[7] / S.dsum[6];
+                for (int k = 0; k < 6; ++k) mt[k] = (float)((S.dsum[k] / S.dsum[6]) * (double)S.ss[k]);
+            } else {
+                iou_f = S.fsum[7] / S.fsum[6];
+                for (int k = 0; k < 6; ++k) mt[k] = (S.fsum[k] / S.fsum[6]) * S.ss[k];
+            }
+            if (cfg.legacy_promotion) {
+                double s[6];
+                for (int k = 0; k < 6; ++k) s[k] = fabs((double)mt[k]) + cfg.min_scale;
+                double nrm = s[0] * s[0];
+                for (int k = 1; k < 6; ++k) nrm = nrm + s[k] * s[k];
+                nrm = sqrt(nrm);
+                for (int k = 3; k < 6; ++k) S.ss[k] = (float)(cfg.shape_coef * iou_d * (s[k] / nrm) + cfg.min_scale);
+                for (int k = 0; k < 3; ++k) S.ss[k] = (float)(cfg.center_coef * iou_d * (s[k] / nrm) + cfg.min_scale);
+            } else {
+                const float ms = (float)cfg.min_scale;
+                float s[6];
+                for (int k = 0; k < 6; ++k) s[k] = fabsf(mt[k]) + ms;
+                float nrm = s[0] * s[0];
+                for (int k = 1; k < 6; ++k) nrm = nrm + s[k] * s[k];
+                nrm = sqrtf(nrm);
+                for (int k = 3; k < 6; ++k) S.ss[k] = (float)cfg.shape_coef * iou_f * (s[k] / nrm) + ms;
+                for (int k = 0; k < 3; ++k) S.ss[k] = (float)cfg.center_coef * iou_f * (s[k] / nrm) + ms;
+            }
+            if (S.prev_success && success) {
+                for (int k = 0; k < 6; ++k) {
+                    if (cfg.legacy_promotion)
+                        S.ss[k] = (float)(cfg.beta * (double)S.ss[k] + (1.0 - cfg.beta) * (double)S.prev[k]);
+                    else
+                        S.ss[k] = (float)cfg.beta * S.ss[k] + (float)(1.0 - cfg.beta) * S.prev[k];
+                }
+            }
+            if (success) {
+                S.need_update = 1;
+                S.prev_success = 1;
+                S.fails = 0;
+                for (int k = 0; k < 6; ++k) S.x[k] += (double)mt[k];
+                for (int k = 0; k < 6; ++k) S.prev[k] = S.ss[k];
+            } else {
+                S.fails++;
+                S.prev_success = 0;
+            }
+            S.iters_done = it + 1;
+            if (S.fails >= 3) S.stop = 1;
+        }
+        __syncthreads();
+        if (S.stop) break;
+    }
+    if (t == 0) {
+        for (int k = 3; k < 6; ++k)
+            if (S.x[k] < 0.01) S.x[k] = 0.01;
+        for (int k = 0; k < 6; ++k) out_box[6 * job + k] = (float)S.x[k];
+        out_updated[job] = S.need_update;
+        out_iters[job] = S.iters_done;
+        if (s_flags) atomicOr(status, s_flags);
+    }
+}
+
+BF_API int bf_fusion_fit(const int32_t* view_off, const int32_t* n_views, int n_jobs,
+                         const float* view_box, const float* view_R, const float* view_score,
+                         const float* view_pose, const float* view_tc, const float* pst,
+                         const bf_fuse_cfg* cfg, float* out_box, int32_t* out_updated,
+                         int32_t* out_iters, float* trace, int32_t* status, void* stream) {
+    if (!cfg || n_jobs < 0) return BF_ERR_ARG;
+    if (n_jobs == 0) return BF_OK;
+    if (!view_off || !n_views || !view_box || !view_R || !view_score || !view_pose || !view_tc ||
+        !pst || !out_box || !out_updated || !out_iters || !status)
+        return BF_ERR_ARG;
+    if (cfg->pst_size <= 0 || cfg->pst_size > FUSE_MAX_PST || (cfg->pst_size % 64) != 0)
+        return BF_ERR_CAPACITY;
+    hipLaunchKernelGGL(k_fuse, dim3(n_jobs), dim3(cfg->pst_size), 0, bf_stream(stream), view_off,
+                       n_views, view_box, view_R, view_score, view_pose, view_tc, pst, *cfg,
+                       out_box, out_updated, out_iters, trace, status);
+    return bf_check_launch();
+}

@@ -1,0 +1,352 @@
+// bf_geom.hip — per-box and per-pixel geometry on gfx950 (HBM/latency-bound, no MFMA).
+//   bf_box_corners          boxes.py:725-778   GeneralInstance3DBoxes.corners
+//   bf_box_transform2world  boxes.py:825-833   GeneralInstance3DBoxes.transform2world
+//   bf_project_boxes        instances.py:333-369 Instances3D.project_3d_boxes
+//   bf_backproject          tools/utils.py:232-287 unproject / get_camera_coords
+//   bf_depth_standardize    preprocessor.py:97-129 Preprocessor.standardize_depth_map
+// Built with -ffp-contract=off so every f32 product/sum rounds like the reference's CPU path.
+#include "bf_common.h"
+
+// ------------------------------------------------------------------------------------------
+// corners: one thread per (box, corner)
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_box_corners(const float* __restrict__ b,
+                                                     const float* __restrict__ R, int n,
+                                                     float* __restrict__ out) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * 8) return;
+    int i = t >> 3, c = t & 7;
+    const float* x = b + 6 * i;
+    const float* r = R + 9 * i;
+    float hl = x[3] / 2, hh = x[4] / 2, hw = x[5] / 2;
+    float v0 = bf_vsign_x(c) > 0 ? hl : -hl;
+    float v1 = bf_vsign_y(c) > 0 ? hh : -hh;
+    float v2 = bf_vsign_z(c) > 0 ? hw : -hw;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        float s = r[3 * j + 0] * v0;
+        s = s + r[3 * j + 1] * v1;
+        s = s + r[3 * j + 2] * v2;
+        out[24 * i + 3 * c + j] = s + x[j];
+    }
+}
+
+BF_API int bf_box_corners(const float* xyzlhw, const float* R, int n, float* corners,
+                          void* stream) {
+    if (n < 0 || (n > 0 && (!xyzlhw || !R || !corners))) return BF_ERR_ARG;
+    if (n == 0) return BF_OK;
+    hipLaunchKernelGGL(k_box_corners, dim3(bf_cdiv(n * 8, 256)), dim3(256), 0, bf_stream(stream),
+                       xyzlhw, R, n, corners);
+    return bf_check_launch();
+}
+
+// ------------------------------------------------------------------------------------------
+// transform2world, in place: xyz <- Rc xyz + tc ; R <- Rc R
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_box_t2w(float* __restrict__ b, float* __restrict__ R,
+                                                 const float* __restrict__ P, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* p = P + 16 * i;
+    float x[3] = {b[6 * i], b[6 * i + 1], b[6 * i + 2]};
+    float r[9];
+    for (int k = 0; k < 9; ++k) r[k] = R[9 * i + k];
+    for (int j = 0; j < 3; ++j) {
+        float s = p[4 * j] * x[0];
+        s = s + p[4 * j + 1] * x[1];
+        s = s + p[4 * j + 2] * x[2];
+        b[6 * i + j] = s + p[4 * j + 3];
+    }
+    for (int j = 0; j < 3; ++j)
+        for (int c = 0; c < 3; ++c) {
+            float s = p[4 * j] * r[c];
+            s = s + p[4 * j + 1] * r[3 + c];
+            s = s + p[4 * j + 2] * r[6 + c];
+            R[9 * i + 3 * j + c] = s;
+        }
+}
+
+BF_API int bf_box_transform2world(float* xyzlhw, float* R, const float* cam_pose, int n,
+                                  void* stream) {
+    if (n < 0 || (n > 0 && (!xyzlhw || !R || !cam_pose))) return BF_ERR_ARG;
+    if (n == 0) return BF_OK;
+    hipLaunchKernelGGL(k_box_t2w, dim3(bf_cdiv(n, 256)), dim3(256), 0, bf_stream(stream), xyzlhw, R,
+                       cam_pose, n);
+    return bf_check_launch();
+}
+
+// ------------------------------------------------------------------------------------------
+// project: one thread per (box, corner); pose inverse per box (f64 cofactors)
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_project(const float* __restrict__ corners,
+                                                 const float* __restrict__ P,
+                                                 const float* __restrict__ K, int n, float W,
+                                                 float H, float* __restrict__ uv) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * 8) return;
+    int i = t >> 3, c = t & 7;
+    float pinv[16];
+    bf_inv4(P + 16 * i, pinv);
+    const float* q = corners + 24 * i + 3 * c;
+    float h[4] = {q[0], q[1], q[2], 1.0f};
+    float cam[3];
+    for (int r = 0; r < 3; ++r) {
+        float s = pinv[4 * r] * h[0];
+        s = s + pinv[4 * r + 1] * h[1];
+        s = s + pinv[4 * r + 2] * h[2];
+        s = s + pinv[4 * r + 3] * h[3];
+        cam[r] = s;
+    }
+    float u = (K[0] * cam[0] / cam[2]) + K[2];
+    float v = (K[4] * cam[1] / cam[2]) + K[5];
+    u = fminf(fmaxf(u, 0.f), W);
+    v = fminf(fmaxf(v, 0.f), H);
+    uv[16 * i + 2 * c] = u;
+    uv[16 * i + 2 * c + 1] = v;
+}
+
+BF_API int bf_project_boxes(const float* corners, const float* cam_pose, const float* K, int n,
+                            float W, float H, float* uv, void* stream) {
+    if (n < 0 || (n > 0 && (!corners || !cam_pose || !K || !uv))) return BF_ERR_ARG;
+    if (n == 0) return BF_OK;
+    hipLaunchKernelGGL(k_project, dim3(bf_cdiv(n * 8, 256)), dim3(256), 0, bf_stream(stream),
+                       corners, cam_pose, K, n, W, H, uv);
+    return bf_check_launch();
+}
+
+// ------------------------------------------------------------------------------------------
+// back-projection: one thread per pixel, K^-1 and RT in registers
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_backproject(const float* __restrict__ d,
+                                                     const float* __restrict__ K,
+                                                     const float* __restrict__ RT, int h, int w,
+                                                     float max_depth, float* __restrict__ xyz,
+                                                     uint8_t* __restrict__ valid) {
+    int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= h * w) return;
+    float K4[16] = {K[0], K[1], K[2], 0.f, K[3], K[4], K[5], 0.f, K[6], K[7], K[8], 0.f,
+                    0.f, 0.f, 0.f, 1.f};
+    float Ki[16];
+    bf_inv4(K4, Ki);
+    float dv = d[p];
+    int u = p % w, v = p / w;
+    float uvd[4] = {(float)u * dv, (float)v * dv, dv, 1.0f};
+    float cam[4];
+    for (int r = 0; r < 4; ++r) {
+        float s = Ki[4 * r] * uvd[0];
+        s = s + Ki[4 * r + 1] * uvd[1];
+        s = s + Ki[4 * r + 2] * uvd[2];
+        s = s + Ki[4 * r + 3] * uvd[3];
+        cam[r] = s;
+    }
+    for (int r = 0; r < 3; ++r) {
+        float s = RT[4 * r] * cam[0];
+        s = s + RT[4 * r + 1] * cam[1];
+        s = s + RT[4 * r + 2] * cam[2];
+        s = s + RT[4 * r + 3] * cam[3];
+        xyz[3 * p + r] = s;
+    }
+    bool ok = dv > 0.f;
+    if (max_depth > 0.f) ok = ok && (dv < max_depth);
+    valid[p] = ok ? 1 : 0;
+}
+
+BF_API int bf_backproject(const float* depth, const float* K, const float* RT, int h, int w,
+                          float max_depth, float* xyz, uint8_t* valid, void* stream) {
+    if (h <= 0 || w <= 0 || !depth || !K || !RT || !xyz || !valid) return BF_ERR_ARG;
+    hipLaunchKernelGGL(k_backproject, dim3(bf_cdiv(h * w, 256)), dim3(256), 0, bf_stream(stream),
+                       depth, K, RT, h, w, max_depth, xyz, valid);
+    return bf_check_launch();
+}
+
+// ------------------------------------------------------------------------------------------
+// depth standardisation: trimmed mean/std by radix select (3 x 11-bit digit passes over the
+// positive-float bit patterns), one 1024-thread workgroup per frame.
+//   valid = d > 0 (NaN and <= 0 are invalid), m = #valid,
+//   slice = sorted[int(0.1 m) : int(0.9 m)]  (preprocessor.py:117)
+// ------------------------------------------------------------------------------------------
+#define DS_THREADS 1024
+#define DS_BINS 2048
+
+__device__ __forceinline__ bool ds_valid(float x) { return x > 0.0f; }
+
+// block-wide exclusive scan over DS_BINS counters in LDS: find the bin holding rank `r`
+// (0-based) and return it; *below receives the count of elements in lower bins.
+__device__ int ds_find_bin(unsigned* hist, long long r, long long* below, int* red) {
+    // each of the 1024 threads owns 2 bins
+    int t = threadIdx.x;
+    unsigned a = hist[2 * t], b = hist[2 * t + 1];
+    unsigned s = a + b;
+    // inclusive scan of s across the block (wave scan + wave offsets)
+    unsigned incl = s;
+    for (int o = 1; o < 64; o <<= 1) {
+        unsigned y = __shfl_up(incl, o, 64);
+        if (bf_lane() >= o) incl += y;
+    }
+    __shared__ unsigned wsum[DS_THREADS / 64];
+    if (bf_lane() == 63) wsum[t >> 6] = incl;
+    __syncthreads();
+    unsigned off = 0;
+    for (int wv = 0; wv < (t >> 6); ++wv) off += wsum[wv];
+    unsigned excl = off + incl - s;  // count before bin 2t
+    if ((long long)excl <= r && r < (long long)(excl + a)) {
+        red[0] = 2 * t;
+        red[1] = (int)excl;
+    } else if ((long long)(excl + a) <= r && r < (long long)(excl + s)) {
+        red[0] = 2 * t + 1;
+        red[1] = (int)(excl + a);
+    }
+    __syncthreads();
+    int bin = red[0];
+    *below = red[1];
+    __syncthreads();
+    return bin;
+}
+
+__global__ void __launch_bounds__(DS_THREADS) k_depth_std(const float* __restrict__ depth, int n,
+                                                          float* __restrict__ out,
+                                                          float* __restrict__ params) {
+    const float* d = depth + (size_t)blockIdx.x * n;
+    float* o = out + (size_t)blockIdx.x * n;
+    __shared__ unsigned hist[2][DS_BINS];
+    __shared__ int red[2];
+    __shared__ long long s_m;
+    __shared__ double s_acc[2][DS_THREADS / 64];
+    __shared__ long long s_cnt[4][DS_THREADS / 64];
+    const int t = threadIdx.x;
+
+    // pass 0: count valid
+    long long m = 0;
+    for (int i = t; i < n; i += DS_THREADS) m += ds_valid(d[i]) ? 1 : 0;
+    m = bf_wave_sum_i64(m);
+    if (bf_lane() == 0) s_cnt[0][t >> 6] = m;
+    __syncthreads();
+    if (t == 0) {
+        long long s = 0;
+        for (int w = 0; w < DS_THREADS / 64; ++w) s += s_cnt[0][w];
+        s_m = s;
+    }
+    __syncthreads();
+    m = s_m;
+    long long klo = (long long)(0.1 * (double)m);
+    long long khi = (long long)((1.0 - 0.1) * (double)m);
+    long long L = khi - klo;
+    float mean_f, std_f;
+    if (L <= 1) {
+        mean_f = 0.0f;
+        std_f = 1.0f;
+    } else {
+        // radix select the values of rank klo and khi-1
+        long long r[2] = {klo, khi - 1};
+        unsigned prefix[2] = {0u, 0u};
+        const int shifts[3] = {21, 10, 0};
+        const unsigned widths[3] = {11, 11, 10};
+        for (int pass = 0; pass < 3; ++pass) {
+            for (int b = t; b < DS_BINS; b += DS_THREADS) { hist[0][b] = 0; hist[1][b] = 0; }
+            __syncthreads();
+            const int sh = shifts[pass];
+            const unsigned hi_shift = sh + widths[pass];
+            for (int i = t; i < n; i += DS_THREADS) {
+                float x = d[i];
+                if (!ds_valid(x)) continue;
+                unsigned u = __float_as_uint(x);
+                unsigned digit = (u >> sh) & ((1u << widths[pass]) - 1u);
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    bool match = (pass == 0) ? true : ((u >> hi_shift) == (prefix[q] >> hi_shift));
+                    if (match) atomicAdd(&hist[q][digit], 1u);
+                }
+            }
+            __syncthreads();
+            for (int q = 0; q < 2; ++q) {
+                long long below;
+                int bin = ds_find_bin(hist[q], r[q], &below, red);
+                prefix[q] |= ((unsigned)bin) << sh;
+                r[q] -= below;
+            }
+        }
+        float vlo = __uint_as_float(prefix[0]);
+        float vhi = __uint_as_float(prefix[1]);
+        // pass 4: sums of the middle, counts around the two order statistics
+        double sum = 0.0, sq = 0.0;
+        long long c_lt_lo = 0, c_eq_lo = 0, c_lt_hi = 0;
+        for (int i = t; i < n; i += DS_THREADS) {
+            float x = d[i];
+            if (!ds_valid(x)) continue;
+            c_lt_lo += x < vlo;
+            c_eq_lo += x == vlo;
+            c_lt_hi += x < vhi;
+            if (x > vlo && x < vhi) {
+                sum += (double)x;
+                sq += (double)x * (double)x;
+            }
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            sum += __shfl_xor(sum, off, 64);
+            sq += __shfl_xor(sq, off, 64);
+        }
+        c_lt_lo = bf_wave_sum_i64(c_lt_lo);
+        c_eq_lo = bf_wave_sum_i64(c_eq_lo);
+        c_lt_hi = bf_wave_sum_i64(c_lt_hi);
+        if (bf_lane() == 0) {
+            s_acc[0][t >> 6] = sum;
+            s_acc[1][t >> 6] = sq;
+            s_cnt[1][t >> 6] = c_lt_lo;
+            s_cnt[2][t >> 6] = c_eq_lo;
+            s_cnt[3][t >> 6] = c_lt_hi;
+        }
+        __syncthreads();
+        __shared__ float s_mean, s_std;
+        if (t == 0) {
+            double S = 0, Q = 0;
+            long long a = 0, e = 0, hl = 0;
+            for (int w = 0; w < DS_THREADS / 64; ++w) {
+                S += s_acc[0][w]; Q += s_acc[1][w];
+                a += s_cnt[1][w]; e += s_cnt[2][w]; hl += s_cnt[3][w];
+            }
+            double dl = (double)vlo, dh = (double)vhi;
+            if (vlo == vhi) {
+                S = (double)L * dl;
+                Q = (double)L * dl * dl;
+            } else {
+                long long n_lo = (a + e) - klo;
+                long long n_hi = khi - hl;
+                S += (double)n_lo * dl + (double)n_hi * dh;
+                Q += (double)n_lo * dl * dl + (double)n_hi * dh * dh;
+            }
+            double mu = S / (double)L;
+            double var = (Q - S * mu) / (double)(L - 1);
+            if (var < 0) var = 0;
+            float mf = (float)mu;
+            float vf = (float)var;
+            s_mean = mf;
+            s_std = sqrtf(vf + 1e-2f);
+        }
+        __syncthreads();
+        mean_f = s_mean;
+        std_f = s_std;
+    }
+    for (int i = t; i < n; i += DS_THREADS) {
+        float x = d[i];
+        float y = ds_valid(x) ? x : mean_f;
+        o[i] = (y - mean_f) / std_f;
+    }
+    if (t == 0) {
+        params[2 * blockIdx.x] = mean_f;
+        params[2 * blockIdx.x + 1] = std_f;
+    }
+}
+
+BF_API size_t bf_depth_standardize_workspace_size(int b, int h, int w) {
+    (void)b; (void)h; (void)w;
+    return 0;
+}
+
+BF_API int bf_depth_standardize(const float* depth, int b, int h, int w, float* out, float* params,
+                                void* workspace, void* stream) {
+    (void)workspace;
+    if (b <= 0 || h <= 0 || w <= 0 || !depth || !out || !params) return BF_ERR_ARG;
+    hipLaunchKernelGGL(k_depth_std, dim3(b), dim3(DS_THREADS), 0, bf_stream(stream), depth, h * w,
+                       out, params);
+    return bf_check_launch();
+}

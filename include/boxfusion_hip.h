@@ -36,6 +36,7 @@ typedef enum {
 #define BF_DEV_OK 0
 #define BF_DEV_FUSION_LIST_OVERFLOW 1   /* a fusion_list row exceeded its capacity */
 #define BF_DEV_HULL_OVERFLOW 2          /* a 2-D hull / clip buffer exceeded its capacity */
+#define BF_DEV_VIEW_OVERFLOW 4          /* a fusion job has 0 or more than 32 views (skipped) */
 
 #define BF_MAX_BOXES 4096               /* NMS / association scan limit per call */
 
@@ -77,10 +78,10 @@ int bf_obb_iou_matrix(const float* corners, int n, double* iou, void* workspace,
  *   + compute_pose_center_disparity (box_manager.py:188-215)
  * ------------------------------------------------------------------------------------------ */
 typedef struct {
-    float iou_threshold;     /* cfg box_fusion.nms_threshold */
-    float translation_gap;   /* cfg association.translation_gap (metres) */
-    float rotation_gap;      /* cfg association.rotation_gap (degrees) */
-    float center_gap;        /* 0.5 m (box_manager.py:55) */
+    double iou_threshold;    /* cfg box_fusion.nms_threshold (compared with f64 IoU) */
+    float translation_gap;   /* cfg association.translation_gap (metres, compared in f32) */
+    float rotation_gap;      /* cfg association.rotation_gap (degrees, compared in f32) */
+    double center_gap;       /* 0.5 m (box_manager.py:55) */
     int   max_list;          /* 5: a fusion list only grows while shorter than this */
     int   list_capacity;     /* row stride (capacity) of fl_items */
 } bf_nms_cfg;
@@ -107,8 +108,8 @@ int bf_nms_scan(const double* iou, const float* corners, const float* scores,
  *   (:670-717) + IoU_2D_box (:643-668) + BoxManager.record_corr (box_manager.py:90-129)
  * ------------------------------------------------------------------------------------------ */
 typedef struct {
-    float small_size;        /* cfg box_fusion.small_size */
-    float threshold;         /* cfg association.small_threshold */
+    double small_size;       /* cfg box_fusion.small_size */
+    double threshold;        /* cfg association.small_threshold (compared with f64 IoU) */
     float translation_gap;
     float rotation_gap;
     float W, H;              /* image size used for the 2-D projection */

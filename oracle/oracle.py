@@ -46,13 +46,13 @@ def _i32(a):
 
 
 class NmsCfg(ctypes.Structure):
-    _fields_ = [("iou_threshold", ctypes.c_float), ("translation_gap", ctypes.c_float),
-                ("rotation_gap", ctypes.c_float), ("center_gap", ctypes.c_float),
+    _fields_ = [("iou_threshold", ctypes.c_double), ("translation_gap", ctypes.c_float),
+                ("rotation_gap", ctypes.c_float), ("center_gap", ctypes.c_double),
                 ("max_list", ctypes.c_int), ("list_capacity", ctypes.c_int)]
 
 
 class CorrCfg(ctypes.Structure):
-    _fields_ = [("small_size", ctypes.c_float), ("threshold", ctypes.c_float),
+    _fields_ = [("small_size", ctypes.c_double), ("threshold", ctypes.c_double),
                 ("translation_gap", ctypes.c_float), ("rotation_gap", ctypes.c_float),
                 ("W", ctypes.c_float), ("H", ctypes.c_float),
                 ("max_list", ctypes.c_int), ("list_capacity", ctypes.c_int)]

@@ -1,0 +1,226 @@
+"""HIP fusion path vs the reference (golden traces) and vs the CPU oracle (seeded inputs).
+Runs only on a HIP device."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as OR
+from tests import trace_util as TU
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+CAP = 64
+
+
+def _t(a, dtype=torch.float32):
+    return torch.as_tensor(np.ascontiguousarray(a)).to(DEV, dtype)
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from boxfusion_amd import _lib
+    return _lib
+
+
+def nms_cfg(L, cap=CAP):
+    c = L.NmsCfg()
+    cfg = TU.SCANNET_CFG
+    c.iou_threshold = cfg["box_fusion"]["nms_threshold"]
+    c.translation_gap = cfg["association"]["translation_gap"]
+    c.rotation_gap = cfg["association"]["rotation_gap"]
+    c.center_gap = 0.5
+    c.max_list = 5
+    c.list_capacity = cap
+    return c
+
+
+def corr_cfg(L, cap=CAP):
+    c = L.CorrCfg()
+    cfg = TU.SCANNET_CFG
+    c.small_size = cfg["box_fusion"]["small_size"]
+    c.threshold = cfg["association"]["small_threshold"]
+    c.translation_gap = cfg["association"]["translation_gap"]
+    c.rotation_gap = cfg["association"]["rotation_gap"]
+    c.W, c.H = 640.0, 480.0
+    c.max_list = 5
+    c.list_capacity = cap
+    return c
+
+
+def fuse_cfg(L, legacy):
+    o = OR.fuse_cfg(TU.SCANNET_CFG, np.eye(4), 480, 640, legacy=legacy)
+    c = L.FuseCfg()
+    for name, _ in L.FuseCfg._fields_:
+        if name == "K":
+            K4 = np.eye(4, dtype=np.float32)
+            K4[:3, :3] = [[574.540771, 0.0, 322.522827], [0.0, 577.583740, 238.558853], [0, 0, 1]]
+            for i in range(16):
+                c.K[i] = float(K4.reshape(-1)[i])
+        else:
+            setattr(c, name, getattr(o, name))
+    return c
+
+
+class HipBackend:
+    def __init__(self, L, legacy=False):
+        self.L = L
+        self.pst = _t(np.load(TU.GOLDEN + "/../../boxfusion_amd/data/pst_1024_0.npy"))
+        self.fcfg = fuse_cfg(L, legacy)
+
+    def corners(self, tensor, R):
+        return self.L.box_corners(_t(tensor), _t(R)).cpu().numpy()
+
+    def iou_matrix(self, corners):
+        return self.L.obb_iou_matrix(_t(corners)).cpu().numpy()
+
+    def nms(self, iou, corners, scores, init_id, cam_poses, fusion_list, valid_num):
+        items, lens = OR.pack_lists(fusion_list, CAP)
+        it, ln, vn = _t(items, torch.int32), _t(lens, torch.int32), _t(valid_num)
+        keep, succ, ev, cnt = self.L.nms_scan(_t(iou, torch.float64), _t(corners), _t(scores),
+                                              _t(init_id, torch.int32), _t(cam_poses), it, ln, vn,
+                                              nms_cfg(self.L))
+        c = cnt.cpu().numpy()
+        assert c[3] == 0
+        return dict(keep=keep.cpu().numpy()[:c[0]], success=succ.cpu().numpy()[:c[1]],
+                    events=ev.cpu().numpy()[:c[2]],
+                    fusion_list=OR.unpack_lists(it.cpu().numpy(), ln.cpu().numpy(),
+                                                len(fusion_list)),
+                    valid_num=vn.cpu().numpy())
+
+    def corr(self, corners, dims, scores, boxes2d, init_id, cam_poses, pose, K, n_glo, keep,
+             success, fusion_list, valid_num):
+        items, lens = OR.pack_lists(fusion_list, CAP)
+        it, ln, vn = _t(items, torch.int32), _t(lens, torch.int32), _t(valid_num)
+        k, ev, cnt = self.L.corr_assoc(_t(corners), _t(dims), _t(scores), _t(boxes2d),
+                                       _t(init_id, torch.int32), _t(cam_poses), _t(pose), _t(K),
+                                       n_glo, _t(keep, torch.int32), _t(success, torch.int32),
+                                       it, ln, vn, corr_cfg(self.L))
+        c = cnt.cpu().numpy()
+        assert c[2] == 0
+        return dict(keep=k.cpu().numpy()[:c[0]],
+                    fusion_list=OR.unpack_lists(it.cpu().numpy(), ln.cpu().numpy(),
+                                                len(fusion_list)),
+                    valid_num=vn.cpu().numpy())
+
+    def fuse(self, views):
+        nv = [len(v[2]) for v in views]
+        off = np.concatenate([[0], np.cumsum(nv)[:-1]]).astype(np.int32)
+        cat = [np.concatenate([v[k] for v in views], 0) for k in range(5)]
+        box, upd, it, st, _ = self.L.fusion_fit(_t(off, torch.int32), _t(nv, torch.int32),
+                                                _t(cat[0]), _t(cat[1]), _t(cat[2]), _t(cat[3]),
+                                                _t(cat[4]), self.pst, self.fcfg)
+        b, u = box.cpu().numpy(), upd.cpu().numpy()
+        return [(b[i], int(u[i])) for i in range(len(views))]
+
+
+@pytest.mark.parametrize("name", ["fusion_trace.npz", "fusion_trace_small.npz"])
+def test_trace_replay_hip(L, name):
+    """NMS keep/success, fusion lists, association and fused boxes bit-exact vs the reference."""
+    stats = TU.replay(TU.load(name), HipBackend(L, legacy=False))
+    assert stats["fused"] > 10
+
+
+def test_obb_iou_pairs_hip(L):
+    g = TU.load("obb_pairs.npz")
+    c = g["corners"].reshape(-1, 8, 3)
+    iou = L.obb_iou_matrix(_t(c)).cpu().numpy()
+    got = np.array([iou[2 * k, 2 * k + 1] for k in range(len(g["iou"]))])
+    np.testing.assert_array_equal(got, g["iou"])
+    np.testing.assert_array_equal(iou, iou.T)
+
+
+def test_obb_iou_matrix_vs_oracle_large(L):
+    rng = np.random.default_rng(7)
+    n = 160
+    xyz = rng.uniform(-2, 2, (n, 3))
+    xyz[n // 2:] = xyz[:n // 2] + rng.normal(0, 0.1, (n // 2, 3))
+    b = np.concatenate([xyz, rng.uniform(0.1, 1.0, (n, 3))], 1).astype(np.float32)
+    yaw = rng.uniform(-np.pi, np.pi, n)
+    R = np.stack([[[np.cos(a), -np.sin(a), 0], [np.sin(a), np.cos(a), 0], [0, 0, 1]]
+                  for a in yaw]).astype(np.float32)
+    corners = OR.box_corners(b, R)
+    np.testing.assert_array_equal(L.box_corners(_t(b), _t(R)).cpu().numpy(), corners)
+    ref = OR.obb_iou_matrix(corners)
+    got = L.obb_iou_matrix(_t(corners)).cpu().numpy()
+    assert (ref[np.triu_indices(n, 1)] > 0).sum() > 50
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_fusion_legacy_promotion_vs_oracle(L):
+    """numpy-1.26 (pinned) promotion mode: f64 host scalars, bit-exact vs the oracle."""
+    t = TU.load("fusion_trace_small.npz")
+    be = HipBackend(L, legacy=True)
+    ocfg = OR.fuse_cfg(TU.SCANNET_CFG, np.array(be.fcfg.K).reshape(4, 4), 480, 640, legacy=True)
+    pst = np.load(TU.GOLDEN + "/../../boxfusion_amd/data/pst_1024_0.npy")
+    views = []
+    for kf in TU.keyframes(t):
+        for _, fl in kf.fusion_jobs():
+            idx = np.asarray(fl)
+            pf = kf.per_frame
+            views.append((pf["tensor"][idx], pf["R"][idx], pf["scores"][idx], pf["pose"][idx],
+                          pf["proj"][idx]))
+    got = be.fuse(views)
+    n_upd = 0
+    for v, (box, upd) in zip(views, got):
+        r = OR.fusion_fit(*v, pst, ocfg)
+        assert upd == r["updated"]
+        np.testing.assert_array_equal(box, r["box"])
+        n_upd += upd
+    assert n_upd > 10
+
+
+def test_fitness_single_vs_oracle(L):
+    t = TU.load("fusion_trace.npz")
+    pf = dict(tensor=t["pf_tensor"], R=t["pf_R"], pose=t["pf_pose"], proj=t["pf_proj"])
+    idx = np.arange(4)
+    be = HipBackend(L)
+    ss = np.array([0.1, 0.1, 0.1, 0.5, 0.5, 0.5], np.float32)
+    box = pf["tensor"][0]
+    got = L.fusion_fitness(_t(box), _t(pf["R"][0]), _t(pf["pose"][idx]), _t(pf["proj"][idx]),
+                           be.pst, _t(ss), be.fcfg).cpu().numpy()
+    ocfg = OR.fuse_cfg(TU.SCANNET_CFG, np.array(be.fcfg.K).reshape(4, 4), 480, 640)
+    ref = OR.fitness(box, pf["R"][0], pf["pose"][idx], pf["proj"][idx], be.pst.cpu().numpy(), ss,
+                     ocfg)
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_geometry_vs_golden(L):
+    g = TU.load("geometry.npz")
+    np.testing.assert_array_equal(L.box_corners(_t(g["xyzlhw"]), _t(g["R"])).cpu().numpy(),
+                                  g["corners_cam"])
+    b, R = _t(g["xyzlhw"]), _t(g["R"])
+    L.box_transform2world(b, R, _t(g["poses"]))
+    np.testing.assert_allclose(b.cpu().numpy(), g["world_tensor"], rtol=0, atol=2e-6)
+    np.testing.assert_allclose(R.cpu().numpy(), g["world_R"], rtol=0, atol=2e-6)
+    c = L.box_corners(b, R)
+    K = _t(np.array([[574.540771, 0, 322.522827], [0, 577.583740, 238.558853], [0, 0, 1]]))
+    uv = L.project_boxes(c, _t(g["poses"]), K, 640.0, 480.0).cpu().numpy()
+    np.testing.assert_allclose(uv, g["projected"], rtol=0, atol=2e-3)
+
+
+def test_depth_standardize_vs_golden_and_oracle(L):
+    g = TU.load("depth.npz")
+    out, params = L.depth_standardize(_t(g["depth"]))
+    out, params = out.cpu().numpy(), params.cpu().numpy()
+    np.testing.assert_allclose(params, g["params"], rtol=2e-6, atol=1e-6)
+    np.testing.assert_allclose(out, g["out"], rtol=0, atol=3e-6)
+    from boxfusion_amd.synthetic import frame_rgbd
+    d = np.stack([frame_rgbd(f)[1] for f in range(3)])
+    o2, p2 = L.depth_standardize(_t(d))
+    for i in range(3):
+        ro, rp = OR.depth_standardize(d[i])
+        np.testing.assert_allclose(p2.cpu().numpy()[i], rp, rtol=1e-6)
+        np.testing.assert_allclose(o2.cpu().numpy()[i], ro, rtol=0, atol=2e-6)
+
+
+def test_backproject_vs_oracle(L):
+    from boxfusion_amd.synthetic import frame_rgbd, Scene, SCANNET_K
+    d = frame_rgbd(3)[1]
+    RT = Scene().pose(3)
+    xyz, valid = L.backproject(_t(d), _t(SCANNET_K), _t(RT), 10.0)
+    rx, rv = OR.backproject(d, SCANNET_K, RT, 10.0)
+    np.testing.assert_array_equal(valid.cpu().numpy(), rv)
+    np.testing.assert_allclose(xyz.cpu().numpy(), rx, rtol=1e-5, atol=1e-5)
