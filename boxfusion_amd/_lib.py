@@ -221,3 +221,115 @@ def backproject(depth, K, RT, max_depth=10.0):
                                 c_float(max_depth if max_depth is not None else 0.0), _ptr(xyz),
                                 _ptr(valid), _stream()), "bf_backproject")
     return xyz, valid.bool()
+
+
+# ------------------------------------------------------------------------------------------
+# MFMA tower kernels
+# ------------------------------------------------------------------------------------------
+ACT = {None: 0, "none": 0, "gelu": 1, "relu": 2}
+
+
+def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype=torch.bfloat16,
+         row_map=None, m=None):
+    """out[orow(r)] = resid[...] + act(a @ w.T + bias); a bf16 [M,K] (row stride a.stride(0)),
+    w bf16 [N,K]. `out` may be given (its row stride is used)."""
+    _need(a, torch.bfloat16, "a")
+    _need(w, torch.bfloat16, "w")
+    M = a.shape[0] if m is None else m
+    N, K = w.shape
+    if out is None:
+        out = torch.empty((M, N), dtype=out_dtype, device=a.device)
+    c_bf16 = 1 if out.dtype == torch.bfloat16 else 0
+    if not c_bf16 and out.dtype != torch.float32:
+        raise HipError("gemm output must be bf16 or f32")
+    if resid is not None:
+        _need(resid, torch.float32, "resid")
+    if bias is not None:
+        _need(bias, torch.float32, "bias")
+    if a.stride(1) != 1 or w.stride(1) != 1 or out.stride(1) != 1:
+        raise HipError("gemm operands need unit column stride")
+    _check(lib().bf_gemm_bf16(c_void_p(a.data_ptr()), c_int(a.stride(0)), c_void_p(w.data_ptr()),
+                              c_int(w.stride(0)), _ptr(bias) if bias is not None else None,
+                              c_void_p(resid.data_ptr()) if resid is not None else None,
+                              c_int(resid.stride(0) if resid is not None else 0), c_int(resid_mod),
+                              c_void_p(out.data_ptr()), c_int(out.stride(0)), c_int(c_bf16),
+                              _ptr(row_map) if row_map is not None else None, c_int(M), c_int(N),
+                              c_int(K), c_int(ACT[act]), _stream()), "bf_gemm_bf16")
+    return out
+
+
+def attention(q, k, v, o, batch, heads, sq, sk, head_dim, scale, q_bs=None, k_bs=None, v_bs=None,
+              o_bs=None):
+    """q/k/v/o are 2-D token-major views [batch*S, >= heads*head_dim] (any row stride)."""
+    for x, n in ((q, "q"), (k, "k"), (v, "v"), (o, "o")):
+        _need(x, torch.bfloat16, n)
+    q_bs = sq * q.stride(0) if q_bs is None else q_bs
+    k_bs = sk * k.stride(0) if k_bs is None else k_bs
+    v_bs = sk * v.stride(0) if v_bs is None else v_bs
+    o_bs = sq * o.stride(0) if o_bs is None else o_bs
+    LL = ctypes.c_longlong
+    _check(lib().bf_attention_bf16(c_void_p(q.data_ptr()), c_void_p(k.data_ptr()),
+                                   c_void_p(v.data_ptr()), c_void_p(o.data_ptr()), c_int(batch),
+                                   c_int(heads), c_int(sq), c_int(sk), c_int(head_dim),
+                                   c_int(q.stride(0)), c_int(k.stride(0)), c_int(v.stride(0)),
+                                   c_int(o.stride(0)), LL(q_bs), LL(k_bs), LL(v_bs), LL(o_bs),
+                                   c_float(scale), _stream()), "bf_attention_bf16")
+    return o
+
+
+def layernorm(x, weight, bias, eps, out=None, row_map=None):
+    _need(x, torch.float32, "x")
+    M, C = x.shape
+    if out is None:
+        out = torch.empty((M, C), dtype=torch.bfloat16, device=x.device)
+    _check(lib().bf_layernorm(c_void_p(x.data_ptr()), c_int(x.stride(0)), _ptr(weight),
+                              _ptr(bias), c_float(eps), c_void_p(out.data_ptr()),
+                              c_int(out.stride(0)),
+                              _ptr(row_map) if row_map is not None else None, c_int(M), c_int(C),
+                              _stream()), "bf_layernorm")
+    return out
+
+
+def _f3(vals):
+    return (c_float * 3)(*[float(v) for v in vals])
+
+
+def im2col_rgb8(img, pad, patch, mean, std, out=None):
+    """img u8 [B,H,W,3] -> bf16 [B*(pad/patch)^2, 3*patch*patch]"""
+    _need(img, torch.uint8, "img")
+    B, H, W, _ = img.shape
+    n = B * (pad // patch) ** 2
+    if out is None:
+        out = torch.empty((n, 3 * patch * patch), dtype=torch.bfloat16, device=img.device)
+    _check(lib().bf_im2col_rgb8(_ptr(img), c_int(B), c_int(H), c_int(W), c_int(pad), c_int(patch),
+                                _f3(mean), _f3(std), c_void_p(out.data_ptr()),
+                                c_int(out.stride(0)), _stream()), "bf_im2col_rgb8")
+    return out
+
+
+def im2col_f32(x, pad, patch, out=None):
+    _need(x, torch.float32, "x")
+    B, H, W = x.shape
+    n = B * (pad // patch) ** 2
+    if out is None:
+        out = torch.empty((n, patch * patch), dtype=torch.bfloat16, device=x.device)
+    _check(lib().bf_im2col_f32(_ptr(x), c_int(B), c_int(H), c_int(W), c_int(pad), c_int(patch),
+                               c_void_p(out.data_ptr()), c_int(out.stride(0)), _stream()),
+           "bf_im2col_f32")
+    return out
+
+
+def crop_resize_im2col(img, boxes, img_idx, size, patch, mean, std, kpad, out=None):
+    """img u8 [F,H,W,3]; boxes i32 [N,4]; img_idx i32 [N] -> bf16 [N*(size/patch)^2, kpad]"""
+    _need(img, torch.uint8, "img")
+    F, H, W, _ = img.shape
+    N = boxes.shape[0]
+    if out is None:
+        out = torch.empty((N * (size // patch) ** 2, kpad), dtype=torch.bfloat16,
+                          device=img.device)
+    _check(lib().bf_crop_resize_im2col(_ptr(img), c_int(H), c_int(W), _ptr(boxes),
+                                       _ptr(img_idx) if img_idx is not None else None, c_int(N),
+                                       c_int(size), c_int(patch), _f3(mean), _f3(std),
+                                       c_void_p(out.data_ptr()), c_int(out.stride(0)), _stream()),
+           "bf_crop_resize_im2col")
+    return out

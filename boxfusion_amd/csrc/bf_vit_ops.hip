@@ -1,0 +1,263 @@
+// bf_vit_ops.hip — memory-bound companions of the MFMA kernels (gfx950):
+//   bf_layernorm      LayerNorm f32 -> bf16 with optional row scatter (window partition, pad rows
+//                     left to the caller's zero-fill) — vit.py:283-291,326 / open_clip ln_1/ln_2
+//   bf_im2col_rgb8    Preprocessor.normalize + ImageList pad + PatchEmbed im2col in one pass
+//                     (preprocessor.py:131-144, imagelist.py:55-115, vit.py:102-128)
+//   bf_im2col_f32     the same for the standardised depth map (1 channel)
+//   bf_crop_resize_im2col  tools/utils.py:405-403 crop -> 224x224 bilinear -> CLIP normalise ->
+//                     14x14 patch im2col (K padded with zeros to a multiple of 64)
+// One wave per LayerNorm row; im2col writes 16-B bf16x8 chunks (coalesced).
+#include "bf_common.h"
+
+typedef unsigned short u16;
+
+__device__ __forceinline__ u16 vf2bf(float f) {
+    __bf16 b = (__bf16)f;
+    return *reinterpret_cast<u16*>(&b);
+}
+
+struct alignas(16) W128 {
+    uint32_t x, y, z, w;
+};
+
+// ------------------------------------------------------------------------------------------
+// LayerNorm: one wave per row, C <= 4096, C % 4 == 0
+// ------------------------------------------------------------------------------------------
+template <int NPL>  // float4 per lane
+__global__ void __launch_bounds__(256) k_layernorm(const float* __restrict__ x, int ldx,
+                                                   const float* __restrict__ g,
+                                                   const float* __restrict__ bb, float eps,
+                                                   u16* __restrict__ out, int ldo,
+                                                   const int32_t* __restrict__ row_map, int M,
+                                                   int C) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= M) return;
+    const float* xr = x + (size_t)row * ldx;
+    float4 v[NPL];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+        int c = (lane + 64 * i) * 4;
+        v[i] = c < C ? *reinterpret_cast<const float4*>(xr + c) : make_float4(0, 0, 0, 0);
+        s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    const float mean = s / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+        int c = (lane + 64 * i) * 4;
+        if (c < C) {
+            float a = v[i].x - mean, b2 = v[i].y - mean, c2 = v[i].z - mean, d = v[i].w - mean;
+            q += (a * a + b2 * b2) + (c2 * c2 + d * d);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+    const float rstd = rsqrtf(q / (float)C + eps);
+    const int orow = row_map ? row_map[row] : row;
+    if (orow < 0) return;
+    u16* yr = out + (size_t)orow * ldo;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+        int c = (lane + 64 * i) * 4;
+        if (c < C) {
+            float4 gg = *reinterpret_cast<const float4*>(g + c);
+            float4 be = *reinterpret_cast<const float4*>(bb + c);
+            uint32_t lo = (uint32_t)vf2bf((v[i].x - mean) * rstd * gg.x + be.x) |
+                          ((uint32_t)vf2bf((v[i].y - mean) * rstd * gg.y + be.y) << 16);
+            uint32_t hi = (uint32_t)vf2bf((v[i].z - mean) * rstd * gg.z + be.z) |
+                          ((uint32_t)vf2bf((v[i].w - mean) * rstd * gg.w + be.w) << 16);
+            *reinterpret_cast<uint2*>(yr + c) = make_uint2(lo, hi);
+        }
+    }
+}
+
+BF_API int bf_layernorm(const float* x, int ldx, const float* gamma, const float* beta, float eps,
+                        void* out, int ldo, const int32_t* row_map, int M, int C, void* stream) {
+    if (!x || !gamma || !beta || !out || M < 0 || C <= 0 || C % 4 || ldx % 4 || ldo % 4)
+        return BF_ERR_ARG;
+    if (M == 0) return BF_OK;
+    dim3 grid((M + 3) / 4), block(256);
+    const int npl = (C / 4 + 63) / 64;
+#define LN(N) hipLaunchKernelGGL(k_layernorm<N>, grid, block, 0, bf_stream(stream), x, ldx, gamma, \
+                                 beta, eps, (u16*)out, ldo, row_map, M, C)
+    if (npl <= 1) LN(1);
+    else if (npl <= 2) LN(2);
+    else if (npl <= 3) LN(3);
+    else if (npl <= 4) LN(4);
+    else if (npl <= 5) LN(5);
+    else if (npl <= 8) LN(8);
+    else if (npl <= 16) LN(16);
+    else return BF_ERR_UNSUPPORTED;
+#undef LN
+    return bf_check_launch();
+}
+
+// ------------------------------------------------------------------------------------------
+// RGB u8 HWC -> normalised, zero-padded to a square of `pad`, patch im2col (K = 3*p*p ordered
+// c, ky, kx like the Conv2d weight), bf16.  One thread per 8 consecutive K elements (same c, ky).
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_im2col_rgb8(const uint8_t* __restrict__ img, int B, int H,
+                                                     int W, int pad, int p, float m0, float m1,
+                                                     float m2, float s0, float s1, float s2,
+                                                     u16* __restrict__ out, int ldo) {
+    const int np = pad / p;
+    const int K = 3 * p * p;
+    const int chunks = K / 8;
+    const long long total = (long long)B * np * np * chunks;
+    long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= total) return;
+    const int ch = (int)(id % chunks);
+    const long long prow = id / chunks;           // b*np*np + py*np + px
+    const int b = (int)(prow / (np * np));
+    const int pp = (int)(prow % (np * np));
+    const int py = pp / np, px = pp % np;
+    const int k0 = ch * 8;
+    const int c = k0 / (p * p), rem = k0 % (p * p);
+    const int ky = rem / p, kx0 = rem % p;
+    const int y = py * p + ky;
+    const float mean = c == 0 ? m0 : (c == 1 ? m1 : m2);
+    const float sd = c == 0 ? s0 : (c == 1 ? s1 : s2);
+    u16 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int x = px * p + kx0 + i;
+        float f = 0.f;
+        if (y < H && x < W) f = ((float)img[(((size_t)b * H + y) * W + x) * 3 + c] - mean) / sd;
+        v[i] = vf2bf(f);
+    }
+    W128 w = {(uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2] | ((uint32_t)v[3] << 16),
+              (uint32_t)v[4] | ((uint32_t)v[5] << 16), (uint32_t)v[6] | ((uint32_t)v[7] << 16)};
+    *reinterpret_cast<W128*>(out + (size_t)prow * ldo + k0) = w;
+}
+
+BF_API int bf_im2col_rgb8(const uint8_t* img, int B, int H, int W, int pad, int patch,
+                          const float* mean3, const float* std3, void* out, int ldo, void* stream) {
+    if (!img || !out || !mean3 || !std3 || B <= 0 || pad % patch || (3 * patch * patch) % 8 || ldo % 8)
+        return BF_ERR_ARG;
+    const int np = pad / patch;
+    const long long total = (long long)B * np * np * (3 * patch * patch / 8);
+    hipLaunchKernelGGL(k_im2col_rgb8, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       bf_stream(stream), img, B, H, W, pad, patch, mean3[0], mean3[1], mean3[2],
+                       std3[0], std3[1], std3[2], (u16*)out, ldo);
+    return bf_check_launch();
+}
+
+// single-channel f32 (standardised depth) -> zero-padded square -> im2col (K = p*p)
+__global__ void __launch_bounds__(256) k_im2col_f32(const float* __restrict__ x, int B, int H,
+                                                    int W, int pad, int p, u16* __restrict__ out,
+                                                    int ldo) {
+    const int np = pad / p;
+    const int chunks = p * p / 8;
+    const long long total = (long long)B * np * np * chunks;
+    long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= total) return;
+    const int ch = (int)(id % chunks);
+    const long long prow = id / chunks;
+    const int b = (int)(prow / (np * np));
+    const int pp = (int)(prow % (np * np));
+    const int py = pp / np, px = pp % np;
+    const int k0 = ch * 8;
+    const int ky = k0 / p, kx0 = k0 % p;
+    const int y = py * p + ky;
+    u16 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int xx = px * p + kx0 + i;
+        float f = (y < H && xx < W) ? x[((size_t)b * H + y) * W + xx] : 0.f;
+        v[i] = vf2bf(f);
+    }
+    W128 w = {(uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2] | ((uint32_t)v[3] << 16),
+              (uint32_t)v[4] | ((uint32_t)v[5] << 16), (uint32_t)v[6] | ((uint32_t)v[7] << 16)};
+    *reinterpret_cast<W128*>(out + (size_t)prow * ldo + k0) = w;
+}
+
+BF_API int bf_im2col_f32(const float* x, int B, int H, int W, int pad, int patch, void* out,
+                         int ldo, void* stream) {
+    if (!x || !out || B <= 0 || pad % patch || (patch * patch) % 8 || ldo % 8) return BF_ERR_ARG;
+    const int np = pad / patch;
+    const long long total = (long long)B * np * np * (patch * patch / 8);
+    hipLaunchKernelGGL(k_im2col_f32, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       bf_stream(stream), x, B, H, W, pad, patch, (u16*)out, ldo);
+    return bf_check_launch();
+}
+
+// ------------------------------------------------------------------------------------------
+// CLIP crops: for crop n with integer box (x1,y1,x2,y2) of frame img_idx[n] (u8 HWC):
+//   crop = img[y1:y2, x1:x2] (empty -> zeros), bilinear resize to S x S with half-pixel centres
+//   (cv2.INTER_LINEAR mapping), /255, (x - mean_c)/std_c, then p x p patch im2col with K padded
+//   to ldo (zeros).  Output rows: n*(S/p)^2 + patch.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_crop_im2col(const uint8_t* __restrict__ img, int H, int W,
+                                                     const int32_t* __restrict__ boxes,
+                                                     const int32_t* __restrict__ img_idx, int N,
+                                                     int S, int p, float m0, float m1, float m2,
+                                                     float s0, float s1, float s2,
+                                                     u16* __restrict__ out, int ldo) {
+    const int np = S / p;
+    const int chunks = ldo / 8;
+    const long long total = (long long)N * np * np * chunks;
+    long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= total) return;
+    const int ch = (int)(id % chunks);
+    const long long prow = id / chunks;
+    const int n = (int)(prow / (np * np));
+    const int pp = (int)(prow % (np * np));
+    const int py = pp / np, px = pp % np;
+    const int K = 3 * p * p;
+    const int x1 = boxes[4 * n], y1 = boxes[4 * n + 1], x2 = boxes[4 * n + 2], y2 = boxes[4 * n + 3];
+    const int cw = x2 - x1, chh = y2 - y1;
+    const uint8_t* im = img + (size_t)(img_idx ? img_idx[n] : 0) * H * W * 3;
+    u16 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int k = ch * 8 + i;
+        float f = 0.f;
+        if (k < K) {
+            const int c = k / (p * p), rem = k % (p * p);
+            const int oy = py * p + rem / p, ox = px * p + rem % p;
+            float val = 0.f;
+            if (cw > 0 && chh > 0) {
+                float sy = ((float)oy + 0.5f) * ((float)chh / (float)S) - 0.5f;
+                float sx = ((float)ox + 0.5f) * ((float)cw / (float)S) - 0.5f;
+                sy = fmaxf(sy, 0.f);
+                sx = fmaxf(sx, 0.f);
+                int iy0 = min((int)sy, chh - 1), ix0 = min((int)sx, cw - 1);
+                int iy1 = min(iy0 + 1, chh - 1), ix1 = min(ix0 + 1, cw - 1);
+                float fy = sy - (float)iy0, fx = sx - (float)ix0;
+                auto px_at = [&](int yy, int xx) {
+                    return (float)im[((size_t)(y1 + yy) * W + (x1 + xx)) * 3 + c];
+                };
+                float top = px_at(iy0, ix0) * (1.f - fx) + px_at(iy0, ix1) * fx;
+                float bot = px_at(iy1, ix0) * (1.f - fx) + px_at(iy1, ix1) * fx;
+                val = top * (1.f - fy) + bot * fy;
+            }
+            const float mean = c == 0 ? m0 : (c == 1 ? m1 : m2);
+            const float sd = c == 0 ? s0 : (c == 1 ? s1 : s2);
+            f = (val / 255.f - mean) / sd;
+        }
+        v[i] = vf2bf(f);
+    }
+    W128 w = {(uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2] | ((uint32_t)v[3] << 16),
+              (uint32_t)v[4] | ((uint32_t)v[5] << 16), (uint32_t)v[6] | ((uint32_t)v[7] << 16)};
+    *reinterpret_cast<W128*>(out + (size_t)prow * ldo + ch * 8) = w;
+}
+
+BF_API int bf_crop_resize_im2col(const uint8_t* img, int H, int W, const int32_t* boxes,
+                                 const int32_t* img_idx, int N, int size, int patch,
+                                 const float* mean3, const float* std3, void* out, int ldo,
+                                 void* stream) {
+    if (!img || !boxes || !out || !mean3 || !std3 || N < 0 || size % patch || ldo % 8 ||
+        ldo < 3 * patch * patch)
+        return BF_ERR_ARG;
+    if (N == 0) return BF_OK;
+    const int np = size / patch;
+    const long long total = (long long)N * np * np * (ldo / 8);
+    hipLaunchKernelGGL(k_crop_im2col, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       bf_stream(stream), img, H, W, boxes, img_idx, N, size, patch, mean3[0],
+                       mean3[1], mean3[2], std3[0], std3[1], std3[2], (u16*)out, ldo);
+    return bf_check_launch();
+}

@@ -191,6 +191,53 @@ int bf_depth_standardize(const float* depth, int b, int h, int w, float* out, fl
 int bf_backproject(const float* depth, const float* K, const float* RT, int h, int w,
                    float max_depth, float* xyz, uint8_t* valid, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * MFMA tower kernels: CuTR RGB-D ViT (boxfusion/vit.py, cubify_transformer.py) and the CLIP
+ * ViT-H/14 crop tower (tools/utils.py:383-403).  bf16 operands, f32 accumulation.
+ * ------------------------------------------------------------------------------------------ */
+
+/* C[orow(r),n] = (resid ? resid[rrow(r),n] : 0) + act(sum_k A[r,k] W[n,k] + bias[n])
+ *   A bf16[M,K] (row stride lda), W bf16[N,K] (nn.Linear layout, stride ldw), bias f32[N] or NULL,
+ *   resid f32 (stride ldr) or NULL, orow(r) = row_map ? row_map[r] : r (< 0 drops the row),
+ *   rrow(r) = resid_mod > 0 ? r % resid_mod : orow(r), C f32 or bf16 (c_bf16), stride ldc,
+ *   act 0 none / 1 GELU(erf) / 2 ReLU.  K % 64 == 0, lda/ldw % 8 == 0.
+ * Replaces the nn.Linear / 1x1-conv / patch-conv GEMMs of vit.py:102-342 and the open_clip
+ * transformer blocks (in_proj, out_proj, c_fc, c_proj, proj). */
+int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bias,
+                 const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
+                 const int32_t* row_map, int M, int N, int K, int act, void* stream);
+
+/* softmax(Q K^T * scale) V per (batch, head); X(b,h,s,d) at X + b*x_bs + s*x_rs + h*D + d,
+ * bf16 in/out, head_dim in {32, 64, 80, 128}.  Replaces vit.py Attention.forward (:170-203,
+ * joint RGB+depth window attention = plain attention over the concatenated 512 tokens) and the
+ * open_clip nn.MultiheadAttention of ViT-H/14. */
+int bf_attention_bf16(const void* q, const void* k, const void* v, void* o, int batch, int heads,
+                      int sq, int sk, int head_dim, int q_rs, int k_rs, int v_rs, int o_rs,
+                      long long q_bs, long long k_bs, long long v_bs, long long o_bs, float scale,
+                      void* stream);
+
+/* LayerNorm f32[M,C] -> bf16, written to row row_map[r] (NULL = r; < 0 skips). */
+int bf_layernorm(const float* x, int ldx, const float* gamma, const float* beta, float eps,
+                 void* out, int ldo, const int32_t* row_map, int M, int C, void* stream);
+
+/* Preprocessor.normalize + square zero pad + PatchEmbed im2col (preprocessor.py:131-144,
+ * imagelist.py:55-115, vit.py:102-128): img u8[B,H,W,3] -> bf16[B*(pad/p)^2, 3*p*p].
+ * mean3/std3 are HOST arrays of 3 floats. */
+int bf_im2col_rgb8(const uint8_t* img, int B, int H, int W, int pad, int patch,
+                   const float* mean3, const float* std3, void* out, int ldo, void* stream);
+
+/* single-channel f32 [B,H,W] -> zero-padded square -> bf16 im2col [B*(pad/p)^2, p*p] */
+int bf_im2col_f32(const float* x, int B, int H, int W, int pad, int patch, void* out, int ldo,
+                  void* stream);
+
+/* CLIP crop path (tools/utils.py:405-476 crop_image/segment_image + retriev's 224x224 resize):
+ * boxes i32[N,4] integer xyxy on frame img_idx[N] of img u8[*,H,W,3] -> bilinear SxS -> /255 ->
+ * (x-mean)/std -> p x p patch im2col bf16 [N*(S/p)^2, ldo] (K = 3p^2 zero-padded to ldo).
+ * mean3/std3 are HOST arrays. */
+int bf_crop_resize_im2col(const uint8_t* img, int H, int W, const int32_t* boxes,
+                          const int32_t* img_idx, int N, int size, int patch, const float* mean3,
+                          const float* std3, void* out, int ldo, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

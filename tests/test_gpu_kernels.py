@@ -1,0 +1,146 @@
+"""MFMA / vision kernels vs plain PyTorch fp32 references of the same ops (GPU only).
+Tolerances are for bf16 operands with f32 accumulation."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from boxfusion_amd import _lib
+    return _lib
+
+
+def rel_err(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
+
+
+@pytest.mark.parametrize("M,N,K", [(1600, 2304, 768), (257, 1280, 1280), (4112, 5120, 1280),
+                                   (100, 4, 256), (130, 136, 64)])
+def test_gemm_plain(L, M, N, K):
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g)
+    ref = a.float() @ w.float().T + b
+    out = L.gemm(a, w, b, out_dtype=torch.float32)
+    assert rel_err(out, ref) < 1e-5
+    outb = L.gemm(a, w, b)
+    assert rel_err(outb, ref) < 5e-3
+
+
+def test_gemm_gelu_resid_rowmap(L):
+    g = torch.Generator(device="cuda").manual_seed(3)
+    M, N, K = 300, 384, 192
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g)
+    resid = torch.randn(M + 10, N, device="cuda", generator=g)
+    perm = torch.randperm(M + 10, device="cuda", generator=g)[:M].int()
+    perm[::7] = -1
+    out = resid.clone()
+    L.gemm(a, w, b, act="gelu", resid=out, out=out, row_map=perm)
+    ref = resid.clone()
+    y = F.gelu(a.float() @ w.float().T + b)
+    keep = perm >= 0
+    ref[perm[keep].long()] += y[keep]
+    assert rel_err(out, ref) < 1e-5
+    # broadcast residual table (pos-embed style)
+    tab = torch.randn(100, N, device="cuda", generator=g)
+    o2 = L.gemm(a, w, b, resid=tab, resid_mod=100, out_dtype=torch.float32)
+    r2 = a.float() @ w.float().T + b + tab[torch.arange(M, device="cuda") % 100]
+    assert rel_err(o2, r2) < 1e-5
+
+
+def _attn_ref(q, k, v, B, H, S, D, scale):
+    qq = q.float().view(B, S, H, D).transpose(1, 2)
+    kk = k.float().view(B, -1, H, D).transpose(1, 2)
+    vv = v.float().view(B, -1, H, D).transpose(1, 2)
+    p = torch.softmax((qq * scale) @ kk.transpose(-1, -2), dim=-1)
+    return (p @ vv).transpose(1, 2).reshape(B * S, H * D)
+
+
+@pytest.mark.parametrize("B,H,S,D", [(9, 12, 512, 64), (2, 12, 1600, 64), (3, 16, 257, 80),
+                                     (2, 8, 302, 32), (1, 4, 70, 128)])
+def test_attention(L, B, H, S, D):
+    g = torch.Generator(device="cuda").manual_seed(B * S + D)
+    qkv = torch.randn(B * S, 3 * H * D, device="cuda", generator=g).bfloat16()
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    o = torch.empty(B * S, H * D, device="cuda", dtype=torch.bfloat16)
+    scale = D ** -0.5
+    L.attention(q, k, v, o, B, H, S, S, D, scale)
+    ref = _attn_ref(q, k, v, B, H, S, D, scale)
+    assert rel_err(o, ref) < 1e-2
+
+
+def test_attention_forced_rescale(L):
+    """a spike key late in the sequence forces the online-softmax rescale branch."""
+    B, H, S, D = 1, 2, 300, 64
+    g = torch.Generator(device="cuda").manual_seed(11)
+    qkv = torch.randn(B * S, 3 * H * D, device="cuda", generator=g)
+    qkv[250, H * D:2 * H * D] = qkv[0, :H * D] * 4.0
+    qkv = qkv.bfloat16()
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    o = torch.empty(B * S, H * D, device="cuda", dtype=torch.bfloat16)
+    L.attention(q, k, v, o, B, H, S, S, D, D ** -0.5)
+    assert rel_err(o, _attn_ref(q, k, v, B, H, S, D, D ** -0.5)) < 1e-2
+
+
+@pytest.mark.parametrize("C", [768, 1280, 256, 384])
+def test_layernorm(L, C):
+    g = torch.Generator(device="cuda").manual_seed(C)
+    x = torch.randn(333, C, device="cuda", generator=g) * 3 + 1
+    w = torch.randn(C, device="cuda", generator=g)
+    b = torch.randn(C, device="cuda", generator=g)
+    out = L.layernorm(x, w, b, 1e-6)
+    ref = F.layer_norm(x, (C,), w, b, 1e-6)
+    assert rel_err(out, ref) < 5e-3
+
+
+def test_im2col_rgb8_and_f32(L):
+    g = torch.Generator(device="cuda").manual_seed(0)
+    img = torch.randint(0, 256, (2, 480, 640, 3), device="cuda", dtype=torch.uint8, generator=g)
+    mean, std = [123.675, 116.28, 103.53], [58.395, 57.12, 57.375]
+    a = L.im2col_rgb8(img, 640, 16, mean, std)
+    x = (img.permute(0, 3, 1, 2).float() - torch.tensor(mean, device="cuda").view(1, 3, 1, 1)) \
+        / torch.tensor(std, device="cuda").view(1, 3, 1, 1)
+    x = F.pad(x, (0, 0, 0, 160))
+    ref = F.unfold(x, 16, stride=16).transpose(1, 2).reshape(-1, 768)
+    assert torch.equal(a, ref.bfloat16())
+    d = torch.rand(2, 480, 640, device="cuda", generator=g)
+    ad = L.im2col_f32(d, 640, 16)
+    refd = F.unfold(F.pad(d[:, None], (0, 0, 0, 160)), 16, stride=16).transpose(1, 2).reshape(-1, 256)
+    assert torch.equal(ad, refd.bfloat16())
+
+
+def test_crop_resize_im2col(L):
+    g = torch.Generator(device="cuda").manual_seed(1)
+    img = torch.randint(0, 256, (2, 480, 640, 3), device="cuda", dtype=torch.uint8, generator=g)
+    boxes = torch.tensor([[10, 20, 200, 150], [0, 0, 640, 480], [300, 300, 301, 310],
+                          [5, 5, 5, 40]], device="cuda", dtype=torch.int32)
+    idx = torch.tensor([0, 1, 1, 0], device="cuda", dtype=torch.int32)
+    mean = [0.48145466, 0.4578275, 0.40821073]
+    std = [0.26862954, 0.26130258, 0.27577711]
+    out = L.crop_resize_im2col(img, boxes, idx, 224, 14, mean, std, 640)
+    assert out.shape == (4 * 256, 640)
+    assert torch.all(out[:, 588:] == 0)
+    # reference: torch bilinear (align_corners=False, no antialias) on the crop
+    for n in range(3):
+        x1, y1, x2, y2 = boxes[n].tolist()
+        crop = img[idx[n], y1:y2, x1:x2].permute(2, 0, 1)[None].float()
+        r = F.interpolate(crop, size=(224, 224), mode="bilinear", align_corners=False)
+        r = (r / 255 - torch.tensor(mean, device="cuda").view(1, 3, 1, 1)) / \
+            torch.tensor(std, device="cuda").view(1, 3, 1, 1)
+        ref = F.unfold(r, 14, stride=14).transpose(1, 2).reshape(-1, 588)
+        got = out[n * 256:(n + 1) * 256, :588].float()
+        assert (got - ref).abs().max().item() < 0.05
+    empty = ((0 - torch.tensor(mean, device="cuda")) / torch.tensor(std, device="cuda"))
+    empty = empty.repeat_interleave(196).bfloat16().float()[None]
+    assert torch.all(out[3 * 256:, :588].float() == empty)
