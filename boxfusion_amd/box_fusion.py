@@ -1,0 +1,115 @@
+"""Multi-view box fusion (reference: boxfusion/box_fusion.py).
+
+`BoxFusion.boxfusion(all_pred_box, per_frame_box, box_manager)` keeps the reference's selection
+rules (>= 3 views, list not already fused; box_fusion.py:631-635) and write-back semantics
+(xyz + lhw refined, lhw >= 0.01, R unchanged; :716-724), but every box is refined in ONE launch of
+bf_fusion_fit with all iterations on the device (no per-iteration host round trip).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from boxfusion_amd import _lib
+
+DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
+
+
+def load_pst(path=None):
+    """particle table [pst_size, 6] f32 (data/pst_1024_0.tiff in the reference)."""
+    if path and path.endswith(".npy") and os.path.exists(path):
+        return np.load(path).astype(np.float32)
+    if path and os.path.exists(path) and path.endswith((".tif", ".tiff")):
+        from PIL import Image
+        return np.array(Image.open(path)).astype(np.float32)
+    return np.load(os.path.join(DATA, "pst_1024_0.npy")).astype(np.float32)
+
+
+class BoxFusion:
+    def __init__(self, cfg, device="cuda", legacy_promotion=True):
+        self.cfg = cfg
+        self.PST = load_pst(cfg["box_fusion"].get("pst_path"))
+        self.K = np.eye(4)
+        cam = cfg.get("cam", {})
+        if "fx" in cam:
+            self.K[:3, :3] = [[cam["fx"], 0.0, cam["cx"]], [0.0, cam["fy"], cam["cy"]], [0, 0, 1]]
+            self.H, self.W = cam["H"], cam["W"]
+        else:
+            self.H, self.W = cam.get("W", 480), cam.get("H", 640)  # CA-1M swaps (box_fusion.py:50-51)
+        self.update_K_flag = False
+        bf = cfg["box_fusion"]
+        ro = bf["random_opt"]
+        self.fusion_iters = int(bf["iters"])
+        self.pst_size = int(bf["pst_size"])
+        self.center_init_size = ro["center_init_size"]
+        self.center_scaling_coefficient = ro["center_scaling_coefficient"]
+        self.shape_init_size = ro["shape_init_size"]
+        self.shape_scaling_coefficient = ro["shape_scaling_coefficient"]
+        # numpy<2 value-based promotion (requirements.txt pins numpy 1.26.4) unless overridden
+        self.legacy_promotion = bool(bf.get("legacy_promotion", legacy_promotion))
+        self.device = torch.device(device)
+        self._pst_dev = torch.from_numpy(self.PST[: self.pst_size]).to(self.device).contiguous()
+        self.last_stats = {}
+
+    def update_intrinsics(self, size, K):
+        self.H = size[1]
+        self.W = size[0]
+        self.K[:3, :3] = K
+
+    def fuse_cfg(self):
+        c = _lib.FuseCfg()
+        c.iters = self.fusion_iters
+        c.pst_size = self.pst_size
+        c.max_accept = 200
+        c.legacy_promotion = 1 if self.legacy_promotion else 0
+        c.center_init = float(self.center_init_size)
+        c.shape_init = float(self.shape_init_size)
+        c.center_coef = float(self.center_scaling_coefficient)
+        c.shape_coef = float(self.shape_scaling_coefficient)
+        c.beta = 0.9
+        c.min_scale = 1e-3
+        c.img_h, c.img_w = float(self.H), float(self.W)
+        k = self.K.astype(np.float32).reshape(-1)
+        for i in range(16):
+            c.K[i] = float(k[i])
+        return c
+
+    def boxfusion(self, all_pred_box, per_frame_box, box_manager, beta=0.9, verbose=False):
+        jobs = [(i, fl) for i, fl in enumerate(box_manager.fusion_list[: len(all_pred_box)])
+                if len(fl) >= 3 and not box_manager.check_if_fusion(fl)]
+        self.last_stats = dict(jobs=len(jobs), updated=0, views=sum(len(f) for _, f in jobs))
+        if not jobs:
+            return
+        dev = self.device
+        flat = torch.as_tensor(np.concatenate([np.asarray(fl, np.int64) for _, fl in jobs]), device=dev)
+        nv = np.array([len(fl) for _, fl in jobs], np.int32)
+        off = np.concatenate([[0], np.cumsum(nv)[:-1]]).astype(np.int32)
+        b3 = per_frame_box.pred_boxes_3d
+        out_box, out_upd, out_it, status, _ = _lib.fusion_fit(
+            torch.as_tensor(off, device=dev), torch.as_tensor(nv, device=dev),
+            b3.tensor.index_select(0, flat).contiguous(), b3.R.index_select(0, flat).contiguous(),
+            per_frame_box.scores.to(dev, torch.float32).index_select(0, flat).contiguous(),
+            per_frame_box.cam_pose.to(dev, torch.float32).index_select(0, flat).contiguous(),
+            per_frame_box.projected_boxes.index_select(0, flat).contiguous(),
+            self._pst_dev, self.fuse_cfg())
+        upd = out_upd.cpu().numpy()
+        st = int(status.cpu().numpy()[0])
+        if st & _lib.BF_DEV_VIEW_OVERFLOW:
+            raise _lib.HipError("bf_fusion_fit: a fusion list has more views than the kernel holds")
+        target = all_pred_box.pred_boxes_3d.tensor
+        rows, src = [], []
+        for j, (i, fl) in enumerate(jobs):
+            if box_manager.check_if_fusion(fl):   # an identical list already fused in this call
+                continue
+            if upd[j]:
+                rows.append(i)
+                src.append(j)
+                box_manager.update_fusion_flag(i)
+                box_manager.add_fusion_ind(fl)
+        if rows:
+            target[torch.as_tensor(rows, device=target.device)] = \
+                out_box[torch.as_tensor(src, device=out_box.device)].to(target.device)
+        self.last_stats["updated"] = len(rows)
+        self.last_stats["iters"] = int(out_it.sum().item())

@@ -1,0 +1,140 @@
+"""Fusion bookkeeping (reference: boxfusion/box_manager.py).
+
+Same public state as the reference — `fusion_list` (list of sorted init_id lists),
+`fusion_flag`, `already_fusion`, `num_record` — kept as Python lists for API compatibility.
+The record()/record_corr() logic itself runs inside the association kernels (bf_nms_scan,
+bf_corr_assoc); `pack`/`unpack` move the lists to and from the kernels' fixed-capacity rows, and
+`replay_flags` applies the kernels' event log to `fusion_flag` (box_manager.py:85-86,126-127).
+"""
+from __future__ import annotations
+
+import copy
+
+import numpy as np
+import torch
+
+from boxfusion_amd import _lib
+
+DEFAULT_LIST_CAPACITY = 64
+
+
+class BoxManager:
+    def __init__(self, cfg):
+        self.fusion_list = []
+        self.last_fusion_frame = []
+        self.fusion_flag = []
+        self.already_fusion = []
+        self.num_record = {}
+        self.cfg = cfg
+        self.rotation_gap = cfg["association"]["rotation_gap"]
+        self.translation_gap = cfg["association"]["translation_gap"]
+        self.small_size = cfg["box_fusion"]["small_size"]
+        self.list_capacity = int(cfg.get("box_fusion", {}).get("list_capacity", DEFAULT_LIST_CAPACITY))
+        self.merge_log = []
+
+    # -- reference API ---------------------------------------------------------------------------
+    def init_new_predictions(self, box_num, all_num):
+        for i in range(box_num):
+            self.fusion_list.append([i + all_num])
+            self.last_fusion_frame.append([0])
+            self.fusion_flag.append(0)
+
+    def add_fusion_ind(self, idx_list):
+        self.already_fusion.append(copy.deepcopy(idx_list))
+
+    def check_if_fusion(self, idx_list):
+        return idx_list in self.already_fusion
+
+    def update(self, keep_idx):
+        self.fusion_list = [self.fusion_list[i] for i in keep_idx]
+
+    def update_fusion_flag(self, idx):
+        self.fusion_flag[idx] = 1
+
+    def get_fusion_idx(self):
+        return [i for i in range(len(self.fusion_flag)) if self.fusion_flag[i] == 1]
+
+    def get_nofusion_idx(self):
+        return [i for i in range(len(self.fusion_flag)) if self.fusion_flag[i] == 0]
+
+    def check_valid_num(self, all_pred_box, count, gap):
+        """box_manager.py:151-166 (off in every shipped config)."""
+        fid = all_pred_box.frame_id
+        vn = all_pred_box.valid_num
+        zero = torch.where((vn == 0) & (fid < (count - gap)))[0]
+        valid = torch.arange(len(all_pred_box))
+        for idx in zero.tolist():
+            valid = valid[valid != idx]
+        self.fusion_list = [self.fusion_list[int(i)] for i in valid]
+        return all_pred_box[valid]
+
+    @staticmethod
+    def check_uv_bounds(uv_coords, W, H, ratio=1.0):
+        """box_manager.py:217-225 (gap = int((1 - ratio) * size): 63 / 47 at 640 / 480, 0.9)."""
+        gap_w = int((1 - ratio) * W)
+        gap_h = int((1 - ratio) * H)
+        u, v = uv_coords[:, 0], uv_coords[:, 1]
+        return (u > gap_w) & (u < (W - gap_w)) & (v > gap_h) & (v < (H - gap_h))
+
+    @staticmethod
+    def check_floor_mask(box_3d, ratio=20):
+        size = box_3d[:, 3:]
+        mx = torch.amax(size, dim=1)
+        mn = torch.amin(size, dim=1)
+        second = torch.sort(size, dim=1, descending=True)[0][:, 1]
+        mask = mx / mn > ratio
+        second_mask = ((mx / mn > ratio / 2) & (mx / second > ratio / 2) & (second / mn < 2.0) &
+                       (second < 0.15) & (mn < 0.15))
+        return mask | second_mask
+
+    @staticmethod
+    def check_large_mask(box_3d, thres=0.5):
+        return torch.amax(box_3d[:, 3:], dim=1) > thres
+
+    # -- device exchange ---------------------------------------------------------------------------
+    def pack(self, device):
+        n = len(self.fusion_list)
+        cap = self.list_capacity
+        items = np.full((max(n, 1), cap), -1, np.int32)
+        lens = np.zeros(max(n, 1), np.int32)
+        for i, row in enumerate(self.fusion_list):
+            if len(row) > cap:
+                raise _lib.HipError(f"fusion list of {len(row)} > capacity {cap}; raise "
+                                    "box_fusion.list_capacity")
+            items[i, :len(row)] = row
+            lens[i] = len(row)
+        return (torch.from_numpy(items).to(device, non_blocking=True),
+                torch.from_numpy(lens).to(device, non_blocking=True))
+
+    def unpack(self, items, lens):
+        it = items.cpu().numpy()
+        ln = lens.cpu().numpy()
+        self.fusion_list = [[int(v) for v in it[i, :ln[i]]] for i in range(len(self.fusion_list))]
+
+    def replay_flags(self, events):
+        """fusion_flag propagation of record/record_corr's branch 2 (the flag is never pruned by
+        update(), so indices refer to a stale layout exactly as in the reference)."""
+        for cur, idx, branch in events:
+            if branch == 2 and idx < len(self.fusion_flag) and self.fusion_flag[idx] == 1:
+                self.fusion_flag[cur] = 1
+
+    def nms_cfg(self, iou_threshold):
+        c = _lib.NmsCfg()
+        c.iou_threshold = float(iou_threshold)
+        c.translation_gap = float(self.translation_gap)
+        c.rotation_gap = float(self.rotation_gap)
+        c.center_gap = 0.5
+        c.max_list = 5
+        c.list_capacity = self.list_capacity
+        return c
+
+    def corr_cfg(self, threshold, W, H):
+        c = _lib.CorrCfg()
+        c.small_size = float(self.small_size)
+        c.threshold = float(threshold)
+        c.translation_gap = float(self.translation_gap)
+        c.rotation_gap = float(self.rotation_gap)
+        c.W, c.H = float(W), float(H)
+        c.max_list = 5
+        c.list_capacity = self.list_capacity
+        return c

@@ -1,0 +1,219 @@
+"""Instances3D field container + association entry points (reference: boxfusion/instances.py).
+
+The container semantics follow the reference (Detectron2-style fields, `cat`, `__getitem__` with
+int / slice / bool / long / numpy indices).  The association methods keep the reference's
+signatures and return values but run on the GPU:
+
+  spatial_association         -> bf_obb_iou_matrix + bf_nms_scan       (instances.py:22-101,372-397)
+  correspondence_association  -> bf_corr_assoc                          (instances.py:411-490)
+  project_3d_boxes            -> bf_project_boxes                       (instances.py:333-369)
+"""
+from __future__ import annotations
+
+import itertools
+import warnings
+from typing import Any, Dict, List, Tuple
+
+import numpy as np
+import torch
+
+from boxfusion_amd import _lib
+
+
+class Instances3D:
+    def __init__(self, image_size: Tuple[int, int] = (0, 0), **kwargs: Any):
+        self._image_size = image_size
+        self._fields: Dict[str, Any] = {}
+        for k, v in kwargs.items():
+            self.set(k, v)
+
+    @property
+    def image_size(self):
+        return self._image_size
+
+    def __setattr__(self, name, val):
+        if name.startswith("_"):
+            super().__setattr__(name, val)
+        else:
+            self.set(name, val)
+
+    def __getattr__(self, name):
+        if name == "_fields" or name not in self._fields:
+            raise AttributeError(f"Cannot find field '{name}' in the given Instances3D!")
+        return self._fields[name]
+
+    def set(self, name, value):
+        with warnings.catch_warnings(record=True):
+            n = len(value)
+        if len(self._fields):
+            assert len(self) == n, f"Adding a field of length {n} to a Instances3D of length {len(self)}"
+        self._fields[name] = value
+
+    def has(self, name):
+        return name in self._fields
+
+    def remove(self, name):
+        del self._fields[name]
+
+    def get(self, name):
+        return self._fields[name]
+
+    def get_fields(self):
+        return self._fields
+
+    def to(self, *args, **kwargs):
+        ret = Instances3D(self._image_size)
+        for k, v in self._fields.items():
+            ret.set(k, v.to(*args, **kwargs) if hasattr(v, "to") else v)
+        return ret
+
+    def __getitem__(self, item):
+        if type(item) == int:
+            if item >= len(self) or item < -len(self):
+                raise IndexError("Instances3D index out of range!")
+            item = slice(item, None, len(self))
+        ret = Instances3D(self._image_size)
+        for k, v in self._fields.items():
+            if isinstance(v, (torch.Tensor, np.ndarray)) or hasattr(v, "tensor"):
+                if isinstance(v, np.ndarray) and isinstance(item, torch.Tensor):
+                    ret.set(k, v[item.cpu().numpy()])
+                elif isinstance(v, torch.Tensor) and isinstance(item, np.ndarray):
+                    ret.set(k, v[torch.as_tensor(item, device=v.device)])
+                elif hasattr(v, "tensor") and isinstance(item, np.ndarray):
+                    ret.set(k, v[torch.as_tensor(item, device=v.tensor.device)])
+                else:
+                    ret.set(k, v[item])
+            elif hasattr(v, "__iter__"):
+                if isinstance(item, np.ndarray) and item.dtype == np.bool_:
+                    ret.set(k, [x for i, x in enumerate(v) if item[i]])
+                elif isinstance(item, torch.Tensor) and item.dtype == torch.bool:
+                    m = item.cpu().tolist()
+                    ret.set(k, [x for i, x in enumerate(v) if m[i]])
+                elif isinstance(item, torch.Tensor) and item.dtype == torch.int64:
+                    ret.set(k, [v[i] for i in item.cpu().tolist()])
+                elif isinstance(item, np.ndarray):
+                    ret.set(k, [v[int(i)] for i in item])
+                elif isinstance(item, slice):
+                    ret.set(k, v[item])
+                else:
+                    raise ValueError("Expected Bool or Long Tensor")
+            else:
+                raise ValueError("Not supported!")
+        return ret
+
+    def __len__(self):
+        for v in self._fields.values():
+            return v.__len__()
+        raise NotImplementedError("Empty Instances3D does not support __len__!")
+
+    def __iter__(self):
+        raise NotImplementedError("`Instances3D` object is not iterable!")
+
+    def clone(self):
+        ret = Instances3D(self._image_size)
+        for k, v in self._fields.items():
+            if hasattr(v, "clone"):
+                v = v.clone()
+            elif isinstance(v, np.ndarray):
+                v = np.copy(v)
+            elif isinstance(v, (str, list, tuple)):
+                v = list(v)
+            ret.set(k, v)
+        return ret
+
+    @staticmethod
+    def cat(instance_lists: List["Instances3D"]) -> "Instances3D":
+        assert len(instance_lists) > 0
+        if len(instance_lists) == 1:
+            return instance_lists[0]
+        ret = Instances3D(instance_lists[0]._image_size)
+        for k in instance_lists[0]._fields.keys():
+            vals = [i.get(k) for i in instance_lists]
+            v0 = vals[0]
+            if isinstance(v0, torch.Tensor):
+                vals = torch.cat(vals, 0)
+            elif isinstance(v0, np.ndarray):
+                vals = np.concatenate(vals, 0)
+            elif isinstance(v0, list):
+                vals = list(itertools.chain(*vals))
+            elif hasattr(type(v0), "cat"):
+                vals = type(v0).cat(vals)
+            else:
+                raise ValueError(f"Unsupported type {type(v0)} for concatenation")
+            ret.set(k, vals)
+        return ret
+
+    def __str__(self):
+        return f"Instances3D(num_instances={len(self)}, fields=[{', '.join(self._fields)}])"
+
+    __repr__ = __str__
+
+    # ------------------------------------------------------------------------------------------
+    # GPU geometry and association
+    # ------------------------------------------------------------------------------------------
+    def project_3d_boxes(self, K, H=480, W=640):
+        boxes = self.get("pred_boxes_3d")
+        corners = boxes.corners
+        K = torch.as_tensor(np.asarray(K, dtype=np.float32) if not isinstance(K, torch.Tensor) else K)
+        self.projected_boxes = _lib.project_boxes(corners, self.cam_pose.to(corners.device, torch.float32),
+                                                  K.to(corners.device, torch.float32), float(W), float(H))
+
+    def spatial_association(instance_lists, threshold, box_manager, cam_poses):
+        """nms_3d over all boxes; returns (keep, success_nms) as sorted lists."""
+        assert len(instance_lists) > 0
+        if len(instance_lists) == 1:
+            return instance_lists  # reference quirk (instances.py:381-382)
+        boxes = instance_lists.get("pred_boxes_3d")
+        dev = boxes.device
+        corners = boxes.corners
+        iou = _lib.obb_iou_matrix(corners)
+        scores = instance_lists.scores.to(dev, torch.float32).contiguous()
+        init_id = instance_lists.init_id.to(dev, torch.int32).contiguous()
+        poses = cam_poses.to(dev, torch.float32).contiguous()
+        vn = instance_lists.valid_num
+        if not (isinstance(vn, torch.Tensor) and vn.is_cuda and vn.dtype == torch.float32 and vn.is_contiguous()):
+            vn = torch.as_tensor(vn).to(dev, torch.float32).contiguous()
+            instance_lists.valid_num = vn
+        items, lens = box_manager.pack(dev)
+        keep, succ, events, counts = _lib.nms_scan(iou, corners, scores, init_id, poses, items, lens,
+                                                   vn, box_manager.nms_cfg(threshold))
+        c = counts.cpu().numpy()
+        if c[3]:
+            raise _lib.HipError(f"bf_nms_scan device status {c[3]} (fusion list capacity)")
+        box_manager.unpack(items, lens)
+        box_manager.replay_flags(events[:c[2]].cpu().numpy().tolist())
+        keep = keep[:c[0]].cpu().numpy().astype(np.int64).tolist()
+        success = succ[:c[1]].cpu().numpy().astype(np.int64).tolist()
+        return keep, success
+
+    def correspondence_association(cfg, box_manager, cur_keep_idx, cur_success_nms, pred_instances,
+                                   global_pred_box, all_pred_box, all_poses, per_frame_ins_cam_pose,
+                                   frame_id, mask, intrinsic, all_kf_pose, threshold=0.33, H=480,
+                                   W=640):
+        """small-box 2-D association against the previous global boxes; returns
+        (all_pred_box[keep_idx], all_poses[keep_idx], keep_idx)."""
+        n_glo = len(global_pred_box)
+        boxes = all_pred_box.get("pred_boxes_3d")
+        dev = boxes.device
+        corners = boxes.corners
+        mask_np = np.asarray(mask, dtype=np.int64)
+        success_all = [i + n_glo for i in cur_success_nms]
+        i32 = dict(dtype=torch.int32, device=dev)
+        vn = all_pred_box.valid_num
+        items, lens = box_manager.pack(dev)
+        cur_pose = torch.as_tensor(np.asarray(all_kf_pose[frame_id], dtype=np.float32), device=dev)
+        K = torch.as_tensor(intrinsic).to(dev, torch.float32)
+        keep, events, counts = _lib.corr_assoc(
+            corners, boxes.dims.contiguous(), all_pred_box.scores.to(dev, torch.float32).contiguous(),
+            all_pred_box.pred_boxes.to(dev, torch.float32).contiguous(),
+            all_pred_box.init_id.to(dev, torch.int32).contiguous(),
+            per_frame_ins_cam_pose.to(dev, torch.float32).contiguous(), cur_pose, K, n_glo,
+            torch.as_tensor(mask_np, **i32), torch.as_tensor(np.asarray(success_all, np.int64), **i32),
+            items, lens, vn, box_manager.corr_cfg(threshold, W, H))
+        c = counts.cpu().numpy()
+        if c[2]:
+            raise _lib.HipError(f"bf_corr_assoc device status {c[2]} (fusion list capacity)")
+        box_manager.unpack(items, lens)
+        box_manager.replay_flags(events[:c[1]].cpu().numpy().tolist())
+        keep_idx = keep[:c[0]].cpu().numpy().astype(np.int64)
+        return all_pred_box[keep_idx], all_poses[keep_idx], keep_idx
