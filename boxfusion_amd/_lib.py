@@ -333,3 +333,55 @@ def crop_resize_im2col(img, boxes, img_idx, size, patch, mean, std, kpad, out=No
                                        c_void_p(out.data_ptr()), c_int(out.stride(0)), _stream()),
            "bf_crop_resize_im2col")
     return out
+
+
+class KernelTimer:
+    """HIP-event timing of selected GEMM launches (used by bench.py for the roofline of the
+    dominant kernel): records (flops, start, end) for every bf_gemm_bf16 launch whose output
+    dtype / activation match while active."""
+
+    def __init__(self, out_bf16=True, act="gelu"):
+        self.out_bf16, self.act = out_bf16, ACT[act]
+        self.records = []
+        self.active = False
+
+    def __enter__(self):
+        global _TIMER
+        _TIMER = self
+        self.active = True
+        return self
+
+    def __exit__(self, *exc):
+        global _TIMER
+        _TIMER = None
+        self.active = False
+
+    def summary(self):
+        torch.cuda.synchronize()
+        if not self.records:
+            return dict(launches=0, flops=0.0, ms=0.0)
+        ms = sum(s.elapsed_time(e) for _, s, e in self.records)
+        fl = sum(f for f, _, _ in self.records)
+        return dict(launches=len(self.records), flops=fl, ms=ms, avg_us=1e3 * ms / len(self.records),
+                    tflops=fl / (ms * 1e-3) / 1e12)
+
+
+_TIMER = None
+_gemm_untimed = gemm
+
+
+def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype=torch.bfloat16,
+         row_map=None, m=None):
+    t = _TIMER
+    if t is None:
+        return _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m)
+    ob = (out.dtype if out is not None else out_dtype) == torch.bfloat16
+    if ob != t.out_bf16 or ACT[act] != t.act:
+        return _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    r = _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m)
+    e.record()
+    M = a.shape[0] if m is None else m
+    t.records.append((2.0 * M * w.shape[0] * w.shape[1], s, e))
+    return r

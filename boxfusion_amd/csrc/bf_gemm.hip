@@ -39,14 +39,14 @@ __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + e
 // byte offset of 16-B chunk `c` (0..7) of row `r` in a [rows][64 bf16] swizzled tile
 __device__ __forceinline__ int swz(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
 
-template <bool OUT_BF16>
+template <bool OUT_BF16, int ACT>
 __global__ void __launch_bounds__(G_THREADS, 2) k_gemm(const u16* __restrict__ A, int lda,
                                                         const u16* __restrict__ W, int ldw,
                                                         const float* __restrict__ bias,
                                                         const float* __restrict__ resid, int ldr,
                                                         int resid_mod, void* __restrict__ Cv,
                                                         int ldc, const int32_t* __restrict__ row_map,
-                                                        int M, int N, int K, int act, int tiles_n,
+                                                        int M, int N, int K, int tiles_n,
                                                         int tiles_m) {
     extern __shared__ __attribute__((aligned(16))) unsigned char g_smem[];
     // stage s: A at s*32K, W at s*32K + 16K
@@ -144,8 +144,8 @@ __global__ void __launch_bounds__(G_THREADS, 2) k_gemm(const u16* __restrict__ A
                 const int orow = row_map ? row_map[m] : m;
                 if (orow < 0) continue;
                 float v = acc[i][j][e] + bv;
-                if (act == 1) v = gelu_erf(v);
-                else if (act == 2) v = fmaxf(v, 0.f);
+                if (ACT == 1) v = gelu_erf(v);
+                else if (ACT == 2) v = fmaxf(v, 0.f);
                 if (resid) {
                     const int rrow = resid_mod > 0 ? (m % resid_mod) : orow;
                     v += resid[(size_t)rrow * ldr + n];
@@ -166,13 +166,20 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
     const int tiles_m = (M + GB_M - 1) / GB_M, tiles_n = (N + GB_N - 1) / GB_N;
     const int nwg = tiles_m * tiles_n;
     const size_t lds = 2 * 32768;
-    if (c_bf16)
-        hipLaunchKernelGGL(k_gemm<true>, dim3(nwg), dim3(G_THREADS), lds, bf_stream(stream),
-                           (const u16*)A, lda, (const u16*)W, ldw, bias, resid, ldr, resid_mod, C,
-                           ldc, row_map, M, N, K, act, tiles_n, tiles_m);
-    else
-        hipLaunchKernelGGL(k_gemm<false>, dim3(nwg), dim3(G_THREADS), lds, bf_stream(stream),
-                           (const u16*)A, lda, (const u16*)W, ldw, bias, resid, ldr, resid_mod, C,
-                           ldc, row_map, M, N, K, act, tiles_n, tiles_m);
+    if (act < 0 || act > 2) return BF_ERR_ARG;
+#define GEMM_LAUNCH(OB, AC)                                                                       \
+    hipLaunchKernelGGL((k_gemm<OB, AC>), dim3(nwg), dim3(G_THREADS), lds, bf_stream(stream),       \
+                       (const u16*)A, lda, (const u16*)W, ldw, bias, resid, ldr, resid_mod, C, ldc, \
+                       row_map, M, N, K, tiles_n, tiles_m)
+    if (c_bf16) {
+        if (act == 0) GEMM_LAUNCH(true, 0);
+        else if (act == 1) GEMM_LAUNCH(true, 1);
+        else GEMM_LAUNCH(true, 2);
+    } else {
+        if (act == 0) GEMM_LAUNCH(false, 0);
+        else if (act == 1) GEMM_LAUNCH(false, 1);
+        else GEMM_LAUNCH(false, 2);
+    }
+#undef GEMM_LAUNCH
     return bf_check_launch();
 }

@@ -38,6 +38,7 @@ class FrameBatch:
     K: torch.Tensor                # [B,3,3] image intrinsics
     T_gravity: Optional[torch.Tensor]  # [B,3,3]
     image_sizes: List[tuple]       # [(h, w)] before padding
+    pad: int = 0                   # square pad size when `image` is not materialised (engine)
 
     @property
     def sizes_wh(self):
@@ -384,7 +385,7 @@ class CubifyTransformer(nn.Module):
         src = self.input_proj[0](feat).flatten(2).transpose(1, 2)
         pos = pos.flatten(2).transpose(1, 2) + self.level_embed[0].view(1, 1, -1)
         metric, enc = self.prompting.prompters
-        clamp_shape = tuple(batch.image.shape[-2:])
+        clamp_shape = tuple(batch.image.shape[-2:]) if batch.image is not None else (batch.pad, batch.pad)
         # encoder proposals + top-k (:918-943)
         memory, props = enc.proposals(src, (h, w))
         st = dict(proposal_boxes=props, clamp_shape=clamp_shape)

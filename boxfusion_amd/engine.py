@@ -1,0 +1,235 @@
+"""MI355X execution engines: the CuTR RGB-D ViT backbone and the CLIP ViT-H/14 crop tower on the
+gfx950 kernels (bf16 MFMA GEMMs with fused epilogues, flash attention, LayerNorm, fused
+preprocessing/im2col).  Weights are packed once to bf16; activations live in preallocated HBM
+buffers sized for the batch; the residual streams stay f32.
+
+CuTR backbone layout (per frame batch B, token grid g x g, window ws, nw windows):
+  X   f32  [2, B, g*g, C]        residual streams (rgb, depth)
+  LNW bf16 [B, nw, 2, ws*ws, C]  window-partitioned LN output; pad positions stay zero, so the
+                                 qkv GEMM yields bias-only keys/values for them exactly like the
+                                 reference's F.pad after norm1 (vit.py:32)
+  QKV bf16 [B*nw*2*ws*ws, 3C] -> flash attention over the 2*ws*ws joint tokens of each window
+  proj GEMM scatters window rows back to token rows (pad rows dropped) and adds the residual.
+Dead compute skipped: after the last depth window block the depth stream is never read
+(vit.py:511-520), so that block runs RGB queries only and no depth MLP.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from boxfusion_amd import _lib
+from boxfusion_amd.clip import CLIP_MEAN, CLIP_STD
+from boxfusion_amd.cubify_transformer import FrameBatch
+from boxfusion_amd.preprocessor import PIXEL_MEAN_U8, PIXEL_STD_U8
+from boxfusion_amd.vit import get_abs_pos
+
+
+def _bf(w):
+    return w.detach().to(torch.bfloat16).contiguous()
+
+
+def _f(w):
+    return w.detach().to(torch.float32).contiguous()
+
+
+class CuTREngine:
+    def __init__(self, model, batch, height=480, width=640, pad=640, device="cuda"):
+        dev = torch.device(device)
+        self.model = model.to(dev).eval()
+        vit = model.backbone.backbone
+        self.dev, self.B, self.H, self.W, self.P = dev, batch, height, width, pad
+        self.C, self.heads = vit.embed_dim, vit.num_heads
+        self.D = self.C // self.heads
+        self.g = pad // vit.patch_size
+        self.ws = vit.window_size
+        self.nwx = math.ceil(self.g / self.ws)
+        self.nw = self.nwx * self.nwx
+        self.T = self.g * self.g
+        self.win_rows = 2 * self.ws * self.ws          # joint rgb+depth tokens per window
+        C, B, T = self.C, self.B, self.T
+        # ---- weights ----------------------------------------------------------------------
+        self.patch_w = _bf(vit.patch_embed.proj.weight.reshape(C, -1))
+        self.patch_b = _f(vit.patch_embed.proj.bias)
+        self.patchd_w = _bf(vit.patch_embed_depth.proj.weight.reshape(C, -1))
+        self.patchd_b = _f(vit.patch_embed_depth.proj.bias)
+        with torch.no_grad():
+            self.pos = _f(get_abs_pos(vit.pos_embed, vit.pretrain_use_cls_token, (self.g, self.g)).reshape(T, C))
+            self.posd = _f(get_abs_pos(vit.pos_embed_depth, vit.pretrain_use_cls_token, (self.g, self.g)).reshape(T, C))
+        self.blocks = []
+        for i, blk in enumerate(vit.blocks):
+            self.blocks.append(dict(
+                window=blk.window_size > 0, depth=blk.depth_modality,
+                n1=(_f(blk.norm1.weight), _f(blk.norm1.bias), blk.norm1.eps),
+                n2=(_f(blk.norm2.weight), _f(blk.norm2.bias), blk.norm2.eps),
+                qkv=(_bf(blk.attn.qkv.weight), _f(blk.attn.qkv.bias)),
+                proj=(_bf(blk.attn.proj.weight), _f(blk.attn.proj.bias)),
+                fc1=(_bf(blk.mlp.fc1.weight), _f(blk.mlp.fc1.bias)),
+                fc2=(_bf(blk.mlp.fc2.weight), _f(blk.mlp.fc2.bias))))
+        depth_blocks = [i for i, b in enumerate(self.blocks) if b["depth"]]
+        self.last_depth = max(depth_blocks) if depth_blocks else -1
+        # ---- buffers ----------------------------------------------------------------------
+        bf16, f32 = dict(dtype=torch.bfloat16, device=dev), dict(dtype=torch.float32, device=dev)
+        nwr = B * self.nw * self.win_rows
+        self.X = torch.zeros((2 * B * T, C), **f32)
+        self.LNW = torch.zeros((nwr, C), **bf16)
+        self.QKV = torch.empty((nwr, 3 * C), **bf16)
+        self.ATT = torch.zeros((nwr, C), **bf16)
+        self.LN2 = torch.empty((2 * B * T, C), **bf16)
+        self.H1 = torch.empty((2 * B * T, 4 * C), **bf16)
+        self.A_rgb = torch.empty((B * T, 3 * 16 * 16), **bf16)
+        self.A_d = torch.empty((B * T, 16 * 16), **bf16)
+        self.win_in, self.win_out = self._window_maps()
+        self._pos_cache = {}
+
+    def _window_maps(self):
+        B, T, g, ws, nwx = self.B, self.T, self.g, self.ws, self.nwx
+        s, b, y, x = np.meshgrid(np.arange(2), np.arange(B), np.arange(g), np.arange(g), indexing="ij")
+        w = (y // ws) * nwx + (x // ws)
+        tw = (y % ws) * ws + (x % ws)
+        win_in = (b * self.nw + w) * self.win_rows + s * ws * ws + tw        # X row -> LNW row
+        nwr = B * self.nw * self.win_rows
+        win_out = -np.ones(nwr, np.int64)
+        xrow = s * B * T + b * T + y * g + x
+        win_out[win_in.reshape(-1)] = xrow.reshape(-1)
+        to = lambda a: torch.as_tensor(a.reshape(-1).astype(np.int32), device=self.dev)
+        return to(win_in), to(win_out)
+
+    def backbone(self, img_u8, depth_std):
+        """img_u8 [B,H,W,3] uint8, depth_std [B,H,W] f32 (standardised) -> features [B,C,g,g] f32"""
+        B, T, C = self.B, self.T, self.C
+        X = self.X
+        Xr = X[: B * T]
+        _lib.im2col_rgb8(img_u8, self.P, 16, PIXEL_MEAN_U8, PIXEL_STD_U8, out=self.A_rgb)
+        _lib.gemm(self.A_rgb, self.patch_w, self.patch_b, resid=self.pos, resid_mod=T, out=Xr)
+        _lib.im2col_f32(depth_std, self.P, 16, out=self.A_d)
+        _lib.gemm(self.A_d, self.patchd_w, self.patchd_b, resid=self.posd, resid_mod=T, out=X[B * T:])
+        scale = self.D ** -0.5
+        for i, blk in enumerate(self.blocks):
+            g1, b1, e1 = blk["n1"]
+            g2, b2, e2 = blk["n2"]
+            if blk["window"] and blk["depth"]:
+                last = i == self.last_depth
+                _lib.layernorm(X, g1, b1, e1, out=self.LNW, row_map=self.win_in)
+                _lib.gemm(self.LNW, *blk["qkv"], out=self.QKV)
+                nb = B * self.nw
+                q = self.QKV[:, :C]
+                _lib.attention(q, self.QKV[:, C:2 * C], self.QKV[:, 2 * C:], self.ATT, nb, self.heads,
+                               self.ws * self.ws if last else self.win_rows, self.win_rows, self.D,
+                               scale, q_bs=self.win_rows * self.QKV.stride(0),
+                               k_bs=self.win_rows * self.QKV.stride(0),
+                               v_bs=self.win_rows * self.QKV.stride(0),
+                               o_bs=self.win_rows * self.ATT.stride(0))
+                _lib.gemm(self.ATT, *blk["proj"], resid=X, out=X, row_map=self.win_out)
+                rows = B * T if last else 2 * B * T
+                Xm = X[:rows]
+            elif blk["window"]:
+                raise NotImplementedError("RGB-only window blocks (non-depth CuTR) are not wired yet")
+            else:
+                _lib.layernorm(Xr, g1, b1, e1, out=self.LN2[: B * T])
+                qkv = self.QKV[: B * T]
+                _lib.gemm(self.LN2[: B * T], *blk["qkv"], out=qkv)
+                att = self.ATT[: B * T]
+                _lib.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], att, B, self.heads, T, T,
+                               self.D, scale)
+                _lib.gemm(att, *blk["proj"], resid=Xr, out=Xr)
+                rows = B * T
+                Xm = Xr
+            _lib.layernorm(Xm, g2, b2, e2, out=self.LN2[:rows])
+            _lib.gemm(self.LN2[:rows], *blk["fc1"], act="gelu", out=self.H1[:rows])
+            _lib.gemm(self.H1[:rows], *blk["fc2"], resid=Xm, out=Xm)
+        return Xr.view(B, self.g, self.g, C).permute(0, 3, 1, 2)
+
+    def ray_embedding(self, K, size_wh):
+        key = (tuple(np.asarray(K.cpu(), np.float32).reshape(-1).tolist()), tuple(size_wh))
+        if key not in self._pos_cache:
+            with torch.no_grad():
+                self._pos_cache[key] = self.model.pos_embedding(K[None].to(self.dev), [size_wh], self.g)[0]
+        return self._pos_cache[key]
+
+    @torch.no_grad()
+    def __call__(self, img_u8, depth_std, depth_params, K, T_gravity, image_sizes):
+        feat = self.backbone(img_u8, depth_std)
+        sizes_wh = [(w, h) for h, w in image_sizes]
+        pos = torch.stack([self.ray_embedding(K[i], sizes_wh[i]) for i in range(self.B)])
+        batch = FrameBatch(image=None, depth=depth_std, depth_params=depth_params, K=K,
+                           T_gravity=T_gravity, image_sizes=image_sizes, pad=self.P)
+        return self.model.decode(feat, batch, pos=pos)
+
+
+class CLIPEngine:
+    """CLIP ViT-H/14 on crops: fused crop+resize+normalise+im2col, 32 MFMA transformer blocks."""
+
+    KPAD = 640  # 3*14*14 = 588 -> 640 (GEMM K multiple of 64)
+
+    def __init__(self, visual, max_crops, device="cuda"):
+        dev = torch.device(device)
+        self.visual = visual.to(dev).eval()
+        v = visual
+        self.dev, self.N = dev, max_crops
+        self.width, self.heads = v.width, v.heads
+        self.D = self.width // self.heads
+        self.np = (v.image_size // v.patch_size) ** 2
+        self.S = self.np + 1
+        W = self.width
+        w = torch.zeros((W, self.KPAD), dtype=torch.float32, device=dev)
+        w[:, : 3 * v.patch_size ** 2] = v.conv1.weight.detach().reshape(W, -1)
+        self.patch_w = _bf(w)
+        self.cls = _f(v.class_embedding)
+        self.pos = _f(v.positional_embedding)
+        self.blocks = []
+        for blk in v.transformer.resblocks:
+            self.blocks.append(dict(
+                n1=(_f(blk.ln_1.weight), _f(blk.ln_1.bias), blk.ln_1.eps),
+                n2=(_f(blk.ln_2.weight), _f(blk.ln_2.bias), blk.ln_2.eps),
+                qkv=(_bf(blk.attn.in_proj_weight), _f(blk.attn.in_proj_bias)),
+                proj=(_bf(blk.attn.out_proj.weight), _f(blk.attn.out_proj.bias)),
+                fc1=(_bf(blk.mlp.c_fc.weight), _f(blk.mlp.c_fc.bias)),
+                fc2=(_bf(blk.mlp.c_proj.weight), _f(blk.mlp.c_proj.bias))))
+        M = max_crops * self.S
+        bf16, f32 = dict(dtype=torch.bfloat16, device=dev), dict(dtype=torch.float32, device=dev)
+        self.A = torch.empty((max_crops * self.np, self.KPAD), **bf16)
+        self.P = torch.empty((max_crops * self.np, W), **f32)
+        self.X = torch.empty((M, W), **f32)
+        self.LN = torch.empty((M, W), **bf16)
+        self.QKV = torch.empty((M, 3 * W), **bf16)
+        self.ATT = torch.empty((M, W), **bf16)
+        self.H1 = torch.empty((M, 4 * W), **bf16)
+
+    @torch.no_grad()
+    def __call__(self, frames_u8, boxes_i32, frame_idx_i32):
+        """frames [F,H,W,3] u8, boxes [N,4] int xyxy, frame index [N] -> features [N, out] f32"""
+        N = boxes_i32.shape[0]
+        if N == 0:
+            return torch.zeros((0, self.visual.output_dim), device=self.dev)
+        if N > self.N:
+            raise _lib.HipError(f"{N} crops > engine capacity {self.N}")
+        W, S, npch = self.width, self.S, self.np
+        A = self.A[: N * npch]
+        _lib.crop_resize_im2col(frames_u8, boxes_i32, frame_idx_i32, self.visual.image_size,
+                                self.visual.patch_size, CLIP_MEAN, CLIP_STD, self.KPAD, out=A)
+        P = _lib.gemm(A, self.patch_w, out=self.P[: N * npch], out_dtype=torch.float32)
+        X = self.X[: N * S]
+        X3 = X.view(N, S, W)
+        X3[:, 1:] = P.view(N, npch, W) + self.pos[1:]
+        X3[:, 0] = self.cls + self.pos[0]
+        X.copy_(F.layer_norm(X, (W,), self.visual.ln_pre.weight, self.visual.ln_pre.bias,
+                             self.visual.ln_pre.eps))
+        M = N * S
+        LN, QKV, ATT, H1 = self.LN[:M], self.QKV[:M], self.ATT[:M], self.H1[:M]
+        scale = self.D ** -0.5
+        for blk in self.blocks:
+            _lib.layernorm(X, *blk["n1"][:2], blk["n1"][2], out=LN)
+            _lib.gemm(LN, *blk["qkv"], out=QKV)
+            _lib.attention(QKV[:, :W], QKV[:, W:2 * W], QKV[:, 2 * W:], ATT, N, self.heads, S, S,
+                           self.D, scale)
+            _lib.gemm(ATT, *blk["proj"], resid=X, out=X)
+            _lib.layernorm(X, *blk["n2"][:2], blk["n2"][2], out=LN)
+            _lib.gemm(LN, *blk["fc1"], act="gelu", out=H1)
+            _lib.gemm(H1, *blk["fc2"], resid=X, out=X)
+        cls = F.layer_norm(X3[:, 0], (W,), self.visual.ln_post.weight, self.visual.ln_post.bias,
+                           self.visual.ln_post.eps)
+        return cls @ self.visual.proj

@@ -1,0 +1,97 @@
+"""HIP engines vs the fp32 PyTorch definition of the same models on the same weights (GPU).
+bf16 MFMA with f32 accumulation: tolerances are relative L2 errors."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda")
+
+
+@pytest.mark.parametrize("dim", [192, 768])
+def test_cutr_backbone_engine_vs_fp32(dev, dim):
+    from boxfusion_amd import _lib
+    from boxfusion_amd.cubify_transformer import make_cubify_transformer
+    from boxfusion_amd.engine import CuTREngine
+    from boxfusion_amd.preprocessor import PIXEL_MEAN_U8, PIXEL_STD_U8
+    from boxfusion_amd.synthetic import frame_rgbd
+    from boxfusion_amd.weights import init_seeded
+    torch.manual_seed(0)
+    model = init_seeded(make_cubify_transformer(dim, True).eval()).to(dev)
+    B = 2
+    rgb = np.stack([frame_rgbd(f)[0] for f in range(B)])
+    depth = np.stack([frame_rgbd(f)[1] for f in range(B)])
+    img = torch.from_numpy(rgb).to(dev)
+    dstd, params = _lib.depth_standardize(torch.from_numpy(depth).to(dev))
+    eng = CuTREngine(model, B)
+    feat = eng.backbone(img, dstd)
+    mean = torch.tensor(PIXEL_MEAN_U8, device=dev).view(1, 3, 1, 1)
+    std = torch.tensor(PIXEL_STD_U8, device=dev).view(1, 3, 1, 1)
+    x = F.pad((img.permute(0, 3, 1, 2).float() - mean) / std, (0, 0, 0, 160))
+    d = F.pad(dstd, (0, 0, 0, 160))
+    with torch.no_grad():
+        ref = model.backbone.backbone.forward_tensors(x, d)
+    err = rel(feat, ref)
+    print("backbone rel err", dim, err)
+    assert err < 3e-2
+
+
+def test_cutr_engine_end_to_end(dev):
+    from boxfusion_amd import _lib
+    from boxfusion_amd.cubify_transformer import FrameBatch, make_cubify_transformer
+    from boxfusion_amd.engine import CuTREngine
+    from boxfusion_amd.sensor import camera_to_gravity
+    from boxfusion_amd.synthetic import Scene, SCANNET_K, frame_rgbd
+    from boxfusion_amd.weights import init_seeded
+    torch.manual_seed(0)
+    model = init_seeded(make_cubify_transformer(384, True).eval()).to(dev)
+    B = 2
+    rgb = torch.from_numpy(np.stack([frame_rgbd(f)[0] for f in range(B)])).to(dev)
+    depth = torch.from_numpy(np.stack([frame_rgbd(f)[1] for f in range(B)])).to(dev)
+    dstd, params = _lib.depth_standardize(depth)
+    K = torch.from_numpy(np.stack([SCANNET_K] * B)).to(dev)
+    Tg = torch.from_numpy(np.stack([camera_to_gravity(Scene().pose(f)) for f in range(B)])).to(dev)
+    eng = CuTREngine(model, B)
+    res = eng(rgb, dstd, params, K, Tg, [(480, 640)] * B)
+    assert len(res) == B and len(res[0]) == 100
+    for r in res:
+        assert torch.isfinite(r.scores).all() and torch.isfinite(r.pred_boxes_3d.tensor).all()
+        assert (r.scores[:-1] >= r.scores[1:]).all()
+
+
+def test_clip_engine_vs_fp32(dev):
+    from boxfusion_amd.clip import CLIP_MEAN, CLIP_STD, VisionTransformer
+    from boxfusion_amd.engine import CLIPEngine
+    from boxfusion_amd.weights import init_seeded
+    torch.manual_seed(0)
+    vis = init_seeded(VisionTransformer(224, 14, 1280, 4, 16, 1024).eval(), seed=3).to(dev)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    frames = torch.randint(0, 256, (2, 480, 640, 3), device=dev, dtype=torch.uint8, generator=g)
+    boxes = torch.tensor([[10, 20, 200, 150], [0, 0, 640, 480], [300, 100, 400, 310]],
+                         device=dev, dtype=torch.int32)
+    idx = torch.tensor([0, 1, 1], device=dev, dtype=torch.int32)
+    eng = CLIPEngine(vis, 8)
+    got = eng(frames, boxes, idx)
+    crops = []
+    for n in range(3):
+        x1, y1, x2, y2 = boxes[n].tolist()
+        c = frames[idx[n], y1:y2, x1:x2].permute(2, 0, 1)[None].float()
+        c = F.interpolate(c, size=(224, 224), mode="bilinear", align_corners=False) / 255
+        crops.append((c - torch.tensor(CLIP_MEAN, device=dev).view(1, 3, 1, 1)) /
+                     torch.tensor(CLIP_STD, device=dev).view(1, 3, 1, 1))
+    with torch.no_grad():
+        ref = vis(torch.cat(crops))
+    err = rel(got, ref)
+    print("clip rel err", err)
+    assert err < 3e-2
