@@ -1,0 +1,296 @@
+#!/usr/bin/env python3
+"""Throughput benchmark: RGB-D frames/s of per-frame detect + multi-view 3D box fusion.
+
+Workload (BASELINE.json configs[2]): synthetic 640x480 RGB-D stream, batch 8 frames
+per step per GPU, every frame a keyframe (gap=1, the per-frame-detect roofline run):
+  per frame  depth standardisation + back-projection, CuTR RGB-D ViT-B (dim 768) forward,
+             detection filters, CLIP ViT-H/14 on the top-16 boxes (16 crops/frame), text match
+             against the 473-class vocabulary;
+  per step   all-gather (RCCL) of every rank's per-frame records (scene detections + CLIP
+             features) -> rank 0 runs the fusion state machine (NMS + association + box fusion)
+             over all gathered frames in global frame order.
+Weights are random (no checkpoint offline); the detections feeding fusion come from the seeded
+30-object scene generator (boxfusion_amd/synthetic.py), since random-weight CuTR boxes are noise.
+Inputs (frames, scene detections) are resident in HBM before the timed region.
+
+  python bench.py [--gpus N --steps K --warmup W]      (N>1 under torch.distributed.run)
+"""
+from __future__ import annotations
+
+import argparse
+import copy
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md), no sparsity
+PEAK_HBM_GBS = 8000.0
+
+CFG = dict(
+    dataset="scannet",
+    data=dict(gap=1),
+    cam=dict(H=480, W=640, fx=574.540771, fy=577.583740, cx=322.522827, cy=238.558853),
+    detection=dict(score_thresh=0.5, uv_bound=True, uv_bound_value=0.9, floor_mask=True,
+                   floor_ratio=15, scale_box=1.5, class_sim_thres=25.0),
+    association=dict(small_threshold=0.1, rotation_gap=30, translation_gap=0.8),
+    box_fusion=dict(use=True, iters=20, pst_size=1024, check_valid=False, nms_threshold=0.1,
+                    small_size=0.35, clip_sim_coeff=1.0,
+                    random_opt=dict(center_init_size=0.1, center_scaling_coefficient=0.1,
+                                    shape_init_size=0.5, shape_scaling_coefficient=0.5)),
+)
+REC_ROWS, REC_W = 64, 22     # per-frame detection record: rows x (score, xyxy, xyzlhw, R, proj_xy)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=125, help="timed steps (125 x 8 = 1000 frames)")
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--batch", type=int, default=8)
+    p.add_argument("--dim", type=int, default=768, help="CuTR ViT width (768 = ViT-B)")
+    p.add_argument("--clip-layers", type=int, default=32)
+    p.add_argument("--crops", type=int, default=16)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-detect-frames", type=int, default=1)
+    p.add_argument("--cpu-fusion-frames", type=int, default=24)
+    return p.parse_args()
+
+
+# ------------------------------------------------------------------------------------------------
+def gen_frames(frame_ids, dev):
+    """seeded synthetic RGB-D frames generated on the device (seed 1234 + frame)."""
+    n = len(frame_ids)
+    rgb = torch.empty((n, 480, 640, 3), dtype=torch.uint8, device=dev)
+    depth = torch.empty((n, 480, 640), dtype=torch.float32, device=dev)
+    g = torch.Generator(device=dev)
+    for j, f in enumerate(frame_ids):
+        g.manual_seed(1234 + int(f))
+        rgb[j].random_(0, 256, generator=g)
+        depth[j].uniform_(0.5, 4.5, generator=g)
+        depth[j].masked_fill_(torch.rand((480, 640), device=dev, generator=g) < 0.05, 0.0)
+    return rgb, depth
+
+
+def pack_records(dets):
+    """scene detections of a batch of frames -> f32 [b, 1 + REC_ROWS*REC_W] records"""
+    out = np.zeros((len(dets), 1 + REC_ROWS * REC_W), np.float32)
+    for j, d in enumerate(dets):
+        n = min(len(d["scores"]), REC_ROWS)
+        rows = np.concatenate([d["scores"][:n, None], d["pred_boxes"][:n], d["xyzlhw"][:n],
+                               d["R"][:n].reshape(n, 9), d["proj_xy"][:n]], 1)
+        out[j, 0] = n
+        out[j, 1:1 + n * REC_W] = rows.reshape(-1)
+    return out
+
+
+def unpack_record(rec, dev):
+    from boxfusion_amd.boxes import GeneralInstance3DBoxes
+    from boxfusion_amd.instances import Instances3D
+    n = int(rec[0].item())
+    rows = rec[1:1 + n * REC_W].view(n, REC_W)
+    p = Instances3D((480, 640))
+    p.scores = rows[:, 0].contiguous()
+    p.pred_boxes = rows[:, 1:5].contiguous()
+    p.pred_boxes_3d = GeneralInstance3DBoxes(rows[:, 5:11], rows[:, 11:20].reshape(n, 3, 3))
+    p.pred_proj_xy = rows[:, 20:22].contiguous()
+    return p
+
+
+def gather_step(recs, feats, poses, dist, world):
+    """Exchange of one step: every rank's per-frame records [b, R] and CLIP features
+    [n_crops, 1024] are all-gathered (RCCL over xGMI on the GPU; gloo in the CPU tests) so that
+    the fusion owner sees the step's frames in global frame order (rank-major = frame order, since
+    rank r holds frames step*b*world + r*b ... + b-1).  Poses travel as a tiny host object."""
+    if dist is None or world == 1:
+        return recs, feats, np.asarray(poses)
+    if recs.is_cuda:
+        g_rec = torch.empty((world * recs.shape[0],) + recs.shape[1:], dtype=recs.dtype, device=recs.device)
+        dist.all_gather_into_tensor(g_rec, recs.contiguous())
+        g_feat = torch.empty((world * feats.shape[0],) + feats.shape[1:], dtype=feats.dtype,
+                             device=feats.device)
+        dist.all_gather_into_tensor(g_feat, feats.contiguous())
+    else:
+        parts = [torch.empty_like(recs) for _ in range(world)]
+        dist.all_gather(parts, recs.contiguous())
+        g_rec = torch.cat(parts)
+        fparts = [torch.empty_like(feats) for _ in range(world)]
+        dist.all_gather(fparts, feats.contiguous())
+        g_feat = torch.cat(fparts)
+    g_pose = [None] * world
+    dist.all_gather_object(g_pose, np.asarray(poses))
+    return g_rec, g_feat, np.concatenate(g_pose)
+
+
+# ------------------------------------------------------------------------------------------------
+def cpu_baseline(cutr, clip_vis, args, scene):
+    """The parity-checked CPU restatement timed on this host: fp32 torch-CPU CuTR + CLIP on
+    `cpu_detect_frames` frames (16 crops each) and the oracle fusion chain (C restatement,
+    oracle/chain.py) over the first `cpu_fusion_frames` frames of the stream."""
+    from oracle.chain import OracleChain
+    from boxfusion_amd.box_fusion import load_pst
+    from boxfusion_amd.cubify_transformer import FrameBatch
+    from boxfusion_amd.preprocessor import PIXEL_MEAN_U8, PIXEL_STD_U8
+    from boxfusion_amd.sensor import camera_to_gravity
+    from boxfusion_amd.synthetic import SCANNET_K, frame_rgbd
+    from boxfusion_amd.clip import CLIP_MEAN, CLIP_STD
+    from oracle import oracle as OR
+    import torch.nn.functional as F
+    cores = len(os.sched_getaffinity(0))
+    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    torch.set_num_threads(cores)
+    cm = copy.deepcopy(cutr).float().cpu().eval()
+    vm = copy.deepcopy(clip_vis).float().cpu().eval()
+    nf = args.cpu_detect_frames
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        for f in range(nf):
+            rgb, depth = frame_rgbd(f)
+            mean = torch.tensor(PIXEL_MEAN_U8).view(3, 1, 1)
+            std = torch.tensor(PIXEL_STD_U8).view(3, 1, 1)
+            img = (torch.from_numpy(np.moveaxis(rgb, -1, 0)).float() - mean) / std
+            img = F.pad(img, (0, 0, 0, 160))[None]
+            d, params = OR.depth_standardize(depth)
+            OR.backproject(depth, SCANNET_K, scene.pose(f))
+            d = F.pad(torch.from_numpy(d), (0, 0, 0, 160))[None]
+            batch = FrameBatch(image=img, depth=d, depth_params=torch.from_numpy(params)[None],
+                               K=torch.from_numpy(SCANNET_K)[None],
+                               T_gravity=torch.from_numpy(camera_to_gravity(scene.pose(f)))[None],
+                               image_sizes=[(480, 640)])
+            r = cm(batch)[0]
+            boxes = r.pred_boxes[: args.crops].numpy().astype(np.int64)
+            crops = []
+            for x1, y1, x2, y2 in boxes:
+                c = torch.from_numpy(rgb[y1:y2, x1:x2]).permute(2, 0, 1).float()[None]
+                c = F.interpolate(c, (224, 224), mode="bilinear", align_corners=False) if c.numel() \
+                    else torch.zeros((1, 3, 224, 224))
+                crops.append(c)
+            x = torch.cat(crops) / 255.0
+            x = (x - torch.tensor(CLIP_MEAN).view(1, 3, 1, 1)) / torch.tensor(CLIP_STD).view(1, 3, 1, 1)
+            vm(x)
+    t_det = (time.perf_counter() - t0) / nf
+    ch = OracleChain(CFG, SCANNET_K, pst=load_pst(), legacy=True)
+    t0 = time.perf_counter()
+    for f in range(args.cpu_fusion_frames):
+        ch.keyframe(f, scene.pose(f), scene.detections(f))
+    t_fuse = (time.perf_counter() - t0) / args.cpu_fusion_frames
+    return {"value": 1.0 / (t_det + t_fuse), "unit": "frames/s", "cores": cores, "kind": "port",
+            "sample": (f"{nf} frame(s) of fp32 torch-CPU CuTR ViT-B + {args.crops} CLIP ViT-H/14 "
+                       f"crops ({t_det:.2f} s/frame) + oracle fusion chain over frames "
+                       f"0..{args.cpu_fusion_frames - 1} ({1e3 * t_fuse:.1f} ms/frame)")}
+
+
+# ------------------------------------------------------------------------------------------------
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    from boxfusion_amd import _lib
+    _lib.lib()                                         # fail loudly without the HIP library
+    from boxfusion_amd.clip import VisionTransformer
+    from boxfusion_amd.cubify_transformer import make_cubify_transformer
+    from boxfusion_amd.fusion_stage import FusionStage
+    from boxfusion_amd.pipeline import DetectStage
+    from boxfusion_amd.synthetic import SCANNET_K, Scene
+
+    torch.manual_seed(0)
+    with torch.device(dev):
+        cutr = make_cubify_transformer(args.dim, True).eval()
+        clip_vis = VisionTransformer(224, 14, 1280, args.clip_layers, 16, 1024).eval()
+    B = args.batch
+    detect = DetectStage(cutr, clip_vis, CFG, B, 480, 640, SCANNET_K, crops_per_frame=args.crops,
+                         crop_source="top", backproject=True, clip_capacity=B * args.crops,
+                         device=dev)
+    scene = Scene(seed=0)
+    N = world
+    per_step = B * N
+    total_steps = args.warmup + args.steps
+
+    def my_frames(step):
+        return [step * per_step + rank * B + j for j in range(B)]
+
+    # ---- inputs resident in HBM before timing -----------------------------------------------
+    all_mine = [f for s in range(total_steps) for f in my_frames(s)]
+    rgb_all, depth_all = gen_frames(all_mine, dev)
+    poses_all = np.stack([scene.pose(f) for f in all_mine]).astype(np.float32)
+    rec_all = torch.from_numpy(pack_records([scene.detections(f) for f in all_mine])).to(dev)
+    torch.cuda.synchronize()
+
+    def run_steps(s0, s1, fusion, timer=None):
+        for s in range(s0, s1):
+            o = s * B
+            sl = slice(o, o + B)
+            detect(rgb_all[sl], depth_all[sl], poses_all[sl])
+            bidx, iidx, cat_idx, feats, sims = detect.last["clip"]
+            recs = rec_all[sl]
+            g_rec, g_feat, g_pose = gather_step(recs, feats, poses_all[sl], dist, N)
+            if rank == 0:
+                base = s * per_step
+                for j in range(g_rec.shape[0]):
+                    fusion.keyframe(base + j - s0 * per_step, g_pose[j], unpack_record(g_rec[j], dev))
+
+    # ---- warmup (own fusion state), then the timed stream from frame 0 ----------------------
+    run_steps(0, args.warmup, FusionStage(CFG, SCANNET_K, device=dev))
+    fusion = FusionStage(CFG, SCANNET_K, device=dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timer = _lib.KernelTimer(out_bf16=True, act="gelu")
+    t0 = time.perf_counter()
+    with timer:
+        run_steps(args.warmup, total_steps, fusion)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ks = timer.summary()
+    frames = per_step * args.steps
+
+    if rank == 0:
+        achieved = ks["tflops"] if ks["launches"] else 0.0
+        line = {
+            "metric": "RGB-D frames/sec (whole node) on 640x480 stream",
+            "value": frames / dt, "unit": "frames/s", "n_gpus": N, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic 640x480 RGB-D stream (seeded), random-init weights, seeded scene detections",
+            "config": {"workload": f"configs[2]: synthetic 640x480 RGB-D, batch {B}/step/GPU, gap=1, "
+                                   f"CuTR ViT-{ {768: 'B', 384: 'S', 192: 'T'}.get(args.dim, args.dim)} "
+                                   f"RGB-D + CLIP ViT-H/14 x{args.crops} crops/frame + fusion",
+                       "frames": frames, "global_batch": per_step, "parallelism": f"dp{N}",
+                       "fused_boxes": fusion.stats["fused"],
+                       "global_boxes": len(fusion.all_pred_box) if fusion.all_pred_box is not None else 0},
+            "roofline": {"bound": "mfma", "kernel": "k_gemm<true,1> (bf16 GEMM + bias + GELU, MLP up-projection)",
+                         "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / PEAK_BF16_TFLOPS, "traffic": None,
+                         "launches": ks["launches"], "avg_us": ks.get("avg_us", 0.0),
+                         "flops_per_launch": ks["flops"] / max(ks["launches"], 1)},
+        }
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(cutr, clip_vis, args, scene)
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

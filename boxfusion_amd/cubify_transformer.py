@@ -365,7 +365,7 @@ class CubifyTransformer(nn.Module):
         C = backbone.backbone.num_channels[0]
         self.input_proj = nn.ModuleList([nn.Sequential(nn.Conv2d(C, decoder.embed_dim, 1),
                                                        nn.GroupNorm(32, decoder.embed_dim))])
-        self.level_embed = nn.Parameter(torch.Tensor(1, decoder.embed_dim))
+        self.level_embed = nn.Parameter(torch.zeros(1, decoder.embed_dim))
         self.topk_per_image = topk_per_image
 
     @property

@@ -1,0 +1,119 @@
+"""The keyframe state machine of demo.py:200-305 on the GPU kernels.
+
+`FusionStage.keyframe(count, pose, pred)` performs exactly the reference's per-keyframe sequence
+with the reference's containers (Instances3D, BoxManager, BoxFusion):
+
+  cam_pose / frame_id / init_id / valid_num fields            demo.py:215-219
+  transform2world -> bf_box_transform2world                    demo.py:220, boxes.py:825-833
+  project_3d_boxes -> bf_project_boxes                         demo.py:221, instances.py:333-369
+  first keyframe: initialise                                   demo.py:226-241
+  else: cat, spatial_association (bf_obb_iou_matrix + bf_nms_scan), then
+        new boxes kept: correspondence_association (bf_corr_assoc), update, check_valid_num,
+                        boxfusion (bf_fusion_fit, one launch for every box)   demo.py:243-299
+        none kept:      all_pred_box[mask]                                     demo.py:300-304
+
+`finish(count, pose)` reproduces the last-frame re-entry of demo.py:200 (`count == len-1` on a
+non-keyframe): the previous keyframe's already world-space `pred_instances` are transformed by the
+last pose a second time and go through association again (`stale_last_frame`
+flag, default on as in the reference).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from boxfusion_amd.box_fusion import BoxFusion
+from boxfusion_amd.box_manager import BoxManager
+from boxfusion_amd.instances import Instances3D
+
+
+class FusionStage:
+    def __init__(self, cfg, K3, H=480, W=640, device="cuda", legacy_promotion=True,
+                 stale_last_frame=True):
+        self.cfg = cfg
+        self.dev = torch.device(device)
+        self.K3 = np.asarray(K3, np.float32)
+        self.H, self.W = H, W
+        self.gap = int(cfg["data"].get("gap", 1)) if "data" in cfg else 1
+        self.box_manager = BoxManager(cfg)
+        self.fuser = BoxFusion(cfg, device=device, legacy_promotion=legacy_promotion)
+        self.fuser.update_intrinsics((W, H), self.K3)
+        self.fuser.update_K_flag = True
+        self.stale_last_frame = stale_last_frame
+        self.all_pred_box = None
+        self.all_poses = None
+        self.per_frame_ins = None
+        self.all_kf_pose = {}
+        self.box_count = 0
+        self.last_pred = None
+        self.stats = dict(keyframes=0, suppressed=0, fused=0)
+
+    def keyframe(self, count, pose, pred):
+        """pred: Instances3D of this keyframe in CAMERA coordinates (after the detection filters
+        and the CLIP step), tensors on the device; it is modified in place like the reference's."""
+        cfg, bm = self.cfg, self.box_manager
+        self.last_pred = pred
+        pose = np.asarray(pose, np.float32)
+        self.all_kf_pose[count] = pose
+        n = len(pred) if pred is not None and len(pred._fields) else 0
+        pose_np = np.repeat(pose[None], n, 0)
+        if n == 0:
+            bm.num_record[count] = self.box_count
+            return
+        self.stats["keyframes"] += 1
+        pred.cam_pose = torch.from_numpy(pose_np).to(self.dev)
+        pred.frame_id = torch.full((n,), count, dtype=torch.int64, device=self.dev)
+        pred.init_id = self.box_count + torch.arange(n, device=self.dev)
+        pred.valid_num = torch.zeros(n, device=self.dev)
+        pred.pred_boxes_3d.transform2world(pred.cam_pose)
+        pred.project_3d_boxes(self.K3, H=self.H, W=self.W)
+        self.box_count += n
+        bm.num_record[count] = self.box_count
+        if self.all_pred_box is None and (count < self.gap or self.per_frame_ins is None):
+            self.all_pred_box = pred
+            self.all_poses = pose_np
+            self.per_frame_ins = pred
+            bm.init_new_predictions(n, 0)
+            return
+        bm.init_new_predictions(n, len(self.per_frame_ins))
+        n_before = len(self.all_pred_box)
+        cur_global = self.all_pred_box
+        all_pred_box = Instances3D.cat([self.all_pred_box, pred])
+        self.per_frame_ins = Instances3D.cat([self.per_frame_ins, pred])
+        all_poses = np.concatenate((self.all_poses, pose_np), axis=0)
+        mask, success = Instances3D.spatial_association(all_pred_box, cfg["box_fusion"]["nms_threshold"],
+                                                        bm, self.per_frame_ins.cam_pose)
+        self.stats["suppressed"] += len(success)
+        cur_keep = [i - n_before for i in mask if i >= n_before]
+        cur_success = [i - n_before for i in success if i >= n_before]
+        keep_idx = np.asarray(mask)
+        if cur_keep:
+            all_pred_box, all_poses, keep_idx = Instances3D.correspondence_association(
+                cfg, bm, cur_keep, cur_success, pred, cur_global, all_pred_box, all_poses,
+                self.per_frame_ins.cam_pose, count, mask, self.K3, self.all_kf_pose,
+                threshold=cfg["association"]["small_threshold"], H=self.H, W=self.W)
+            bm.update(keep_idx)
+            if cfg["box_fusion"].get("check_valid", False):
+                all_pred_box = bm.check_valid_num(all_pred_box, count, self.gap)
+            if cfg["box_fusion"].get("use", True):
+                self.fuser.boxfusion(all_pred_box, self.per_frame_ins, bm)
+                self.stats["fused"] += self.fuser.last_stats.get("updated", 0)
+        else:
+            all_pred_box = all_pred_box[torch.as_tensor(keep_idx, device=self.dev)]
+            all_poses = all_poses[keep_idx]
+            bm.update(keep_idx)
+        self.all_pred_box, self.all_poses = all_pred_box, all_poses
+
+    def finish(self, count, pose, last_was_keyframe):
+        """demo.py:200 `count == len(dataset) - 1` re-entry on a non-keyframe last frame."""
+        if last_was_keyframe or not self.stale_last_frame or self.last_pred is None:
+            return
+        self.keyframe(count, pose, self.last_pred)
+
+    # -- results ---------------------------------------------------------------------------------
+    def boxes(self):
+        """global boxes (xyzlhw [N,6], R [N,3,3]) on the host"""
+        if self.all_pred_box is None:
+            return np.zeros((0, 6), np.float32), np.zeros((0, 3, 3), np.float32)
+        b = self.all_pred_box.pred_boxes_3d
+        return b.tensor.cpu().numpy(), b.R.cpu().numpy()

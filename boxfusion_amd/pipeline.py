@@ -1,0 +1,207 @@
+"""Per-frame detect + multi-view fusion, in demo.py `run()` order (demo.py:88-332), on the GPU.
+
+    DetectStage  (independent per frame; batched B frames per call)
+      a1  depth standardisation            bf_depth_standardize          preprocessor.py:97-129
+      a13 depth back-projection            bf_backproject                 tools/utils.py:232-287
+      a2-a9 CuTR RGB-D forward             CuTREngine (MFMA kernels)      cubify_transformer.py
+      a10 detection filters                torch on device                demo.py:138-148
+      a11 scale_boxes + crop + CLIP        CLIPEngine (fused crop/resize  tools/utils.py:355-495
+          + text match                      im2col + MFMA ViT-H/14)       demo.py:162-171
+    FusionStage  (serial over keyframes, fusion_stage.py)                demo.py:200-305
+
+`Pipeline.run(stream)` drives both over a frame stream with the reference's keyframe rule
+(`count % gap == 0`, plus the last-frame re-entry).  The detection batch is the unit that shards
+across GPUs (bench.py); fusion consumes keyframes strictly in frame order.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from boxfusion_amd import _lib
+from boxfusion_amd.box_manager import BoxManager
+from boxfusion_amd.engine import CLIPEngine, CuTREngine
+from boxfusion_amd.fusion_stage import FusionStage
+from boxfusion_amd.instances import Instances3D
+from boxfusion_amd.preprocessor import square_pad_size
+from boxfusion_amd.sensor import camera_to_gravity
+
+DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
+
+# keys read by demo.py that only cubicle.yaml defines: documented defaults
+DETECTION_DEFAULTS = dict(class_sim_thres=25.0, size_max_thres=None)
+FUSION_DEFAULTS = dict(clip_sim_coeff=1.0)
+
+
+def load_class_names():
+    with open(os.path.join(DATA, "panoptic_categories_nomerge.txt")) as f:
+        return [ln.strip() for ln in f if ln.strip()]
+
+
+def load_class_features():
+    return torch.from_numpy(np.load(os.path.join(DATA, "class_features.npy")).astype(np.float32))
+
+
+def scale_boxes(boxes, H, W, scale=1.2):
+    """tools/utils.py:355-381 on device (same f32 expression order)."""
+    cx = (boxes[:, 0] + boxes[:, 2]) / 2
+    cy = (boxes[:, 1] + boxes[:, 3]) / 2
+    w = (boxes[:, 2] - boxes[:, 0]) * scale
+    h = (boxes[:, 3] - boxes[:, 1]) * scale
+    return torch.stack([torch.clamp(cx - w / 2, 0, W), torch.clamp(cy - h / 2, 0, H),
+                        torch.clamp(cx + w / 2, 0, W), torch.clamp(cy + h / 2, 0, H)], 1)
+
+
+def detection_mask(scores, proj_xy, box3d, cfg, H, W):
+    """demo.py:138-148 filters for a [B,100] batch: score, uv bound, floor, large."""
+    det = cfg["detection"]
+    m = scores >= float(det.get("score_thresh", 0.0))
+    if det.get("uv_bound"):
+        ratio = det["uv_bound_value"]
+        m &= BoxManager.check_uv_bounds(proj_xy.reshape(-1, 2), W, H, ratio).view_as(m)
+    if det.get("floor_mask"):
+        m &= ~BoxManager.check_floor_mask(box3d.reshape(-1, 6), det["floor_ratio"]).view_as(m)
+    if det.get("size_max_thres"):
+        m &= ~BoxManager.check_large_mask(box3d.reshape(-1, 6), det["size_max_thres"]).view_as(m)
+    return m
+
+
+class DetectStage:
+    """Everything demo.py does per frame before the fusion step, for a batch of B frames.
+
+    crop_source: "filtered" (reference: CLIP on every instance surviving the filters) or
+    "top" (throughput runs with random weights: CLIP on the top `crops_per_frame` instances of
+    every frame, so the CLIP tower does the work it would do on real detections)."""
+
+    def __init__(self, cutr_model, clip_visual, cfg, batch, H=480, W=640, K3=None, text_features=None,
+                 class_names=None, crops_per_frame=16, crop_source="filtered", backproject=True,
+                 clip_capacity=256, device="cuda"):
+        self.cfg = cfg
+        self.dev = torch.device(device)
+        self.B, self.H, self.W = batch, H, W
+        self.pad = square_pad_size(H, W)
+        self.cutr = CuTREngine(cutr_model, batch, H, W, pad=self.pad, device=device)
+        self.clip = CLIPEngine(clip_visual, clip_capacity, device=device) if clip_visual is not None else None
+        self.K3 = np.asarray(K3, np.float32)
+        self.K_dev = torch.from_numpy(np.stack([self.K3] * batch)).to(self.dev)
+        self.text = (text_features if text_features is not None else load_class_features()).to(self.dev).contiguous()
+        names = class_names if class_names is not None else load_class_names()
+        self.prompt = np.concatenate([np.asarray(names), np.full(1, "")])
+        self.crops_per_frame = crops_per_frame
+        self.crop_source = crop_source
+        self.backproject = backproject
+        det = dict(DETECTION_DEFAULTS, **cfg["detection"])
+        self.sim_thres = float(det["class_sim_thres"])
+        self.scale_box = float(det.get("scale_box", 1.2))
+        self.coeff = float(dict(FUSION_DEFAULTS, **cfg["box_fusion"])["clip_sim_coeff"])
+        self.last = {}
+
+    def text_prompt(self, frames_u8, boxes, frame_idx):
+        """tools/utils.py:478-495 + retriev :383-403 for crops of several frames at once.
+        Returns (category index [N] into self.prompt, L2-normalised features [N,1024], max sims)."""
+        feats = []
+        cap = self.clip.N
+        bi = scale_boxes(boxes, self.H, self.W, self.scale_box).to(torch.int32)
+        for s in range(0, boxes.shape[0], cap):
+            feats.append(self.clip(frames_u8, bi[s:s + cap].contiguous(), frame_idx[s:s + cap].contiguous()))
+        f = torch.cat(feats, 0) if len(feats) > 1 else feats[0]
+        f = f / f.norm(dim=-1, keepdim=True)
+        self.text /= self.text.norm(dim=-1, keepdim=True)   # in-place renorm every call (quirk 4)
+        probs = 100.0 * f @ self.text.T
+        probs = torch.cat([probs, torch.full_like(probs, self.sim_thres)[..., :1]], dim=-1)
+        mx, idx = torch.max(probs, dim=-1)
+        return idx, f, mx
+
+    @torch.no_grad()
+    def __call__(self, rgb_u8, depth, poses):
+        """rgb_u8 [B,H,W,3] u8, depth [B,H,W] f32 (device), poses [B,4,4] host -> list of B
+        Instances3D (camera frame, filtered, with categories / features / CLIP-adjusted scores)."""
+        B, H, W = self.B, self.H, self.W
+        assert rgb_u8.shape == (B, H, W, 3) and depth.shape == (B, H, W)
+        dstd, params = _lib.depth_standardize(depth)
+        if self.backproject:
+            poses_dev = torch.from_numpy(np.asarray(poses, np.float32)).to(self.dev)
+            self.last["xyz"] = [_lib.backproject(depth[b], self.K_dev[b], poses_dev[b]) for b in range(B)]
+        Tg = torch.from_numpy(np.stack([camera_to_gravity(p) for p in poses])).to(self.dev)
+        res = self.cutr(rgb_u8, dstd, params, self.K_dev, Tg, [(H, W)] * B)
+        scores = torch.stack([r.scores for r in res])
+        proj = torch.stack([r.pred_proj_xy for r in res])
+        box3d = torch.stack([r.pred_boxes_3d.tensor for r in res])
+        keep = detection_mask(scores, proj, box3d, self.cfg, H, W)
+        if self.clip is None:
+            return [r[keep[b]] for b, r in enumerate(res)]
+        boxes2d = torch.stack([r.pred_boxes for r in res])                       # [B,100,4]
+        if self.crop_source == "top":
+            k = self.crops_per_frame
+            sel = torch.zeros_like(keep)
+            sel[:, :k] = True                                                     # scores sorted desc
+        else:
+            sel = keep
+        bidx, iidx = sel.nonzero(as_tuple=True)
+        out = [r[keep[b]] for b, r in enumerate(res)]
+        if bidx.numel() == 0:
+            return out
+        cat_idx, feats, sims = self.text_prompt(rgb_u8, boxes2d[bidx, iidx].contiguous(), bidx.to(torch.int32))
+        self.last["clip"] = (bidx, iidx, cat_idx, feats, sims)
+        if self.crop_source == "top":
+            return out
+        # scatter back per frame (sel == keep): categories, features, scores += coeff * sim / 100
+        counts = keep.sum(1).tolist()
+        ci = cat_idx.cpu().numpy()
+        o = 0
+        final = []
+        for b, r in enumerate(out):
+            n = counts[b]
+            if n == 0:
+                final.append(r)
+                continue
+            r.categories = self.prompt[ci[o:o + n]]
+            r.features = feats[o:o + n]
+            r.scores = r.scores + self.coeff * sims[o:o + n] / 100.0
+            final.append(r[r.categories != ""])
+            o += n
+        return final
+
+
+def scene_instances(det, device, H=480, W=640):
+    """Instances3D from a synthetic-scene detection dict (boxfusion_amd.synthetic.Scene)."""
+    from boxfusion_amd.boxes import GeneralInstance3DBoxes
+    p = Instances3D((H, W))
+    p.scores = torch.from_numpy(det["scores"]).to(device)
+    p.pred_boxes = torch.from_numpy(det["pred_boxes"]).to(device)
+    p.pred_boxes_3d = GeneralInstance3DBoxes(torch.from_numpy(det["xyzlhw"]).to(device),
+                                             torch.from_numpy(det["R"]).to(device))
+    p.pred_proj_xy = torch.from_numpy(det["proj_xy"]).to(device)
+    return p
+
+
+class Pipeline:
+    """demo.py run() over a stream of (rgb, depth, pose) frames: every frame goes through the
+    per-frame preprocessing, keyframes (count % gap == 0) through CuTR + CLIP, and the fusion
+    state machine in frame order."""
+
+    def __init__(self, detect: DetectStage, fusion: FusionStage, gap):
+        self.detect, self.fusion, self.gap = detect, fusion, gap
+
+    def run(self, frames, n_frames):
+        """frames(i0, i1) -> (rgb [b,H,W,3] u8 dev, depth [b,H,W] f32 dev, poses [b,4,4] host)"""
+        B = self.detect.B
+        kf = [i for i in range(n_frames) if i % self.gap == 0]
+        for s in range(0, len(kf), B):
+            ids = kf[s:s + B]
+            rgb, depth, poses = frames(ids)
+            if len(ids) < B:   # ragged tail: pad the batch with the last frame, drop its results
+                pad = B - len(ids)
+                rgb = torch.cat([rgb, rgb[-1:].expand(pad, -1, -1, -1)])
+                depth = torch.cat([depth, depth[-1:].expand(pad, -1, -1)])
+                poses = np.concatenate([poses, np.repeat(poses[-1:], pad, 0)])
+            preds = self.detect(rgb.contiguous(), depth.contiguous(), poses)
+            for j, i in enumerate(ids):
+                self.fusion.keyframe(i, poses[j], preds[j])
+        last = n_frames - 1
+        if last % self.gap != 0:
+            _, _, p = frames([last])
+            self.fusion.finish(last, p[0], False)
+        return self.fusion

@@ -1,0 +1,56 @@
+"""bench.gather_step over gloo with world_size 2 (CPU): the fusion owner receives every rank's
+per-frame records in global frame order."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from boxfusion_amd.synthetic import Scene
+    scene = Scene(seed=0)
+    B, step = 4, 3
+    frames = [step * B * world + rank * B + j for j in range(B)]
+    recs = torch.from_numpy(bench.pack_records([scene.detections(f) for f in frames]))
+    feats = torch.full((B * 2, 8), float(rank))
+    poses = np.stack([scene.pose(f) for f in frames])
+    g_rec, g_feat, g_pose = bench.gather_step(recs, feats, poses, dist, world)
+    if rank == 0:
+        want = [step * B * world + j for j in range(B * world)]
+        exp = bench.pack_records([scene.detections(f) for f in want])
+        ok = (np.array_equal(g_rec.numpy(), exp)
+              and np.array_equal(g_pose, np.stack([scene.pose(f) for f in want]))
+              and g_feat[:B * 2].eq(0).all().item() and g_feat[B * 2:].eq(1).all().item())
+        unpacked = bench.unpack_record(g_rec[1], "cpu")
+        ok = ok and len(unpacked) == int(exp[1, 0])
+        q.put(bool(ok))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_step_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+    assert res
+    assert all(p.exitcode == 0 for p in procs)
