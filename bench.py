@@ -58,6 +58,7 @@ def parse():
     p.add_argument("--clip-layers", type=int, default=32)
     p.add_argument("--crops", type=int, default=16)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--breakdown", action="store_true", help="sync between stages, report ms/step of each")
     p.add_argument("--cpu-detect-frames", type=int, default=1)
     p.add_argument("--cpu-fusion-frames", type=int, default=24)
     return p.parse_args()
@@ -230,11 +231,18 @@ def main():
     rec_all = torch.from_numpy(pack_records([scene.detections(f) for f in all_mine])).to(dev)
     torch.cuda.synchronize()
 
+    brk = dict(detect=0.0, fusion=0.0)
+
     def run_steps(s0, s1, fusion, timer=None):
         for s in range(s0, s1):
             o = s * B
             sl = slice(o, o + B)
+            tb = time.perf_counter()
             detect(rgb_all[sl], depth_all[sl], poses_all[sl])
+            if args.breakdown:
+                torch.cuda.synchronize()
+                brk["detect"] += time.perf_counter() - tb
+                tb = time.perf_counter()
             bidx, iidx, cat_idx, feats, sims = detect.last["clip"]
             recs = rec_all[sl]
             g_rec, g_feat, g_pose = gather_step(recs, feats, poses_all[sl], dist, N)
@@ -242,10 +250,14 @@ def main():
                 base = s * per_step
                 for j in range(g_rec.shape[0]):
                     fusion.keyframe(base + j - s0 * per_step, g_pose[j], unpack_record(g_rec[j], dev))
+            if args.breakdown:
+                torch.cuda.synchronize()
+                brk["fusion"] += time.perf_counter() - tb
 
     # ---- warmup (own fusion state), then the timed stream from frame 0 ----------------------
     run_steps(0, args.warmup, FusionStage(CFG, SCANNET_K, device=dev))
     fusion = FusionStage(CFG, SCANNET_K, device=dev)
+    brk.update(detect=0.0, fusion=0.0)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -284,6 +296,8 @@ def main():
                          "launches": ks["launches"], "avg_us": ks.get("avg_us", 0.0),
                          "flops_per_launch": ks["flops"] / max(ks["launches"], 1)},
         }
+        if args.breakdown:
+            line["breakdown_ms_per_step"] = {k: 1e3 * v / args.steps for k, v in brk.items()}
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cutr, clip_vis, args, scene)
         print(json.dumps(line), flush=True)

@@ -74,9 +74,17 @@ def _stream():
     return c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+_SYNC_DEBUG = os.environ.get("BF_SYNC_DEBUG", "0") == "1"
+
+
 def _check(rc, name):
     if rc != 0:
         raise HipError(f"{name} failed with bf_status {rc}")
+    if _SYNC_DEBUG:   # debugging aid: attribute asynchronous faults to the launching entry point
+        try:
+            torch.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001
+            raise HipError(f"{name}: device fault after launch: {e}") from e
 
 
 def _need(t, dtype, name):

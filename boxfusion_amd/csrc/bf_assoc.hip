@@ -109,8 +109,9 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_nms_scan(
         int nrest = 0, nsupp = 0;
         for (int base = 1; base < no; base += SCAN_THREADS) {
             int q = base + t;
-            int j = (q < no) ? order[q] : -1;
-            double v = (q < no) ? iou[(size_t)i * n + j] : 0.0;
+            const bool live = q < no;
+            const int j = order[live ? q : no - 1];          // valid index: the load is always safe
+            const double v = live ? iou[(size_t)i * n + j] : 0.0;
             bool fr = (q < no) && (v <= cfg.iou_threshold);
             bool fs = (q < no) && (v > cfg.iou_threshold);
             int tr, ts;

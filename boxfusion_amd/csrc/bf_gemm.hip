@@ -103,7 +103,9 @@ __global__ void __launch_bounds__(G_THREADS, 2) k_gemm(const u16* __restrict__ A
     const int fr = lane & 31, fh = lane >> 5;
     for (int kt = 0; kt < nk; ++kt) {
         const int st = kt & 1;
-        if (kt + 1 < nk) G_LOAD((kt + 1) * GB_K);
+        // the prefetch address stays inside the operands on the last step as well (the compiler
+        // may issue these loads unconditionally; an offset of K would read past the last row)
+        G_LOAD((kt + 1 < nk ? kt + 1 : kt) * GB_K);
         const unsigned char* sa = g_smem + st * 32768;
         const unsigned char* sw = sa + 16384;
 #pragma unroll

@@ -39,7 +39,8 @@ __global__ void __launch_bounds__(256) k_layernorm(const float* __restrict__ x, 
 #pragma unroll
     for (int i = 0; i < NPL; ++i) {
         int c = (lane + 64 * i) * 4;
-        v[i] = c < C ? *reinterpret_cast<const float4*>(xr + c) : make_float4(0, 0, 0, 0);
+        v[i] = *reinterpret_cast<const float4*>(xr + min(c, C - 4));   // address always in-row
+        if (c >= C) v[i] = make_float4(0, 0, 0, 0);
         s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
     }
 #pragma unroll
@@ -64,8 +65,8 @@ __global__ void __launch_bounds__(256) k_layernorm(const float* __restrict__ x, 
     for (int i = 0; i < NPL; ++i) {
         int c = (lane + 64 * i) * 4;
         if (c < C) {
-            float4 gg = *reinterpret_cast<const float4*>(g + c);
-            float4 be = *reinterpret_cast<const float4*>(bb + c);
+            float4 gg = *reinterpret_cast<const float4*>(g + min(c, C - 4));
+            float4 be = *reinterpret_cast<const float4*>(bb + min(c, C - 4));
             uint32_t lo = (uint32_t)vf2bf((v[i].x - mean) * rstd * gg.x + be.x) |
                           ((uint32_t)vf2bf((v[i].y - mean) * rstd * gg.y + be.y) << 16);
             uint32_t hi = (uint32_t)vf2bf((v[i].z - mean) * rstd * gg.z + be.z) |
@@ -125,9 +126,8 @@ __global__ void __launch_bounds__(256) k_im2col_rgb8(const uint8_t* __restrict__
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int x = px * p + kx0 + i;
-        float f = 0.f;
-        if (y < H && x < W) f = ((float)img[(((size_t)b * H + y) * W + x) * 3 + c] - mean) / sd;
-        v[i] = vf2bf(f);
+        const float px_v = (float)img[(((size_t)b * H + min(y, H - 1)) * W + min(x, W - 1)) * 3 + c];
+        v[i] = vf2bf((y < H && x < W) ? (px_v - mean) / sd : 0.f);
     }
     W128 w = {(uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2] | ((uint32_t)v[3] << 16),
               (uint32_t)v[4] | ((uint32_t)v[5] << 16), (uint32_t)v[6] | ((uint32_t)v[7] << 16)};
@@ -167,8 +167,8 @@ __global__ void __launch_bounds__(256) k_im2col_f32(const float* __restrict__ x,
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int xx = px * p + kx0 + i;
-        float f = (y < H && xx < W) ? x[((size_t)b * H + y) * W + xx] : 0.f;
-        v[i] = vf2bf(f);
+        const float dv = x[((size_t)b * H + min(y, H - 1)) * W + min(xx, W - 1)];
+        v[i] = vf2bf((y < H && xx < W) ? dv : 0.f);
     }
     W128 w = {(uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2] | ((uint32_t)v[3] << 16),
               (uint32_t)v[4] | ((uint32_t)v[5] << 16), (uint32_t)v[6] | ((uint32_t)v[7] << 16)};
@@ -210,36 +210,35 @@ __global__ void __launch_bounds__(256) k_crop_im2col(const uint8_t* __restrict__
     const int K = 3 * p * p;
     const int x1 = boxes[4 * n], y1 = boxes[4 * n + 1], x2 = boxes[4 * n + 2], y2 = boxes[4 * n + 3];
     const int cw = x2 - x1, chh = y2 - y1;
-    const uint8_t* im = img + (size_t)(img_idx ? img_idx[n] : 0) * H * W * 3;
+    const bool nonempty = cw > 0 && chh > 0;
+    const uint8_t* im = img + (size_t)max(img_idx ? img_idx[n] : 0, 0) * H * W * 3;
+    // every pixel address is clamped into the frame, so the loads are safe even where the value
+    // is discarded (empty crop, K padding); the sampling itself never leaves the crop
+    auto px_at = [&](int yy, int xx, int c) {
+        const int gy = min(max(y1 + yy, 0), H - 1), gx = min(max(x1 + xx, 0), W - 1);
+        return (float)im[((size_t)gy * W + gx) * 3 + c];
+    };
+    const float fcw = (float)max(cw, 1) / (float)S, fch = (float)max(chh, 1) / (float)S;
     u16 v[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int k = ch * 8 + i;
-        float f = 0.f;
-        if (k < K) {
-            const int c = k / (p * p), rem = k % (p * p);
-            const int oy = py * p + rem / p, ox = px * p + rem % p;
-            float val = 0.f;
-            if (cw > 0 && chh > 0) {
-                float sy = ((float)oy + 0.5f) * ((float)chh / (float)S) - 0.5f;
-                float sx = ((float)ox + 0.5f) * ((float)cw / (float)S) - 0.5f;
-                sy = fmaxf(sy, 0.f);
-                sx = fmaxf(sx, 0.f);
-                int iy0 = min((int)sy, chh - 1), ix0 = min((int)sx, cw - 1);
-                int iy1 = min(iy0 + 1, chh - 1), ix1 = min(ix0 + 1, cw - 1);
-                float fy = sy - (float)iy0, fx = sx - (float)ix0;
-                auto px_at = [&](int yy, int xx) {
-                    return (float)im[((size_t)(y1 + yy) * W + (x1 + xx)) * 3 + c];
-                };
-                float top = px_at(iy0, ix0) * (1.f - fx) + px_at(iy0, ix1) * fx;
-                float bot = px_at(iy1, ix0) * (1.f - fx) + px_at(iy1, ix1) * fx;
-                val = top * (1.f - fy) + bot * fy;
-            }
-            const float mean = c == 0 ? m0 : (c == 1 ? m1 : m2);
-            const float sd = c == 0 ? s0 : (c == 1 ? s1 : s2);
-            f = (val / 255.f - mean) / sd;
-        }
-        v[i] = vf2bf(f);
+        const int kk = min(k, K - 1);
+        const int c = kk / (p * p), rem = kk % (p * p);
+        const int oy = py * p + rem / p, ox = px * p + rem % p;
+        float sy = fmaxf(((float)oy + 0.5f) * fch - 0.5f, 0.f);
+        float sx = fmaxf(((float)ox + 0.5f) * fcw - 0.5f, 0.f);
+        const int iy0 = min((int)sy, max(chh, 1) - 1), ix0 = min((int)sx, max(cw, 1) - 1);
+        const int iy1 = min(iy0 + 1, max(chh, 1) - 1), ix1 = min(ix0 + 1, max(cw, 1) - 1);
+        const float fy = sy - (float)iy0, fx = sx - (float)ix0;
+        const float top = px_at(iy0, ix0, c) * (1.f - fx) + px_at(iy0, ix1, c) * fx;
+        const float bot = px_at(iy1, ix0, c) * (1.f - fx) + px_at(iy1, ix1, c) * fx;
+        // the resized crop is a uint8 image in the reference (cv2.resize of a u8 crop)
+        const float val = nonempty ? rintf(top * (1.f - fy) + bot * fy) : 0.f;
+        const float mean = c == 0 ? m0 : (c == 1 ? m1 : m2);
+        const float sd = c == 0 ? s0 : (c == 1 ? s1 : s2);
+        const float f = (val / 255.f - mean) / sd;
+        v[i] = vf2bf(k < K ? f : 0.f);
     }
     W128 w = {(uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2] | ((uint32_t)v[3] << 16),
               (uint32_t)v[4] | ((uint32_t)v[5] << 16), (uint32_t)v[6] | ((uint32_t)v[7] << 16)};
