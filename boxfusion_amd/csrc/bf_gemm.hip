@@ -7,11 +7,12 @@
 //     act: 0 none, 1 GELU (erf, nn.GELU default), 2 ReLU;  C is f32 or bf16.
 //
 // Tiling: 128x128 output tile per 256-thread workgroup (2x2 waves, 64x64 per wave as 2x2
-// v_mfma_f32_32x32x16_bf16 tiles), BK = 64, two LDS stages (64 KiB) fed by register staging:
-// the next K-tile's global loads are issued before the current tile's MFMAs and written to the
-// other LDS stage after them.  LDS rows are 128 B with a 16-B-chunk XOR swizzle (chunk ^ row&7)
-// so the 32-row fragment reads (ds_read_b128) spread over the banks.  XCD-aware block order:
-// consecutive output tiles of one A row-panel land on the same XCD (shared L2).
+// v_mfma_f32_32x32x16_bf16 tiles), BK = 64, two LDS stages (64 KiB) filled by direct-to-LDS
+// loads (global_load_lds_dwordx4): the next K-tile is issued before the current tile's MFMAs,
+// one vmcnt(0) + barrier per K-tile.  LDS rows are 128 B with a 16-B-chunk XOR swizzle
+// (chunk ^ row&7, applied on the source address) so the 32-row fragment reads (ds_read_b128)
+// spread over the banks.  XCD-aware block order: consecutive output tiles of one A row-panel
+// land on the same XCD (shared L2).
 #include "bf_common.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -34,7 +35,19 @@ __device__ __forceinline__ u16 f2bf(float f) {
     return *reinterpret_cast<u16*>(&b);
 }
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// nn.GELU (erf form).  erf by Abramowitz-Stegun 7.1.26 (|error| <= 1.5e-7, far below the bf16
+// output rounding): one v_rcp, one v_exp and a handful of FMAs instead of the library erff.
+__device__ __forceinline__ float erf_as(float x) {
+    const float a = fabsf(x);
+    const float t = __frcp_rn(fmaf(0.3275911f, a, 1.0f));
+    float p = fmaf(1.061405429f, t, -1.453152027f);
+    p = fmaf(p, t, 1.421413741f);
+    p = fmaf(p, t, -0.284496736f);
+    p = fmaf(p, t, 0.254829592f);
+    const float y = 1.0f - p * t * __expf(-a * a);
+    return copysignf(y, x);
+}
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_as(x * 0.70710678118654752f)); }
 
 // byte offset of 16-B chunk `c` (0..7) of row `r` in a [rows][64 bf16] swizzled tile
 __device__ __forceinline__ int swz(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
@@ -47,7 +60,7 @@ __global__ void __launch_bounds__(G_THREADS, 2) k_gemm(const u16* __restrict__ A
                                                         int resid_mod, void* __restrict__ Cv,
                                                         int ldc, const int32_t* __restrict__ row_map,
                                                         int M, int N, int K, int tiles_n,
-                                                        int tiles_m) {
+                                                        int tiles_m, int vec_epi) {
     extern __shared__ __attribute__((aligned(16))) unsigned char g_smem[];
     // stage s: A at s*32K, W at s*32K + 16K
     const int t = threadIdx.x;
@@ -63,30 +76,32 @@ __global__ void __launch_bounds__(G_THREADS, 2) k_gemm(const u16* __restrict__ A
     const int m0 = tm * GB_M, n0 = tn * GB_N;
     const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
 
-    // global load assignment: 1024 16-B chunks per operand tile, 4 per thread
-    U128 ra0, ra1, ra2, ra3, rw0, rw1, rw2, rw3;
-#define G_LOAD1(i, RA, RW, k0)                                                                   \
-    {                                                                                            \
-        const int ch = t + (i) * G_THREADS, r = ch >> 3, c = ch & 7;                             \
-        const int gm = m0 + r, gn = n0 + r, gk = (k0) + c * 8;                                   \
-        RA = *reinterpret_cast<const U128*>(A + (size_t)min(gm, M - 1) * lda + gk);              \
-        RW = *reinterpret_cast<const U128*>(W + (size_t)min(gn, N - 1) * ldw + gk);              \
-        if (gm >= M) RA.x = RA.y = RA.z = RA.w = 0u;                                             \
-        if (gn >= N) RW.x = RW.y = RW.z = RW.w = 0u;                                             \
+    // Direct-to-LDS staging (global_load_lds_dwordx4): one wave-instruction fills 1 KiB = 8 tile
+    // rows of 128 B at a wave-uniform LDS base, lane l at +16*l.  The XOR swizzle therefore moves
+    // to the per-lane SOURCE address: lane l of the instruction covering rows 8q..8q+7 writes
+    // physical chunk p = l&7 of row r = 8q + (l>>3), which must hold logical chunk p ^ (r&7).
+    // Each wave issues 4 instructions per operand per K-tile (16 KiB per operand per stage).
+    // Rows past M / N are clamped to the last row (valid addresses; those outputs are not stored).
+    const u16* ga[4];
+    const u16* gw[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = (wave * 4 + i) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ (r & 7);
+        ga[i] = A + (size_t)min(m0 + r, M - 1) * lda + c * 8;
+        gw[i] = W + (size_t)min(n0 + r, N - 1) * ldw + c * 8;
     }
-#define G_LOAD(k0)                                                                               \
-    G_LOAD1(0, ra0, rw0, k0) G_LOAD1(1, ra1, rw1, k0) G_LOAD1(2, ra2, rw2, k0)                    \
-        G_LOAD1(3, ra3, rw3, k0)
-#define G_STORE1(i, RA, RW, stage)                                                               \
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+#define G_STAGE(stage, k0)                                                                       \
     {                                                                                            \
-        const int ch = t + (i) * G_THREADS, r = ch >> 3, c = ch & 7;                             \
-        unsigned char* sa_ = g_smem + (stage) * 32768;                                           \
-        *reinterpret_cast<U128*>(sa_ + swz(r, c)) = RA;                                          \
-        *reinterpret_cast<U128*>(sa_ + 16384 + swz(r, c)) = RW;                                  \
+        unsigned char* sa_ = g_smem + (stage) * 32768 + wave * 4096;                             \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                          \
+            __builtin_amdgcn_global_load_lds((const void*)(ga[i] + (k0)),                        \
+                                             (lds_ptr_t)(sa_ + i * 1024), 16, 0, 0);             \
+            __builtin_amdgcn_global_load_lds((const void*)(gw[i] + (k0)),                        \
+                                             (lds_ptr_t)(sa_ + 16384 + i * 1024), 16, 0, 0);     \
+        }                                                                                        \
     }
-#define G_STORE(stage)                                                                           \
-    G_STORE1(0, ra0, rw0, stage) G_STORE1(1, ra1, rw1, stage) G_STORE1(2, ra2, rw2, stage)        \
-        G_STORE1(3, ra3, rw3, stage)
 
     f32x16 acc[2][2];
 #pragma unroll
@@ -97,15 +112,15 @@ __global__ void __launch_bounds__(G_THREADS, 2) k_gemm(const u16* __restrict__ A
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
     const int nk = K / GB_K;
-    G_LOAD(0);
-    G_STORE(0);
+    G_STAGE(0, 0);
+    __builtin_amdgcn_s_waitcnt(0);     // vmcnt(0): the first tile has landed in LDS
     __syncthreads();
     const int fr = lane & 31, fh = lane >> 5;
     for (int kt = 0; kt < nk; ++kt) {
         const int st = kt & 1;
-        // the prefetch address stays inside the operands on the last step as well (the compiler
-        // may issue these loads unconditionally; an offset of K would read past the last row)
-        G_LOAD((kt + 1 < nk ? kt + 1 : kt) * GB_K);
+        // prefetch the next K-tile into the other stage (its last readers passed the barrier
+        // that ended the previous iteration)
+        if (kt + 1 < nk) G_STAGE(st ^ 1, (kt + 1) * GB_K);
         const unsigned char* sa = g_smem + st * 32768;
         const unsigned char* sw = sa + 16384;
 #pragma unroll
@@ -127,16 +142,81 @@ __global__ void __launch_bounds__(G_THREADS, 2) k_gemm(const u16* __restrict__ A
                 for (int j = 0; j < 2; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
         }
-        if (kt + 1 < nk) G_STORE(st ^ 1);
+        // the LDS-DMA of the next tile is a pending VM op: retire it, then one barrier makes it
+        // visible to every wave and ends all reads of this stage
+        __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
     }
+#undef G_STAGE
 
-    // epilogue: C/D layout col = lane&31, row = (e&3) + 8*(e>>2) + 4*(lane>>5)
+    // ---- epilogue ----------------------------------------------------------------------------
+    // C/D layout: col = lane&31, row = (e&3) + 8*(e>>2) + 4*(lane>>5).  Every lane holds columns,
+    // so the tile is transposed through LDS (free after the K loop) and written row-wise in 16-B
+    // chunks: coalesced stores and coalesced residual reads.  bias + activation are applied
+    // before the transpose, the residual after it.
+    if (vec_epi) {
+        float* T = reinterpret_cast<float*>(g_smem);   // [128][128] f32, column XOR-swizzled
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int nl = wn + j * 32 + fr;
+            const float bv = (bias && n0 + nl < N) ? bias[min(n0 + nl, N - 1)] : 0.f;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int ml = wm + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh;
+                    float v = acc[i][j][e] + bv;
+                    if (ACT == 1) v = gelu_erf(v);
+                    else if (ACT == 2) v = fmaxf(v, 0.f);
+                    T[ml * 128 + (nl ^ (((ml >> 2) & 1) << 5))] = v;   // rows r, r+4: other banks
+                }
+        }
+        __syncthreads();
+        constexpr int CW = OUT_BF16 ? 8 : 4;            // output elements per 16-B chunk
+        constexpr int CPR = 128 / CW;                   // chunks per tile row
+#pragma unroll 4
+        for (int id = t; id < 128 * CPR; id += G_THREADS) {
+            const int ml = id / CPR, cl = (id % CPR) * CW;
+            const int m = m0 + ml, n = n0 + cl;
+            if (m >= M || n >= N) continue;
+            const int orow = row_map ? row_map[m] : m;
+            if (orow < 0) continue;
+            const int sw = ((ml >> 2) & 1) << 5;
+            float v[CW];
+#pragma unroll
+            for (int q = 0; q < CW; q += 4) {
+                const float4 x = *reinterpret_cast<const float4*>(T + ml * 128 + ((cl + q) ^ sw));
+                v[q] = x.x; v[q + 1] = x.y; v[q + 2] = x.z; v[q + 3] = x.w;
+            }
+            if (resid) {
+                const int rrow = resid_mod > 0 ? (m % resid_mod) : orow;
+                const float* rp = resid + (size_t)rrow * ldr + n;
+#pragma unroll
+                for (int q = 0; q < CW; q += 4) {
+                    const float4 x = *reinterpret_cast<const float4*>(rp + q);
+                    v[q] += x.x; v[q + 1] += x.y; v[q + 2] += x.z; v[q + 3] += x.w;
+                }
+            }
+            if (OUT_BF16) {
+                U128 o;
+                o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+                o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+                o.z = (uint32_t)f2bf(v[4 % CW]) | ((uint32_t)f2bf(v[5 % CW]) << 16);
+                o.w = (uint32_t)f2bf(v[6 % CW]) | ((uint32_t)f2bf(v[7 % CW]) << 16);
+                *reinterpret_cast<U128*>(reinterpret_cast<u16*>(Cv) + (size_t)orow * ldc + n) = o;
+            } else {
+                *reinterpret_cast<float4*>(reinterpret_cast<float*>(Cv) + (size_t)orow * ldc + n) =
+                    make_float4(v[0], v[1], v[2], v[3]);
+            }
+        }
+        return;
+    }
+    // scalar fallback (unaligned / ragged N): one element per register
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int n = n0 + wn + j * 32 + fr;
         if (n >= N) continue;
-        const float bv = bias ? bias[n] : 0.f;
+        const float bv = bias ? bias[min(n, N - 1)] : 0.f;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -169,10 +249,14 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
     const int nwg = tiles_m * tiles_n;
     const size_t lds = 2 * 32768;
     if (act < 0 || act > 2) return BF_ERR_ARG;
+    // 16-B row chunks need N % 8 (bf16) / N % 4 (f32) and 16-B aligned rows of C and resid
+    const int cw = c_bf16 ? 8 : 4;
+    const int vec_epi = (N % cw == 0) && ((uintptr_t)C % 16 == 0) && ((size_t)ldc * (c_bf16 ? 2 : 4) % 16 == 0) &&
+                        (!resid || (((uintptr_t)resid % 16 == 0) && (ldr % 4 == 0)));
 #define GEMM_LAUNCH(OB, AC)                                                                       \
     hipLaunchKernelGGL((k_gemm<OB, AC>), dim3(nwg), dim3(G_THREADS), lds, bf_stream(stream),       \
                        (const u16*)A, lda, (const u16*)W, ldw, bias, resid, ldr, resid_mod, C, ldc, \
-                       row_map, M, N, K, tiles_n, tiles_m)
+                       row_map, M, N, K, tiles_n, tiles_m, vec_epi)
     if (c_bf16) {
         if (act == 0) GEMM_LAUNCH(true, 0);
         else if (act == 1) GEMM_LAUNCH(true, 1);
