@@ -58,7 +58,10 @@ def parse():
     p.add_argument("--clip-layers", type=int, default=32)
     p.add_argument("--crops", type=int, default=16)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--breakdown", action="store_true", help="sync between stages, report ms/step of each")
+    p.add_argument("--breakdown", action="store_true",
+                   help="synchronous fusion, sync between stages, report ms/step of each")
+    p.add_argument("--sync-fusion", action="store_true",
+                   help="run the fusion state machine inline instead of on the worker stream")
     p.add_argument("--cpu-detect-frames", type=int, default=1)
     p.add_argument("--cpu-fusion-frames", type=int, default=24)
     return p.parse_args()
@@ -190,6 +193,8 @@ def cpu_baseline(cutr, clip_vis, args, scene):
 # ------------------------------------------------------------------------------------------------
 def main():
     args = parse()
+    if args.breakdown:
+        args.sync_fusion = True
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -204,7 +209,7 @@ def main():
     _lib.lib()                                         # fail loudly without the HIP library
     from boxfusion_amd.clip import VisionTransformer
     from boxfusion_amd.cubify_transformer import make_cubify_transformer
-    from boxfusion_amd.fusion_stage import FusionStage
+    from boxfusion_amd.fusion_stage import AsyncFusion, FusionStage
     from boxfusion_amd.pipeline import DetectStage
     from boxfusion_amd.synthetic import SCANNET_K, Scene
 
@@ -248,15 +253,31 @@ def main():
             g_rec, g_feat, g_pose = gather_step(recs, feats, poses_all[sl], dist, N)
             if rank == 0:
                 base = s * per_step
-                for j in range(g_rec.shape[0]):
-                    fusion.keyframe(base + j - s0 * per_step, g_pose[j], unpack_record(g_rec[j], dev))
+                if args.sync_fusion:
+                    for j in range(g_rec.shape[0]):
+                        fusion.keyframe(base + j - s0 * per_step, g_pose[j], unpack_record(g_rec[j], dev))
+                else:
+                    # hand the step's frames to the fusion worker (side stream), keep detecting
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    g_rec.record_stream(fusion.stream)
+                    for j in range(g_rec.shape[0]):
+                        fusion.submit(base + j - s0 * per_step, g_pose[j],
+                                      (lambda r=g_rec[j]: unpack_record(r, dev)), ev)
             if args.breakdown:
                 torch.cuda.synchronize()
                 brk["fusion"] += time.perf_counter() - tb
 
     # ---- warmup (own fusion state), then the timed stream from frame 0 ----------------------
-    run_steps(0, args.warmup, FusionStage(CFG, SCANNET_K, device=dev))
-    fusion = FusionStage(CFG, SCANNET_K, device=dev)
+    def make_fusion():
+        st = FusionStage(CFG, SCANNET_K, device=dev)
+        return st if args.sync_fusion else AsyncFusion(st)
+
+    wf = make_fusion()
+    run_steps(0, args.warmup, wf)
+    if not args.sync_fusion:
+        wf.join()
+    fusion = make_fusion()
     brk.update(detect=0.0, fusion=0.0)
     if dist is not None:
         dist.barrier()
@@ -265,6 +286,8 @@ def main():
     t0 = time.perf_counter()
     with timer:
         run_steps(args.warmup, total_steps, fusion)
+        if not args.sync_fusion:
+            fusion = fusion.join()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()

@@ -180,7 +180,8 @@ def corr_assoc(corners, dims, scores, boxes2d, init_id, cam_poses, cur_pose, K, 
 # fusion
 # ------------------------------------------------------------------------------------------
 def fusion_fit(view_off, n_views, view_box, view_R, view_score, view_pose, view_tc, pst,
-               cfg: FuseCfg, trace=False):
+               cfg: FuseCfg, trace=False, max_views=None):
+    """max_views: host-known bound on n_views (avoids a device read when given)."""
     dev = view_box.device
     n_jobs = view_off.shape[0]
     out_box = torch.empty((n_jobs, 6), dtype=torch.float32, device=dev)
@@ -189,10 +190,18 @@ def fusion_fit(view_off, n_views, view_box, view_R, view_score, view_pose, view_
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     tr = (torch.empty((n_jobs, cfg.iters, cfg.pst_size), dtype=torch.float32, device=dev)
           if trace else None)
-    _check(lib().bf_fusion_fit(_ptr(view_off), _ptr(n_views), c_int(n_jobs), _ptr(view_box),
-                               _ptr(view_R), _ptr(view_score), _ptr(view_pose), _ptr(view_tc),
-                               _ptr(pst), ctypes.byref(cfg), _ptr(out_box), _ptr(out_upd),
-                               _ptr(out_it), _ptr(tr), _ptr(status), _stream()), "bf_fusion_fit")
+    if max_views is None:
+        max_views = int(n_views.max().item()) if n_views.numel() else 1
+    max_views = max(1, min(int(max_views), 32))
+    L = lib()
+    L.bf_fusion_fit_workspace_size.restype = ctypes.c_size_t
+    nbytes = L.bf_fusion_fit_workspace_size(c_int(n_jobs), c_int(max_views), c_int(cfg.pst_size))
+    ws = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=dev)
+    _check(L.bf_fusion_fit(_ptr(view_off), _ptr(n_views), c_int(n_jobs), c_int(max_views),
+                           _ptr(view_box), _ptr(view_R), _ptr(view_score), _ptr(view_pose),
+                           _ptr(view_tc), _ptr(pst), ctypes.byref(cfg), _ptr(out_box),
+                           _ptr(out_upd), _ptr(out_it), _ptr(tr), _ptr(status), _ptr(ws),
+                           _stream()), "bf_fusion_fit")
     return out_box, out_upd, out_it, status, tr
 
 

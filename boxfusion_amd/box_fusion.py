@@ -2,8 +2,9 @@
 
 `BoxFusion.boxfusion(all_pred_box, per_frame_box, box_manager)` keeps the reference's selection
 rules (>= 3 views, list not already fused; box_fusion.py:631-635) and write-back semantics
-(xyz + lhw refined, lhw >= 0.01, R unchanged; :716-724), but every box is refined in ONE launch of
-bf_fusion_fit with all iterations on the device (no per-iteration host round trip).
+(xyz + lhw refined, lhw >= 0.01, R unchanged; :716-724), but every box is refined by ONE call of
+bf_fusion_fit with all iterations on the device (no per-iteration host round trip; the particle
+evaluations of all boxes spread over the whole chip).
 """
 from __future__ import annotations
 
@@ -93,7 +94,7 @@ class BoxFusion:
             per_frame_box.scores.to(dev, torch.float32).index_select(0, flat).contiguous(),
             per_frame_box.cam_pose.to(dev, torch.float32).index_select(0, flat).contiguous(),
             per_frame_box.projected_boxes.index_select(0, flat).contiguous(),
-            self._pst_dev, self.fuse_cfg())
+            self._pst_dev, self.fuse_cfg(), max_views=min(int(nv.max()), 32))
         upd = out_upd.cpu().numpy()
         st = int(status.cpu().numpy()[0])
         if st & _lib.BF_DEV_VIEW_OVERFLOW:

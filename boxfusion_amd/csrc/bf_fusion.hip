@@ -3,8 +3,9 @@
 // Reference: BoxFusion.boxfusion (box_fusion.py:622-724).  The reference launches its CUDA
 // kernel compute_iou_value (:264-405) once per iteration per box, with a host round trip, a
 // Python loop over 1023 particles (cal_transform :475-535) and host scalar updates (update_PST
-// :537-563, momentum :685-706).  Here ONE launch refines every job: workgroup = one fused box,
-// lane = one particle (pst_size <= 1024 lanes = 16 wave64), and all iterations run on the device:
+// :537-563, momentum :685-706).  Here one call refines every job with all iterations on the
+// device (no host round trip): per iteration one launch evaluates every (job, view, particle)
+// pair across the chip and one launch per job does the sequential update:
 //
 //   per iteration:  fitness[p] = sum_v |1 - IoU2D(hull(proj_v(box (+) PST[p]*s)), hull(tc_v))|
 //                                / (V + 1e-6)            (views summed in order: deterministic,
@@ -222,7 +223,14 @@ BF_API int bf_fusion_fitness(const float* box, const float* R, int n_views, cons
 }
 
 // ------------------------------------------------------------------------------------------
-// full refinement: one workgroup per job
+// full refinement: per iteration two launches over all jobs
+//   k_fuse_terms  grid (pairs/256, job): thread = (view, particle), |1 - IoU2D| of that pair.
+//                 A job's V*P independent pairs spread over many CUs (the single-workgroup
+//                 form ran every particle of a job on one CU and was latency-bound).
+//   k_fuse_step   one workgroup per job: fitness[p] = (sum of the V terms in view order)
+//                 / (V + 1e-6) (the reference kernel's per-particle f32 accumulation order),
+//                 accepted-set prefix, cal_transform sums, update_PST / momentum / accept.
+// A job that stopped (3 consecutive failures) skips the remaining launches.
 // ------------------------------------------------------------------------------------------
 struct FuseState {
     double x[6];        // global_xyzlwh (f64, box_fusion.py:655)
@@ -230,226 +238,287 @@ struct FuseState {
     float prev[6];      // previous_search_size (f32)
     float R[9];         // mean_rot
     float box32[6];     // x cast to f32 for the kernel
-    double dsum[8];     // cal_transform sums (legacy promotion)
-    float fsum[8];      // cal_transform sums (NEP 50 promotion)
-    int n_acc;
-    int prev_success, fails, need_update, stop, iters_done;
+    int nv, off;
+    int prev_success, fails, need_update, stop, iters_done, flags;
 };
 
-__global__ void __launch_bounds__(1024) k_fuse(const int32_t* __restrict__ view_off,
-                                               const int32_t* __restrict__ n_views,
-                                               const float* __restrict__ vbox,
-                                               const float* __restrict__ vR,
-                                               const float* __restrict__ vscore,
-                                               const float* __restrict__ vpose,
-                                               const float* __restrict__ vtc,
-                                               const float* __restrict__ pst, bf_fuse_cfg cfg,
-                                               float* __restrict__ out_box,
-                                               int32_t* __restrict__ out_updated,
-                                               int32_t* __restrict__ out_iters,
-                                               float* __restrict__ trace,
-                                               int32_t* __restrict__ status) {
+__global__ void __launch_bounds__(64) k_fuse_init(const int32_t* __restrict__ view_off,
+                                                  const int32_t* __restrict__ n_views, int max_views,
+                                                  const float* __restrict__ vbox,
+                                                  const float* __restrict__ vR,
+                                                  const float* __restrict__ vscore,
+                                                  bf_fuse_cfg cfg, FuseState* __restrict__ states) {
+    const int job = blockIdx.x;
+    if (threadIdx.x != 0) return;
+    FuseState& S = states[job];
+    const int nv = n_views[job];
+    const int off = view_off[job];
+    S.nv = nv;
+    S.off = off;
+    S.prev_success = 0; S.fails = 0; S.need_update = 0; S.iters_done = 0; S.flags = 0;
+    if (nv <= 0 || nv > FUSE_MAX_VIEWS || nv > max_views) {
+        S.stop = 1;
+        S.flags = BF_DEV_VIEW_OVERFLOW;
+        for (int k = 0; k < 6; ++k) { S.x[k] = 0.0; S.box32[k] = 0.f; }
+        return;
+    }
+    S.stop = 0;
+    // init_opt_params (box_fusion.py:566-600)
+    const float* vb = vbox + (size_t)off * 6;
+    const float* vs = vscore + off;
+    int best = 0;
+    for (int v = 1; v < nv; ++v)
+        if (vs[v] > vs[best]) best = v;
+    for (int k = 0; k < 3; ++k) {
+        float s = vb[k];
+        for (int v = 1; v < nv; ++v) s = s + vb[6 * v + k];
+        S.x[k] = (double)(s / (float)nv);
+    }
+    const float* bd = vb + 6 * best + 3;
+    int si[3] = {0, 1, 2};
+    for (int i = 1; i < 3; ++i) {
+        int tt = si[i], j = i - 1;
+        while (j >= 0 && bd[si[j]] > bd[tt]) { si[j + 1] = si[j]; --j; }
+        si[j + 1] = tt;
+    }
+    int rank[3];
+    for (int r = 0; r < 3; ++r) rank[si[r]] = r;
+    float acc[3] = {0, 0, 0};
+    for (int v = 0; v < nv; ++v) {
+        float d[3] = {vb[6 * v + 3], vb[6 * v + 4], vb[6 * v + 5]};
+        for (int i = 1; i < 3; ++i) {
+            float tt = d[i];
+            int j = i - 1;
+            while (j >= 0 && d[j] > tt) { d[j + 1] = d[j]; --j; }
+            d[j + 1] = tt;
+        }
+        for (int k = 0; k < 3; ++k) acc[k] = (v == 0) ? d[rank[k]] : acc[k] + d[rank[k]];
+    }
+    for (int k = 0; k < 3; ++k) S.x[3 + k] = (double)(acc[k] / (float)nv);
+    for (int k = 0; k < 9; ++k) S.R[k] = vR[(size_t)(off + best) * 9 + k];
+    for (int k = 0; k < 3; ++k) {
+        S.ss[k] = (float)cfg.center_init;
+        S.ss[3 + k] = (float)cfg.shape_init;
+        S.prev[k] = 0.f;
+        S.prev[3 + k] = 0.f;
+    }
+    for (int k = 0; k < 6; ++k) S.box32[k] = (float)S.x[k];
+}
+
+#define TERM_THREADS 256
+__global__ void __launch_bounds__(TERM_THREADS) k_fuse_terms(const float* __restrict__ vpose,
+                                                             const float* __restrict__ vtc,
+                                                             const float* __restrict__ pst,
+                                                             bf_fuse_cfg cfg,
+                                                             FuseState* __restrict__ states,
+                                                             float* __restrict__ terms, int max_views) {
+    const int job = blockIdx.y;
+    const FuseState& S = states[job];
+    if (S.stop) return;                                   // uniform per workgroup
+    const int P = cfg.pst_size;                           // multiple of TERM_THREADS' divisor 64
+    const int pair = blockIdx.x * TERM_THREADS + threadIdx.x;
+    const int v = pair / P, p = pair % P;                 // P % 64 == 0: v is uniform per wave
+    if (v >= S.nv) return;
+    __shared__ float s_view[TERM_THREADS / 64][32];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const size_t vi = (size_t)S.off + v;
+    if (lane < 16) s_view[w][lane] = vpose[vi * 16 + lane];
+    else if (lane < 32) s_view[w][lane] = vtc[vi * 16 + (lane - 16)];
+    __builtin_amdgcn_wave_barrier();
+    float b[6], r[9], ss[6], corners[24];
+    for (int k = 0; k < 6; ++k) { b[k] = S.box32[k]; ss[k] = S.ss[k]; }
+    for (int k = 0; k < 9; ++k) r[k] = S.R[k];
+    particle_corners(b, r, pst + 6 * p, ss, corners);
+    const float* Pm = s_view[w];
+    P2 c0[8], ct[8];
+    for (int j = 0; j < 8; ++j) {
+        float vx = corners[3 * j] - Pm[3], vy = corners[3 * j + 1] - Pm[7], vz = corners[3 * j + 2] - Pm[11];
+        float cx = Pm[0] * vx + Pm[4] * vy + Pm[8] * vz;
+        float cy = Pm[1] * vx + Pm[5] * vy + Pm[9] * vz;
+        float cz = Pm[2] * vx + Pm[6] * vy + Pm[10] * vz;
+        float px = ((cx * cfg.K[0]) / cz + cfg.K[2]);
+        float py = ((cy * cfg.K[5]) / cz + cfg.K[6]);
+        c0[j].x = (px > cfg.img_w) ? cfg.img_w : (px < 0) ? 0 : px;
+        c0[j].y = (py > cfg.img_h) ? cfg.img_h : (py < 0) ? 0 : py;
+        ct[j].x = Pm[16 + 2 * j];
+        ct[j].y = Pm[16 + 2 * j + 1];
+    }
+    int flags = 0;
+    const float iou = iou_hulls(c0, ct, &flags);
+    terms[((size_t)job * max_views + v) * P + p] = fabsf(1 - iou);
+    if (flags) atomicOr(&states[job].flags, flags);
+}
+
+__global__ void __launch_bounds__(1024) k_fuse_step(const float* __restrict__ pst, bf_fuse_cfg cfg,
+                                                    FuseState* __restrict__ states,
+                                                    const float* __restrict__ terms, int max_views,
+                                                    int it, float* __restrict__ trace) {
     const int job = blockIdx.x;
     const int t = threadIdx.x;
     const int P = cfg.pst_size;
-    const int nv = n_views[job];
-    const int off = view_off[job];
-    __shared__ FuseViews V;
-    __shared__ float s_pst[FUSE_MAX_PST][6];
+    FuseState* G = states + job;
+    if (G->stop) return;
     __shared__ float s_fit[FUSE_MAX_PST];
     __shared__ int s_acc[FUSE_MAX_PST];
     __shared__ int s_wave[FUSE_MAX_PST / 64];
-    __shared__ FuseState S;
-    __shared__ int s_flags;
-    if (nv <= 0 || nv > FUSE_MAX_VIEWS) {  // uniform per workgroup
-        if (t == 0) {
-            out_updated[job] = 0;
-            out_iters[job] = 0;
-            atomicOr(status, BF_DEV_VIEW_OVERFLOW);
-        }
-        return;
-    }
-
-    for (int q = t; q < nv * 16; q += blockDim.x) {
-        V.pose[q / 16][q % 16] = vpose[(size_t)off * 16 + q];
-        V.tc[q / 16][q % 16] = vtc[(size_t)off * 16 + q];
-    }
-    for (int q = t; q < P * 6; q += blockDim.x) s_pst[q / 6][q % 6] = pst[q];
-    if (t == 0) {
-        s_flags = 0;
-        // init_opt_params (box_fusion.py:566-600)
-        const float* vb = vbox + (size_t)off * 6;
-        const float* vs = vscore + off;
-        int best = 0;
-        for (int v = 1; v < nv; ++v)
-            if (vs[v] > vs[best]) best = v;
-        for (int k = 0; k < 3; ++k) {
-            float s = vb[k];
-            for (int v = 1; v < nv; ++v) s = s + vb[6 * v + k];
-            S.x[k] = (double)(s / (float)nv);
-        }
-        const float* bd = vb + 6 * best + 3;
-        int si[3] = {0, 1, 2};
-        for (int i = 1; i < 3; ++i) {
-            int tt = si[i], j = i - 1;
-            while (j >= 0 && bd[si[j]] > bd[tt]) { si[j + 1] = si[j]; --j; }
-            si[j + 1] = tt;
-        }
-        int rank[3];
-        for (int r = 0; r < 3; ++r) rank[si[r]] = r;
-        float acc[3] = {0, 0, 0};
+    __shared__ double s_dsum[8];
+    __shared__ float s_fsum[8];
+    const int nv = G->nv;
+    // ---- fitness: the reference's per-particle loop `val += |1 - iou|; cnt += 1` -------------
+    if (t < P) {
+        float val = 0.0f, cnt = 0.0f;
+        const float* tp = terms + (size_t)job * max_views * P + t;
         for (int v = 0; v < nv; ++v) {
-            float d[3] = {vb[6 * v + 3], vb[6 * v + 4], vb[6 * v + 5]};
-            for (int i = 1; i < 3; ++i) {
-                float tt = d[i];
-                int j = i - 1;
-                while (j >= 0 && d[j] > tt) { d[j + 1] = d[j]; --j; }
-                d[j + 1] = tt;
-            }
-            for (int k = 0; k < 3; ++k) acc[k] = (v == 0) ? d[rank[k]] : acc[k] + d[rank[k]];
+            val += tp[(size_t)v * P];
+            cnt += 1.0f;
         }
-        for (int k = 0; k < 3; ++k) S.x[3 + k] = (double)(acc[k] / (float)nv);
-        for (int k = 0; k < 9; ++k) S.R[k] = vR[(size_t)(off + best) * 9 + k];
-        for (int k = 0; k < 3; ++k) {
-            S.ss[k] = (float)cfg.center_init;
-            S.ss[3 + k] = (float)cfg.shape_init;
-            S.prev[k] = 0.f;
-            S.prev[3 + k] = 0.f;
-        }
-        S.prev_success = 0; S.fails = 0; S.need_update = 0; S.stop = 0; S.iters_done = 0;
+        const float f = val / (cnt + 1e-6f);
+        s_fit[t] = f;
+        if (trace) trace[((size_t)job * cfg.iters + it) * P + t] = f;
     }
     __syncthreads();
-
-    for (int it = 0; it < cfg.iters; ++it) {
-        if (t == 0)
-            for (int k = 0; k < 6; ++k) S.box32[k] = (float)S.x[k];
-        __syncthreads();
-        // ---- fitness of particle t ---------------------------------------------------------
-        if (t < P) {
-            float corners[24];
-            float b[6], r[9], ss[6];
-            for (int k = 0; k < 6; ++k) { b[k] = S.box32[k]; ss[k] = S.ss[k]; }
-            for (int k = 0; k < 9; ++k) r[k] = S.R[k];
-            particle_corners(b, r, s_pst[t], ss, corners);
-            int flags = 0;
-            float f = particle_fitness(corners, V, nv, cfg, &flags);
-            s_fit[t] = f;
-            if (flags) atomicOr(&s_flags, flags);
-            if (trace) trace[((size_t)job * cfg.iters + it) * P + t] = f;
-        }
-        __syncthreads();
-        // ---- accepted particles: j >= 1, fit[j] < fit[0], first max_accept in index order ----
-        const float f0 = s_fit[0];
-        bool flag = (t >= 1) && (t < P) && (s_fit[t] < f0);
-        unsigned long long m = __ballot(flag);
-        if (bf_lane() == 0) s_wave[t >> 6] = __popcll(m);
-        __syncthreads();
-        int before = 0, total = 0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
-            if (w < (t >> 6)) before += s_wave[w];
-            total += s_wave[w];
-        }
-        int rnk = before + bf_lanes_below(m);
-        if (flag && rnk < cfg.max_accept) s_acc[rnk] = t;
-        const int n_acc = total < cfg.max_accept ? total : cfg.max_accept;
-        __syncthreads();
-        // ---- cal_transform sums in reference order (8 independent sequential sums) ---------
-        if (t < 8) {
-            double ds = 0.0;
-            float fs = 0.0f;
-            for (int k = 0; k < n_acc; ++k) {
-                int j = s_acc[k];
-                float w = f0 - s_fit[j];
-                float prod = (t < 6) ? s_pst[j][t] * w : (t == 6 ? w : s_fit[j] * w);
-                if (cfg.legacy_promotion) ds += (double)prod;
-                else fs = fs + prod;
-            }
-            S.dsum[t] = ds;
-            S.fsum[t] = fs;
-        }
-        __syncthreads();
-        // ---- lane 0: cal_transform tail, update_PST, momentum, accept ----------------------
-        if (t == 0) {
-            const bool success = n_acc > 0;
-            float mt[6] = {0, 0, 0, 0, 0, 0};
-            double iou_d = 0;
-            float iou_f = 0;
-            if (!success) {
-                iou_d = f0;
-                iou_f = f0;
-            } else if (cfg.legacy_promotion) {
-                iou_d = S.dsum[7] / S.dsum[6];
-                for (int k = 0; k < 6; ++k) mt[k] = (float)((S.dsum[k] / S.dsum[6]) * (double)S.ss[k]);
-            } else {
-                iou_f = S.fsum[7] / S.fsum[6];
-                for (int k = 0; k < 6; ++k) mt[k] = (S.fsum[k] / S.fsum[6]) * S.ss[k];
-            }
-            if (cfg.legacy_promotion) {
-                double s[6];
-                for (int k = 0; k < 6; ++k) s[k] = fabs((double)mt[k]) + cfg.min_scale;
-                double nrm = s[0] * s[0];
-                for (int k = 1; k < 6; ++k) nrm = nrm + s[k] * s[k];
-                nrm = sqrt(nrm);
-                for (int k = 3; k < 6; ++k) S.ss[k] = (float)(cfg.shape_coef * iou_d * (s[k] / nrm) + cfg.min_scale);
-                for (int k = 0; k < 3; ++k) S.ss[k] = (float)(cfg.center_coef * iou_d * (s[k] / nrm) + cfg.min_scale);
-            } else {
-                const float ms = (float)cfg.min_scale;
-                float s[6];
-                for (int k = 0; k < 6; ++k) s[k] = fabsf(mt[k]) + ms;
-                float nrm = s[0] * s[0];
-                for (int k = 1; k < 6; ++k) nrm = nrm + s[k] * s[k];
-                nrm = sqrtf(nrm);
-                for (int k = 3; k < 6; ++k) S.ss[k] = (float)cfg.shape_coef * iou_f * (s[k] / nrm) + ms;
-                for (int k = 0; k < 3; ++k) S.ss[k] = (float)cfg.center_coef * iou_f * (s[k] / nrm) + ms;
-            }
-            if (S.prev_success && success) {
-                for (int k = 0; k < 6; ++k) {
-                    if (cfg.legacy_promotion)
-                        S.ss[k] = (float)(cfg.beta * (double)S.ss[k] + (1.0 - cfg.beta) * (double)S.prev[k]);
-                    else
-                        S.ss[k] = (float)cfg.beta * S.ss[k] + (float)(1.0 - cfg.beta) * S.prev[k];
-                }
-            }
-            if (success) {
-                S.need_update = 1;
-                S.prev_success = 1;
-                S.fails = 0;
-                for (int k = 0; k < 6; ++k) S.x[k] += (double)mt[k];
-                for (int k = 0; k < 6; ++k) S.prev[k] = S.ss[k];
-            } else {
-                S.fails++;
-                S.prev_success = 0;
-            }
-            S.iters_done = it + 1;
-            if (S.fails >= 3) S.stop = 1;
-        }
-        __syncthreads();
-        if (S.stop) break;
+    // ---- accepted particles: j >= 1, fit[j] < fit[0], first max_accept in index order ------
+    const float f0 = s_fit[0];
+    bool flag = (t >= 1) && (t < P) && (s_fit[t] < f0);
+    unsigned long long m = __ballot(flag);
+    if (bf_lane() == 0) s_wave[t >> 6] = __popcll(m);
+    __syncthreads();
+    int before = 0, total = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+        if (w < (t >> 6)) before += s_wave[w];
+        total += s_wave[w];
     }
+    int rnk = before + bf_lanes_below(m);
+    if (flag && rnk < cfg.max_accept) s_acc[rnk] = t;
+    const int n_acc = total < cfg.max_accept ? total : cfg.max_accept;
+    __syncthreads();
+    // ---- cal_transform sums in reference order (8 independent sequential sums) -------------
+    if (t < 8) {
+        double ds = 0.0;
+        float fs = 0.0f;
+        for (int k = 0; k < n_acc; ++k) {
+            int j = s_acc[k];
+            float w = f0 - s_fit[j];
+            float prod = (t < 6) ? pst[6 * j + t] * w : (t == 6 ? w : s_fit[j] * w);
+            if (cfg.legacy_promotion) ds += (double)prod;
+            else fs = fs + prod;
+        }
+        s_dsum[t] = ds;
+        s_fsum[t] = fs;
+    }
+    __syncthreads();
+    // ---- lane 0: cal_transform tail, update_PST, momentum, accept ----------------------------
     if (t == 0) {
-        for (int k = 3; k < 6; ++k)
-            if (S.x[k] < 0.01) S.x[k] = 0.01;
-        for (int k = 0; k < 6; ++k) out_box[6 * job + k] = (float)S.x[k];
-        out_updated[job] = S.need_update;
-        out_iters[job] = S.iters_done;
-        if (s_flags) atomicOr(status, s_flags);
+        FuseState S = *G;
+        const bool success = n_acc > 0;
+        float mt[6] = {0, 0, 0, 0, 0, 0};
+        double iou_d = 0;
+        float iou_f = 0;
+        if (!success) {
+            iou_d = f0;
+            iou_f = f0;
+        } else if (cfg.legacy_promotion) {
+            iou_d = s_dsum[7] / s_dsum[6];
+            for (int k = 0; k < 6; ++k) mt[k] = (float)((s_dsum[k] / s_dsum[6]) * (double)S.ss[k]);
+        } else {
+            iou_f = s_fsum[7] / s_fsum[6];
+            for (int k = 0; k < 6; ++k) mt[k] = (s_fsum[k] / s_fsum[6]) * S.ss[k];
+        }
+        if (cfg.legacy_promotion) {
+            double sc[6];
+            for (int k = 0; k < 6; ++k) sc[k] = fabs((double)mt[k]) + cfg.min_scale;
+            double nrm = sc[0] * sc[0];
+            for (int k = 1; k < 6; ++k) nrm = nrm + sc[k] * sc[k];
+            nrm = sqrt(nrm);
+            for (int k = 3; k < 6; ++k) S.ss[k] = (float)(cfg.shape_coef * iou_d * (sc[k] / nrm) + cfg.min_scale);
+            for (int k = 0; k < 3; ++k) S.ss[k] = (float)(cfg.center_coef * iou_d * (sc[k] / nrm) + cfg.min_scale);
+        } else {
+            const float ms = (float)cfg.min_scale;
+            float sc[6];
+            for (int k = 0; k < 6; ++k) sc[k] = fabsf(mt[k]) + ms;
+            float nrm = sc[0] * sc[0];
+            for (int k = 1; k < 6; ++k) nrm = nrm + sc[k] * sc[k];
+            nrm = sqrtf(nrm);
+            for (int k = 3; k < 6; ++k) S.ss[k] = (float)cfg.shape_coef * iou_f * (sc[k] / nrm) + ms;
+            for (int k = 0; k < 3; ++k) S.ss[k] = (float)cfg.center_coef * iou_f * (sc[k] / nrm) + ms;
+        }
+        if (S.prev_success && success) {
+            for (int k = 0; k < 6; ++k) {
+                if (cfg.legacy_promotion)
+                    S.ss[k] = (float)(cfg.beta * (double)S.ss[k] + (1.0 - cfg.beta) * (double)S.prev[k]);
+                else
+                    S.ss[k] = (float)cfg.beta * S.ss[k] + (float)(1.0 - cfg.beta) * S.prev[k];
+            }
+        }
+        if (success) {
+            S.need_update = 1;
+            S.prev_success = 1;
+            S.fails = 0;
+            for (int k = 0; k < 6; ++k) S.x[k] += (double)mt[k];
+            for (int k = 0; k < 6; ++k) S.prev[k] = S.ss[k];
+        } else {
+            S.fails++;
+            S.prev_success = 0;
+        }
+        S.iters_done = it + 1;
+        if (S.fails >= 3) S.stop = 1;
+        for (int k = 0; k < 6; ++k) S.box32[k] = (float)S.x[k];
+        S.flags = G->flags;                       // term kernels may have OR-ed flags in
+        *G = S;
     }
 }
 
+__global__ void __launch_bounds__(64) k_fuse_final(const FuseState* __restrict__ states, int n_jobs,
+                                                   float* __restrict__ out_box,
+                                                   int32_t* __restrict__ out_updated,
+                                                   int32_t* __restrict__ out_iters,
+                                                   int32_t* __restrict__ status) {
+    const int job = blockIdx.x * blockDim.x + threadIdx.x;
+    if (job >= n_jobs) return;
+    FuseState S = states[job];
+    for (int k = 3; k < 6; ++k)
+        if (S.x[k] < 0.01) S.x[k] = 0.01;
+    for (int k = 0; k < 6; ++k) out_box[6 * job + k] = (float)S.x[k];
+    out_updated[job] = S.need_update;
+    out_iters[job] = S.iters_done;
+    if (S.flags) atomicOr(status, S.flags);
+}
+
+BF_API size_t bf_fusion_fit_workspace_size(int n_jobs, int max_views, int pst_size) {
+    if (n_jobs <= 0 || max_views <= 0 || pst_size <= 0) return 0;
+    const size_t st = ((size_t)n_jobs * sizeof(FuseState) + 255) & ~(size_t)255;
+    return st + (size_t)n_jobs * max_views * pst_size * sizeof(float);
+}
+
 BF_API int bf_fusion_fit(const int32_t* view_off, const int32_t* n_views, int n_jobs,
-                         const float* view_box, const float* view_R, const float* view_score,
-                         const float* view_pose, const float* view_tc, const float* pst,
-                         const bf_fuse_cfg* cfg, float* out_box, int32_t* out_updated,
-                         int32_t* out_iters, float* trace, int32_t* status, void* stream) {
+                         int max_views, const float* view_box, const float* view_R,
+                         const float* view_score, const float* view_pose, const float* view_tc,
+                         const float* pst, const bf_fuse_cfg* cfg, float* out_box,
+                         int32_t* out_updated, int32_t* out_iters, float* trace,
+                         int32_t* status, void* workspace, void* stream) {
     if (!cfg || n_jobs < 0) return BF_ERR_ARG;
     if (n_jobs == 0) return BF_OK;
     if (!view_off || !n_views || !view_box || !view_R || !view_score || !view_pose || !view_tc ||
-        !pst || !out_box || !out_updated || !out_iters || !status)
+        !pst || !out_box || !out_updated || !out_iters || !status || !workspace)
         return BF_ERR_ARG;
+    if (max_views <= 0 || max_views > FUSE_MAX_VIEWS) return BF_ERR_CAPACITY;
     if (cfg->pst_size <= 0 || cfg->pst_size > FUSE_MAX_PST || (cfg->pst_size % 64) != 0)
         return BF_ERR_CAPACITY;
-    hipLaunchKernelGGL(k_fuse, dim3(n_jobs), dim3(cfg->pst_size), 0, bf_stream(stream), view_off,
-                       n_views, view_box, view_R, view_score, view_pose, view_tc, pst, *cfg,
-                       out_box, out_updated, out_iters, trace, status);
+    hipStream_t s = bf_stream(stream);
+    FuseState* states = reinterpret_cast<FuseState*>(workspace);
+    const size_t st = ((size_t)n_jobs * sizeof(FuseState) + 255) & ~(size_t)255;
+    float* terms = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + st);
+    const int P = cfg->pst_size;
+    hipLaunchKernelGGL(k_fuse_init, dim3(n_jobs), dim3(64), 0, s, view_off, n_views, max_views,
+                       view_box, view_R, view_score, *cfg, states);
+    const dim3 tgrid((unsigned)bf_cdiv(max_views * P, TERM_THREADS), (unsigned)n_jobs);
+    for (int it = 0; it < cfg->iters; ++it) {
+        hipLaunchKernelGGL(k_fuse_terms, tgrid, dim3(TERM_THREADS), 0, s, view_pose, view_tc, pst,
+                           *cfg, states, terms, max_views);
+        hipLaunchKernelGGL(k_fuse_step, dim3(n_jobs), dim3(P), 0, s, pst, *cfg, states, terms,
+                           max_views, it, trace);
+    }
+    hipLaunchKernelGGL(k_fuse_final, dim3(bf_cdiv(n_jobs, 64)), dim3(64), 0, s, states, n_jobs,
+                       out_box, out_updated, out_iters, status);
     return bf_check_launch();
 }

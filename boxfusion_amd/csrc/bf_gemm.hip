@@ -39,12 +39,12 @@ __device__ __forceinline__ u16 f2bf(float f) {
 // output rounding): one v_rcp, one v_exp and a handful of FMAs instead of the library erff.
 __device__ __forceinline__ float erf_as(float x) {
     const float a = fabsf(x);
-    const float t = __frcp_rn(fmaf(0.3275911f, a, 1.0f));
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.0f));   // v_rcp_f32 (1 ulp)
     float p = fmaf(1.061405429f, t, -1.453152027f);
     p = fmaf(p, t, 1.421413741f);
     p = fmaf(p, t, -0.284496736f);
     p = fmaf(p, t, 0.254829592f);
-    const float y = 1.0f - p * t * __expf(-a * a);
+    const float y = 1.0f - p * t * __builtin_amdgcn_exp2f(-a * a * 1.4426950408889634f);
     return copysignf(y, x);
 }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_as(x * 0.70710678118654752f)); }

@@ -19,6 +19,9 @@ flag, default on as in the reference).
 """
 from __future__ import annotations
 
+import queue
+import threading
+
 import numpy as np
 import torch
 
@@ -117,3 +120,48 @@ class FusionStage:
             return np.zeros((0, 6), np.float32), np.zeros((0, 3, 3), np.float32)
         b = self.all_pred_box.pred_boxes_3d
         return b.tensor.cpu().numpy(), b.R.cpu().numpy()
+
+
+class AsyncFusion:
+    """Runs a FusionStage on a worker thread with its own HIP stream, so the serial keyframe
+    state machine of keyframes k overlaps the (independent) detection of later frames on the
+    main stream.  Keyframes are consumed strictly in submission (= frame) order; `make_pred` is
+    called on the worker, after its stream waited for `ready` (an event on the producer stream),
+    so it may read the producer's buffers."""
+
+    def __init__(self, stage: FusionStage):
+        self.stage = stage
+        self.device_index = stage.dev.index if stage.dev.index is not None else torch.cuda.current_device()
+        self.stream = torch.cuda.Stream(device=self.device_index)
+        self.q = queue.Queue()
+        self.err = None
+        self.thread = threading.Thread(target=self._run, name="boxfusion-fusion", daemon=True)
+        self.thread.start()
+
+    def submit(self, count, pose, make_pred, ready=None):
+        self.q.put((count, pose, make_pred, ready))
+
+    def _run(self):
+        torch.cuda.set_device(self.device_index)
+        with torch.cuda.stream(self.stream):
+            while True:
+                item = self.q.get()
+                if item is None:
+                    return
+                if self.err is not None:
+                    continue
+                count, pose, make_pred, ready = item
+                try:
+                    if ready is not None:
+                        self.stream.wait_event(ready)
+                    self.stage.keyframe(count, pose, make_pred())
+                except BaseException as e:  # noqa: BLE001 - re-raised on join()
+                    self.err = e
+
+    def join(self):
+        self.q.put(None)
+        self.thread.join()
+        self.stream.synchronize()
+        if self.err is not None:
+            raise self.err
+        return self.stage

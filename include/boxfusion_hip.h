@@ -160,12 +160,18 @@ typedef struct {
  *   (per_frame_box.projected_boxes rows).  pst f32[pst_size,6] (row 0 must be zeros).
  *   out_box f32[n_jobs,6]: refined xyzlhw (lhw >= 0.01), only meaningful where out_updated==1.
  *   out_iters i32[n_jobs]: iterations executed.  trace (nullable) f32[n_jobs, iters, pst_size]
- *   receives every iteration's fitness vector. */
-int bf_fusion_fit(const int32_t* view_off, const int32_t* n_views, int n_jobs,
+ *   receives every iteration's fitness vector.  max_views (<= 32) bounds every n_views[j] (a job
+ *   above it is skipped with BF_DEV_VIEW_OVERFLOW); `workspace` holds
+ *   bf_fusion_fit_workspace_size(n_jobs, max_views, pst_size) bytes (per-job state + the
+ *   per-iteration |1 - IoU| terms).  Per iteration: one launch over all (job, view, particle)
+ *   pairs, one launch per job for the sequential update; no host synchronisation. */
+size_t bf_fusion_fit_workspace_size(int n_jobs, int max_views, int pst_size);
+int bf_fusion_fit(const int32_t* view_off, const int32_t* n_views, int n_jobs, int max_views,
                   const float* view_box, const float* view_R, const float* view_score,
                   const float* view_pose, const float* view_tc, const float* pst,
                   const bf_fuse_cfg* cfg, float* out_box, int32_t* out_updated,
-                  int32_t* out_iters, float* trace, int32_t* status, void* stream);
+                  int32_t* out_iters, float* trace, int32_t* status, void* workspace,
+                  void* stream);
 
 /* Single evaluation of the reference fitness kernel (compute_iou_value + evaluate_iou):
  *   box f32[6], R f32[9], views as above (n_views), search_size f32[6] -> fitness f32[pst_size]

@@ -131,3 +131,25 @@ def test_detect_stage_filtered(dev):
         assert (r.categories != "").all()
     xyz, valid = det.last["xyz"][0]
     assert xyz.shape == (480, 640, 3) and valid.float().mean() > 0.9
+
+
+def test_async_fusion_equals_sync(dev):
+    """AsyncFusion (worker thread + side stream) produces exactly the synchronous state."""
+    from boxfusion_amd.fusion_stage import AsyncFusion, FusionStage
+    from boxfusion_amd.pipeline import scene_instances
+    from boxfusion_amd.synthetic import SCANNET_K, Scene
+    cfg = dict(TU.SCANNET_CFG, data=dict(gap=1))
+    scene = Scene(seed=0)
+    sync = FusionStage(cfg, SCANNET_K, device=dev)
+    asyn = AsyncFusion(FusionStage(cfg, SCANNET_K, device=dev))
+    for f in range(30):
+        d = scene.detections(f)
+        sync.keyframe(f, scene.pose(f), scene_instances(d, dev))
+        ev = torch.cuda.Event()
+        ev.record()
+        asyn.submit(f, scene.pose(f), (lambda d=d: scene_instances(d, dev)), ev)
+    st = asyn.join()
+    assert st.box_manager.fusion_list == sync.box_manager.fusion_list
+    assert st.box_manager.already_fusion == sync.box_manager.already_fusion
+    np.testing.assert_array_equal(st.boxes()[0], sync.boxes()[0])
+    assert st.stats == sync.stats
