@@ -239,6 +239,198 @@ __global__ void __launch_bounds__(G_THREADS, 2) k_gemm(const u16* __restrict__ A
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// 256x256 tile, 8 waves (2 M x 4 N, 128x64 per wave = 4x2 v_mfma_f32_32x32x16_bf16 tiles),
+// BK = 64, two 64-KiB LDS stages filled by global_load_lds with a prefetch distance of TWO
+// K-tiles: tile t+2 is issued into tile t's stage as soon as every wave has read tile t into
+// registers, so the loads overlap two tiles of MFMA work.  The stage's fragments are read in two
+// k-halves (48 VGPRs each) so 128 accumulators + operands fit the 256-register budget of two
+// waves per SIMD.  Waits are counted (vmcnt(8) keeps the younger tile in flight) and barriers are
+// raw s_barrier, so no barrier drains the prefetch.
+// ------------------------------------------------------------------------------------------
+#define G2_THREADS 512
+#define G2_LDS (2 * 65536)
+#define CBAR() asm volatile("" ::: "memory")
+#define RAW_BARRIER() do { CBAR(); __builtin_amdgcn_s_barrier(); CBAR(); } while (0)
+
+template <bool OUT_BF16, int ACT>
+__global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict__ A, int lda,
+                                                           const u16* __restrict__ W, int ldw,
+                                                           const float* __restrict__ bias,
+                                                           const float* __restrict__ resid, int ldr,
+                                                           int resid_mod, void* __restrict__ Cv,
+                                                           int ldc, const int32_t* __restrict__ row_map,
+                                                           int M, int N, int K, int tiles_n,
+                                                           int tiles_m) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char g_smem[];
+    const int t = threadIdx.x;
+    const int lane = t & 63, wave = t >> 6;
+    const int nwg = tiles_m * tiles_n;
+    int bid = blockIdx.x;
+    {
+        const int xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    }
+    const int tm = bid / tiles_n, tn = bid % tiles_n;
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int wr = wave >> 2, wc = wave & 3;
+    const int fr = lane & 31, fh = lane >> 5;
+
+    // staging: stage s = [A 256x64 | W 256x64] at s*64K; wave w fills rows 32w..32w+31 of both
+    const u16* ga[4];
+    const u16* gw[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = (wave * 4 + i) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ (r & 7);
+        ga[i] = A + (size_t)min(m0 + r, M - 1) * lda + c * 8;
+        gw[i] = W + (size_t)min(n0 + r, N - 1) * ldw + c * 8;
+    }
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+#define G2_STAGE(stage, k0)                                                                      \
+    {                                                                                            \
+        unsigned char* sa_ = g_smem + (stage) * 65536 + wave * 4096;                             \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                          \
+            __builtin_amdgcn_global_load_lds((const void*)(ga[i] + (k0)),                        \
+                                             (lds_ptr_t)(sa_ + i * 1024), 16, 0, 0);             \
+            __builtin_amdgcn_global_load_lds((const void*)(gw[i] + (k0)),                        \
+                                             (lds_ptr_t)(sa_ + 32768 + i * 1024), 16, 0, 0);     \
+        }                                                                                        \
+    }
+
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    const int nk = K / GB_K;
+    G2_STAGE(0, 0);
+    if (nk > 1) G2_STAGE(1, GB_K);
+    for (int kt = 0; kt < nk; ++kt) {
+        const int st = kt & 1;
+        // tile kt landed: 8 glds per thread per tile; the younger tile (kt+1) may stay in flight
+        if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        RAW_BARRIER();
+        const unsigned char* sa = g_smem + st * 65536;
+        const unsigned char* sw = sa + 32768;
+        bf16x8 af[4][2], bfr[2][2];
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                const int ks = half * 2 + kk;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    af[i][kk] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + i * 32 + fr, ks * 2 + fh));
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    bfr[j][kk] = *reinterpret_cast<const bf16x8*>(sw + swz(wc * 64 + j * 32 + fr, ks * 2 + fh));
+            }
+            if (half == 1) {
+                // every wave has this stage in registers: refill it with tile kt+2
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                RAW_BARRIER();
+                if (kt + 2 < nk) G2_STAGE(st, (kt + 2) * GB_K);
+            }
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][kk], bfr[j][kk], acc[i][j], 0, 0, 0);
+        }
+    }
+#undef G2_STAGE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    // ---- epilogue: two passes of 128 rows through LDS ([128][256] f32, column XOR-swizzled) ---
+    float* T = reinterpret_cast<float*>(g_smem);
+    constexpr int CW = OUT_BF16 ? 8 : 4;
+    constexpr int CPR = 256 / CW;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+        RAW_BARRIER();   // LDS free (last tile's reads / previous pass's row reads done)
+        if (wr == pass) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int nl = wc * 64 + j * 32 + fr;
+                const float bv = (bias && n0 + nl < N) ? bias[min(n0 + nl, N - 1)] : 0.f;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) {
+                        const int ml = i * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh;
+                        float v = acc[i][j][e] + bv;
+                        if (ACT == 1) v = gelu_erf(v);
+                        else if (ACT == 2) v = fmaxf(v, 0.f);
+                        T[ml * 256 + (nl ^ (((ml >> 2) & 1) << 5))] = v;
+                    }
+            }
+        }
+        RAW_BARRIER();
+#pragma unroll 4
+        for (int id = t; id < 128 * CPR; id += G2_THREADS) {
+            const int ml = id / CPR, cl = (id % CPR) * CW;
+            const int m = m0 + pass * 128 + ml, n = n0 + cl;
+            if (m >= M || n >= N) continue;
+            const int orow = row_map ? row_map[m] : m;
+            if (orow < 0) continue;
+            const int sw = ((ml >> 2) & 1) << 5;
+            float v[CW];
+#pragma unroll
+            for (int q = 0; q < CW; q += 4) {
+                const float4 x = *reinterpret_cast<const float4*>(T + ml * 256 + ((cl + q) ^ sw));
+                v[q] = x.x; v[q + 1] = x.y; v[q + 2] = x.z; v[q + 3] = x.w;
+            }
+            if (resid) {
+                const int rrow = resid_mod > 0 ? (m % resid_mod) : orow;
+                const float* rp = resid + (size_t)rrow * ldr + n;
+#pragma unroll
+                for (int q = 0; q < CW; q += 4) {
+                    const float4 x = *reinterpret_cast<const float4*>(rp + q);
+                    v[q] += x.x; v[q + 1] += x.y; v[q + 2] += x.z; v[q + 3] += x.w;
+                }
+            }
+            if (OUT_BF16) {
+                U128 o;
+                o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+                o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+                o.z = (uint32_t)f2bf(v[4 % CW]) | ((uint32_t)f2bf(v[5 % CW]) << 16);
+                o.w = (uint32_t)f2bf(v[6 % CW]) | ((uint32_t)f2bf(v[7 % CW]) << 16);
+                *reinterpret_cast<U128*>(reinterpret_cast<u16*>(Cv) + (size_t)orow * ldc + n) = o;
+            } else {
+                *reinterpret_cast<float4*>(reinterpret_cast<float*>(Cv) + (size_t)orow * ldc + n) =
+                    make_float4(v[0], v[1], v[2], v[3]);
+            }
+        }
+    }
+}
+
+template <bool OB, int AC>
+static void launch_gemm256(dim3 grid, hipStream_t st, const void* A, int lda, const void* W, int ldw,
+                           const float* bias, const float* resid, int ldr, int resid_mod, void* C,
+                           int ldc, const int32_t* row_map, int M, int N, int K, int tiles_n,
+                           int tiles_m) {
+    static bool attr = false;
+    if (!attr) {
+        hipFuncSetAttribute((const void*)k_gemm256<OB, AC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            G2_LDS);
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_gemm256<OB, AC>), grid, dim3(G2_THREADS), G2_LDS, st, (const u16*)A, lda,
+                       (const u16*)W, ldw, bias, resid, ldr, resid_mod, C, ldc, row_map, M, N, K,
+                       tiles_n, tiles_m);
+}
+
+static int g_force_small = 0;
+// test hook: 1 forces the 128x128 kernel for every shape (both kernels stay covered by tests)
+BF_API void bf_gemm_force_small_tiles(int on) { g_force_small = on; }
+
 BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bias,
                         const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
                         const int32_t* row_map, int M, int N, int K, int act, void* stream) {
@@ -253,6 +445,23 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
     const int cw = c_bf16 ? 8 : 4;
     const int vec_epi = (N % cw == 0) && ((uintptr_t)C % 16 == 0) && ((size_t)ldc * (c_bf16 ? 2 : 4) % 16 == 0) &&
                         (!resid || (((uintptr_t)resid % 16 == 0) && (ldr % 4 == 0)));
+    // large problems: the 256x256 8-wave kernel (needs the row-chunk epilogue)
+    const int t2m = (M + 255) / 256, t2n = (N + 255) / 256;
+    if (vec_epi && N >= 512 && t2m * t2n >= 128 && !g_force_small) {
+#define GEMM2(OB, AC) launch_gemm256<OB, AC>(dim3(t2m * t2n), bf_stream(stream), A, lda, W, ldw, bias, \
+                                            resid, ldr, resid_mod, C, ldc, row_map, M, N, K, t2n, t2m)
+        if (c_bf16) {
+            if (act == 0) GEMM2(true, 0);
+            else if (act == 1) GEMM2(true, 1);
+            else GEMM2(true, 2);
+        } else {
+            if (act == 0) GEMM2(false, 0);
+            else if (act == 1) GEMM2(false, 1);
+            else GEMM2(false, 2);
+        }
+#undef GEMM2
+        return bf_check_launch();
+    }
 #define GEMM_LAUNCH(OB, AC)                                                                       \
     hipLaunchKernelGGL((k_gemm<OB, AC>), dim3(nwg), dim3(G_THREADS), lds, bf_stream(stream),       \
                        (const u16*)A, lda, (const u16*)W, ldw, bias, resid, ldr, resid_mod, C, ldc, \

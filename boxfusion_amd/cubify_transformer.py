@@ -39,10 +39,19 @@ class FrameBatch:
     T_gravity: Optional[torch.Tensor]  # [B,3,3]
     image_sizes: List[tuple]       # [(h, w)] before padding
     pad: int = 0                   # square pad size when `image` is not materialised (engine)
+    K_inv: Optional[torch.Tensor] = None   # [B,3,3] precomputed inverse (keeps decode sync-free)
 
     @property
     def sizes_wh(self):
         return [(w, h) for h, w in self.image_sizes]
+
+
+def clamp_xy(b, xmax, ymax):
+    """clamp [..., 2k] x-columns to [0, xmax] and [..., 2k+1] y-columns to [0, ymax] with scalar
+    bounds (same values as clamping against a [0..]/[W, H, ...] tensor; no host->device copy, so
+    the decode stays graph-capturable)."""
+    cols = [b[..., c].clamp(0, xmax if c % 2 == 0 else ymax) for c in range(b.shape[-1])]
+    return torch.stack(cols, -1)
 
 
 def box_cxcywh_to_xyxy(x):
@@ -188,10 +197,7 @@ class DeltaBox2DTransform(nn.Module):
         gxy = pxy + pwh * dxy
         gwh = pwh * dwh.exp()
         b = torch.cat([gxy - gwh * 0.5, gxy + gwh * 0.5], dim=-1)
-        lo = torch.zeros((1, 4), device=boxes.device)
-        hi = torch.tensor([[clamp_shape[1], clamp_shape[0], clamp_shape[1], clamp_shape[0]]],
-                          device=boxes.device)
-        return b.clamp(min=lo, max=hi)
+        return clamp_xy(b, clamp_shape[1], clamp_shape[0])
 
 
 class DeltaBox2DPredictor(nn.Module):
@@ -231,8 +237,7 @@ class AbsoluteBox3DPredictor(nn.Module):
         dims = torch.exp(dims.clip(max=5)) * scale
         cs = state["clamp_shape"]
         pxy = state["pred_boxes"][..., :2] + d2 * state["pred_boxes"][..., 2:]
-        pxy = pxy.clamp(min=torch.zeros((1, 2), device=x.device),
-                        max=torch.tensor([[cs[1], cs[0]]], device=x.device))
+        pxy = clamp_xy(pxy, cs[1], cs[0])
         state.update(pred_proj_xy=pxy, pred_z_unscaled=z, pred_z_scaled=z_scaled, pred_dims=dims,
                      pred_pose=pose)
         return x
@@ -313,8 +318,11 @@ class EncoderProposals(nn.Module):
             props.append(torch.cat((grid, wh), -1).view(B, -1, 4))
         props = torch.cat(props, 1)
         stride0 = self.level_strides[0]
-        img = torch.tensor([w * stride0, h * stride0, w * stride0, h * stride0], device=memory.device)
-        valid = ((props > 0.01 * img) & (props < 0.99 * img)).all(-1, keepdim=True)
+        # (props > 0.01 * img) & (props < 0.99 * img) with img = [W, H, W, H] in f32, per column
+        lim = [(float(np.float32(0.01) * np.float32(v)), float(np.float32(0.99) * np.float32(v)))
+               for v in (w * stride0, h * stride0, w * stride0, h * stride0)]
+        valid = torch.stack([(props[..., c] > lo) & (props[..., c] < hi) for c, (lo, hi) in enumerate(lim)],
+                            -1).all(-1, keepdim=True)
         props = props.masked_fill(~valid, max(h, w) * stride0)
         out_mem = out_mem.masked_fill(~valid, 0.0)
         return self.enc_output_norm(self.enc_output(out_mem)), props
@@ -403,8 +411,7 @@ class CubifyTransformer(nn.Module):
         self_mask = torch.ones((n, n), dtype=torch.bool, device=feat.device)
         self_mask[:2, :2] = False
         self_mask[2:, 2:] = False
-        box_mask = torch.cat([torch.zeros(2, dtype=torch.bool, device=feat.device),
-                              torch.ones(nq, dtype=torch.bool, device=feat.device)])
+        box_mask = slice(2, None)      # the nq box queries follow the 2 metric queries
         out = query
         for lid, layer in enumerate(self.decoder.layers):
             out = layer(out, qpos, ref_boxes.detach()[:, :, None], src, pos, (h, w), self_mask, box_mask)
@@ -424,7 +431,9 @@ class CubifyTransformer(nn.Module):
             K = batch.K[i][None].expand(st["pred_z_scaled"].shape[1], -1, -1)
             z = st["pred_z_scaled"][i]
             uvz = torch.cat((z * st["pred_proj_xy"][i], z), dim=-1)[..., None]
-            xyz = torch.bmm(torch.linalg.inv(K), uvz)[..., 0]
+            Kinv = (torch.linalg.inv(K) if batch.K_inv is None
+                    else batch.K_inv[i][None].expand(K.shape[0], -1, -1))
+            xyz = torch.bmm(Kinv, uvz)[..., 0]
             pose = st["pred_pose"][i]
             if batch.T_gravity is not None:
                 pose = batch.T_gravity[i][None] @ pose
@@ -440,13 +449,11 @@ class CubifyTransformer(nn.Module):
         r.scores = vals
         r.pred_classes = labels
         boxes = box_cxcywh_to_xyxy(st["pred_boxes"][i])[boxes_i]
-        boxes.clip_(min=torch.tensor([0.0, 0.0, 0.0, 0.0], device=boxes.device),
-                    max=torch.tensor([image_size[1], image_size[0], image_size[1], image_size[0]],
-                                     device=boxes.device))
+        boxes = clamp_xy(boxes, image_size[1], image_size[0])
         r.pred_boxes = boxes
         r.pred_logits = st["pred_logits"][i][boxes_i]
         dims = st["pred_dims"][i][boxes_i]
-        r.pred_boxes_3d = GeneralInstance3DBoxes(torch.cat((xyz[boxes_i], dims[:, [2, 1, 0]]), dim=-1),
+        r.pred_boxes_3d = GeneralInstance3DBoxes(torch.cat((xyz[boxes_i], dims.flip(-1)), dim=-1),
                                                  pose[boxes_i])
         r.object_desc = st["object_desc"][i][boxes_i]
         r.pred_proj_xy = st["pred_proj_xy"][i][boxes_i]

@@ -143,20 +143,35 @@ class CuTREngine:
             _lib.gemm(self.H1[:rows], *blk["fc2"], resid=Xm, out=Xm)
         return Xr.view(B, self.g, self.g, C).permute(0, 3, 1, 2)
 
-    def ray_embedding(self, K, size_wh):
-        key = (tuple(np.asarray(K.cpu(), np.float32).reshape(-1).tolist()), tuple(size_wh))
+    def ray_embedding(self, K_host, size_wh):
+        """CameraRayEmbedding depends only on (K, image size): computed once per camera."""
+        K_host = np.asarray(K_host, np.float32)
+        key = (tuple(K_host.reshape(-1).tolist()), tuple(size_wh))
         if key not in self._pos_cache:
             with torch.no_grad():
-                self._pos_cache[key] = self.model.pos_embedding(K[None].to(self.dev), [size_wh], self.g)[0]
+                K = torch.from_numpy(K_host).to(self.dev)
+                self._pos_cache[key] = self.model.pos_embedding(K[None], [size_wh], self.g)[0]
+        return self._pos_cache[key]
+
+    def positions(self, K_host, image_sizes):
+        key = (np.asarray(K_host, np.float32).tobytes(), tuple(image_sizes))
+        if key not in self._pos_cache:
+            sizes_wh = [(w, h) for h, w in image_sizes]
+            self._pos_cache[key] = torch.stack([self.ray_embedding(K_host[i], sizes_wh[i])
+                                                for i in range(self.B)])
         return self._pos_cache[key]
 
     @torch.no_grad()
-    def __call__(self, img_u8, depth_std, depth_params, K, T_gravity, image_sizes):
+    def __call__(self, img_u8, depth_std, depth_params, K, T_gravity, image_sizes, K_host=None,
+                 K_inv=None):
+        """K: device [B,3,3]; K_host (numpy, same values) keys the ray-embedding cache so the call
+        never reads device memory (graph-capturable once the cache is warm)."""
+        if K_host is None:
+            K_host = K.detach().cpu().numpy()
+        pos = self.positions(K_host, image_sizes)
         feat = self.backbone(img_u8, depth_std)
-        sizes_wh = [(w, h) for h, w in image_sizes]
-        pos = torch.stack([self.ray_embedding(K[i], sizes_wh[i]) for i in range(self.B)])
         batch = FrameBatch(image=None, depth=depth_std, depth_params=depth_params, K=K,
-                           T_gravity=T_gravity, image_sizes=image_sizes, pad=self.P)
+                           T_gravity=T_gravity, image_sizes=image_sizes, pad=self.P, K_inv=K_inv)
         return self.model.decode(feat, batch, pos=pos)
 
 

@@ -212,6 +212,10 @@ int bf_backproject(const float* depth, const float* K, const float* RT, int h, i
 int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bias,
                  const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
                  const int32_t* row_map, int M, int N, int K, int act, void* stream);
+/* Tile selection: large problems (N >= 512, >= 128 tiles of 256x256, 16-B aligned output rows)
+ * run the 256x256 8-wave kernel, the rest the 128x128 4-wave kernel.  Test hook: a non-zero
+ * argument forces the 128x128 kernel for every shape (process-wide). */
+void bf_gemm_force_small_tiles(int on);
 
 /* softmax(Q K^T * scale) V per (batch, head); X(b,h,s,d) at X + b*x_bs + s*x_rs + h*D + d,
  * bf16 in/out, head_dim in {32, 64, 80, 128}.  Replaces vit.py Attention.forward (:170-203,

@@ -59,6 +59,42 @@ def test_gemm_gelu_resid_rowmap(L):
     assert rel_err(o2, r2) < 1e-5
 
 
+@pytest.mark.parametrize("small", [False, True])
+@pytest.mark.parametrize("act,out_bf16,use_resid", [(None, True, False), ("gelu", True, False),
+                                                   (None, False, True), ("relu", False, False)])
+def test_gemm_large_tiles(L, small, act, out_bf16, use_resid):
+    """shapes that select the 256x256 8-wave kernel (and, forced, the 128x128 one): partial
+    M/N tiles, bias, activation, residual + row scatter."""
+    from boxfusion_amd._lib import lib
+    g = torch.Generator(device="cuda").manual_seed(11)
+    M, N, K = 3000, 2816, 320
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g)
+    y = a.float() @ w.float().T + b
+    if act == "gelu":
+        y = F.gelu(y)
+    elif act == "relu":
+        y = F.relu(y)
+    lib().bf_gemm_force_small_tiles(1 if small else 0)
+    try:
+        if use_resid:
+            resid = torch.randn(M + 40, N, device="cuda", generator=g)
+            perm = torch.randperm(M + 40, device="cuda", generator=g)[:M].int()
+            perm[::5] = -1
+            out = resid.clone()
+            L.gemm(a, w, b, act=act, resid=out, out=out, row_map=perm)
+            ref = resid.clone()
+            keep = perm >= 0
+            ref[perm[keep].long()] += y[keep]
+            assert rel_err(out, ref) < 1e-5
+        else:
+            out = L.gemm(a, w, b, act=act, out_dtype=torch.bfloat16 if out_bf16 else torch.float32)
+            assert rel_err(out, y) < (5e-3 if out_bf16 else 1e-5)
+    finally:
+        lib().bf_gemm_force_small_tiles(0)
+
+
 def _attn_ref(q, k, v, B, H, S, D, scale):
     qq = q.float().view(B, S, H, D).transpose(1, 2)
     kk = k.float().view(B, -1, H, D).transpose(1, 2)

@@ -153,3 +153,33 @@ def test_async_fusion_equals_sync(dev):
     assert st.box_manager.already_fusion == sync.box_manager.already_fusion
     np.testing.assert_array_equal(st.boxes()[0], sync.boxes()[0])
     assert st.stats == sync.stats
+
+
+def test_detect_stage_graph_equals_eager(dev):
+    """HIP-graph replay of the detect stage reproduces the eager run on new inputs."""
+    from boxfusion_amd.clip import VisionTransformer
+    from boxfusion_amd.cubify_transformer import make_cubify_transformer
+    from boxfusion_amd.pipeline import DetectStage
+    from boxfusion_amd.synthetic import SCANNET_K, Scene, frame_rgbd
+    torch.manual_seed(0)
+    with torch.device(dev):
+        cutr = make_cubify_transformer(192, True).eval()
+        vis = VisionTransformer(224, 14, 1280, 2, 16, 1024).eval()
+    B = 2
+    kw = dict(crop_source="top", crops_per_frame=4, clip_capacity=8, device=dev)
+    eager = DetectStage(cutr, vis, TU.SCANNET_CFG, B, 480, 640, SCANNET_K, **kw)
+    graph = DetectStage(cutr, vis, TU.SCANNET_CFG, B, 480, 640, SCANNET_K, graph=True, **kw)
+    for start in (0, 5, 9):
+        fr = range(start, start + B)
+        rgb = torch.from_numpy(np.stack([frame_rgbd(f)[0] for f in fr])).to(dev)
+        depth = torch.from_numpy(np.stack([frame_rgbd(f)[1] for f in fr])).to(dev)
+        poses = np.stack([Scene().pose(f) for f in fr])
+        eager(rgb, depth, poses, return_instances=False)
+        graph(rgb, depth, poses, return_instances=False)
+        torch.cuda.synchronize()
+        # library kernels (rocBLAS / hipBLASLt) may pick other algorithms under capture: ulps
+        for a, b in zip(eager.last["clip"][3:], graph.last["clip"][3:]):
+            torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+        for ra, rb in zip(eager.last["res"], graph.last["res"]):
+            torch.testing.assert_close(ra.scores, rb.scores, rtol=1e-4, atol=1e-6)
+            torch.testing.assert_close(ra.pred_boxes_3d.tensor, rb.pred_boxes_3d.tensor, rtol=1e-4, atol=1e-4)
