@@ -39,8 +39,8 @@ __device__ __forceinline__ u16 at_f2bf(float f) {
     return *reinterpret_cast<u16*>(&b);
 }
 
-template <int D>
-__global__ void __launch_bounds__(AT_THREADS) k_attn(const u16* __restrict__ Q, const u16* __restrict__ K,
+template <int D, int NW>   // NW waves of 32 queries per workgroup
+__global__ void __launch_bounds__(NW * 64) k_attn(const u16* __restrict__ Q, const u16* __restrict__ K,
                                                      const u16* __restrict__ V, u16* __restrict__ O,
                                                      int sq, int sk, int q_rs, int k_rs, int v_rs,
                                                      int o_rs, long long q_bs, long long k_bs,
@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(AT_THREADS) k_attn(const u16* __restrict__ Q, 
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int h = blockIdx.y, b = blockIdx.z;
     const int fr = lane & 31, fh = lane >> 5;
-    const int q = blockIdx.x * AT_QT + wave * 32 + fr;  // this lane's query
+    const int q = blockIdx.x * (NW * 32) + wave * 32 + fr;  // this lane's query
     const u16* Qb = Q + b * q_bs + h * D;
     const u16* Kb = K + b * k_bs + h * D;
     const u16* Vb = V + b * v_bs + h * D;
@@ -68,7 +68,7 @@ __global__ void __launch_bounds__(AT_THREADS) k_attn(const u16* __restrict__ Q, 
         qf[ks] = *reinterpret_cast<const bf16x8*>(Qb + (size_t)min(q, sq - 1) * q_rs + 16 * ks + 8 * fh);
     }
     // zero the padded V^T rows once (only matter for D % 32 != 0)
-    for (int i = t; i < (DP - D) * VROW; i += AT_THREADS) sV[D * VROW + i] = 0;
+    for (int i = t; i < (DP - D) * VROW; i += NW * 64) sV[D * VROW + i] = 0;
 
     f32x16 o[DB];
 #pragma unroll
@@ -81,7 +81,7 @@ __global__ void __launch_bounds__(AT_THREADS) k_attn(const u16* __restrict__ Q, 
         __syncthreads();
         // ---- stage K tile (row-major) ------------------------------------------------------
         constexpr int KCH = AT_KT * D / 8;  // 16-B chunks
-        for (int c = t; c < KCH; c += AT_THREADS) {
+        for (int c = t; c < KCH; c += NW * 64) {
             int r = c / (D / 8), cc = c % (D / 8);
             V128 v = *reinterpret_cast<const V128*>(Kb + (size_t)min(k0 + r, sk - 1) * k_rs + cc * 8);
             if (k0 + r >= sk) v.x = v.y = v.z = v.w = 0u;
@@ -89,7 +89,7 @@ __global__ void __launch_bounds__(AT_THREADS) k_attn(const u16* __restrict__ Q, 
         }
         // ---- stage V^T tile: thread handles 4 keys x 8 dims, writes 8 x (4 keys) ------------
         constexpr int VTASK = (AT_KT / 4) * (D / 8);
-        for (int c = t; c < VTASK; c += AT_THREADS) {
+        for (int c = t; c < VTASK; c += NW * 64) {
             int kq = c / (D / 8), dq = c % (D / 8);
             V128 rv[4];
 #pragma unroll
@@ -197,12 +197,17 @@ BF_API int bf_attention_bf16(const void* q, const void* k, const void* v, void* 
                              long long o_bs, float scale, void* stream) {
     if (!q || !k || !v || !o || batch <= 0 || heads <= 0 || sq <= 0 || sk <= 0) return BF_ERR_ARG;
     if ((q_rs | k_rs | v_rs) % 8 != 0 || o_rs % 4 != 0) return BF_ERR_UNSUPPORTED;
-    dim3 grid((sq + AT_QT - 1) / AT_QT, heads, batch);
     const float sl2 = scale * 1.4426950408889634f;
+    // short sequences (CLIP: 257 tokens) run every query of a (batch, head) in ONE workgroup of
+    // ceil(sq/32) waves, so K/V are staged once and no 128-query tile is almost empty
+    const int nw_one = (sq + 31) / 32;
+#define LAUNCH_NW(DD, NWV)                                                                        \
+    hipLaunchKernelGGL((k_attn<DD, NWV>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch),     \
+                       dim3(NWV * 64), 0, bf_stream(stream), (const u16*)q, (const u16*)k,          \
+                       (const u16*)v, (u16*)o, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs,    \
+                       o_bs, sl2)
 #define LAUNCH(DD)                                                                                \
-    hipLaunchKernelGGL(k_attn<DD>, grid, dim3(AT_THREADS), 0, bf_stream(stream), (const u16*)q,    \
-                       (const u16*)k, (const u16*)v, (u16*)o, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs, \
-                       k_bs, v_bs, o_bs, sl2)
+    if (nw_one > 4 && nw_one <= 9) { LAUNCH_NW(DD, 9); } else { LAUNCH_NW(DD, 4); }
     switch (head_dim) {
         case 32: LAUNCH(32); break;
         case 64: LAUNCH(64); break;
@@ -211,5 +216,6 @@ BF_API int bf_attention_bf16(const void* q, const void* k, const void* v, void* 
         default: return BF_ERR_UNSUPPORTED;
     }
 #undef LAUNCH
+#undef LAUNCH_NW
     return bf_check_launch();
 }

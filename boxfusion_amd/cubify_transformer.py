@@ -46,6 +46,31 @@ class FrameBatch:
         return [(w, h) for h, w in self.image_sizes]
 
 
+def conv_patch(conv, x):
+    """Conv2d with kernel == stride and no padding (1x1 projections, 2x2/2 downsamplers) as one
+    matmul over space-to-depth patches: the same contraction as the convolution, without the
+    library's per-shape convolution search (which is unavailable inside a captured graph)."""
+    k = conv.kernel_size[0]
+    if conv.kernel_size != (k, k) or conv.stride != (k, k) or conv.padding != (0, 0) or conv.groups != 1:
+        return conv(x)
+    B, C, H, W = x.shape
+    h, w = H // k, W // k
+    p = x[:, :, :h * k, :w * k].reshape(B, C, h, k, w, k).permute(0, 2, 4, 1, 3, 5).reshape(B * h * w, C * k * k)
+    y = F.linear(p, conv.weight.reshape(conv.out_channels, -1), conv.bias)
+    return y.view(B, h, w, -1).permute(0, 3, 1, 2)
+
+
+def run_seq(seq, x):
+    """nn.Sequential forward with conv_patch for its patch convolutions"""
+    if isinstance(seq, nn.Conv2d):
+        return conv_patch(seq, x)
+    if not isinstance(seq, nn.Sequential):
+        return seq(x)
+    for m in seq:
+        x = conv_patch(m, x) if isinstance(m, nn.Conv2d) else m(x)
+    return x
+
+
 def clamp_xy(b, xmax, ymax):
     """clamp [..., 2k] x-columns to [0, xmax] and [..., 2k+1] y-columns to [0, ymax] with scalar
     bounds (same values as clamping against a [0..]/[W, H, ...] tensor; no host->device copy, so
@@ -304,7 +329,7 @@ class EncoderProposals(nn.Module):
         B, _, C = memory.shape
         h, w = hw
         m = memory.view(B, h, w, C).permute(0, 3, 1, 2)
-        mems = [proj(m) for proj in self.enc_output_proj]
+        mems = [run_seq(proj, m) for proj in self.enc_output_proj]
         out_mem = torch.cat([x.flatten(2).transpose(1, 2) for x in mems], dim=1)
         props = []
         for lvl, x in enumerate(mems):
@@ -390,7 +415,7 @@ class CubifyTransformer(nn.Module):
         B, _, h, w = feat.shape
         if pos is None:
             pos = self.pos_embedding(batch.K, batch.sizes_wh, w)
-        src = self.input_proj[0](feat).flatten(2).transpose(1, 2)
+        src = run_seq(self.input_proj[0], feat).flatten(2).transpose(1, 2)
         pos = pos.flatten(2).transpose(1, 2) + self.level_embed[0].view(1, 1, -1)
         metric, enc = self.prompting.prompters
         clamp_shape = tuple(batch.image.shape[-2:]) if batch.image is not None else (batch.pad, batch.pad)
