@@ -241,12 +241,10 @@ __global__ void __launch_bounds__(G_THREADS, 2) k_gemm(const u16* __restrict__ A
 
 // ------------------------------------------------------------------------------------------
 // 256x256 tile, 8 waves (2 M x 4 N, 128x64 per wave = 4x2 v_mfma_f32_32x32x16_bf16 tiles),
-// BK = 64, two 64-KiB LDS stages filled by global_load_lds with a prefetch distance of TWO
-// K-tiles: tile t+2 is issued into tile t's stage as soon as every wave has read tile t into
-// registers, so the loads overlap two tiles of MFMA work.  The stage's fragments are read in two
-// k-halves (48 VGPRs each) so 128 accumulators + operands fit the 256-register budget of two
-// waves per SIMD.  Waits are counted (vmcnt(8) keeps the younger tile in flight) and barriers are
-// raw s_barrier, so no barrier drains the prefetch.
+// BK = 64, two 64-KiB LDS stages filled by global_load_lds (tile t+2 is issued into tile t's
+// stage as soon as every wave has read it), fragments software-pipelined one k-step ahead in two
+// register sets (128 accumulators + 2x24 operand VGPRs fit the 256-register budget of two waves
+// per SIMD), one raw s_barrier per K-tile.
 // ------------------------------------------------------------------------------------------
 #define G2_THREADS 512
 #define G2_LDS (2 * 65536)
@@ -306,45 +304,48 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
+    // Software pipeline, ONE barrier per K-tile.  Fragments of k-step ks+1 are read while the
+    // MFMAs of ks run (two register sets FA/FB).  At the barrier before the last k-step of tile
+    // kt: (WAR) every wave has read all of stage kt&1, (RAW) tile kt+1 has landed (waited with
+    // vmcnt(0); it was issued one tile earlier).  After it, the last k-step's MFMAs are
+    // interleaved with the refill of stage kt&1 (tile kt+2) and the first reads of tile kt+1.
+    bf16x8 fa0[4], fb0[2], fa1[4], fb1[2];
+#define G2_READ(FA, FB, stage, ks)                                                               \
+    {                                                                                            \
+        const unsigned char* sa_ = g_smem + (stage) * 65536;                                     \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) FA[i] =                                    \
+            *reinterpret_cast<const bf16x8*>(sa_ + swz(wr * 128 + i * 32 + fr, (ks) * 2 + fh));  \
+        _Pragma("unroll") for (int j = 0; j < 2; ++j) FB[j] = *reinterpret_cast<const bf16x8*>(  \
+            sa_ + 32768 + swz(wc * 64 + j * 32 + fr, (ks) * 2 + fh));                            \
+    }
+#define G2_MFMA(FA, FB)                                                                          \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) \
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(FA[i], FB[j], acc[i][j], 0, 0, 0);
+
     const int nk = K / GB_K;
     G2_STAGE(0, 0);
     if (nk > 1) G2_STAGE(1, GB_K);
+    if (nk > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    RAW_BARRIER();
+    G2_READ(fa0, fb0, 0, 0);
     for (int kt = 0; kt < nk; ++kt) {
         const int st = kt & 1;
-        // tile kt landed: 8 glds per thread per tile; the younger tile (kt+1) may stay in flight
-        if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        G2_READ(fa1, fb1, st, 1);
+        G2_MFMA(fa0, fb0);
+        G2_READ(fa0, fb0, st, 2);
+        G2_MFMA(fa1, fb1);
+        G2_READ(fa1, fb1, st, 3);
+        G2_MFMA(fa0, fb0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // tile kt+1 (the only one in flight)
         RAW_BARRIER();
-        const unsigned char* sa = g_smem + st * 65536;
-        const unsigned char* sw = sa + 32768;
-        bf16x8 af[4][2], bfr[2][2];
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-#pragma unroll
-            for (int kk = 0; kk < 2; ++kk) {
-                const int ks = half * 2 + kk;
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    af[i][kk] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + i * 32 + fr, ks * 2 + fh));
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    bfr[j][kk] = *reinterpret_cast<const bf16x8*>(sw + swz(wc * 64 + j * 32 + fr, ks * 2 + fh));
-            }
-            if (half == 1) {
-                // every wave has this stage in registers: refill it with tile kt+2
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                RAW_BARRIER();
-                if (kt + 2 < nk) G2_STAGE(st, (kt + 2) * GB_K);
-            }
-#pragma unroll
-            for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][kk], bfr[j][kk], acc[i][j], 0, 0, 0);
-        }
+        if (kt + 2 < nk) G2_STAGE(st, (kt + 2) * GB_K);
+        if (kt + 1 < nk) G2_READ(fa0, fb0, st ^ 1, 0);
+        G2_MFMA(fa1, fb1);
     }
+#undef G2_READ
+#undef G2_MFMA
 #undef G2_STAGE
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
@@ -445,9 +446,21 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
     const int cw = c_bf16 ? 8 : 4;
     const int vec_epi = (N % cw == 0) && ((uintptr_t)C % 16 == 0) && ((size_t)ldc * (c_bf16 ? 2 : 4) % 16 == 0) &&
                         (!resid || (((uintptr_t)resid % 16 == 0) && (ldr % 4 == 0)));
-    // large problems: the 256x256 8-wave kernel (needs the row-chunk epilogue)
+    // large problems: the 256x256 8-wave kernel (needs the row-chunk epilogue) unless its last
+    // round of tiles leaves clearly more of the chip idle than the 128x128 kernel's would
+    // (1 block/CU for 256x256, 2 blocks/CU for 128x128)
+    static int n_cu = 0;
+    if (n_cu == 0) {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        n_cu = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+                   ? prop.multiProcessorCount : 256;
+    }
     const int t2m = (M + 255) / 256, t2n = (N + 255) / 256;
-    if (vec_epi && N >= 512 && t2m * t2n >= 128 && !g_force_small) {
+    const long long t2 = (long long)t2m * t2n, t1 = (long long)nwg;
+    const double e2 = (double)t2 / (double)(((t2 + n_cu - 1) / n_cu) * n_cu);
+    const double e1 = (double)t1 / (double)(((t1 + 2 * n_cu - 1) / (2 * n_cu)) * 2 * n_cu);
+    if (vec_epi && N >= 512 && t2 >= n_cu / 2 && e2 >= e1 - 0.02 && !g_force_small) {
 #define GEMM2(OB, AC) launch_gemm256<OB, AC>(dim3(t2m * t2n), bf_stream(stream), A, lda, W, ldw, bias, \
                                             resid, ldr, resid_mod, C, ldc, row_map, M, N, K, t2n, t2m)
         if (c_bf16) {
