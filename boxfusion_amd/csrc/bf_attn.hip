@@ -39,7 +39,10 @@ __device__ __forceinline__ u16 at_f2bf(float f) {
     return *reinterpret_cast<u16*>(&b);
 }
 
-template <int D, int NW>   // NW waves of 32 queries per workgroup
+// NW waves of 32 queries per workgroup; NT key tiles resident in LDS at once: NT == 1 streams
+// the keys tile by tile, NT > 1 (short sequences, sk <= 64*NT) stages every key and V^T column
+// of the (batch, head) once and runs the whole key loop without barriers.
+template <int D, int NW, int NT>
 __global__ void __launch_bounds__(NW * 64) k_attn(const u16* __restrict__ Q, const u16* __restrict__ K,
                                                      const u16* __restrict__ V, u16* __restrict__ O,
                                                      int sq, int sk, int q_rs, int k_rs, int v_rs,
@@ -49,8 +52,8 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const u16* __restrict__ Q, con
     constexpr int DB = (D + 31) / 32;     // 32-row blocks of O^T
     constexpr int DP = DB * 32;           // padded head dim (V^T rows)
     constexpr int KROW = D + 8;           // K tile row stride (elements), 16-B aligned, de-banked
-    constexpr int VROW = AT_KT + 8;       // V^T row stride (elements)
-    __shared__ __attribute__((aligned(16))) u16 sK[AT_KT * KROW];
+    constexpr int VROW = NT * AT_KT + 8;  // V^T row stride (elements)
+    __shared__ __attribute__((aligned(16))) u16 sK[NT * AT_KT * KROW];
     __shared__ __attribute__((aligned(16))) u16 sV[DP * VROW];
 
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -78,23 +81,27 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const u16* __restrict__ Q, con
     float m_run = -INFINITY, l_run = 0.f;
 
     for (int k0 = 0; k0 < sk; k0 += AT_KT) {
+      // LDS key offset of this tile: 0 when streaming, k0 when every tile is resident
+      const int kl = (NT == 1) ? 0 : k0;
+      if (NT == 1 || k0 == 0) {
+        const int k0s = (NT == 1) ? k0 : 0;
         __syncthreads();
-        // ---- stage K tile (row-major) ------------------------------------------------------
-        constexpr int KCH = AT_KT * D / 8;  // 16-B chunks
+        // ---- stage K tile(s) (row-major) ---------------------------------------------------
+        constexpr int KCH = NT * AT_KT * D / 8;  // 16-B chunks
         for (int c = t; c < KCH; c += NW * 64) {
             int r = c / (D / 8), cc = c % (D / 8);
-            V128 v = *reinterpret_cast<const V128*>(Kb + (size_t)min(k0 + r, sk - 1) * k_rs + cc * 8);
-            if (k0 + r >= sk) v.x = v.y = v.z = v.w = 0u;
+            V128 v = *reinterpret_cast<const V128*>(Kb + (size_t)min(k0s + r, sk - 1) * k_rs + cc * 8);
+            if (k0s + r >= sk) v.x = v.y = v.z = v.w = 0u;
             *reinterpret_cast<V128*>(sK + r * KROW + cc * 8) = v;
         }
         // ---- stage V^T tile: thread handles 4 keys x 8 dims, writes 8 x (4 keys) ------------
-        constexpr int VTASK = (AT_KT / 4) * (D / 8);
+        constexpr int VTASK = (NT * AT_KT / 4) * (D / 8);
         for (int c = t; c < VTASK; c += NW * 64) {
             int kq = c / (D / 8), dq = c % (D / 8);
             V128 rv[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                int key = k0 + kq * 4 + i;
+                int key = k0s + kq * 4 + i;
                 V128 v = *reinterpret_cast<const V128*>(Vb + (size_t)min(key, sk - 1) * v_rs + dq * 8);
                 if (key >= sk) v.x = v.y = v.z = v.w = 0u;
                 rv[i] = v;
@@ -110,6 +117,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const u16* __restrict__ Q, con
 #undef VT_WORD
         }
         __syncthreads();
+      }
 
         // ---- S^T = K Q^T for two 32-key sub-tiles ------------------------------------------
         f32x16 s[2];
@@ -119,7 +127,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const u16* __restrict__ Q, con
             for (int e = 0; e < 16; ++e) s[sub][e] = 0.f;
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
-                bf16x8 kf = *reinterpret_cast<const bf16x8*>(sK + (sub * 32 + fr) * KROW + 16 * ks + 8 * fh);
+                bf16x8 kf = *reinterpret_cast<const bf16x8*>(sK + (kl + sub * 32 + fr) * KROW + 16 * ks + 8 * fh);
                 s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[sub], 0, 0, 0);
             }
         }
@@ -163,7 +171,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const u16* __restrict__ Q, con
             for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
                 for (int ss = 0; ss < 2; ++ss) {
-                    const int kb = 32 * sub + 16 * ss + 4 * fh;
+                    const int kb = kl + 32 * sub + 16 * ss + 4 * fh;
                     V64 lo = *reinterpret_cast<const V64*>(vrow + kb);
                     V64 hi = *reinterpret_cast<const V64*>(vrow + kb + 8);
                     bf16x8 vf;
@@ -201,21 +209,26 @@ BF_API int bf_attention_bf16(const void* q, const void* k, const void* v, void* 
     // short sequences (CLIP: 257 tokens) run every query of a (batch, head) in ONE workgroup of
     // ceil(sq/32) waves, so K/V are staged once and no 128-query tile is almost empty
     const int nw_one = (sq + 31) / 32;
-#define LAUNCH_NW(DD, NWV)                                                                        \
-    hipLaunchKernelGGL((k_attn<DD, NWV>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch),     \
+#define LAUNCH_NW(DD, NWV, NTV)                                                                   \
+    hipLaunchKernelGGL((k_attn<DD, NWV, NTV>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch), \
                        dim3(NWV * 64), 0, bf_stream(stream), (const u16*)q, (const u16*)k,          \
                        (const u16*)v, (u16*)o, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs,    \
                        o_bs, sl2)
 #define LAUNCH(DD)                                                                                \
-    if (nw_one > 4 && nw_one <= 9) { LAUNCH_NW(DD, 9); } else { LAUNCH_NW(DD, 4); }
+    if (nw_one > 4 && nw_one <= 9 && sk <= 5 * AT_KT) { LAUNCH_NW(DD, 9, 5); }                     \
+    else if (nw_one > 4 && nw_one <= 9) { LAUNCH_NW(DD, 9, 1); }                                  \
+    else { LAUNCH_NW(DD, 4, 1); }
+#define LAUNCH_STREAM(DD)                                                                         \
+    if (nw_one > 4 && nw_one <= 9) { LAUNCH_NW(DD, 9, 1); } else { LAUNCH_NW(DD, 4, 1); }
     switch (head_dim) {
         case 32: LAUNCH(32); break;
         case 64: LAUNCH(64); break;
         case 80: LAUNCH(80); break;
-        case 128: LAUNCH(128); break;
+        case 128: LAUNCH_STREAM(128); break;   // resident K/V would exceed the 160 KiB LDS
         default: return BF_ERR_UNSUPPORTED;
     }
 #undef LAUNCH
+#undef LAUNCH_STREAM
 #undef LAUNCH_NW
     return bf_check_launch();
 }

@@ -104,7 +104,8 @@ def _attn_ref(q, k, v, B, H, S, D, scale):
 
 
 @pytest.mark.parametrize("B,H,S,D", [(9, 12, 512, 64), (2, 12, 1600, 64), (3, 16, 257, 80),
-                                     (2, 8, 302, 32), (1, 4, 70, 128)])
+                                     (2, 8, 302, 32), (1, 4, 70, 128), (2, 4, 200, 64),
+                                     (2, 4, 288, 80), (2, 2, 257, 128)])
 def test_attention(L, B, H, S, D):
     g = torch.Generator(device="cuda").manual_seed(B * S + D)
     qkv = torch.randn(B * S, 3 * H * D, device="cuda", generator=g).bfloat16()
