@@ -50,7 +50,11 @@ __device__ __forceinline__ float erf_as(float x) {
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_as(x * 0.70710678118654752f)); }
 
 // byte offset of 16-B chunk `c` (0..7) of row `r` in a [rows][64 bf16] swizzled tile
-__device__ __forceinline__ int swz(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
+// Two 128-B tile rows share one 256-B LDS bank row, so the XOR key is (r >> 1) & 7: the 16 rows
+// of every ds_read_b128 lane group ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...) then hit 16
+// distinct 16-B slots (conflict-free; the key r & 7 left them 2-way).
+__device__ __forceinline__ int swz_key(int r) { return (r >> 1) & 7; }
+__device__ __forceinline__ int swz(int r, int c) { return r * 128 + ((c ^ swz_key(r)) << 4); }
 
 template <bool OUT_BF16, int ACT>
 __global__ void __launch_bounds__(G_THREADS, 2) k_gemm(const u16* __restrict__ A, int lda,
@@ -79,7 +83,7 @@ __global__ void __launch_bounds__(G_THREADS, 2) k_gemm(const u16* __restrict__ A
     // Direct-to-LDS staging (global_load_lds_dwordx4): one wave-instruction fills 1 KiB = 8 tile
     // rows of 128 B at a wave-uniform LDS base, lane l at +16*l.  The XOR swizzle therefore moves
     // to the per-lane SOURCE address: lane l of the instruction covering rows 8q..8q+7 writes
-    // physical chunk p = l&7 of row r = 8q + (l>>3), which must hold logical chunk p ^ (r&7).
+    // physical chunk p = l&7 of row r = 8q + (l>>3), which must hold logical chunk p ^ key(r).
     // Each wave issues 4 instructions per operand per K-tile (16 KiB per operand per stage).
     // Rows past M / N are clamped to the last row (valid addresses; those outputs are not stored).
     const u16* ga[4];
@@ -87,7 +91,7 @@ __global__ void __launch_bounds__(G_THREADS, 2) k_gemm(const u16* __restrict__ A
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int r = (wave * 4 + i) * 8 + (lane >> 3);
-        const int c = (lane & 7) ^ (r & 7);
+        const int c = (lane & 7) ^ swz_key(r);
         ga[i] = A + (size_t)min(m0 + r, M - 1) * lda + c * 8;
         gw[i] = W + (size_t)min(n0 + r, N - 1) * ldw + c * 8;
     }
@@ -240,14 +244,20 @@ __global__ void __launch_bounds__(G_THREADS, 2) k_gemm(const u16* __restrict__ A
 }
 
 // ------------------------------------------------------------------------------------------
-// 256x256 tile, 8 waves (2 M x 4 N, 128x64 per wave = 4x2 v_mfma_f32_32x32x16_bf16 tiles),
-// BK = 64, two 64-KiB LDS stages filled by global_load_lds (tile t+2 is issued into tile t's
-// stage as soon as every wave has read it), fragments software-pipelined one k-step ahead in two
-// register sets (128 accumulators + 2x24 operand VGPRs fit the 256-register budget of two waves
-// per SIMD), one raw s_barrier per K-tile.
+// Persistent 256x256 kernel: one 512-thread workgroup per CU walks its tiles (round r gives block
+// b the tile r*grid + xcd_slot(b), so 32 consecutive tiles -- one A row panel -- share an XCD's
+// L2).  Per tile: 8 waves (2 M x 4 N), 128x64 per wave = 4x2 v_mfma_f32_32x32x16_bf16 tiles,
+// BK = 64.  The K-tile ring runs ACROSS tiles: two 64-KiB LDS stages filled by global_load_lds,
+// K-tile g+2 (possibly of the next tile) issued into stage g&1 once every wave has read it;
+// fragments software-pipelined one k-step ahead (register sets FA/FB); one raw s_barrier per
+// K-tile.  The epilogue is wave-private (each wave transposes its 128x64 sub-tile 16 rows at a
+// time through its own 4-KiB slice of the remaining 32 KiB of LDS, no block barrier) and runs
+// while the next tile's first two K-tiles are in flight; its global stores drain under the next
+// tile's MFMAs.
 // ------------------------------------------------------------------------------------------
 #define G2_THREADS 512
-#define G2_LDS (2 * 65536)
+#define G2_STAGES_BYTES (2 * 65536)
+#define G2_LDS (G2_STAGES_BYTES + 8 * 4096)
 #define CBAR() asm volatile("" ::: "memory")
 #define RAW_BARRIER() do { CBAR(); __builtin_amdgcn_s_barrier(); CBAR(); } while (0)
 
@@ -263,38 +273,39 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict
     extern __shared__ __attribute__((aligned(16))) unsigned char g_smem[];
     const int t = threadIdx.x;
     const int lane = t & 63, wave = t >> 6;
-    const int nwg = tiles_m * tiles_n;
-    int bid = blockIdx.x;
-    {
-        const int xcd = bid % 8, q = nwg / 8, r = nwg % 8;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
-    }
-    const int tm = bid / tiles_n, tn = bid % tiles_n;
-    const int m0 = tm * 256, n0 = tn * 256;
     const int wr = wave >> 2, wc = wave & 3;
     const int fr = lane & 31, fh = lane >> 5;
+    const int ntiles = tiles_m * tiles_n;
+    const int G = gridDim.x;
+    // XCD-aware slot: blocks b with b % 8 == x share an XCD; give them 32 consecutive tiles
+    const int slot = (G % 8 == 0) ? ((int)blockIdx.x % 8) * (G / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
+    const int my_tiles = ntiles > slot ? (ntiles - slot + G - 1) / G : 0;
+    const int nk = K / GB_K;
+    const int total = my_tiles * nk;             // K-tiles this block walks
+    if (total == 0) return;
 
-    // staging: stage s = [A 256x64 | W 256x64] at s*64K; wave w fills rows 32w..32w+31 of both
-    const u16* ga[4];
-    const u16* gw[4];
+    // per-lane staging coordinates (row within the 256-row operand tile, swizzled 16-B chunk)
+    int srow[4], scol[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int r = (wave * 4 + i) * 8 + (lane >> 3);
-        const int c = (lane & 7) ^ (r & 7);
-        ga[i] = A + (size_t)min(m0 + r, M - 1) * lda + c * 8;
-        gw[i] = W + (size_t)min(n0 + r, N - 1) * ldw + c * 8;
+        srow[i] = (wave * 4 + i) * 8 + (lane >> 3);
+        scol[i] = ((lane & 7) ^ swz_key(srow[i])) * 8;
     }
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
-#define G2_STAGE(stage, k0)                                                                      \
-    {                                                                                            \
-        unsigned char* sa_ = g_smem + (stage) * 65536 + wave * 4096;                             \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                          \
-            __builtin_amdgcn_global_load_lds((const void*)(ga[i] + (k0)),                        \
-                                             (lds_ptr_t)(sa_ + i * 1024), 16, 0, 0);             \
-            __builtin_amdgcn_global_load_lds((const void*)(gw[i] + (k0)),                        \
-                                             (lds_ptr_t)(sa_ + 32768 + i * 1024), 16, 0, 0);     \
-        }                                                                                        \
-    }
+    // issue K-tile g of this block's walk into LDS stage `stage`
+    auto stage_tile = [&](int stage, int g) {
+        const int tile = slot + (g / nk) * G;
+        const int k0 = (g % nk) * GB_K;
+        const int m0 = (tile / tiles_n) * 256, n0 = (tile % tiles_n) * 256;
+        unsigned char* sa = g_smem + stage * 65536 + wave * 4096;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const u16* ga = A + (size_t)min(m0 + srow[i], M - 1) * lda + k0 + scol[i];
+            const u16* gw = W + (size_t)min(n0 + srow[i], N - 1) * ldw + k0 + scol[i];
+            __builtin_amdgcn_global_load_lds((const void*)ga, (lds_ptr_t)(sa + i * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)gw, (lds_ptr_t)(sa + 32768 + i * 1024), 16, 0, 0);
+        }
+    };
 
     f32x16 acc[4][2];
 #pragma unroll
@@ -304,11 +315,6 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-    // Software pipeline, ONE barrier per K-tile.  Fragments of k-step ks+1 are read while the
-    // MFMAs of ks run (two register sets FA/FB).  At the barrier before the last k-step of tile
-    // kt: (WAR) every wave has read all of stage kt&1, (RAW) tile kt+1 has landed (waited with
-    // vmcnt(0); it was issued one tile earlier).  After it, the last k-step's MFMAs are
-    // interleaved with the refill of stage kt&1 (tile kt+2) and the first reads of tile kt+1.
     bf16x8 fa0[4], fb0[2], fa1[4], fb1[2];
 #define G2_READ(FA, FB, stage, ks)                                                               \
     {                                                                                            \
@@ -322,15 +328,16 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict
     _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) \
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(FA[i], FB[j], acc[i][j], 0, 0, 0);
 
-    const int nk = K / GB_K;
-    G2_STAGE(0, 0);
-    if (nk > 1) G2_STAGE(1, GB_K);
-    if (nk > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    stage_tile(0, 0);
+    if (total > 1) stage_tile(1, 1);
+    if (total > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     RAW_BARRIER();
     G2_READ(fa0, fb0, 0, 0);
-    for (int kt = 0; kt < nk; ++kt) {
-        const int st = kt & 1;
+    float* scratch = reinterpret_cast<float*>(g_smem + G2_STAGES_BYTES + wave * 4096);  // [16][64]
+    constexpr int CW = OUT_BF16 ? 8 : 4;            // outputs per 16-B chunk
+    for (int g = 0; g < total; ++g) {
+        const int st = g & 1;
         G2_READ(fa1, fb1, st, 1);
         G2_MFMA(fa0, fb0);
         G2_READ(fa0, fb0, st, 2);
@@ -338,82 +345,94 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict
         G2_READ(fa1, fb1, st, 3);
         G2_MFMA(fa0, fb0);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // tile kt+1 (the only one in flight)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // K-tile g+1 (the only one in flight)
         RAW_BARRIER();
-        if (kt + 2 < nk) G2_STAGE(st, (kt + 2) * GB_K);
-        if (kt + 1 < nk) G2_READ(fa0, fb0, st ^ 1, 0);
+        if (g + 2 < total) stage_tile(st, g + 2);
+        if (g + 1 < total) G2_READ(fa0, fb0, st ^ 1, 0);
         G2_MFMA(fa1, fb1);
+        if (g % nk != nk - 1) continue;
+
+        // ---- epilogue of this tile (wave-private, 16 rows per pass) --------------------------
+        const int tile = slot + (g / nk) * G;
+        const int m0 = (tile / tiles_n) * 256 + wr * 128, n0 = (tile % tiles_n) * 256 + wc * 64;
+        float bv[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int n = n0 + j * 32 + fr;
+            bv[j] = (bias && n < N) ? bias[min(n, N - 1)] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int eh = 0; eh < 2; ++eh) {
+                // rows i*32 + 16*eh + [0,16): accumulator elements e = 8*eh .. 8*eh+7
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const int e = 8 * eh + q;
+                        const int rl = (e & 3) + 8 * ((e >> 2) & 1) + 4 * fh;   // 0..15
+                        float v = acc[i][j][e] + bv[j];
+                        if (ACT == 1) v = gelu_erf(v);
+                        else if (ACT == 2) v = fmaxf(v, 0.f);
+                        scratch[rl * 64 + ((j * 32 + fr) ^ (((rl >> 2) & 1) << 5))] = v;
+                    }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                // 16 rows x 64 columns: CW-wide chunks, 64/CW per row
+#pragma unroll
+                for (int it = 0; it < 16 * (64 / CW) / 64; ++it) {
+                    const int id = it * 64 + lane;
+                    const int rl = id / (64 / CW), cl = (id % (64 / CW)) * CW;
+                    const int m = m0 + i * 32 + 16 * eh + rl, n = n0 + cl;
+                    const int sw = ((rl >> 2) & 1) << 5;
+                    float v[CW];
+#pragma unroll
+                    for (int q = 0; q < CW; q += 4) {
+                        const float4 x = *reinterpret_cast<const float4*>(scratch + rl * 64 + ((cl + q) ^ sw));
+                        v[q] = x.x; v[q + 1] = x.y; v[q + 2] = x.z; v[q + 3] = x.w;
+                    }
+                    if (m < M && n < N) {
+                        const int orow = row_map ? row_map[m] : m;
+                        if (orow >= 0) {
+                            if (resid) {
+                                const int rrow = resid_mod > 0 ? (m % resid_mod) : orow;
+                                const float* rp = resid + (size_t)rrow * ldr + n;
+#pragma unroll
+                                for (int q = 0; q < CW; q += 4) {
+                                    const float4 x = *reinterpret_cast<const float4*>(rp + q);
+                                    v[q] += x.x; v[q + 1] += x.y; v[q + 2] += x.z; v[q + 3] += x.w;
+                                }
+                            }
+                            if (OUT_BF16) {
+                                U128 o;
+                                o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+                                o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+                                o.z = (uint32_t)f2bf(v[4 % CW]) | ((uint32_t)f2bf(v[5 % CW]) << 16);
+                                o.w = (uint32_t)f2bf(v[6 % CW]) | ((uint32_t)f2bf(v[7 % CW]) << 16);
+                                *reinterpret_cast<U128*>(reinterpret_cast<u16*>(Cv) + (size_t)orow * ldc + n) = o;
+                            } else {
+                                *reinterpret_cast<float4*>(reinterpret_cast<float*>(Cv) + (size_t)orow * ldc + n) =
+                                    make_float4(v[0], v[1], v[2], v[3]);
+                            }
+                        }
+                    }
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // scratch reads done before reuse
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
     }
 #undef G2_READ
 #undef G2_MFMA
-#undef G2_STAGE
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-    // ---- epilogue: two passes of 128 rows through LDS ([128][256] f32, column XOR-swizzled) ---
-    float* T = reinterpret_cast<float*>(g_smem);
-    constexpr int CW = OUT_BF16 ? 8 : 4;
-    constexpr int CPR = 256 / CW;
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-        RAW_BARRIER();   // LDS free (last tile's reads / previous pass's row reads done)
-        if (wr == pass) {
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int nl = wc * 64 + j * 32 + fr;
-                const float bv = (bias && n0 + nl < N) ? bias[min(n0 + nl, N - 1)] : 0.f;
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) {
-                        const int ml = i * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh;
-                        float v = acc[i][j][e] + bv;
-                        if (ACT == 1) v = gelu_erf(v);
-                        else if (ACT == 2) v = fmaxf(v, 0.f);
-                        T[ml * 256 + (nl ^ (((ml >> 2) & 1) << 5))] = v;
-                    }
-            }
-        }
-        RAW_BARRIER();
-#pragma unroll 4
-        for (int id = t; id < 128 * CPR; id += G2_THREADS) {
-            const int ml = id / CPR, cl = (id % CPR) * CW;
-            const int m = m0 + pass * 128 + ml, n = n0 + cl;
-            if (m >= M || n >= N) continue;
-            const int orow = row_map ? row_map[m] : m;
-            if (orow < 0) continue;
-            const int sw = ((ml >> 2) & 1) << 5;
-            float v[CW];
-#pragma unroll
-            for (int q = 0; q < CW; q += 4) {
-                const float4 x = *reinterpret_cast<const float4*>(T + ml * 256 + ((cl + q) ^ sw));
-                v[q] = x.x; v[q + 1] = x.y; v[q + 2] = x.z; v[q + 3] = x.w;
-            }
-            if (resid) {
-                const int rrow = resid_mod > 0 ? (m % resid_mod) : orow;
-                const float* rp = resid + (size_t)rrow * ldr + n;
-#pragma unroll
-                for (int q = 0; q < CW; q += 4) {
-                    const float4 x = *reinterpret_cast<const float4*>(rp + q);
-                    v[q] += x.x; v[q + 1] += x.y; v[q + 2] += x.z; v[q + 3] += x.w;
-                }
-            }
-            if (OUT_BF16) {
-                U128 o;
-                o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-                o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-                o.z = (uint32_t)f2bf(v[4 % CW]) | ((uint32_t)f2bf(v[5 % CW]) << 16);
-                o.w = (uint32_t)f2bf(v[6 % CW]) | ((uint32_t)f2bf(v[7 % CW]) << 16);
-                *reinterpret_cast<U128*>(reinterpret_cast<u16*>(Cv) + (size_t)orow * ldc + n) = o;
-            } else {
-                *reinterpret_cast<float4*>(reinterpret_cast<float*>(Cv) + (size_t)orow * ldc + n) =
-                    make_float4(v[0], v[1], v[2], v[3]);
-            }
-        }
-    }
 }
 
 template <bool OB, int AC>
-static void launch_gemm256(dim3 grid, hipStream_t st, const void* A, int lda, const void* W, int ldw,
+static void launch_gemm256(int grid, hipStream_t st, const void* A, int lda, const void* W, int ldw,
                            const float* bias, const float* resid, int ldr, int resid_mod, void* C,
                            int ldc, const int32_t* row_map, int M, int N, int K, int tiles_n,
                            int tiles_m) {
@@ -423,7 +442,7 @@ static void launch_gemm256(dim3 grid, hipStream_t st, const void* A, int lda, co
                             G2_LDS);
         attr = true;
     }
-    hipLaunchKernelGGL((k_gemm256<OB, AC>), grid, dim3(G2_THREADS), G2_LDS, st, (const u16*)A, lda,
+    hipLaunchKernelGGL((k_gemm256<OB, AC>), dim3(grid), dim3(G2_THREADS), G2_LDS, st, (const u16*)A, lda,
                        (const u16*)W, ldw, bias, resid, ldr, resid_mod, C, ldc, row_map, M, N, K,
                        tiles_n, tiles_m);
 }
@@ -464,7 +483,8 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
     // K>=4096: its fixed prologue/epilogue is amortised over more k-steps)
     const double adv = 1.0 + 0.2 * (double)(K < 4096 ? K : 4096) / 4096.0;
     if (vec_epi && N >= 512 && t2 >= n_cu / 2 && e2 * adv >= e1 && !g_force_small) {
-#define GEMM2(OB, AC) launch_gemm256<OB, AC>(dim3(t2m * t2n), bf_stream(stream), A, lda, W, ldw, bias, \
+        const int grid2 = (int)(t2 < n_cu ? t2 : n_cu);   // persistent: one workgroup per CU
+#define GEMM2(OB, AC) launch_gemm256<OB, AC>(grid2, bf_stream(stream), A, lda, W, ldw, bias, \
                                             resid, ldr, resid_mod, C, ldc, row_map, M, N, K, t2n, t2m)
         if (c_bf16) {
             if (act == 0) GEMM2(true, 0);

@@ -60,14 +60,16 @@ def test_gemm_gelu_resid_rowmap(L):
 
 
 @pytest.mark.parametrize("small", [False, True])
+@pytest.mark.parametrize("shape", [(3000, 2816, 320), (8292, 4352, 192), (8292, 4352, 64)])
 @pytest.mark.parametrize("act,out_bf16,use_resid", [(None, True, False), ("gelu", True, False),
                                                    (None, False, True), ("relu", False, False)])
-def test_gemm_large_tiles(L, small, act, out_bf16, use_resid):
-    """shapes that select the 256x256 8-wave kernel (and, forced, the 128x128 one): partial
-    M/N tiles, bias, activation, residual + row scatter."""
+def test_gemm_large_tiles(L, small, shape, act, out_bf16, use_resid):
+    """shapes that select the persistent 256x256 8-wave kernel (and, forced, the 128x128 one):
+    fewer / more tiles than CUs (the K-tile ring crosses tiles), a single K-tile, partial M/N
+    tiles, bias, activation, residual + row scatter."""
     from boxfusion_amd._lib import lib
     g = torch.Generator(device="cuda").manual_seed(11)
-    M, N, K = 3000, 2816, 320
+    M, N, K = shape
     a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
     w = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).bfloat16()
     b = torch.randn(N, device="cuda", generator=g)
