@@ -49,6 +49,31 @@ __device__ __forceinline__ float erf_as(float x) {
 }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_as(x * 0.70710678118654752f)); }
 
+// the same GELU on two values with packed f32 VALU ops (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32
+// on gfx950): identical arithmetic per component, half the issue slots in the epilogue
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
+    const f32x2 z = x * 0.70710678118654752f;
+    const f32x2 a = __builtin_elementwise_abs(z);
+    const f32x2 d = 0.3275911f * a + 1.0f;
+    f32x2 tt;
+    tt.x = __builtin_amdgcn_rcpf(d.x);
+    tt.y = __builtin_amdgcn_rcpf(d.y);
+    f32x2 p = 1.061405429f * tt - 1.453152027f;
+    p = p * tt + 1.421413741f;
+    p = p * tt - 0.284496736f;
+    p = p * tt + 0.254829592f;
+    const f32x2 q = -a * a * 1.4426950408889634f;
+    f32x2 ex;
+    ex.x = __builtin_amdgcn_exp2f(q.x);
+    ex.y = __builtin_amdgcn_exp2f(q.y);
+    const f32x2 y = 1.0f - p * tt * ex;
+    f32x2 er;
+    er.x = copysignf(y.x, z.x);
+    er.y = copysignf(y.y, z.y);
+    return 0.5f * x * (1.0f + er);
+}
+
 // byte offset of 16-B chunk `c` (0..7) of row `r` in a [rows][64 bf16] swizzled tile
 // Two 128-B tile rows share one 256-B LDS bank row, so the XOR key is (r >> 1) & 7: the 16 rows
 // of every ds_read_b128 lane group ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...) then hit 16
@@ -347,9 +372,33 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // K-tile g+1 (the only one in flight)
         RAW_BARRIER();
-        if (g + 2 < total) stage_tile(st, g + 2);
-        if (g + 1 < total) G2_READ(fa0, fb0, st ^ 1, 0);
-        G2_MFMA(fa1, fb1);
+        // last k-step: each of the 8 MFMAs carries one LDS-DMA issue of K-tile g+2 and one
+        // fragment read of K-tile g+1, pinned in that order (an issue hides under an MFMA).
+        // Unconditional (clamped): past the end they refill / re-read a stage nothing reads.
+        {
+            const int gn = min(g + 2, total - 1);
+            const int tile_n = slot + (gn / nk) * G;
+            const int k0n = (gn % nk) * GB_K;
+            const int m0n = (tile_n / tiles_n) * 256, n0n = (tile_n % tiles_n) * 256;
+            unsigned char* sa_n = g_smem + st * 65536 + wave * 4096;
+            const unsigned char* sr = g_smem + (st ^ 1) * 65536;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int i = q >> 1, j = q & 1;
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa1[i], fb1[j], acc[i][j], 0, 0, 0);
+                const int si = q >> 1;
+                if ((q & 1) == 0) {
+                    const u16* ga = A + (size_t)min(m0n + srow[si], M - 1) * lda + k0n + scol[si];
+                    __builtin_amdgcn_global_load_lds((const void*)ga, (lds_ptr_t)(sa_n + si * 1024), 16, 0, 0);
+                } else {
+                    const u16* gw = W + (size_t)min(n0n + srow[si], N - 1) * ldw + k0n + scol[si];
+                    __builtin_amdgcn_global_load_lds((const void*)gw, (lds_ptr_t)(sa_n + 32768 + si * 1024), 16, 0, 0);
+                }
+                if (q < 4) fa0[q] = *reinterpret_cast<const bf16x8*>(sr + swz(wr * 128 + q * 32 + fr, fh));
+                else if (q < 6) fb0[q - 4] = *reinterpret_cast<const bf16x8*>(sr + 32768 + swz(wc * 64 + (q - 4) * 32 + fr, fh));
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
         if (g % nk != nk - 1) continue;
 
         // ---- epilogue of this tile (wave-private, 16 rows per pass) --------------------------
@@ -369,13 +418,16 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
 #pragma unroll
-                    for (int q = 0; q < 8; ++q) {
+                    for (int q = 0; q < 8; q += 2) {
                         const int e = 8 * eh + q;
-                        const int rl = (e & 3) + 8 * ((e >> 2) & 1) + 4 * fh;   // 0..15
-                        float v = acc[i][j][e] + bv[j];
-                        if (ACT == 1) v = gelu_erf(v);
-                        else if (ACT == 2) v = fmaxf(v, 0.f);
-                        scratch[rl * 64 + ((j * 32 + fr) ^ (((rl >> 2) & 1) << 5))] = v;
+                        f32x2 v2 = {acc[i][j][e] + bv[j], acc[i][j][e + 1] + bv[j]};
+                        if (ACT == 1) v2 = gelu_erf2(v2);
+                        else if (ACT == 2) { v2.x = fmaxf(v2.x, 0.f); v2.y = fmaxf(v2.y, 0.f); }
+#pragma unroll
+                        for (int u = 0; u < 2; ++u) {
+                            const int rl = ((e + u) & 3) + 8 * (((e + u) >> 2) & 1) + 4 * fh;   // 0..15
+                            scratch[rl * 64 + ((j * 32 + fr) ^ (((rl >> 2) & 1) << 5))] = u ? v2.y : v2.x;
+                        }
                     }
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 // 16 rows x 64 columns: CW-wide chunks, 64/CW per row
@@ -427,6 +479,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict
 #pragma unroll
                 for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outstanding at exit
 #undef G2_READ
 #undef G2_MFMA
 }
