@@ -192,6 +192,19 @@ def cpu_baseline(cutr, clip_vis, args, scene):
                        f"0..{args.cpu_fusion_frames - 1} ({1e3 * t_fuse:.1f} ms/frame)")}
 
 
+def load_pmc_traffic():
+    """HBM-side bytes per launch of the roofline kernel from the committed PMC passes
+    (profiles/*_pmc_gelu_gemm.json, newest round); counters cannot be read from inside the run."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_gelu_gemm.json")))
+    if not files:
+        return {}
+    with open(files[-1]) as f:
+        d = json.load(f)
+    d["source"] = os.path.relpath(files[-1], ROOT) + " (FETCH_SIZE x2 + WRITE_SIZE, separate --pmc passes)"
+    return d
+
+
 # ------------------------------------------------------------------------------------------------
 def main():
     args = parse()
@@ -318,6 +331,7 @@ def main():
 
     if rank == 0:
         achieved = ks["tflops"] if ks["launches"] else 0.0
+        pmc = load_pmc_traffic()
         line = {
             "metric": "RGB-D frames/sec (whole node) on 640x480 stream",
             "value": frames / dt, "unit": "frames/s", "n_gpus": N, "steps": args.steps,
@@ -332,7 +346,8 @@ def main():
                        "global_boxes": len(fusion.all_pred_box) if fusion.all_pred_box is not None else 0},
             "roofline": {"bound": "mfma", "kernel": "k_gemm<true,1> (bf16 GEMM + bias + GELU, MLP up-projection)",
                          "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_BF16_TFLOPS, "traffic": None,
+                         "frac": achieved / PEAK_BF16_TFLOPS, "traffic": pmc.get("bytes_per_launch"),
+                         "traffic_source": pmc.get("source"),
                          "launches": ks["launches"], "avg_us": ks.get("avg_us", 0.0),
                          "flops_per_launch": ks["flops"] / max(ks["launches"], 1),
                          "measured": ks["source"]},
