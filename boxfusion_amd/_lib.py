@@ -357,8 +357,10 @@ class KernelTimer:
     dominant kernel): records (flops, start, end) for every bf_gemm_bf16 launch whose output
     dtype / activation match while active."""
 
-    def __init__(self, out_bf16=True, act="gelu"):
+    def __init__(self, out_bf16=True, act="gelu", large_tiles=None):
+        """large_tiles: True / False restricts to launches of k_gemm256 / k_gemm (None: both)."""
         self.out_bf16, self.act = out_bf16, ACT[act]
+        self.large_tiles = large_tiles
         self.records = []
         self.active = False
 
@@ -395,10 +397,13 @@ def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype
     ob = (out.dtype if out is not None else out_dtype) == torch.bfloat16
     if ob != t.out_bf16 or ACT[act] != t.act:
         return _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m)
+    M = a.shape[0] if m is None else m
+    if t.large_tiles is not None and bool(lib().bf_gemm_large_tiles(c_int(M), c_int(w.shape[0]),
+                                                                     c_int(w.shape[1]))) != t.large_tiles:
+        return _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     r = _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m)
     e.record()
-    M = a.shape[0] if m is None else m
     t.records.append((2.0 * M * w.shape[0] * w.shape[1], s, e))
     return r

@@ -504,6 +504,33 @@ static int g_force_small = 0;
 // test hook: 1 forces the 128x128 kernel for every shape (both kernels stay covered by tests)
 BF_API void bf_gemm_force_small_tiles(int on) { g_force_small = on; }
 
+static int gemm_cu_count() {
+    static int n_cu = 0;
+    if (n_cu == 0) {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        n_cu = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+                   ? prop.multiProcessorCount : 256;
+    }
+    return n_cu;
+}
+
+// Large problems run the persistent 256x256 kernel unless its last round of tiles leaves clearly
+// more of the chip idle than the 128x128 kernel's would (1 block/CU vs 2 blocks/CU); the per-tile
+// advantage of the 256x256 kernel grows with K (measured ~1.04x at K=768, ~1.2x at K>=4096).
+static bool gemm_large_tiles(int M, int N, int K) {
+    const int n_cu = gemm_cu_count();
+    const long long t2 = (long long)((M + 255) / 256) * ((N + 255) / 256);
+    const long long t1 = (long long)((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N);
+    const double e2 = (double)t2 / (double)(((t2 + n_cu - 1) / n_cu) * n_cu);
+    const double e1 = (double)t1 / (double)(((t1 + 2 * n_cu - 1) / (2 * n_cu)) * 2 * n_cu);
+    const double adv = 1.0 + 0.2 * (double)(K < 4096 ? K : 4096) / 4096.0;
+    return N >= 512 && t2 >= n_cu / 2 && e2 * adv >= e1;
+}
+
+// which kernel bf_gemm_bf16 runs for an aligned problem of this shape (1 = 256x256 persistent)
+BF_API int bf_gemm_large_tiles(int M, int N, int K) { return gemm_large_tiles(M, N, K) && !g_force_small ? 1 : 0; }
+
 BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bias,
                         const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
                         const int32_t* row_map, int M, int N, int K, int act, void* stream) {
@@ -518,24 +545,10 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
     const int cw = c_bf16 ? 8 : 4;
     const int vec_epi = (N % cw == 0) && ((uintptr_t)C % 16 == 0) && ((size_t)ldc * (c_bf16 ? 2 : 4) % 16 == 0) &&
                         (!resid || (((uintptr_t)resid % 16 == 0) && (ldr % 4 == 0)));
-    // large problems: the 256x256 8-wave kernel (needs the row-chunk epilogue) unless its last
-    // round of tiles leaves clearly more of the chip idle than the 128x128 kernel's would
-    // (1 block/CU for 256x256, 2 blocks/CU for 128x128)
-    static int n_cu = 0;
-    if (n_cu == 0) {
-        int dev = 0;
-        hipDeviceProp_t prop;
-        n_cu = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-                   ? prop.multiProcessorCount : 256;
-    }
     const int t2m = (M + 255) / 256, t2n = (N + 255) / 256;
-    const long long t2 = (long long)t2m * t2n, t1 = (long long)nwg;
-    const double e2 = (double)t2 / (double)(((t2 + n_cu - 1) / n_cu) * n_cu);
-    const double e1 = (double)t1 / (double)(((t1 + 2 * n_cu - 1) / (2 * n_cu)) * 2 * n_cu);
-    // per-tile advantage of the 256x256 kernel grows with K (measured ~1.04x at K=768, ~1.2x at
-    // K>=4096: its fixed prologue/epilogue is amortised over more k-steps)
-    const double adv = 1.0 + 0.2 * (double)(K < 4096 ? K : 4096) / 4096.0;
-    if (vec_epi && N >= 512 && t2 >= n_cu / 2 && e2 * adv >= e1 && !g_force_small) {
+    const long long t2 = (long long)t2m * t2n;
+    const int n_cu = gemm_cu_count();
+    if (vec_epi && gemm_large_tiles(M, N, K) && !g_force_small) {
         const int grid2 = (int)(t2 < n_cu ? t2 : n_cu);   // persistent: one workgroup per CU
 #define GEMM2(OB, AC) launch_gemm256<OB, AC>(grid2, bf_stream(stream), A, lda, W, ldw, bias, \
                                             resid, ldr, resid_mod, C, ldc, row_map, M, N, K, t2n, t2m)

@@ -216,6 +216,9 @@ int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bi
  * run the 256x256 8-wave kernel, the rest the 128x128 4-wave kernel.  Test hook: a non-zero
  * argument forces the 128x128 kernel for every shape (process-wide). */
 void bf_gemm_force_small_tiles(int on);
+/* 1 if an aligned (16-B rows) problem of this shape runs the 256x256 kernel (k_gemm256), 0 if the
+ * 128x128 one (k_gemm) — lets profilers attribute launches to kernels. */
+int bf_gemm_large_tiles(int M, int N, int K);
 
 /* softmax(Q K^T * scale) V per (batch, head); X(b,h,s,d) at X + b*x_bs + s*x_rs + h*D + d,
  * bf16 in/out, head_dim in {32, 64, 80, 128}.  Replaces vit.py Attention.forward (:170-203,
