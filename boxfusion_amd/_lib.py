@@ -140,15 +140,20 @@ def obb_iou_matrix(corners):
 # ------------------------------------------------------------------------------------------
 # association
 # ------------------------------------------------------------------------------------------
-def nms_scan(iou, corners, scores, init_id, cam_poses, fl_items, fl_len, valid_num, cfg: NmsCfg):
-    """returns device tensors: keep, n_keep, success, n_success, events, n_events, status"""
+def nms_scan(iou, corners, scores, init_id, cam_poses, fl_items, fl_len, valid_num, cfg: NmsCfg,
+             out=None):
+    """returns device tensors: keep, succ, events, counts (n_keep, n_success, n_events, status);
+    `out` = (keep, succ, events, counts) preallocated views (e.g. of one buffer read back once)"""
     dev = iou.device
     n = scores.shape[0]
     i32 = dict(dtype=torch.int32, device=dev)
-    keep = torch.empty(n + 1, **i32)
-    succ = torch.empty(n + 1, **i32)
-    events = torch.empty((n + 1, 3), **i32)
-    counts = torch.zeros(4, **i32)  # n_keep, n_success, n_events, status
+    if out is not None:
+        keep, succ, events, counts = out
+    else:
+        keep = torch.empty(n + 1, **i32)
+        succ = torch.empty(n + 1, **i32)
+        events = torch.empty((n + 1, 3), **i32)
+        counts = torch.zeros(4, **i32)  # n_keep, n_success, n_events, status
     _check(lib().bf_nms_scan(_ptr(iou), _ptr(corners), _ptr(scores), _ptr(init_id),
                              _ptr(cam_poses), c_int(n), _ptr(fl_items), _ptr(fl_len),
                              _ptr(valid_num), _ptr(keep), _ptr(counts[0:1]), _ptr(succ),
@@ -158,13 +163,17 @@ def nms_scan(iou, corners, scores, init_id, cam_poses, fl_items, fl_len, valid_n
 
 
 def corr_assoc(corners, dims, scores, boxes2d, init_id, cam_poses, cur_pose, K, n_glo, mask,
-               success, fl_items, fl_len, valid_num, cfg: CorrCfg):
+               success, fl_items, fl_len, valid_num, cfg: CorrCfg, out=None):
+    """returns device tensors keep, events, counts (n_keep, n_events, status); `out` as nms_scan"""
     dev = corners.device
     n_all = scores.shape[0]
     i32 = dict(dtype=torch.int32, device=dev)
-    keep = torch.empty(max(1, mask.shape[0]), **i32)
-    events = torch.empty((n_all + 1, 3), **i32)
-    counts = torch.zeros(3, **i32)  # n_keep, n_events, status
+    if out is not None:
+        keep, events, counts = out
+    else:
+        keep = torch.empty(max(1, mask.shape[0]), **i32)
+        events = torch.empty((n_all + 1, 3), **i32)
+        counts = torch.zeros(3, **i32)  # n_keep, n_events, status
     succ = success if success.numel() else torch.zeros(1, **i32)
     _check(lib().bf_corr_assoc(_ptr(corners), _ptr(dims), _ptr(scores), _ptr(boxes2d),
                                _ptr(init_id), _ptr(cam_poses), _ptr(cur_pose), _ptr(K),

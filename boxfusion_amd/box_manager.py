@@ -106,6 +106,23 @@ class BoxManager:
         return (torch.from_numpy(items).to(device, non_blocking=True),
                 torch.from_numpy(lens).to(device, non_blocking=True))
 
+    def pack_host(self):
+        """fusion lists as host arrays (items [n, cap] padded with -1, lengths [n])"""
+        n = len(self.fusion_list)
+        cap = self.list_capacity
+        items = np.full((max(n, 1), cap), -1, np.int32)
+        lens = np.zeros(max(n, 1), np.int32)
+        for i, row in enumerate(self.fusion_list):
+            if len(row) > cap:
+                raise _lib.HipError(f"fusion list of {len(row)} > capacity {cap}; raise "
+                                    "box_fusion.list_capacity")
+            items[i, :len(row)] = row
+            lens[i] = len(row)
+        return items, lens
+
+    def unpack_host(self, items, lens):
+        self.fusion_list = [[int(v) for v in items[i, :lens[i]]] for i in range(len(self.fusion_list))]
+
     def unpack(self, items, lens):
         it = items.cpu().numpy()
         ln = lens.cpu().numpy()

@@ -93,11 +93,20 @@ __device__ __forceinline__ bool point_in_polygon(P2 p, const P2* poly, int n) {
     return in;
 }
 
-// IoU of the hulls of two 8-point sets (polygon_intersection :202-261 + :374-396)
-__device__ float iou_hulls(P2* c0, P2* ct, int* flags) {
-    P2 h0[8], ht[8];
+// segments whose bounding boxes are more than 1e-3 px apart cannot produce an accepted
+// intersection: line_intersection accepts parameters in [-1e-8, 1 + 1e-8], i.e. at most
+// ~1e-5 px outside a segment of an image-sized extent.  Skipping them changes no result and
+// avoids the two f64 divisions.
+__device__ __forceinline__ bool seg_boxes_apart(P2 a1, P2 a2, P2 b1, P2 b2) {
+    const float m = 1e-3f;
+    return fmaxf(a1.x, a2.x) + m < fminf(b1.x, b2.x) || fmaxf(b1.x, b2.x) + m < fminf(a1.x, a2.x) ||
+           fmaxf(a1.y, a2.y) + m < fminf(b1.y, b2.y) || fmaxf(b1.y, b2.y) + m < fminf(a1.y, a2.y);
+}
+
+// IoU of hull(c0) with a precomputed hull ht[nt] (polygon_intersection :202-261 + :374-396)
+__device__ float iou_hull_pre(P2* c0, const P2* ht, int nt, float at, int* flags) {
+    P2 h0[8];
     int n0 = convex_hull<8>(c0, 8, h0);
-    int nt = convex_hull<8>(ct, 8, ht);
     P2 cand[CAND_CAP];
     int nc = 0;
     for (int i = 0; i < n0; ++i)
@@ -106,8 +115,10 @@ __device__ float iou_hulls(P2* c0, P2* ct, int* flags) {
         if (point_in_polygon(ht[i], h0, n0) && nc < CAND_CAP) cand[nc++] = ht[i];
     for (int i = 0; i < n0; ++i)
         for (int j = 0; j < nt; ++j) {
+            const P2 a1 = h0[i], a2 = h0[(i + 1) % n0], b1 = ht[j], b2 = ht[(j + 1) % nt];
+            if (seg_boxes_apart(a1, a2, b1, b2)) continue;
             P2 pt;
-            if (line_intersection(h0[i], h0[(i + 1) % n0], ht[j], ht[(j + 1) % nt], &pt)) {
+            if (line_intersection(a1, a2, b1, b2, &pt)) {
                 if (nc < CAND_CAP) cand[nc++] = pt;
                 else *flags |= BF_DEV_HULL_OVERFLOW;
             }
@@ -118,11 +129,17 @@ __device__ float iou_hulls(P2* c0, P2* ct, int* flags) {
     if (ni > 8) *flags |= BF_DEV_HULL_OVERFLOW;
     float inter = polygon_area(hi, ni);
     float a0 = polygon_area(h0, n0);
-    float at = polygon_area(ht, nt);
     float uni = a0 + at - inter;
     float iou = 0;
     if (uni > 0) iou = (float)((double)inter / ((double)uni + 0.00001));
     return iou;
+}
+
+// IoU of the hulls of two 8-point sets
+__device__ float iou_hulls(P2* c0, P2* ct, int* flags) {
+    P2 ht[8];
+    const int nt = convex_hull<8>(ct, 8, ht);
+    return iou_hull_pre(c0, ht, nt, polygon_area(ht, nt), flags);
 }
 
 struct FuseViews {
@@ -343,8 +360,12 @@ __global__ void __launch_bounds__(TERM_THREADS) k_fuse_terms(const float* __rest
         ct[j].x = Pm[16 + 2 * j];
         ct[j].y = Pm[16 + 2 * j + 1];
     }
+    // the view's target hull is the same for every particle (computed per lane: identical
+    // inputs, identical result, no cross-lane traffic)
+    P2 ht[8];
+    const int nt = convex_hull<8>(ct, 8, ht);
     int flags = 0;
-    const float iou = iou_hulls(c0, ct, &flags);
+    const float iou = iou_hull_pre(c0, ht, nt, polygon_area(ht, nt), &flags);
     terms[((size_t)job * max_views + v) * P + p] = fabsf(1 - iou);
     if (flags) atomicOr(&states[job].flags, flags);
 }

@@ -20,6 +20,32 @@ import torch
 from boxfusion_amd import _lib
 
 
+class Exchange:
+    """One int32 host<->device exchange buffer for an association kernel: named host arrays are
+    uploaded with a single copy, named sizes are device outputs; `fetch()` reads everything back
+    with a single copy (one synchronisation per association step)."""
+
+    def __init__(self, dev, **fields):
+        self.layout = {}
+        off = 0
+        for k, v in fields.items():
+            n = int(np.asarray(v).size) if isinstance(v, np.ndarray) else int(v)
+            shape = v.shape if isinstance(v, np.ndarray) else (n,)
+            self.layout[k] = (off, n, shape)
+            off += n
+        host = np.zeros(max(off, 1), np.int32)
+        for k, v in fields.items():
+            if isinstance(v, np.ndarray):
+                o, n, _ = self.layout[k]
+                host[o:o + n] = v.reshape(-1)
+        self.buf = torch.from_numpy(host).to(dev)
+        self.dev = {k: self.buf[o:o + n].view(*shape) for k, (o, n, shape) in self.layout.items()}
+
+    def fetch(self):
+        h = self.buf.cpu().numpy()
+        return {k: h[o:o + n].reshape(shape) for k, (o, n, shape) in self.layout.items()}
+
+
 class Instances3D:
     def __init__(self, image_size: Tuple[int, int] = (0, 0), **kwargs: Any):
         self._image_size = image_size
@@ -174,16 +200,22 @@ class Instances3D:
         if not (isinstance(vn, torch.Tensor) and vn.is_cuda and vn.dtype == torch.float32 and vn.is_contiguous()):
             vn = torch.as_tensor(vn).to(dev, torch.float32).contiguous()
             instance_lists.valid_num = vn
-        items, lens = box_manager.pack(dev)
-        keep, succ, events, counts = _lib.nms_scan(iou, corners, scores, init_id, poses, items, lens,
-                                                   vn, box_manager.nms_cfg(threshold))
-        c = counts.cpu().numpy()
+        # one host->device copy in (fusion lists), one device->host copy out (lists + results)
+        items, lens = box_manager.pack_host()
+        n = scores.shape[0]
+        x = Exchange(dev, items=items, lens=lens, counts=np.zeros(4, np.int32),
+                     keep=n + 1, succ=n + 1, events=3 * (n + 1))
+        _lib.nms_scan(iou, corners, scores, init_id, poses, x.dev["items"], x.dev["lens"], vn,
+                      box_manager.nms_cfg(threshold),
+                      out=(x.dev["keep"], x.dev["succ"], x.dev["events"].view(-1, 3), x.dev["counts"]))
+        h = x.fetch()
+        c = h["counts"]
         if c[3]:
             raise _lib.HipError(f"bf_nms_scan device status {c[3]} (fusion list capacity)")
-        box_manager.unpack(items, lens)
-        box_manager.replay_flags(events[:c[2]].cpu().numpy().tolist())
-        keep = keep[:c[0]].cpu().numpy().astype(np.int64).tolist()
-        success = succ[:c[1]].cpu().numpy().astype(np.int64).tolist()
+        box_manager.unpack_host(h["items"], h["lens"])
+        box_manager.replay_flags(h["events"].reshape(-1, 3)[:c[2]].tolist())
+        keep = h["keep"][:c[0]].astype(np.int64).tolist()
+        success = h["succ"][:c[1]].astype(np.int64).tolist()
         return keep, success
 
     def correspondence_association(cfg, box_manager, cur_keep_idx, cur_success_nms, pred_instances,
@@ -198,22 +230,28 @@ class Instances3D:
         corners = boxes.corners
         mask_np = np.asarray(mask, dtype=np.int64)
         success_all = [i + n_glo for i in cur_success_nms]
-        i32 = dict(dtype=torch.int32, device=dev)
         vn = all_pred_box.valid_num
-        items, lens = box_manager.pack(dev)
+        items, lens = box_manager.pack_host()
+        n_all = len(all_pred_box)
+        x = Exchange(dev, items=items, lens=lens, mask=mask_np.astype(np.int32),
+                     succ=np.asarray(success_all if success_all else [0], np.int32),
+                     counts=np.zeros(3, np.int32), keep=max(1, len(mask_np)), events=3 * (n_all + 1))
         cur_pose = torch.as_tensor(np.asarray(all_kf_pose[frame_id], dtype=np.float32), device=dev)
         K = torch.as_tensor(intrinsic).to(dev, torch.float32)
-        keep, events, counts = _lib.corr_assoc(
+        succ_dev = x.dev["succ"][:len(success_all)]
+        _lib.corr_assoc(
             corners, boxes.dims.contiguous(), all_pred_box.scores.to(dev, torch.float32).contiguous(),
             all_pred_box.pred_boxes.to(dev, torch.float32).contiguous(),
             all_pred_box.init_id.to(dev, torch.int32).contiguous(),
             per_frame_ins_cam_pose.to(dev, torch.float32).contiguous(), cur_pose, K, n_glo,
-            torch.as_tensor(mask_np, **i32), torch.as_tensor(np.asarray(success_all, np.int64), **i32),
-            items, lens, vn, box_manager.corr_cfg(threshold, W, H))
-        c = counts.cpu().numpy()
+            x.dev["mask"], succ_dev, x.dev["items"], x.dev["lens"], vn,
+            box_manager.corr_cfg(threshold, W, H),
+            out=(x.dev["keep"], x.dev["events"].view(-1, 3), x.dev["counts"]))
+        h = x.fetch()
+        c = h["counts"]
         if c[2]:
             raise _lib.HipError(f"bf_corr_assoc device status {c[2]} (fusion list capacity)")
-        box_manager.unpack(items, lens)
-        box_manager.replay_flags(events[:c[1]].cpu().numpy().tolist())
-        keep_idx = keep[:c[0]].cpu().numpy().astype(np.int64)
+        box_manager.unpack_host(h["items"], h["lens"])
+        box_manager.replay_flags(h["events"].reshape(-1, 3)[:c[1]].tolist())
+        keep_idx = h["keep"][:c[0]].astype(np.int64)
         return all_pred_box[keep_idx], all_poses[keep_idx], keep_idx
