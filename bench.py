@@ -62,6 +62,10 @@ def parse():
                    help="synchronous fusion, sync between stages, report ms/step of each")
     p.add_argument("--eager", action="store_true", help="no HIP graph for the detect stage")
     p.add_argument("--roofline-steps", type=int, default=2)
+    p.add_argument("--fusion-cus", type=int, default=-1,
+                   help="CUs reserved for the fusion stream (-1: 16 on rank 0 when N > 1, else 0)")
+    p.add_argument("--sim-ranks", type=int, default=1,
+                   help="stress test at N=1: rank 0 also fuses the frames of R virtual ranks per step")
     p.add_argument("--sync-fusion", action="store_true",
                    help="run the fusion state machine inline instead of on the worker stream")
     p.add_argument("--cpu-detect-frames", type=int, default=1)
@@ -249,6 +253,15 @@ def main():
     rgb_all, depth_all = gen_frames(all_mine, dev)
     poses_all = np.stack([scene.pose(f) for f in all_mine]).astype(np.float32)
     rec_all = torch.from_numpy(pack_records([scene.detections(f) for f in all_mine])).to(dev)
+    sim = None
+    if args.sim_ranks > 1 and world == 1:
+        # what rank 0 of an R-GPU run fuses: R*B frames per step (stress test, not the metric)
+        R = args.sim_ranks
+        sim = {"rec": [], "pose": []}
+        for s_ in range(total_steps):
+            fr = [s_ * B * R + j for j in range(B * R)]
+            sim["rec"].append(torch.from_numpy(pack_records([scene.detections(f) for f in fr])).to(dev))
+            sim["pose"].append(np.stack([scene.pose(f) for f in fr]).astype(np.float32))
     torch.cuda.synchronize()
 
     brk = dict(detect=0.0, fusion=0.0)
@@ -266,27 +279,39 @@ def main():
             bidx, iidx, cat_idx, feats, sims = detect.last["clip"]
             recs = rec_all[sl]
             g_rec, g_feat, g_pose = gather_step(recs, feats, poses_all[sl], dist, N)
+            if sim is not None:       # --sim-ranks: rank 0 fuses the frames of R virtual ranks
+                g_rec, g_pose = sim["rec"][s], sim["pose"][s]
             if rank == 0:
-                base = s * per_step
+                base = s * (per_step if sim is None else B * args.sim_ranks)
                 if args.sync_fusion:
                     for j in range(g_rec.shape[0]):
-                        fusion.keyframe(base + j - s0 * per_step, g_pose[j], unpack_record(g_rec[j], dev))
+                        fusion.keyframe(base + j - s0 * (g_rec.shape[0]), g_pose[j], unpack_record(g_rec[j], dev))
                 else:
                     # hand the step's frames to the fusion worker (side stream), keep detecting
                     ev = torch.cuda.Event()
                     ev.record()
                     g_rec.record_stream(fusion.stream)
                     for j in range(g_rec.shape[0]):
-                        fusion.submit(base + j - s0 * per_step, g_pose[j],
+                        fusion.submit(base + j - s0 * (g_rec.shape[0]), g_pose[j],
                                       (lambda r=g_rec[j]: unpack_record(r, dev)), ev)
             if args.breakdown:
                 torch.cuda.synchronize()
                 brk["fusion"] += time.perf_counter() - tb
 
     # ---- warmup (own fusion state), then the timed stream from frame 0 ----------------------
+    # rank 0 owns the serial fusion state machine; when it fuses more frames than it detects
+    # (N > 1), a few CUs are reserved for it so the persistent GEMMs cannot starve it
+    fusion_cus = args.fusion_cus
+    if fusion_cus < 0:
+        fusion_cus = 16 if rank == 0 and (world > 1 or args.sim_ranks > 1) else 0
+    det_stream, fus_stream = (_lib.partition_streams(fusion_cus, local) if fusion_cus > 0
+                              else (torch.cuda.current_stream(), None))
+    torch.cuda.synchronize()
+    torch.cuda.set_stream(det_stream)          # detection (graph replays, gathers) on its CUs
+
     def make_fusion():
         st = FusionStage(CFG, SCANNET_K, device=dev)
-        return st if args.sync_fusion else AsyncFusion(st)
+        return st if args.sync_fusion else AsyncFusion(st, stream=fus_stream)
 
     wf = make_fusion()
     run_steps(0, args.warmup, wf)

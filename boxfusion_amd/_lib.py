@@ -416,3 +416,42 @@ def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype
     e.record()
     t.records.append((2.0 * M * w.shape[0] * w.shape[1], s, e))
     return r
+
+
+# ------------------------------------------------------------------------------------------
+# chip partitioning: CU-masked HIP streams (fusion on a few CUs, detection on the rest)
+# ------------------------------------------------------------------------------------------
+def cu_masked_stream(cus, device=None):
+    """torch ExternalStream on a new HIP stream restricted to the CUs in `cus` (indices as the
+    runtime enumerates them) via hipExtStreamCreateWithCUMask."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    dev = torch.cuda.current_device() if device is None else device
+    n = torch.cuda.get_device_properties(dev).multi_processor_count
+    words = (ctypes.c_uint32 * ((n + 31) // 32))()
+    for c in cus:
+        if not 0 <= c < n:
+            raise HipError(f"CU index {c} outside 0..{n - 1}")
+        words[c // 32] |= 1 << (c % 32)
+    s = ctypes.c_void_p()
+    with torch.cuda.device(dev):
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(s), ctypes.c_uint32(len(words)), words)
+    if rc != 0:
+        raise HipError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+    return torch.cuda.ExternalStream(s.value, device=dev)
+
+
+def partition_streams(n_reserved, device=None, masked=False):
+    """(detect_stream, fusion_stream) for a rank that also runs the fusion state machine.
+    The persistent GEMMs are told to leave `n_reserved` CUs free (their grid is n_cu - n_reserved
+    workgroups, one per CU), so the fusion kernels always find CUs while a GEMM runs; the fusion
+    stream gets high priority for the CUs that free up in between.  masked=True additionally
+    confines each stream to its CUs with hipExtStreamCreateWithCUMask."""
+    dev = torch.cuda.current_device() if device is None else device
+    n = torch.cuda.get_device_properties(dev).multi_processor_count
+    lib().bf_gemm_set_cu_budget(c_int(n - n_reserved))
+    if not masked:
+        return torch.cuda.current_stream(dev), torch.cuda.Stream(device=dev, priority=-1)
+    step = max(1, n // max(1, n_reserved))
+    fus = [i for i in range(0, n, step)][:n_reserved]
+    det = [i for i in range(n) if i not in set(fus)]
+    return cu_masked_stream(det, dev), cu_masked_stream(fus, dev)

@@ -504,7 +504,13 @@ static int g_force_small = 0;
 // test hook: 1 forces the 128x128 kernel for every shape (both kernels stay covered by tests)
 BF_API void bf_gemm_force_small_tiles(int on) { g_force_small = on; }
 
+static int g_cu_budget = 0;
+// CUs the GEMMs may assume (persistent grid size); 0 = every CU of the device.  Set it when the
+// launching stream is CU-masked (e.g. part of the chip is reserved for the fusion stream).
+BF_API void bf_gemm_set_cu_budget(int n) { g_cu_budget = n > 0 ? n : 0; }
+
 static int gemm_cu_count() {
+    if (g_cu_budget > 0) return g_cu_budget;
     static int n_cu = 0;
     if (n_cu == 0) {
         int dev = 0;

@@ -129,10 +129,10 @@ class AsyncFusion:
     called on the worker, after its stream waited for `ready` (an event on the producer stream),
     so it may read the producer's buffers."""
 
-    def __init__(self, stage: FusionStage):
+    def __init__(self, stage: FusionStage, stream=None):
         self.stage = stage
         self.device_index = stage.dev.index if stage.dev.index is not None else torch.cuda.current_device()
-        self.stream = torch.cuda.Stream(device=self.device_index)
+        self.stream = stream if stream is not None else torch.cuda.Stream(device=self.device_index)
         self.q = queue.Queue()
         self.err = None
         self.thread = threading.Thread(target=self._run, name="boxfusion-fusion", daemon=True)

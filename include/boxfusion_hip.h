@@ -219,6 +219,9 @@ void bf_gemm_force_small_tiles(int on);
 /* 1 if an aligned (16-B rows) problem of this shape runs the 256x256 kernel (k_gemm256), 0 if the
  * 128x128 one (k_gemm) — lets profilers attribute launches to kernels. */
 int bf_gemm_large_tiles(int M, int N, int K);
+/* Number of CUs the GEMM may assume (sizes the persistent grid); 0 = all CUs of the device.
+ * Set when GEMMs launch on a CU-masked stream. */
+void bf_gemm_set_cu_budget(int n);
 
 /* softmax(Q K^T * scale) V per (batch, head); X(b,h,s,d) at X + b*x_bs + s*x_rs + h*D + d,
  * bf16 in/out, head_dim in {32, 64, 80, 128}.  Replaces vit.py Attention.forward (:170-203,
