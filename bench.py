@@ -63,7 +63,7 @@ def parse():
     p.add_argument("--eager", action="store_true", help="no HIP graph for the detect stage")
     p.add_argument("--roofline-steps", type=int, default=2)
     p.add_argument("--fusion-cus", type=int, default=-1,
-                   help="CUs reserved for the fusion stream (-1: 16 on rank 0 when N > 1, else 0)")
+                   help="CUs reserved for the fusion stream (-1: 32 on rank 0 when N > 1, else 0)")
     p.add_argument("--sim-ranks", type=int, default=1,
                    help="stress test at N=1: rank 0 also fuses the frames of R virtual ranks per step")
     p.add_argument("--sync-fusion", action="store_true",
@@ -100,10 +100,13 @@ def pack_records(dets):
     return out
 
 
-def unpack_record(rec, dev):
+def unpack_record(rec, dev, n=None):
+    """record -> Instances3D; `n` (detections in the record) from the host when known, so the
+    fusion worker does not read the device to learn it"""
     from boxfusion_amd.boxes import GeneralInstance3DBoxes
     from boxfusion_amd.instances import Instances3D
-    n = int(rec[0].item())
+    if n is None:
+        n = int(rec[0].item())
     rows = rec[1:1 + n * REC_W].view(n, REC_W)
     p = Instances3D((480, 640))
     p.scores = rows[:, 0].contiguous()
@@ -117,9 +120,10 @@ def gather_step(recs, feats, poses, dist, world):
     """Exchange of one step: every rank's per-frame records [b, R] and CLIP features
     [n_crops, 1024] are all-gathered (RCCL over xGMI on the GPU; gloo in the CPU tests) so that
     the fusion owner sees the step's frames in global frame order (rank-major = frame order, since
-    rank r holds frames step*b*world + r*b ... + b-1).  Poses travel as a tiny host object."""
+    rank r holds frames step*b*world + r*b ... + b-1).  `poses` is a tuple of small per-frame host
+    arrays (poses, detection counts) gathered as one host object."""
     if dist is None or world == 1:
-        return recs, feats, np.asarray(poses)
+        return recs, feats, tuple(np.asarray(x) for x in poses)
     if recs.is_cuda:
         g_rec = torch.empty((world * recs.shape[0],) + recs.shape[1:], dtype=recs.dtype, device=recs.device)
         dist.all_gather_into_tensor(g_rec, recs.contiguous())
@@ -133,9 +137,9 @@ def gather_step(recs, feats, poses, dist, world):
         fparts = [torch.empty_like(feats) for _ in range(world)]
         dist.all_gather(fparts, feats.contiguous())
         g_feat = torch.cat(fparts)
-    g_pose = [None] * world
-    dist.all_gather_object(g_pose, np.asarray(poses))
-    return g_rec, g_feat, np.concatenate(g_pose)
+    g_meta = [None] * world
+    dist.all_gather_object(g_meta, tuple(np.asarray(x) for x in poses))
+    return g_rec, g_feat, tuple(np.concatenate([m[i] for m in g_meta]) for i in range(len(g_meta[0])))
 
 
 # ------------------------------------------------------------------------------------------------
@@ -252,15 +256,19 @@ def main():
     all_mine = [f for s in range(total_steps) for f in my_frames(s)]
     rgb_all, depth_all = gen_frames(all_mine, dev)
     poses_all = np.stack([scene.pose(f) for f in all_mine]).astype(np.float32)
-    rec_all = torch.from_numpy(pack_records([scene.detections(f) for f in all_mine])).to(dev)
+    rec_host = pack_records([scene.detections(f) for f in all_mine])
+    rec_all = torch.from_numpy(rec_host).to(dev)
+    cnt_all = rec_host[:, 0].astype(np.int64)
     sim = None
     if args.sim_ranks > 1 and world == 1:
         # what rank 0 of an R-GPU run fuses: R*B frames per step (stress test, not the metric)
         R = args.sim_ranks
-        sim = {"rec": [], "pose": []}
+        sim = {"rec": [], "pose": [], "cnt": []}
         for s_ in range(total_steps):
             fr = [s_ * B * R + j for j in range(B * R)]
-            sim["rec"].append(torch.from_numpy(pack_records([scene.detections(f) for f in fr])).to(dev))
+            rh = pack_records([scene.detections(f) for f in fr])
+            sim["rec"].append(torch.from_numpy(rh).to(dev))
+            sim["cnt"].append(rh[:, 0].astype(np.int64))
             sim["pose"].append(np.stack([scene.pose(f) for f in fr]).astype(np.float32))
     torch.cuda.synchronize()
 
@@ -278,14 +286,16 @@ def main():
                 tb = time.perf_counter()
             bidx, iidx, cat_idx, feats, sims = detect.last["clip"]
             recs = rec_all[sl]
-            g_rec, g_feat, g_pose = gather_step(recs, feats, poses_all[sl], dist, N)
+            g_rec, g_feat, g_meta = gather_step(recs, feats, (poses_all[sl], cnt_all[sl]), dist, N)
+            g_pose, g_cnt = g_meta
             if sim is not None:       # --sim-ranks: rank 0 fuses the frames of R virtual ranks
-                g_rec, g_pose = sim["rec"][s], sim["pose"][s]
+                g_rec, g_pose, g_cnt = sim["rec"][s], sim["pose"][s], sim["cnt"][s]
             if rank == 0:
                 base = s * (per_step if sim is None else B * args.sim_ranks)
                 if args.sync_fusion:
                     for j in range(g_rec.shape[0]):
-                        fusion.keyframe(base + j - s0 * (g_rec.shape[0]), g_pose[j], unpack_record(g_rec[j], dev))
+                        fusion.keyframe(base + j - s0 * (g_rec.shape[0]), g_pose[j],
+                                        unpack_record(g_rec[j], dev, int(g_cnt[j])))
                 else:
                     # hand the step's frames to the fusion worker (side stream), keep detecting
                     ev = torch.cuda.Event()
@@ -293,7 +303,7 @@ def main():
                     g_rec.record_stream(fusion.stream)
                     for j in range(g_rec.shape[0]):
                         fusion.submit(base + j - s0 * (g_rec.shape[0]), g_pose[j],
-                                      (lambda r=g_rec[j]: unpack_record(r, dev)), ev)
+                                      (lambda r=g_rec[j], n=int(g_cnt[j]): unpack_record(r, dev, n)), ev)
             if args.breakdown:
                 torch.cuda.synchronize()
                 brk["fusion"] += time.perf_counter() - tb
@@ -303,7 +313,7 @@ def main():
     # (N > 1), a few CUs are reserved for it so the persistent GEMMs cannot starve it
     fusion_cus = args.fusion_cus
     if fusion_cus < 0:
-        fusion_cus = 16 if rank == 0 and (world > 1 or args.sim_ranks > 1) else 0
+        fusion_cus = 32 if rank == 0 and (world > 1 or args.sim_ranks > 1) else 0
     det_stream, fus_stream = (_lib.partition_streams(fusion_cus, local) if fusion_cus > 0
                               else (torch.cuda.current_stream(), None))
     torch.cuda.synchronize()

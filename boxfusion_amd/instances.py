@@ -99,14 +99,21 @@ class Instances3D:
                 raise IndexError("Instances3D index out of range!")
             item = slice(item, None, len(self))
         ret = Instances3D(self._image_size)
+        # a host index used on device fields is uploaded once, not once per field
+        dev_index = {}
+
+        def on(device):
+            if device not in dev_index:
+                dev_index[device] = torch.as_tensor(item, device=device)
+            return dev_index[device]
         for k, v in self._fields.items():
             if isinstance(v, (torch.Tensor, np.ndarray)) or hasattr(v, "tensor"):
                 if isinstance(v, np.ndarray) and isinstance(item, torch.Tensor):
                     ret.set(k, v[item.cpu().numpy()])
                 elif isinstance(v, torch.Tensor) and isinstance(item, np.ndarray):
-                    ret.set(k, v[torch.as_tensor(item, device=v.device)])
+                    ret.set(k, v[on(v.device)])
                 elif hasattr(v, "tensor") and isinstance(item, np.ndarray):
-                    ret.set(k, v[torch.as_tensor(item, device=v.tensor.device)])
+                    ret.set(k, v[on(v.tensor.device)])
                 else:
                     ret.set(k, v[item])
             elif hasattr(v, "__iter__"):
