@@ -17,6 +17,7 @@
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
 
 #define GB_M 128
@@ -332,26 +333,29 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict
         }
     };
 
-    f32x16 acc[4][2];
+    // v_mfma_f32_16x16x32_bf16: wave tile 128x64 = 8 row blocks x 4 column blocks of 16x16,
+    // K-tile of 64 = 2 k-steps of 32.  Lane l holds A[row l&15][k 8(l>>4)..+7] (16 B) per block.
+    f32x4 acc[8][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+            for (int e = 0; e < 4; ++e) acc[i][j][e] = 0.f;
 
-    bf16x8 fa0[4], fb0[2], fa1[4], fb1[2];
+    const int lr = lane & 15, lq = lane >> 4;     // fragment row / k-quarter
+    bf16x8 fa0[8], fb0[4], fa1[8], fb1[4];
 #define G2_READ(FA, FB, stage, ks)                                                               \
     {                                                                                            \
         const unsigned char* sa_ = g_smem + (stage) * 65536;                                     \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) FA[i] =                                    \
-            *reinterpret_cast<const bf16x8*>(sa_ + swz(wr * 128 + i * 32 + fr, (ks) * 2 + fh));  \
-        _Pragma("unroll") for (int j = 0; j < 2; ++j) FB[j] = *reinterpret_cast<const bf16x8*>(  \
-            sa_ + 32768 + swz(wc * 64 + j * 32 + fr, (ks) * 2 + fh));                            \
+        _Pragma("unroll") for (int i = 0; i < 8; ++i) FA[i] =                                    \
+            *reinterpret_cast<const bf16x8*>(sa_ + swz(wr * 128 + i * 16 + lr, (ks) * 4 + lq));  \
+        _Pragma("unroll") for (int j = 0; j < 4; ++j) FB[j] = *reinterpret_cast<const bf16x8*>(  \
+            sa_ + 32768 + swz(wc * 64 + j * 16 + lr, (ks) * 4 + lq));                            \
     }
 #define G2_MFMA(FA, FB)                                                                          \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) \
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(FA[i], FB[j], acc[i][j], 0, 0, 0);
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 4; ++j) \
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA[i], FB[j], acc[i][j], 0, 0, 0);
 
     stage_tile(0, 0);
     if (total > 1) stage_tile(1, 1);
@@ -365,16 +369,11 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict
         const int st = g & 1;
         G2_READ(fa1, fb1, st, 1);
         G2_MFMA(fa0, fb0);
-        G2_READ(fa0, fb0, st, 2);
-        G2_MFMA(fa1, fb1);
-        G2_READ(fa1, fb1, st, 3);
-        G2_MFMA(fa0, fb0);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // K-tile g+1 (the only one in flight)
         RAW_BARRIER();
-        // last k-step: each of the 8 MFMAs carries one LDS-DMA issue of K-tile g+2 and one
-        // fragment read of K-tile g+1, pinned in that order (an issue hides under an MFMA).
-        // Unconditional (clamped): past the end they refill / re-read a stage nothing reads.
+        // second k-step: its 32 MFMAs carry the 8 LDS-DMA issues of K-tile g+2 and the 12
+        // fragment reads of K-tile g+1 (unconditional, clamped past the end)
         {
             const int gn = min(g + 2, total - 1);
             const int tile_n = slot + (gn / nk) * G;
@@ -383,101 +382,104 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict
             unsigned char* sa_n = g_smem + st * 65536 + wave * 4096;
             const unsigned char* sr = g_smem + (st ^ 1) * 65536;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int i = q >> 1, j = q & 1;
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa1[i], fb1[j], acc[i][j], 0, 0, 0);
-                const int si = q >> 1;
-                if ((q & 1) == 0) {
-                    const u16* ga = A + (size_t)min(m0n + srow[si], M - 1) * lda + k0n + scol[si];
-                    __builtin_amdgcn_global_load_lds((const void*)ga, (lds_ptr_t)(sa_n + si * 1024), 16, 0, 0);
-                } else {
-                    const u16* gw = W + (size_t)min(n0n + srow[si], N - 1) * ldw + k0n + scol[si];
-                    __builtin_amdgcn_global_load_lds((const void*)gw, (lds_ptr_t)(sa_n + 32768 + si * 1024), 16, 0, 0);
+            for (int q = 0; q < 32; ++q) {
+                const int i = q >> 2, j = q & 3;
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[i], fb1[j], acc[i][j], 0, 0, 0);
+                if ((q & 3) == 0) {
+                    const int si = (q >> 3);
+                    if (((q >> 2) & 1) == 0) {
+                        const u16* ga = A + (size_t)min(m0n + srow[si], M - 1) * lda + k0n + scol[si];
+                        __builtin_amdgcn_global_load_lds((const void*)ga, (lds_ptr_t)(sa_n + si * 1024), 16, 0, 0);
+                    } else {
+                        const u16* gw = W + (size_t)min(n0n + srow[si], N - 1) * ldw + k0n + scol[si];
+                        __builtin_amdgcn_global_load_lds((const void*)gw, (lds_ptr_t)(sa_n + 32768 + si * 1024), 16, 0, 0);
+                    }
                 }
-                if (q < 4) fa0[q] = *reinterpret_cast<const bf16x8*>(sr + swz(wr * 128 + q * 32 + fr, fh));
-                else if (q < 6) fb0[q - 4] = *reinterpret_cast<const bf16x8*>(sr + 32768 + swz(wc * 64 + (q - 4) * 32 + fr, fh));
+                if ((q & 1) == 1 && q < 24) {
+                    const int r = q >> 1;     // 0..11
+                    if (r < 8) fa0[r] = *reinterpret_cast<const bf16x8*>(sr + swz(wr * 128 + r * 16 + lr, lq));
+                    else fb0[r - 8] = *reinterpret_cast<const bf16x8*>(sr + 32768 + swz(wc * 64 + (r - 8) * 16 + lr, lq));
+                }
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
         if (g % nk != nk - 1) continue;
 
-        // ---- epilogue of this tile (wave-private, 16 rows per pass) --------------------------
+        // ---- epilogue of this tile (wave-private, 16 rows = one row block per pass) ----------
         const int tile = slot + (g / nk) * G;
         const int m0 = (tile / tiles_n) * 256 + wr * 128, n0 = (tile % tiles_n) * 256 + wc * 64;
-        float bv[2];
+        float bv[4];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int n = n0 + j * 32 + fr;
+        for (int j = 0; j < 4; ++j) {
+            const int n = n0 + j * 16 + lr;
             bv[j] = (bias && n < N) ? bias[min(n, N - 1)] : 0.f;
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < 8; ++i) {
+            // C/D layout: col = lane&15, row = 4*(lane>>4) + e; rows r and r+4 in other banks
 #pragma unroll
-            for (int eh = 0; eh < 2; ++eh) {
-                // rows i*32 + 16*eh + [0,16): accumulator elements e = 8*eh .. 8*eh+7
+            for (int j = 0; j < 4; ++j) {
+                f32x2 v01 = {acc[i][j][0] + bv[j], acc[i][j][1] + bv[j]};
+                f32x2 v23 = {acc[i][j][2] + bv[j], acc[i][j][3] + bv[j]};
+                if (ACT == 1) { v01 = gelu_erf2(v01); v23 = gelu_erf2(v23); }
+                else if (ACT == 2) {
+                    v01.x = fmaxf(v01.x, 0.f); v01.y = fmaxf(v01.y, 0.f);
+                    v23.x = fmaxf(v23.x, 0.f); v23.y = fmaxf(v23.y, 0.f);
+                }
+                const int rl = 4 * lq;
+                const int col = (j * 16 + lr) ^ (lq << 4);
+                scratch[(rl + 0) * 64 + col] = v01.x;
+                scratch[(rl + 1) * 64 + col] = v01.y;
+                scratch[(rl + 2) * 64 + col] = v23.x;
+                scratch[(rl + 3) * 64 + col] = v23.y;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
+            for (int it = 0; it < 16 * (64 / CW) / 64; ++it) {
+                const int id = it * 64 + lane;
+                const int rl = id / (64 / CW), cl = (id % (64 / CW)) * CW;
+                const int m = m0 + i * 16 + rl, n = n0 + cl;
+                const int sw = ((rl >> 2) & 3) << 4;
+                float v[CW];
 #pragma unroll
-                    for (int q = 0; q < 8; q += 2) {
-                        const int e = 8 * eh + q;
-                        f32x2 v2 = {acc[i][j][e] + bv[j], acc[i][j][e + 1] + bv[j]};
-                        if (ACT == 1) v2 = gelu_erf2(v2);
-                        else if (ACT == 2) { v2.x = fmaxf(v2.x, 0.f); v2.y = fmaxf(v2.y, 0.f); }
+                for (int q = 0; q < CW; q += 4) {
+                    const float4 x = *reinterpret_cast<const float4*>(scratch + rl * 64 + ((cl + q) ^ sw));
+                    v[q] = x.x; v[q + 1] = x.y; v[q + 2] = x.z; v[q + 3] = x.w;
+                }
+                if (m < M && n < N) {
+                    const int orow = row_map ? row_map[m] : m;
+                    if (orow >= 0) {
+                        if (resid) {
+                            const int rrow = resid_mod > 0 ? (m % resid_mod) : orow;
+                            const float* rp = resid + (size_t)rrow * ldr + n;
 #pragma unroll
-                        for (int u = 0; u < 2; ++u) {
-                            const int rl = ((e + u) & 3) + 8 * (((e + u) >> 2) & 1) + 4 * fh;   // 0..15
-                            scratch[rl * 64 + ((j * 32 + fr) ^ (((rl >> 2) & 1) << 5))] = u ? v2.y : v2.x;
+                            for (int q = 0; q < CW; q += 4) {
+                                const float4 x = *reinterpret_cast<const float4*>(rp + q);
+                                v[q] += x.x; v[q + 1] += x.y; v[q + 2] += x.z; v[q + 3] += x.w;
+                            }
                         }
-                    }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                // 16 rows x 64 columns: CW-wide chunks, 64/CW per row
-#pragma unroll
-                for (int it = 0; it < 16 * (64 / CW) / 64; ++it) {
-                    const int id = it * 64 + lane;
-                    const int rl = id / (64 / CW), cl = (id % (64 / CW)) * CW;
-                    const int m = m0 + i * 32 + 16 * eh + rl, n = n0 + cl;
-                    const int sw = ((rl >> 2) & 1) << 5;
-                    float v[CW];
-#pragma unroll
-                    for (int q = 0; q < CW; q += 4) {
-                        const float4 x = *reinterpret_cast<const float4*>(scratch + rl * 64 + ((cl + q) ^ sw));
-                        v[q] = x.x; v[q + 1] = x.y; v[q + 2] = x.z; v[q + 3] = x.w;
-                    }
-                    if (m < M && n < N) {
-                        const int orow = row_map ? row_map[m] : m;
-                        if (orow >= 0) {
-                            if (resid) {
-                                const int rrow = resid_mod > 0 ? (m % resid_mod) : orow;
-                                const float* rp = resid + (size_t)rrow * ldr + n;
-#pragma unroll
-                                for (int q = 0; q < CW; q += 4) {
-                                    const float4 x = *reinterpret_cast<const float4*>(rp + q);
-                                    v[q] += x.x; v[q + 1] += x.y; v[q + 2] += x.z; v[q + 3] += x.w;
-                                }
-                            }
-                            if (OUT_BF16) {
-                                U128 o;
-                                o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-                                o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-                                o.z = (uint32_t)f2bf(v[4 % CW]) | ((uint32_t)f2bf(v[5 % CW]) << 16);
-                                o.w = (uint32_t)f2bf(v[6 % CW]) | ((uint32_t)f2bf(v[7 % CW]) << 16);
-                                *reinterpret_cast<U128*>(reinterpret_cast<u16*>(Cv) + (size_t)orow * ldc + n) = o;
-                            } else {
-                                *reinterpret_cast<float4*>(reinterpret_cast<float*>(Cv) + (size_t)orow * ldc + n) =
-                                    make_float4(v[0], v[1], v[2], v[3]);
-                            }
+                        if (OUT_BF16) {
+                            U128 o;
+                            o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+                            o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+                            o.z = (uint32_t)f2bf(v[4 % CW]) | ((uint32_t)f2bf(v[5 % CW]) << 16);
+                            o.w = (uint32_t)f2bf(v[6 % CW]) | ((uint32_t)f2bf(v[7 % CW]) << 16);
+                            *reinterpret_cast<U128*>(reinterpret_cast<u16*>(Cv) + (size_t)orow * ldc + n) = o;
+                        } else {
+                            *reinterpret_cast<float4*>(reinterpret_cast<float*>(Cv) + (size_t)orow * ldc + n) =
+                                make_float4(v[0], v[1], v[2], v[3]);
                         }
                     }
                 }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // scratch reads done before reuse
             }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // scratch reads done before reuse
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 8; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+            for (int j = 0; j < 4; ++j)
 #pragma unroll
-                for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+                for (int e = 0; e < 4; ++e) acc[i][j][e] = 0.f;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outstanding at exit
 #undef G2_READ
