@@ -379,7 +379,7 @@ def main():
                        "frames": frames, "global_batch": per_step, "parallelism": f"dp{N}",
                        "fused_boxes": fusion.stats["fused"],
                        "global_boxes": len(fusion.all_pred_box) if fusion.all_pred_box is not None else 0},
-            "roofline": {"bound": "mfma", "kernel": "k_gemm256<true,1> (persistent bf16 GEMM + bias + GELU: MLP up-projections of CLIP ViT-H and CuTR window blocks)",
+            "roofline": {"bound": "mfma", "kernel": "k_gemm256p<true,1> (persistent bf16 GEMM + bias + GELU: MLP up-projections of CLIP ViT-H and CuTR window blocks)",
                          "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_BF16_TFLOPS, "traffic": pmc.get("bytes_per_launch"),
                          "traffic_source": pmc.get("source"),

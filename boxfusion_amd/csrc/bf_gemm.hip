@@ -287,6 +287,27 @@ __global__ void __launch_bounds__(G_THREADS, 2) k_gemm(const u16* __restrict__ A
 #define CBAR() asm volatile("" ::: "memory")
 #define RAW_BARRIER() do { CBAR(); __builtin_amdgcn_s_barrier(); CBAR(); } while (0)
 
+// 16-B LDS-DMA through a buffer descriptor: byte offset `vo` (per lane) + `so` (wave-uniform)
+// from `base` (`nbytes` readable), written at the wave-uniform LDS address `lds` + 16*lane.
+__device__ __forceinline__ void glds_buf16(const void* base, int nbytes, void* lds, int vo, int so) {
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, nbytes, 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, vo, so, 0, 0);
+}
+
+// Grouped tile order of the persistent kernels: the linear tile index walks column-major inside
+// groups of `gm` row panels, so the 32 tiles an XCD runs concurrently (consecutive indices) form a
+// gm x (32/gm) patch -- gm A panels and 32/gm W panels per K-step in that XCD's L2 instead of
+// ~1.6 A panels and every W panel of the problem.  gm <= 1: plain row-major order.
+__device__ __forceinline__ void tile_coords(int tile, int tiles_m, int tiles_n, int gm, int& m0, int& n0) {
+    if (gm <= 1) { m0 = (tile / tiles_n) * 256; n0 = (tile % tiles_n) * 256; return; }
+    const int per = gm * tiles_n;
+    const int grp = tile / per, in = tile - grp * per;
+    const int rows = min(gm, tiles_m - grp * gm);
+    m0 = (grp * gm + in % rows) * 256;
+    n0 = (in / rows) * 256;
+}
+
 template <bool OUT_BF16, int ACT>
 __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict__ A, int lda,
                                                            const u16* __restrict__ W, int ldw,
@@ -295,7 +316,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict
                                                            int resid_mod, void* __restrict__ Cv,
                                                            int ldc, const int32_t* __restrict__ row_map,
                                                            int M, int N, int K, int tiles_n,
-                                                           int tiles_m) {
+                                                           int tiles_m, int gm) {
     extern __shared__ __attribute__((aligned(16))) unsigned char g_smem[];
     const int t = threadIdx.x;
     const int lane = t & 63, wave = t >> 6;
@@ -322,7 +343,8 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict
     auto stage_tile = [&](int stage, int g) {
         const int tile = slot + (g / nk) * G;
         const int k0 = (g % nk) * GB_K;
-        const int m0 = (tile / tiles_n) * 256, n0 = (tile % tiles_n) * 256;
+        int m0, n0;
+        tile_coords(tile, tiles_m, tiles_n, gm, m0, n0);
         unsigned char* sa = g_smem + stage * 65536 + wave * 4096;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -378,7 +400,8 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict
             const int gn = min(g + 2, total - 1);
             const int tile_n = slot + (gn / nk) * G;
             const int k0n = (gn % nk) * GB_K;
-            const int m0n = (tile_n / tiles_n) * 256, n0n = (tile_n % tiles_n) * 256;
+            int m0n, n0n;
+            tile_coords(tile_n, tiles_m, tiles_n, gm, m0n, n0n);
             unsigned char* sa_n = g_smem + st * 65536 + wave * 4096;
             const unsigned char* sr = g_smem + (st ^ 1) * 65536;
 #pragma unroll
@@ -407,7 +430,9 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict
 
         // ---- epilogue of this tile (wave-private, 16 rows = one row block per pass) ----------
         const int tile = slot + (g / nk) * G;
-        const int m0 = (tile / tiles_n) * 256 + wr * 128, n0 = (tile % tiles_n) * 256 + wc * 64;
+        int m0, n0;
+        tile_coords(tile, tiles_m, tiles_n, gm, m0, n0);
+        m0 += wr * 128; n0 += wc * 64;
         float bv[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -486,6 +511,286 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict
 #undef G2_MFMA
 }
 
+// ------------------------------------------------------------------------------------------
+// Persistent 256x256 kernel, staggered 4-phase schedule (k_gemm256p).
+//
+// Same tile, waves (2 M x 4 N, 128x64 per wave, v_mfma_f32_16x16x32_bf16) and persistent K-tile
+// walk as k_gemm256, but every K-tile (BK = 64) runs as 4 phases, one output quadrant (64x32) of
+// the wave each:  P1 (0,0)  P2 (0,1)  P3 (1,1)  P4 (1,0).  A phase = memory section (fragment
+// reads + one half-tile of LDS-DMA staging) | s_barrier | 16 MFMAs | s_barrier.  Waves 4-7 run one
+// barrier behind waves 0-3, so on every SIMD one wave's memory section overlaps its partner's
+// MFMAs.
+//
+// LDS stage (64 KiB) = four 16-KiB half-tiles: A-half h holds the rows {wr*128 + h*64 + [0,64)},
+// B-half h the columns {wc*64 + h*32 + [0,32)} of all waves, so quadrant (mi, ni) reads exactly
+// A-half mi and B-half ni.  Reads:  P1 B0 then A0 (the 4 B0 reads retired before the barrier),
+// P2 B1 (retired before the barrier), P3 A1, P4 none (A1 and B0 still in registers).  Each half is
+// restaged (for K-tile g+2, same stage) one phase after its reads were retired, two after
+// otherwise:  P2 B0, P3 A0, P4 B1, next P1 A1.  One counted wait per K-tile, vmcnt(6) in P4 before
+// its first barrier, retires K-tile g+1 with three half-tiles (6 LDS-DMA) still in flight; the
+// staggered half's readers are covered because every read sits one phase after that wait.
+// ------------------------------------------------------------------------------------------
+#define SB0() __builtin_amdgcn_sched_barrier(0)
+#define PHASE_BARRIER() do { SB0(); CBAR(); __builtin_amdgcn_s_barrier(); CBAR(); SB0(); } while (0)
+
+template <bool OUT_BF16, int ACT>
+__global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restrict__ A, int lda,
+                                                            const u16* __restrict__ W, int ldw,
+                                                            const float* __restrict__ bias,
+                                                            const float* __restrict__ resid, int ldr,
+                                                            int resid_mod, void* __restrict__ Cv,
+                                                            int ldc, const int32_t* __restrict__ row_map,
+                                                            int M, int N, int K, int tiles_n,
+                                                            int tiles_m, int stagger, int gm) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char g_smem[];
+    const int t = threadIdx.x;
+    const int lane = t & 63, wave = t >> 6;
+    const int wr = wave >> 2, wc = wave & 3;
+    const int lr = lane & 15, lq = lane >> 4;
+    const int ntiles = tiles_m * tiles_n;
+    const int G = gridDim.x;
+    const int slot = (G % 8 == 0) ? ((int)blockIdx.x % 8) * (G / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
+    const int my_tiles = ntiles > slot ? (ntiles - slot + G - 1) / G : 0;
+    const int nk = K / GB_K;
+    const int total = my_tiles * nk;
+    if (total == 0) return;
+
+    // half-tile staging: wave w, instruction i fills local rows (2w+i)*8 + lane/8 of a half.
+    // Buffer loads (LDS-DMA form): per-lane 32-bit byte offsets of the rows, computed once per
+    // output tile; the K position is the scalar soffset.
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    int a_row[2][2], b_row[2][2], scol[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int L = (wave * 2 + i) * 8 + (lane >> 3);
+        scol[i] = ((lane & 7) ^ swz_key(L)) * 16;                 // bytes
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            a_row[h][i] = (L >> 6) * 128 + h * 64 + (L & 63);     // tile row of A-half h
+            b_row[h][i] = (L >> 5) * 64 + h * 32 + (L & 31);      // tile column of B-half h
+        }
+    }
+    const int bytesA = (int)(((size_t)(M - 1) * lda + K) * 2);    // < 2^31 (checked on the host)
+    const int bytesW = (int)(((size_t)(N - 1) * ldw + K) * 2);
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    // K-tile coordinates of the walk, advanced incrementally (a division only at tile boundaries);
+    // past the end of the walk the last K-tile is repeated (same bytes into the same stage)
+    struct KT { int idx, m0, n0, k0, buf; };
+    auto kt_at_tile = [&](int tile_k, int idx) {
+        const int tile = slot + tile_k * G;
+        KT r;
+        r.idx = idx; tile_coords(tile, tiles_m, tiles_n, gm, r.m0, r.n0); r.k0 = 0; r.buf = idx & 1;
+        return r;
+    };
+    int tile_ord = 0;       // tile ordinal (within this block's walk) of the newest KT built
+    auto kt_next = [&](KT c) {
+        if (c.idx >= total - 1) return c;
+        if (c.k0 + GB_K < K) { c.k0 += GB_K; c.idx += 1; c.buf ^= 1; return c; }
+        ++tile_ord;
+        return kt_at_tile(tile_ord, c.idx + 1);
+    };
+    // per-lane row byte offsets of a K-tile's tile ([0..1] A-half h row i, [2..3] B-half)
+    struct VO { int a[2][2], b[2][2]; };
+    auto vo_of = [&](const KT& c) {
+        VO v;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                v.a[h][i] = min(c.m0 + a_row[h][i], M - 1) * lda * 2 + scol[i];
+                v.b[h][i] = min(c.n0 + b_row[h][i], N - 1) * ldw * 2 + scol[i];
+            }
+        return v;
+    };
+    // issue half `which` (0 A0, 1 A1, 2 B0, 3 B1) of K-tile c into its stage
+#define STAGE_HALF(c, v, which)                                                                    \
+    {                                                                                              \
+        unsigned char* dst_ = g_smem + (c).buf * 65536 + (which) * 16384 + wave_u * 2048;          \
+        _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                         \
+            if ((which) < 2)                                                                       \
+                glds_buf16(A, bytesA, dst_ + i_ * 1024, (v).a[(which) & 1][i_], (c).k0 * 2);       \
+            else                                                                                   \
+                glds_buf16(W, bytesW, dst_ + i_ * 1024, (v).b[(which) & 1][i_], (c).k0 * 2);       \
+        }                                                                                          \
+    }
+
+    f32x4 acc[8][4];
+    // In-place style residual (C = resid + A W^T + bias, no row map / broadcast): the accumulators
+    // start from the residual tile (loaded with 64-B row segments per 16 lanes), so the epilogue
+    // has no loads queued behind its own stores.
+    const bool acc_init = resid != nullptr && row_map == nullptr && resid_mod <= 0;
+#define ACC_INIT(m0_, n0_)                                                                         \
+    {                                                                                              \
+        if (acc_init) {                                                                            \
+            _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int e = 0; e < 4; ++e) { \
+                const float* rp_ = resid + (size_t)min((m0_) + wr * 128 + i * 16 + 4 * lq + e, M - 1) * ldr; \
+                _Pragma("unroll") for (int j = 0; j < 4; ++j)                                      \
+                    acc[i][j][e] = rp_[min((n0_) + wc * 64 + j * 16 + lr, N - 1)];                 \
+            }                                                                                      \
+        } else {                                                                                   \
+            _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 4; ++j) \
+                _Pragma("unroll") for (int e = 0; e < 4; ++e) acc[i][j][e] = 0.f;                  \
+        }                                                                                          \
+    }
+
+    bf16x8 fa[8], fb0[4], fb1[4];     // fa: A-half fragments [i*2 + ks]; fb*: [j*2 + ks]
+#define RD_A(stage, mi)                                                                            \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) \
+        fa[i * 2 + ks] = *reinterpret_cast<const bf16x8*>(                                         \
+            g_smem + (stage) * 65536 + (mi) * 16384 + swz(wr * 64 + i * 16 + lr, ks * 4 + lq));
+#define RD_B(FB, stage, ni)                                                                        \
+    _Pragma("unroll") for (int j = 0; j < 2; ++j) _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) \
+        FB[j * 2 + ks] = *reinterpret_cast<const bf16x8*>(                                         \
+            g_smem + (stage) * 65536 + 32768 + (ni) * 16384 + swz(wc * 32 + j * 16 + lr, ks * 4 + lq));
+#define MFMA_Q(mi, ni, FB)                                                                         \
+    {                                                                                              \
+        __builtin_amdgcn_s_setprio(1);                                                             \
+        _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i) \
+            _Pragma("unroll") for (int j = 0; j < 2; ++j) acc[(mi) * 4 + i][(ni) * 2 + j] =        \
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i * 2 + ks], FB[j * 2 + ks],            \
+                                                        acc[(mi) * 4 + i][(ni) * 2 + j], 0, 0, 0); \
+        __builtin_amdgcn_s_setprio(0);                                                             \
+    }
+
+    // prologue: K-tile 0 complete, three halves of K-tile 1 in flight
+    KT kc = kt_at_tile(0, 0);
+    KT k1 = kt_next(kc);
+    KT k2 = kt_next(k1);
+    VO v1 = vo_of(k1), v2 = vo_of(k2);
+    ACC_INIT(kc.m0, kc.n0);
+    {
+        const VO v0 = vo_of(kc);
+        STAGE_HALF(kc, v0, 2); STAGE_HALF(kc, v0, 0); STAGE_HALF(kc, v0, 3); STAGE_HALF(kc, v0, 1);
+    }
+    STAGE_HALF(k1, v1, 2); STAGE_HALF(k1, v1, 0); STAGE_HALF(k1, v1, 3);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    PHASE_BARRIER();
+    if (stagger && wr == 1) PHASE_BARRIER();      // stagger: waves 4-7 run one barrier behind
+
+    float* scratch = reinterpret_cast<float*>(g_smem + G2_STAGES_BYTES + wave * 4096);  // [16][64]
+    constexpr int CW = OUT_BF16 ? 8 : 4;
+    for (int g = 0; g < total; ++g) {
+        const int st = g & 1;
+        // ---- P1: quadrant (0,0); reads B0 (retired before the barrier) then A0; stage A1 of g+1
+        RD_B(fb0, st, 0);
+        SB0();
+        RD_A(st, 0);
+        STAGE_HALF(k1, v1, 1);
+        asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+        PHASE_BARRIER();
+        MFMA_Q(0, 0, fb0);
+        PHASE_BARRIER();
+        // ---- P2: quadrant (0,1); reads B1 (retired before the barrier); stage B0 of g+2
+        RD_B(fb1, st, 1);
+        STAGE_HALF(k2, v2, 2);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        PHASE_BARRIER();
+        MFMA_Q(0, 1, fb1);
+        PHASE_BARRIER();
+        // ---- P3: quadrant (1,1); reads A1; stage A0 of g+2
+        RD_A(st, 1);
+        STAGE_HALF(k2, v2, 0);
+        PHASE_BARRIER();
+        MFMA_Q(1, 1, fb1);
+        PHASE_BARRIER();
+        // ---- P4: quadrant (1,0) from registers; stage B1 of g+2; retire K-tile g+1
+        STAGE_HALF(k2, v2, 3);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        PHASE_BARRIER();
+        MFMA_Q(1, 0, fb0);
+        PHASE_BARRIER();
+        const KT kd = kc;
+        kc = k1; k1 = k2; v1 = v2;
+        {
+            const KT kn = kt_next(k2);
+            if (kn.k0 == 0 && kn.idx != k2.idx) v2 = vo_of(kn);   // entered a new tile
+            k2 = kn;
+        }
+        if (kd.k0 != K - GB_K) continue;
+
+        // ---- epilogue of this tile (wave-private, 16 rows = one row block per pass) ----------
+        const int m0 = kd.m0 + wr * 128, n0 = kd.n0 + wc * 64;
+        float bv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = n0 + j * 16 + lr;
+            bv[j] = (bias && n < N) ? bias[min(n, N - 1)] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                f32x2 v01 = {acc[i][j][0] + bv[j], acc[i][j][1] + bv[j]};
+                f32x2 v23 = {acc[i][j][2] + bv[j], acc[i][j][3] + bv[j]};
+                if (ACT == 1) { v01 = gelu_erf2(v01); v23 = gelu_erf2(v23); }
+                else if (ACT == 2) {
+                    v01.x = fmaxf(v01.x, 0.f); v01.y = fmaxf(v01.y, 0.f);
+                    v23.x = fmaxf(v23.x, 0.f); v23.y = fmaxf(v23.y, 0.f);
+                }
+                const int rl = 4 * lq;
+                const int col = (j * 16 + lr) ^ (lq << 4);
+                scratch[(rl + 0) * 64 + col] = v01.x;
+                scratch[(rl + 1) * 64 + col] = v01.y;
+                scratch[(rl + 2) * 64 + col] = v23.x;
+                scratch[(rl + 3) * 64 + col] = v23.y;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int it = 0; it < 16 * (64 / CW) / 64; ++it) {
+                const int id = it * 64 + lane;
+                const int rl = id / (64 / CW), cl = (id % (64 / CW)) * CW;
+                const int m = m0 + i * 16 + rl, n = n0 + cl;
+                const int sw = ((rl >> 2) & 3) << 4;
+                float v[CW];
+#pragma unroll
+                for (int q = 0; q < CW; q += 4) {
+                    const float4 x = *reinterpret_cast<const float4*>(scratch + rl * 64 + ((cl + q) ^ sw));
+                    v[q] = x.x; v[q + 1] = x.y; v[q + 2] = x.z; v[q + 3] = x.w;
+                }
+                if (m < M && n < N) {
+                    const int orow = row_map ? row_map[m] : m;
+                    if (orow >= 0) {
+                        if (resid && !acc_init) {
+                            const int rrow = resid_mod > 0 ? (m % resid_mod) : orow;
+                            const float* rp = resid + (size_t)rrow * ldr + n;
+#pragma unroll
+                            for (int q = 0; q < CW; q += 4) {
+                                const float4 x = *reinterpret_cast<const float4*>(rp + q);
+                                v[q] += x.x; v[q + 1] += x.y; v[q + 2] += x.z; v[q + 3] += x.w;
+                            }
+                        }
+                        if (OUT_BF16) {
+                            U128 o;
+                            o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+                            o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+                            o.z = (uint32_t)f2bf(v[4 % CW]) | ((uint32_t)f2bf(v[5 % CW]) << 16);
+                            o.w = (uint32_t)f2bf(v[6 % CW]) | ((uint32_t)f2bf(v[7 % CW]) << 16);
+                            *reinterpret_cast<U128*>(reinterpret_cast<u16*>(Cv) + (size_t)orow * ldc + n) = o;
+                        } else {
+                            *reinterpret_cast<float4*>(reinterpret_cast<float*>(Cv) + (size_t)orow * ldc + n) =
+                                make_float4(v[0], v[1], v[2], v[3]);
+                        }
+                    }
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // scratch reads done before reuse
+        }
+        ACC_INIT(kc.m0, kc.n0);    // the next tile (kc is its first K-tile; a repeat past the end)
+    }
+    if (stagger && wr == 0) PHASE_BARRIER();      // both halves leave with the same barrier count
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outstanding at exit
+#undef RD_A
+#undef RD_B
+#undef MFMA_Q
+#undef STAGE_HALF
+#undef ACC_INIT
+}
+
+static int g_gemm_variant = 1;   // 0: k_gemm256, 1: k_gemm256p (staggered 4-phase schedule), 2: k_gemm256p unstaggered
+BF_API void bf_gemm_set_variant(int v) { g_gemm_variant = v; }
+static int g_group_m = 8;        // row panels per tile group (tile_coords); 1 = row-major
+BF_API void bf_gemm_set_group_m(int g) { g_group_m = g; }
+
 template <bool OB, int AC>
 static void launch_gemm256(int grid, hipStream_t st, const void* A, int lda, const void* W, int ldw,
                            const float* bias, const float* resid, int ldr, int resid_mod, void* C,
@@ -495,11 +800,18 @@ static void launch_gemm256(int grid, hipStream_t st, const void* A, int lda, con
     if (!attr) {
         hipFuncSetAttribute((const void*)k_gemm256<OB, AC>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             G2_LDS);
+        hipFuncSetAttribute((const void*)k_gemm256p<OB, AC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            G2_LDS);
         attr = true;
     }
-    hipLaunchKernelGGL((k_gemm256<OB, AC>), dim3(grid), dim3(G2_THREADS), G2_LDS, st, (const u16*)A, lda,
-                       (const u16*)W, ldw, bias, resid, ldr, resid_mod, C, ldc, row_map, M, N, K,
-                       tiles_n, tiles_m);
+    if (g_gemm_variant >= 1)
+        hipLaunchKernelGGL((k_gemm256p<OB, AC>), dim3(grid), dim3(G2_THREADS), G2_LDS, st, (const u16*)A,
+                           lda, (const u16*)W, ldw, bias, resid, ldr, resid_mod, C, ldc, row_map, M, N,
+                           K, tiles_n, tiles_m, g_gemm_variant == 1 ? 1 : 0, g_group_m);
+    else
+        hipLaunchKernelGGL((k_gemm256<OB, AC>), dim3(grid), dim3(G2_THREADS), G2_LDS, st, (const u16*)A,
+                           lda, (const u16*)W, ldw, bias, resid, ldr, resid_mod, C, ldc, row_map, M, N,
+                           K, tiles_n, tiles_m, g_group_m);
 }
 
 static int g_force_small = 0;

@@ -216,6 +216,12 @@ int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bi
  * run the 256x256 8-wave kernel, the rest the 128x128 4-wave kernel.  Test hook: a non-zero
  * argument forces the 128x128 kernel for every shape (process-wide). */
 void bf_gemm_force_small_tiles(int on);
+/* Persistent 256x256 kernel variant: 0 = k_gemm256 (one barrier per K-tile), 1 = k_gemm256p
+ * (staggered 4-phase schedule, default).  Test/benchmark hook; results are identical in value. */
+void bf_gemm_set_variant(int v);
+/* Row panels per tile group of the persistent kernels' tile order (default 8; 1 = row-major).
+ * Test/benchmark hook; results are identical in value. */
+void bf_gemm_set_group_m(int g);
 /* 1 if an aligned (16-B rows) problem of this shape runs the 256x256 kernel (k_gemm256), 0 if the
  * 128x128 one (k_gemm) — lets profilers attribute launches to kernels. */
 int bf_gemm_large_tiles(int M, int N, int K);

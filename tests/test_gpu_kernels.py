@@ -97,6 +97,36 @@ def test_gemm_large_tiles(L, small, shape, act, out_bf16, use_resid):
         lib().bf_gemm_force_small_tiles(0)
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("shape", [(3000, 2816, 320), (8292, 1280, 640), (600, 384, 64)])
+@pytest.mark.parametrize("inplace,out_bf16", [(True, False), (False, False), (False, True)])
+def test_gemm_resid_persistent(L, variant, shape, inplace, out_bf16):
+    """residual without a row map (the accumulator-initialised path of k_gemm256p) and the
+    schedule variants: in place (x += proj(h)) and out of place, partial tiles, f32 and bf16 out"""
+    from boxfusion_amd._lib import lib
+    g = torch.Generator(device="cuda").manual_seed(5)
+    M, N, K = shape
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g)
+    resid = torch.randn(M, N, device="cuda", generator=g)
+    ref = resid + a.float() @ w.float().T + b
+    lib().bf_gemm_set_variant(variant)
+    try:
+        if inplace:
+            out = resid.clone()
+            L.gemm(a, w, b, resid=out, out=out)
+        else:
+            out = L.gemm(a, w, b, resid=resid, out_dtype=torch.bfloat16 if out_bf16 else torch.float32)
+        assert rel_err(out, ref) < (5e-3 if out_bf16 else 1e-5)
+        # a second call on the same output buffer (persistent walk state must not leak)
+        if not inplace:
+            out2 = L.gemm(a, w, b, resid=resid, out_dtype=out.dtype)
+            assert torch.equal(out2, out)
+    finally:
+        lib().bf_gemm_set_variant(1)
+
+
 def _attn_ref(q, k, v, B, H, S, D, scale):
     qq = q.float().view(B, S, H, D).transpose(1, 2)
     kk = k.float().view(B, -1, H, D).transpose(1, 2)
