@@ -189,14 +189,16 @@ def corr_assoc(corners, dims, scores, boxes2d, init_id, cam_poses, cur_pose, K, 
 # fusion
 # ------------------------------------------------------------------------------------------
 def fusion_fit(view_off, n_views, view_box, view_R, view_score, view_pose, view_tc, pst,
-               cfg: FuseCfg, trace=False, max_views=None):
-    """max_views: host-known bound on n_views (avoids a device read when given)."""
+               cfg: FuseCfg, trace=False, max_views=None, packed_out=False):
+    """max_views: host-known bound on n_views (avoids a device read when given).
+    packed_out: return (out_box, packed, trace) with packed = int32 [updated(n_jobs),
+    iterations(n_jobs), status] (one device->host copy for the caller)."""
     dev = view_box.device
     n_jobs = view_off.shape[0]
     out_box = torch.empty((n_jobs, 6), dtype=torch.float32, device=dev)
-    out_upd = torch.empty(n_jobs, dtype=torch.int32, device=dev)
-    out_it = torch.empty(n_jobs, dtype=torch.int32, device=dev)
-    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    # updated flags, iteration counts and the status word in one buffer: one read-back
+    packed = torch.zeros(2 * n_jobs + 1, dtype=torch.int32, device=dev)
+    out_upd, out_it, status = packed[:n_jobs], packed[n_jobs:2 * n_jobs], packed[2 * n_jobs:]
     tr = (torch.empty((n_jobs, cfg.iters, cfg.pst_size), dtype=torch.float32, device=dev)
           if trace else None)
     if max_views is None:
@@ -211,6 +213,8 @@ def fusion_fit(view_off, n_views, view_box, view_R, view_score, view_pose, view_
                            _ptr(view_tc), _ptr(pst), ctypes.byref(cfg), _ptr(out_box),
                            _ptr(out_upd), _ptr(out_it), _ptr(tr), _ptr(status), _ptr(ws),
                            _stream()), "bf_fusion_fit")
+    if packed_out:
+        return out_box, packed, tr
     return out_box, out_upd, out_it, status, tr
 
 

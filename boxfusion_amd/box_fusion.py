@@ -84,19 +84,23 @@ class BoxFusion:
         if not jobs:
             return
         dev = self.device
-        flat = torch.as_tensor(np.concatenate([np.asarray(fl, np.int64) for _, fl in jobs]), device=dev)
         nv = np.array([len(fl) for _, fl in jobs], np.int32)
         off = np.concatenate([[0], np.cumsum(nv)[:-1]]).astype(np.int32)
+        # one upload: view offsets, view counts, flattened view indices
+        host = np.concatenate([off, nv] + [np.asarray(fl, np.int32) for _, fl in jobs])
+        idx = torch.from_numpy(host).to(dev, non_blocking=True)
+        nj = len(jobs)
+        flat = idx[2 * nj:]
         b3 = per_frame_box.pred_boxes_3d
-        out_box, out_upd, out_it, status, _ = _lib.fusion_fit(
-            torch.as_tensor(off, device=dev), torch.as_tensor(nv, device=dev),
+        out_box, packed, _ = _lib.fusion_fit(
+            idx[:nj], idx[nj:2 * nj],
             b3.tensor.index_select(0, flat).contiguous(), b3.R.index_select(0, flat).contiguous(),
             per_frame_box.scores.to(dev, torch.float32).index_select(0, flat).contiguous(),
             per_frame_box.cam_pose.to(dev, torch.float32).index_select(0, flat).contiguous(),
             per_frame_box.projected_boxes.index_select(0, flat).contiguous(),
-            self._pst_dev, self.fuse_cfg(), max_views=min(int(nv.max()), 32))
-        upd = out_upd.cpu().numpy()
-        st = int(status.cpu().numpy()[0])
+            self._pst_dev, self.fuse_cfg(), max_views=min(int(nv.max()), 32), packed_out=True)
+        h = packed.cpu().numpy()              # the only device->host read of the call
+        upd, iters, st = h[:nj], h[nj:2 * nj], int(h[2 * nj])
         if st & _lib.BF_DEV_VIEW_OVERFLOW:
             raise _lib.HipError("bf_fusion_fit: a fusion list has more views than the kernel holds")
         target = all_pred_box.pred_boxes_3d.tensor
@@ -113,4 +117,4 @@ class BoxFusion:
             target[torch.as_tensor(rows, device=target.device)] = \
                 out_box[torch.as_tensor(src, device=out_box.device)].to(target.device)
         self.last_stats["updated"] = len(rows)
-        self.last_stats["iters"] = int(out_it.sum().item())
+        self.last_stats["iters"] = int(iters.sum())

@@ -541,7 +541,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
                                                             int resid_mod, void* __restrict__ Cv,
                                                             int ldc, const int32_t* __restrict__ row_map,
                                                             int M, int N, int K, int tiles_n,
-                                                            int tiles_m, int stagger, int gm) {
+                                                            int tiles_m, int stagger, int gm, int ablate) {
     extern __shared__ __attribute__((aligned(16))) unsigned char g_smem[];
     const int t = threadIdx.x;
     const int lane = t & 63, wave = t >> 6;
@@ -652,30 +652,42 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
         __builtin_amdgcn_s_setprio(0);                                                             \
     }
 
-    // prologue: K-tile 0 complete, three halves of K-tile 1 in flight
+    // prologue: K-tile 0 complete, K-tile 1 in flight
     KT kc = kt_at_tile(0, 0);
     KT k1 = kt_next(kc);
     KT k2 = kt_next(k1);
-    VO v1 = vo_of(k1), v2 = vo_of(k2);
+    VO v2 = vo_of(k2);
     ACC_INIT(kc.m0, kc.n0);
     {
         const VO v0 = vo_of(kc);
         STAGE_HALF(kc, v0, 2); STAGE_HALF(kc, v0, 0); STAGE_HALF(kc, v0, 3); STAGE_HALF(kc, v0, 1);
     }
-    STAGE_HALF(k1, v1, 2); STAGE_HALF(k1, v1, 0); STAGE_HALF(k1, v1, 3);
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    {
+        const VO v1 = vo_of(k1);
+        STAGE_HALF(k1, v1, 2); STAGE_HALF(k1, v1, 0); STAGE_HALF(k1, v1, 3); STAGE_HALF(k1, v1, 1);
+    }
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     PHASE_BARRIER();
     if (stagger && wr == 1) PHASE_BARRIER();      // stagger: waves 4-7 run one barrier behind
 
     float* scratch = reinterpret_cast<float*>(g_smem + G2_STAGES_BYTES + wave * 4096);  // [16][64]
     constexpr int CW = OUT_BF16 ? 8 : 4;
+    constexpr int NIT = 16 * (64 / CW) / 64;      // 16-B stores per lane per 16-row pass
+    int stores_pending = 0;   // stores of a full-tile epilogue issued after K-tile g+1's halves
+    float bv[4];
     for (int g = 0; g < total; ++g) {
         const int st = g & 1;
-        // ---- P1: quadrant (0,0); reads B0 (retired before the barrier) then A0; stage A1 of g+1
+        if (kc.k0 == 0) {     // first K-tile of a tile: its bias columns (loaded well before use)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int n = kc.n0 + wc * 64 + j * 16 + lr;
+                bv[j] = bias ? bias[min(n, N - 1)] : 0.f;
+            }
+        }
+        // ---- P1: quadrant (0,0); reads B0 (retired before the barrier) then A0
         RD_B(fb0, st, 0);
         SB0();
         RD_A(st, 0);
-        STAGE_HALF(k1, v1, 1);
         asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
         PHASE_BARRIER();
         MFMA_Q(0, 0, fb0);
@@ -687,35 +699,50 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
         PHASE_BARRIER();
         MFMA_Q(0, 1, fb1);
         PHASE_BARRIER();
-        // ---- P3: quadrant (1,1); reads A1; stage A0 of g+2
+        // ---- P3: quadrant (1,1); reads A1 (retired before the barrier); stage A0 of g+2
         RD_A(st, 1);
         STAGE_HALF(k2, v2, 0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         PHASE_BARRIER();
         MFMA_Q(1, 1, fb1);
         PHASE_BARRIER();
-        // ---- P4: quadrant (1,0) from registers; stage B1 of g+2; retire K-tile g+1
+        // ---- P4: quadrant (1,0) from registers; stage B1 and A1 of g+2; retire K-tile g+1 (the
+        // stores of an epilogue issued since K-tile g+1 was staged may stay in flight)
         STAGE_HALF(k2, v2, 3);
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        STAGE_HALF(k2, v2, 1);
+        if (stores_pending) {
+            if (OUT_BF16) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");   // 8 + 8*NIT
+            else asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+            stores_pending = 0;
+        } else {
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        }
         PHASE_BARRIER();
         MFMA_Q(1, 0, fb0);
         PHASE_BARRIER();
         const KT kd = kc;
-        kc = k1; k1 = k2; v1 = v2;
+        kc = k1; k1 = k2;
         {
             const KT kn = kt_next(k2);
             if (kn.k0 == 0 && kn.idx != k2.idx) v2 = vo_of(kn);   // entered a new tile
             k2 = kn;
         }
         if (kd.k0 != K - GB_K) continue;
+        if (ablate == 1) {          // diagnostic: no epilogue at all (keeps acc live)
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) asm volatile("" :: "v"(acc[i][j]));
+            ACC_INIT(kc.m0, kc.n0);
+            continue;
+        }
 
         // ---- epilogue of this tile (wave-private, 16 rows = one row block per pass) ----------
+        // Full in-bounds sub-tiles without a row map or residual loads take the fast path: no
+        // bounds tests, exactly 8*NIT stores, which the next K-tile's counted wait leaves in flight.
         const int m0 = kd.m0 + wr * 128, n0 = kd.n0 + wc * 64;
-        float bv[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int n = n0 + j * 16 + lr;
-            bv[j] = (bias && n < N) ? bias[min(n, N - 1)] : 0.f;
-        }
+        const bool fast = row_map == nullptr && (resid == nullptr || acc_init) && m0 + 128 <= M &&
+                          n0 + 64 <= N && ablate == 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
 #pragma unroll
@@ -736,7 +763,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-            for (int it = 0; it < 16 * (64 / CW) / 64; ++it) {
+            for (int it = 0; it < NIT; ++it) {
                 const int id = it * 64 + lane;
                 const int rl = id / (64 / CW), cl = (id % (64 / CW)) * CW;
                 const int m = m0 + i * 16 + rl, n = n0 + cl;
@@ -747,34 +774,44 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
                     const float4 x = *reinterpret_cast<const float4*>(scratch + rl * 64 + ((cl + q) ^ sw));
                     v[q] = x.x; v[q + 1] = x.y; v[q + 2] = x.z; v[q + 3] = x.w;
                 }
-                if (m < M && n < N) {
-                    const int orow = row_map ? row_map[m] : m;
-                    if (orow >= 0) {
-                        if (resid && !acc_init) {
-                            const int rrow = resid_mod > 0 ? (m % resid_mod) : orow;
-                            const float* rp = resid + (size_t)rrow * ldr + n;
+                int orow = m;
+                bool keep = true;
+                if (ablate == 2) {   // diagnostic: no global stores
 #pragma unroll
-                            for (int q = 0; q < CW; q += 4) {
-                                const float4 x = *reinterpret_cast<const float4*>(rp + q);
-                                v[q] += x.x; v[q + 1] += x.y; v[q + 2] += x.z; v[q + 3] += x.w;
-                            }
+                    for (int q = 0; q < CW; ++q) asm volatile("" :: "v"(v[q]));
+                    keep = false;
+                } else if (!fast) {
+                    keep = m < M && n < N;
+                    if (keep && row_map) orow = row_map[m];
+                    keep = keep && orow >= 0;
+                    if (keep && resid && !acc_init) {
+                        const int rrow = resid_mod > 0 ? (m % resid_mod) : orow;
+                        const float* rp = resid + (size_t)rrow * ldr + n;
+#pragma unroll
+                        for (int q = 0; q < CW; q += 4) {
+                            const float4 x = *reinterpret_cast<const float4*>(rp + q);
+                            v[q] += x.x; v[q + 1] += x.y; v[q + 2] += x.z; v[q + 3] += x.w;
                         }
-                        if (OUT_BF16) {
-                            U128 o;
-                            o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-                            o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-                            o.z = (uint32_t)f2bf(v[4 % CW]) | ((uint32_t)f2bf(v[5 % CW]) << 16);
-                            o.w = (uint32_t)f2bf(v[6 % CW]) | ((uint32_t)f2bf(v[7 % CW]) << 16);
-                            *reinterpret_cast<U128*>(reinterpret_cast<u16*>(Cv) + (size_t)orow * ldc + n) = o;
-                        } else {
-                            *reinterpret_cast<float4*>(reinterpret_cast<float*>(Cv) + (size_t)orow * ldc + n) =
-                                make_float4(v[0], v[1], v[2], v[3]);
-                        }
+                    }
+                }
+                if (keep) {
+                    if (OUT_BF16) {
+                        U128 o;
+                        o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+                        o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+                        o.z = (uint32_t)f2bf(v[4 % CW]) | ((uint32_t)f2bf(v[5 % CW]) << 16);
+                        o.w = (uint32_t)f2bf(v[6 % CW]) | ((uint32_t)f2bf(v[7 % CW]) << 16);
+                        *reinterpret_cast<U128*>(reinterpret_cast<u16*>(Cv) + (size_t)orow * ldc + n) = o;
+                    } else {
+                        *reinterpret_cast<float4*>(reinterpret_cast<float*>(Cv) + (size_t)orow * ldc + n) =
+                            make_float4(v[0], v[1], v[2], v[3]);
                     }
                 }
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // scratch reads done before reuse
         }
+        // the next tile's accumulator init loads would be ordered behind these stores
+        stores_pending = (fast && !acc_init) ? 1 : 0;
         ACC_INIT(kc.m0, kc.n0);    // the next tile (kc is its first K-tile; a repeat past the end)
     }
     if (stagger && wr == 0) PHASE_BARRIER();      // both halves leave with the same barrier count
@@ -807,7 +844,7 @@ static void launch_gemm256(int grid, hipStream_t st, const void* A, int lda, con
     if (g_gemm_variant >= 1)
         hipLaunchKernelGGL((k_gemm256p<OB, AC>), dim3(grid), dim3(G2_THREADS), G2_LDS, st, (const u16*)A,
                            lda, (const u16*)W, ldw, bias, resid, ldr, resid_mod, C, ldc, row_map, M, N,
-                           K, tiles_n, tiles_m, g_gemm_variant == 1 ? 1 : 0, g_group_m);
+                           K, tiles_n, tiles_m, g_gemm_variant == 2 ? 0 : 1, g_group_m, g_gemm_variant >= 3 ? g_gemm_variant - 2 : 0);
     else
         hipLaunchKernelGGL((k_gemm256<OB, AC>), dim3(grid), dim3(G2_THREADS), G2_LDS, st, (const u16*)A,
                            lda, (const u16*)W, ldw, bias, resid, ldr, resid_mod, C, ldc, row_map, M, N,

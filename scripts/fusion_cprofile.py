@@ -23,4 +23,5 @@ for f in range(60):
     st.keyframe(f, scene.pose(f), dets[f])
 torch.cuda.synchronize()
 pr.disable()
-pstats.Stats(pr).sort_stats("tottime").print_stats(30)
+pstats.Stats(pr).sort_stats("tottime").print_stats(25)
+pstats.Stats(pr).sort_stats("cumtime").print_stats(45)
