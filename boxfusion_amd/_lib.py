@@ -71,7 +71,9 @@ def _ptr(t):
 
 
 def _stream():
-    return c_void_p(torch.cuda.current_stream().cuda_stream)
+    # the raw handle of the calling thread's current stream (torch.cuda.current_stream() builds a
+    # Stream object through several device-index lookups: ~10 us per call on the fusion path)
+    return c_void_p(torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice()))
 
 
 _SYNC_DEBUG = os.environ.get("BF_SYNC_DEBUG", "0") == "1"

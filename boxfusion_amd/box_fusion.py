@@ -53,6 +53,7 @@ class BoxFusion:
         self.device = torch.device(device)
         self._pst_dev = torch.from_numpy(self.PST[: self.pst_size]).to(self.device).contiguous()
         self.last_stats = {}
+        self.updated_total = 0    # boxes updated over every call (resolved results)
 
     def update_intrinsics(self, size, K):
         self.H = size[1]
@@ -77,20 +78,32 @@ class BoxFusion:
             c.K[i] = float(k[i])
         return c
 
-    def boxfusion(self, all_pred_box, per_frame_box, box_manager, beta=0.9, verbose=False):
-        jobs = [(i, fl) for i, fl in enumerate(box_manager.fusion_list[: len(all_pred_box)])
-                if len(fl) >= 3 and not box_manager.check_if_fusion(fl)]
+    def boxfusion(self, all_pred_box, per_frame_box, box_manager, beta=0.9, verbose=False,
+                  defer=False):
+        """box_fusion.py:622-724 on bf_fusion_fit.  defer=True (FusionStage) writes the fused boxes
+        back on the device and leaves the host bookkeeping (fusion_flag, already_fusion, stats)
+        to the box manager's next read of that state, so no synchronisation happens here."""
+        box_manager.flush()
+        jobs, seen = [], set()
+        for i, fl in enumerate(box_manager.fusion_list[: len(all_pred_box)]):
+            if len(fl) >= 3 and not box_manager.check_if_fusion(fl):
+                key = tuple(fl)
+                if key in seen:   # an identical list earlier in this call wins (its result is the same)
+                    continue
+                seen.add(key)
+                jobs.append((i, fl))
         self.last_stats = dict(jobs=len(jobs), updated=0, views=sum(len(f) for _, f in jobs))
         if not jobs:
             return
         dev = self.device
+        nj = len(jobs)
         nv = np.array([len(fl) for _, fl in jobs], np.int32)
         off = np.concatenate([[0], np.cumsum(nv)[:-1]]).astype(np.int32)
-        # one upload: view offsets, view counts, flattened view indices
-        host = np.concatenate([off, nv] + [np.asarray(fl, np.int32) for _, fl in jobs])
+        rows = np.array([i for i, _ in jobs], np.int32)
+        # one upload: view offsets, view counts, target rows, flattened view indices
+        host = np.concatenate([off, nv, rows] + [np.asarray(fl, np.int32) for _, fl in jobs])
         idx = torch.from_numpy(host).to(dev, non_blocking=True)
-        nj = len(jobs)
-        flat = idx[2 * nj:]
+        flat = idx[3 * nj:]
         b3 = per_frame_box.pred_boxes_3d
         out_box, packed, _ = _lib.fusion_fit(
             idx[:nj], idx[nj:2 * nj],
@@ -99,22 +112,29 @@ class BoxFusion:
             per_frame_box.cam_pose.to(dev, torch.float32).index_select(0, flat).contiguous(),
             per_frame_box.projected_boxes.index_select(0, flat).contiguous(),
             self._pst_dev, self.fuse_cfg(), max_views=min(int(nv.max()), 32), packed_out=True)
-        h = packed.cpu().numpy()              # the only device->host read of the call
-        upd, iters, st = h[:nj], h[nj:2 * nj], int(h[2 * nj])
-        if st & _lib.BF_DEV_VIEW_OVERFLOW:
-            raise _lib.HipError("bf_fusion_fit: a fusion list has more views than the kernel holds")
+        # write-back of the updated rows on the device (xyz + lhw; R unchanged, quirk 6)
         target = all_pred_box.pred_boxes_3d.tensor
-        rows, src = [], []
-        for j, (i, fl) in enumerate(jobs):
-            if box_manager.check_if_fusion(fl):   # an identical list already fused in this call
-                continue
-            if upd[j]:
-                rows.append(i)
-                src.append(j)
-                box_manager.update_fusion_flag(i)
-                box_manager.add_fusion_ind(fl)
-        if rows:
-            target[torch.as_tensor(rows, device=target.device)] = \
-                out_box[torch.as_tensor(src, device=out_box.device)].to(target.device)
-        self.last_stats["updated"] = len(rows)
-        self.last_stats["iters"] = int(iters.sum())
+        rows_dev = idx[2 * nj:3 * nj].long()
+        upd_dev = packed[:nj]
+        target[rows_dev] = torch.where(upd_dev[:, None] != 0, out_box.to(target.device),
+                                       target.index_select(0, rows_dev))
+
+        def resolve():
+            h = packed.cpu().numpy()
+            upd, iters, st = h[:nj], h[nj:2 * nj], int(h[2 * nj])
+            if st & _lib.BF_DEV_VIEW_OVERFLOW:
+                raise _lib.HipError("bf_fusion_fit: a fusion list has more views than the kernel holds")
+            n_upd = 0
+            for j, (i, fl) in enumerate(jobs):
+                if upd[j]:
+                    n_upd += 1
+                    box_manager.update_fusion_flag(i)
+                    box_manager.add_fusion_ind(fl)
+            self.last_stats["updated"] = n_upd
+            self.last_stats["iters"] = int(iters.sum())
+            self.updated_total += n_upd
+
+        if defer:
+            box_manager._pending = resolve
+        else:
+            resolve()

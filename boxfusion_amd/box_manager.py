@@ -22,8 +22,9 @@ class BoxManager:
     def __init__(self, cfg):
         self.fusion_list = []
         self.last_fusion_frame = []
-        self.fusion_flag = []
-        self.already_fusion = []
+        self._fusion_flag = []
+        self._already_fusion = []
+        self._pending = None      # resolves a deferred BoxFusion result (box_fusion.py)
         self.num_record = {}
         self.cfg = cfg
         self.rotation_gap = cfg["association"]["rotation_gap"]
@@ -32,15 +33,40 @@ class BoxManager:
         self.list_capacity = int(cfg.get("box_fusion", {}).get("list_capacity", DEFAULT_LIST_CAPACITY))
         self.merge_log = []
 
+    # fusion_flag / already_fusion are plain lists in the reference; here every read first applies
+    # a deferred BoxFusion.boxfusion result, so callers always see the reference's state
+    @property
+    def fusion_flag(self):
+        self.flush()
+        return self._fusion_flag
+
+    @fusion_flag.setter
+    def fusion_flag(self, v):
+        self._fusion_flag = v
+
+    @property
+    def already_fusion(self):
+        self.flush()
+        return self._already_fusion
+
+    @already_fusion.setter
+    def already_fusion(self, v):
+        self._already_fusion = v
+
+    def flush(self):
+        if self._pending is not None:
+            f, self._pending = self._pending, None
+            f()
+
     # -- reference API ---------------------------------------------------------------------------
     def init_new_predictions(self, box_num, all_num):
         for i in range(box_num):
             self.fusion_list.append([i + all_num])
             self.last_fusion_frame.append([0])
-            self.fusion_flag.append(0)
+            self._fusion_flag.append(0)     # order-independent of a pending fusion result
 
     def add_fusion_ind(self, idx_list):
-        self.already_fusion.append(copy.deepcopy(idx_list))
+        self._already_fusion.append(copy.deepcopy(idx_list))
 
     def check_if_fusion(self, idx_list):
         return idx_list in self.already_fusion
@@ -49,7 +75,7 @@ class BoxManager:
         self.fusion_list = [self.fusion_list[i] for i in keep_idx]
 
     def update_fusion_flag(self, idx):
-        self.fusion_flag[idx] = 1
+        self._fusion_flag[idx] = 1
 
     def get_fusion_idx(self):
         return [i for i in range(len(self.fusion_flag)) if self.fusion_flag[i] == 1]

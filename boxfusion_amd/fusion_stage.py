@@ -49,7 +49,14 @@ class FusionStage:
         self.all_kf_pose = {}
         self.box_count = 0
         self.last_pred = None
-        self.stats = dict(keyframes=0, suppressed=0, fused=0)
+        self._stats = dict(keyframes=0, suppressed=0)
+        self.K_dev = torch.from_numpy(self.K3).to(self.dev)     # uploaded once
+
+    @property
+    def stats(self):
+        """keyframes, suppressed boxes, fused boxes (resolves a deferred fusion result)"""
+        self.box_manager.flush()
+        return dict(self._stats, fused=self.fuser.updated_total)
 
     def keyframe(self, count, pose, pred):
         """pred: Instances3D of this keyframe in CAMERA coordinates (after the detection filters
@@ -63,13 +70,13 @@ class FusionStage:
         if n == 0:
             bm.num_record[count] = self.box_count
             return
-        self.stats["keyframes"] += 1
+        self._stats["keyframes"] += 1
         pred.cam_pose = torch.from_numpy(pose_np).to(self.dev)
         pred.frame_id = torch.full((n,), count, dtype=torch.int64, device=self.dev)
         pred.init_id = self.box_count + torch.arange(n, device=self.dev)
         pred.valid_num = torch.zeros(n, device=self.dev)
         pred.pred_boxes_3d.transform2world(pred.cam_pose)
-        pred.project_3d_boxes(self.K3, H=self.H, W=self.W)
+        pred.project_3d_boxes(self.K_dev, H=self.H, W=self.W)
         self.box_count += n
         bm.num_record[count] = self.box_count
         if self.all_pred_box is None and (count < self.gap or self.per_frame_ins is None):
@@ -84,23 +91,24 @@ class FusionStage:
         all_pred_box = Instances3D.cat([self.all_pred_box, pred])
         self.per_frame_ins = Instances3D.cat([self.per_frame_ins, pred])
         all_poses = np.concatenate((self.all_poses, pose_np), axis=0)
+        corners = all_pred_box.pred_boxes_3d.corners       # shared by both association steps
         mask, success = Instances3D.spatial_association(all_pred_box, cfg["box_fusion"]["nms_threshold"],
-                                                        bm, self.per_frame_ins.cam_pose)
-        self.stats["suppressed"] += len(success)
+                                                        bm, self.per_frame_ins.cam_pose, corners=corners)
+        self._stats["suppressed"] += len(success)
         cur_keep = [i - n_before for i in mask if i >= n_before]
         cur_success = [i - n_before for i in success if i >= n_before]
         keep_idx = np.asarray(mask)
         if cur_keep:
             all_pred_box, all_poses, keep_idx = Instances3D.correspondence_association(
                 cfg, bm, cur_keep, cur_success, pred, cur_global, all_pred_box, all_poses,
-                self.per_frame_ins.cam_pose, count, mask, self.K3, self.all_kf_pose,
-                threshold=cfg["association"]["small_threshold"], H=self.H, W=self.W)
+                self.per_frame_ins.cam_pose, count, mask, self.K_dev, self.all_kf_pose,
+                threshold=cfg["association"]["small_threshold"], H=self.H, W=self.W,
+                corners=corners, cur_pose=pred.cam_pose[0])
             bm.update(keep_idx)
             if cfg["box_fusion"].get("check_valid", False):
                 all_pred_box = bm.check_valid_num(all_pred_box, count, self.gap)
             if cfg["box_fusion"].get("use", True):
-                self.fuser.boxfusion(all_pred_box, self.per_frame_ins, bm)
-                self.stats["fused"] += self.fuser.last_stats.get("updated", 0)
+                self.fuser.boxfusion(all_pred_box, self.per_frame_ins, bm, defer=True)
         else:
             all_pred_box = all_pred_box[torch.as_tensor(keep_idx, device=self.dev)]
             all_poses = all_poses[keep_idx]

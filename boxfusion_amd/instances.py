@@ -191,14 +191,16 @@ class Instances3D:
         self.projected_boxes = _lib.project_boxes(corners, self.cam_pose.to(corners.device, torch.float32),
                                                   K.to(corners.device, torch.float32), float(W), float(H))
 
-    def spatial_association(instance_lists, threshold, box_manager, cam_poses):
-        """nms_3d over all boxes; returns (keep, success_nms) as sorted lists."""
+    def spatial_association(instance_lists, threshold, box_manager, cam_poses, corners=None):
+        """nms_3d over all boxes; returns (keep, success_nms) as sorted lists.
+        corners: the boxes' [N,8,3] corners when the caller already has them."""
         assert len(instance_lists) > 0
         if len(instance_lists) == 1:
             return instance_lists  # reference quirk (instances.py:381-382)
         boxes = instance_lists.get("pred_boxes_3d")
         dev = boxes.device
-        corners = boxes.corners
+        if corners is None:
+            corners = boxes.corners
         iou = _lib.obb_iou_matrix(corners)
         scores = instance_lists.scores.to(dev, torch.float32).contiguous()
         init_id = instance_lists.init_id.to(dev, torch.int32).contiguous()
@@ -228,13 +230,16 @@ class Instances3D:
     def correspondence_association(cfg, box_manager, cur_keep_idx, cur_success_nms, pred_instances,
                                    global_pred_box, all_pred_box, all_poses, per_frame_ins_cam_pose,
                                    frame_id, mask, intrinsic, all_kf_pose, threshold=0.33, H=480,
-                                   W=640):
+                                   W=640, corners=None, cur_pose=None):
         """small-box 2-D association against the previous global boxes; returns
-        (all_pred_box[keep_idx], all_poses[keep_idx], keep_idx)."""
+        (all_pred_box[keep_idx], all_poses[keep_idx], keep_idx).
+        corners / cur_pose: all_pred_box's corners and this keyframe's pose as device tensors
+        when the caller already has them (`intrinsic` may also be a device tensor)."""
         n_glo = len(global_pred_box)
         boxes = all_pred_box.get("pred_boxes_3d")
         dev = boxes.device
-        corners = boxes.corners
+        if corners is None:
+            corners = boxes.corners
         mask_np = np.asarray(mask, dtype=np.int64)
         success_all = [i + n_glo for i in cur_success_nms]
         vn = all_pred_box.valid_num
@@ -243,7 +248,8 @@ class Instances3D:
         x = Exchange(dev, items=items, lens=lens, mask=mask_np.astype(np.int32),
                      succ=np.asarray(success_all if success_all else [0], np.int32),
                      counts=np.zeros(3, np.int32), keep=max(1, len(mask_np)), events=3 * (n_all + 1))
-        cur_pose = torch.as_tensor(np.asarray(all_kf_pose[frame_id], dtype=np.float32), device=dev)
+        if cur_pose is None:
+            cur_pose = torch.as_tensor(np.asarray(all_kf_pose[frame_id], dtype=np.float32), device=dev)
         K = torch.as_tensor(intrinsic).to(dev, torch.float32)
         succ_dev = x.dev["succ"][:len(success_all)]
         _lib.corr_assoc(
