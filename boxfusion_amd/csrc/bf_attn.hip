@@ -199,6 +199,418 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const u16* __restrict__ Q, con
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Streaming variant (k_attn_s): K/V pass through a double-buffered LDS ring of 64-key tiles.
+// The global loads of tile t+1 are issued into registers before tile t's MFMAs and written to
+// the other buffer after them (one barrier per tile), so HBM latency overlaps the compute.
+// V stays row-major ([key][VROW], VROW*2 = 64 or 192 mod 256 bytes so the 4 rows of one
+// transposed read land in disjoint banks) and the A operand of O^T = V^T P^T is read with
+// ds_read_b64_tr_b16: per 16-lane group a 4-key x 16-column block arrives column-major, two such
+// reads (keys base..base+3 and base+8..base+11) form the 32x32x16 fragment in the k order of the
+// S^T accumulator.  K rows are padded to D+8 elements (conflict-free ds_read_b128 fragments).
+// ------------------------------------------------------------------------------------------
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+// Online-softmax step over one 64-key tile held as S^T (raw scores, query on the lane, keys in
+// the accumulator registers + lane half): returns the bf16 P^T fragments and rescales O^T.
+//  * the score scale (scale * log2 e) is folded into the exponent: p = 2^(s*c - m), m = max(s)*c,
+//    one FMA per element; the raw v_exp_f32 is enough (arguments <= 0; results below 2^-126 do
+//    not change an f32 row sum of terms >= 1)
+//  * keys past sk are masked only on the tile that has them
+template <int DB>
+__device__ __forceinline__ void attn_softmax_tile(f32x16 (&s)[2], int k0, int sk, int fh, float c,
+                                                  float& m_run, float& l_run, f32x16 (&o)[DB],
+                                                  bf16x8 (&pf)[2][2]) {
+    if (k0 + AT_KT > sk) {
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int key = k0 + sub * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh;
+                s[sub][e] = (key < sk) ? s[sub][e] : -INFINITY;
+            }
+    }
+    float mt = s[0][0];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) mt = fmaxf(mt, s[sub][e]);
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float m_new = fmaxf(m_run, mt * c);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);   // m_run = -inf -> 0
+    float ls = 0.f;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(s[sub][e], c, -m_new));
+            ls += p;
+            pf[sub][e >> 3][e & 7] = (__bf16)p;
+        }
+    ls += __shfl_xor(ls, 32, 64);
+    l_run = l_run * alpha + ls;
+    m_run = m_new;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[db][e] *= alpha;
+}
+
+__host__ __device__ constexpr int attn_vrow_bytes(int d) {
+    int sb = 2 * d;
+    while (sb % 256 != 64 && sb % 256 != 192) sb += 32;
+    return sb;
+}
+
+template <int D, int NW>
+__global__ void __launch_bounds__(NW * 64) k_attn_s(const u16* __restrict__ Q, const u16* __restrict__ K,
+                                                       const u16* __restrict__ V, u16* __restrict__ O,
+                                                       int sq, int sk, int q_rs, int k_rs, int v_rs,
+                                                       int o_rs, long long q_bs, long long k_bs,
+                                                       long long v_bs, long long o_bs, float scale_log2) {
+    constexpr int KS = D / 16;
+    constexpr int DB = (D + 31) / 32;
+    constexpr int KROW = D + 8;
+    constexpr int VROW = attn_vrow_bytes(D) / 2;
+    constexpr int KTILE = AT_KT * KROW;
+    constexpr int VTILE = AT_KT * VROW;
+    constexpr int CPR = D / 8;                       // 16-B chunks per row
+    constexpr int CH = AT_KT * CPR;                  // chunks per operand tile
+    constexpr int NT = NW * 64;
+    __shared__ __attribute__((aligned(16))) u16 sK[2 * KTILE];
+    __shared__ __attribute__((aligned(16))) u16 sV[2 * VTILE];
+
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int h = blockIdx.y, b = blockIdx.z;
+    const int fr = lane & 31, fh = lane >> 5;
+    const int q = blockIdx.x * (NW * 32) + wave * 32 + fr;
+    const u16* Qb = Q + b * q_bs + h * D;
+    const u16* Kb = K + b * k_bs + h * D;
+    const u16* Vb = V + b * v_bs + h * D;
+
+    bf16x8 qf[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+        qf[ks] = *reinterpret_cast<const bf16x8*>(Qb + (size_t)min(q, sq - 1) * q_rs + 16 * ks + 8 * fh);
+    // padded V columns (read by the last 32-row block of O^T when D % 32 != 0): zero once
+    if (VROW > D)
+        for (int i = t; i < 2 * AT_KT * (VROW - D); i += NT) {
+            const int r = i / (VROW - D), c = i % (VROW - D);
+            sV[r * VROW + D + c] = 0;
+        }
+
+    // staging: thread t moves chunk c = t + i*NT (key row c / CPR, 16-B column c % CPR) of both
+    // the K and the V tile; row / column computed once, per tile only the key clamp and two
+    // addresses.  CH and NT are multiples of 64, so the i-guard is wave-uniform.
+    static_assert(CH % 64 == 0 && NT % 64 == 0, "wave-uniform staging guard");
+    constexpr int NSO = (CH + NT - 1) / NT;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 stk[NSO], stv[NSO];
+    int srow[NSO], scol[NSO];
+#pragma unroll
+    for (int i = 0; i < NSO; ++i) {
+        const int c = min(t + i * NT, CH - 1);
+        srow[i] = c / CPR;
+        scol[i] = (c % CPR) * 8;
+    }
+#define ATS_LOAD(k0_)                                                                             \
+    _Pragma("unroll") for (int i = 0; i < NSO; ++i) {                                            \
+        const int key = min((k0_) + srow[i], sk - 1);                                             \
+        stk[i] = *reinterpret_cast<const u32x4*>(Kb + (size_t)key * k_rs + scol[i]);              \
+        stv[i] = *reinterpret_cast<const u32x4*>(Vb + (size_t)key * v_rs + scol[i]);              \
+    }
+#define ATS_STORE(buf_)                                                                           \
+    _Pragma("unroll") for (int i = 0; i < NSO; ++i) {                                            \
+        if (t + i * NT < CH) {                                                                    \
+            *reinterpret_cast<u32x4*>(sK + (buf_) * KTILE + srow[i] * KROW + scol[i]) = stk[i];   \
+            *reinterpret_cast<u32x4*>(sV + (buf_) * VTILE + srow[i] * VROW + scol[i]) = stv[i];   \
+        }                                                                                         \
+    }
+
+    f32x16 o[DB];
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[db][e] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+
+    // transposed-read lane roles: 16-lane group (d half g16), row q4 / column quad p4 of the block
+    const int g16 = (lane >> 4) & 1, q4 = (lane & 15) >> 2, p4 = lane & 3;
+    const int ntiles = (sk + AT_KT - 1) / AT_KT;
+    ATS_LOAD(0);
+    ATS_STORE(0);
+    __syncthreads();
+    for (int tile = 0; tile < ntiles; ++tile) {
+        const int k0 = tile * AT_KT, buf = tile & 1;
+        const bool more = tile + 1 < ntiles;
+        if (more) { ATS_LOAD(k0 + AT_KT); }              // in flight during this tile
+        const u16* kt = sK + buf * KTILE;
+        const u16* vt = sV + buf * VTILE;
+        // ---- S^T = K Q^T for two 32-key sub-tiles ------------------------------------------
+        f32x16 s[2];
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                bf16x8 kf = *reinterpret_cast<const bf16x8*>(kt + (sub * 32 + fr) * KROW + 16 * ks + 8 * fh);
+                s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], ks == 0 ? f32x16{} : s[sub], 0, 0, 0);
+            }
+        }
+        // ---- online softmax ----------------------------------------------------------------
+        bf16x8 pf[2][2];
+        attn_softmax_tile<DB>(s, k0, sk, fh, scale_log2, m_run, l_run, o, pf);
+        // ---- O^T += V^T P^T, V^T fragments by transposed reads -------------------------------
+#pragma unroll
+        for (int db = 0; db < DB; ++db) {
+            const int d0 = db * 32 + g16 * 16 + 4 * p4;
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+                    const int kb = 32 * sub + 16 * ss + 4 * fh + q4;
+                    typedef __attribute__((address_space(3))) s16x4* lds_s4;
+                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (lds_s4)(vt + kb * VROW + d0));
+                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (lds_s4)(vt + (kb + 8) * VROW + d0));
+                    typedef short s16x8 __attribute__((ext_vector_type(8)));
+                    const s16x8 lohi = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                    const bf16x8 vf = __builtin_bit_cast(bf16x8, lohi);
+                    o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[sub][ss], o[db], 0, 0, 0);
+                }
+        }
+        if (more) { ATS_STORE(buf ^ 1); }
+        __syncthreads();
+    }
+    if (q < sq) {
+        const float inv = 1.0f / l_run;
+        u16* orow = O + b * o_bs + (size_t)q * o_rs + h * D;
+#pragma unroll
+        for (int db = 0; db < DB; ++db)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int d0 = db * 32 + 8 * g + 4 * fh;
+                if (d0 >= D) continue;
+                V64 w;
+                w.x = (uint32_t)at_f2bf(o[db][4 * g + 0] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 1] * inv) << 16);
+                w.y = (uint32_t)at_f2bf(o[db][4 * g + 2] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 3] * inv) << 16);
+                *reinterpret_cast<V64*>(orow + d0) = w;
+            }
+    }
+}
+
+#undef ATS_LOAD
+#undef ATS_STORE
+
+// ------------------------------------------------------------------------------------------
+// Resident variant for short sequences (k_attn_r, sk <= 64*NTILE: CLIP's 257 tokens): the whole
+// K and V of the (batch, head) go to LDS as [keys][D] images by LDS-DMA (global_load_lds, 1-KiB
+// pieces, per-lane source rows), every piece issued up front after the Q loads; key tile t waits
+// only for its own pieces with a counted vmcnt (the pieces of later tiles stay in flight under
+// this tile's MFMAs), then one barrier.  No buffer is reused, so there is no WAR hazard.
+// Rows past sk are clamped copies (their scores are masked); a zeroed slack after V covers the
+// padded head-dim columns that the last O^T row block reads past the last key row.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void attn_wait_vm(int n) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+        case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+        case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+        case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+        case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+        case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+        case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
+        case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+        case 19: asm volatile("s_waitcnt vmcnt(19)" ::: "memory"); break;
+        case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+        case 21: asm volatile("s_waitcnt vmcnt(21)" ::: "memory"); break;
+        case 22: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); break;
+        case 23: asm volatile("s_waitcnt vmcnt(23)" ::: "memory"); break;
+        case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+        case 25: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
+        case 26: asm volatile("s_waitcnt vmcnt(26)" ::: "memory"); break;
+        case 27: asm volatile("s_waitcnt vmcnt(27)" ::: "memory"); break;
+        case 28: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
+        case 29: asm volatile("s_waitcnt vmcnt(29)" ::: "memory"); break;
+        case 30: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(31)" ::: "memory"); break;
+    }
+}
+
+template <int D, int NW, int NTILE>
+__global__ void __launch_bounds__(NW * 64) k_attn_r(const u16* __restrict__ Q, const u16* __restrict__ K,
+                                                       const u16* __restrict__ V, u16* __restrict__ O,
+                                                       int sq, int sk, int q_rs, int k_rs, int v_rs,
+                                                       int o_rs, long long q_bs, long long k_bs,
+                                                       long long v_bs, long long o_bs, float scale_log2) {
+    constexpr int KS = D / 16;
+    constexpr int DB = (D + 31) / 32;
+    constexpr int ROWS = NTILE * AT_KT;
+    constexpr int OPB = ROWS * D * 2;                // bytes of one operand image
+    constexpr int PPT = AT_KT * D * 2 / 1024;        // 1-KiB pieces per operand per tile
+    constexpr int QP = NW * 32 * D * 2 / 1024;       // pieces of the Q image (all NW*32 queries)
+    constexpr int NPIECE = QP + NTILE * 2 * PPT;     // issue order: Q, then tile, operand, piece
+    constexpr int SLACK = 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char at_smem[];
+    u16* sQ = reinterpret_cast<u16*>(at_smem);
+    u16* sK = reinterpret_cast<u16*>(at_smem + QP * 1024);
+    u16* sV = reinterpret_cast<u16*>(at_smem + QP * 1024 + OPB);
+    static_assert(PPT * 1024 == AT_KT * D * 2, "tile must be whole 1-KiB pieces");
+    static_assert(QP * 1024 == NW * 32 * D * 2, "Q image must be whole 1-KiB pieces");
+
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int h = blockIdx.y, b = blockIdx.z;
+    const int fr = lane & 31, fh = lane >> 5;
+    const int q = blockIdx.x * (NW * 32) + wave * 32 + fr;
+    const int q_base = blockIdx.x * (NW * 32);
+    const u16* Qb = Q + b * q_bs + h * D;
+    const u16* Kb = K + b * k_bs + h * D;
+    const u16* Vb = V + b * v_bs + h * D;
+
+    if (t < SLACK / 2) reinterpret_cast<u16*>(at_smem + QP * 1024 + 2 * OPB)[t] = 0;
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    // Q, K and V all arrive by LDS-DMA (no plain global loads in the kernel, so the compiler adds
+    // no waits of its own); every wave issues exactly PW pieces (a surplus slot repeats the
+    // wave's last piece: same bytes, same place)
+    constexpr int PW = (NPIECE + NW - 1) / NW;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+        int g = wave + i * NW;
+        if (g >= NPIECE) g -= NW;
+        const u16* src;
+        int dst;
+        if (g < QP) {
+            const int e = g * 512 + lane * 8;
+            src = Qb + (size_t)min(q_base + e / D, sq - 1) * q_rs + e % D;
+            dst = g * 1024;
+        } else {
+            const int gg = g - QP;
+            const int tile = gg / (2 * PPT), rem = gg % (2 * PPT);
+            const int op = rem / PPT, pc = tile * PPT + rem % PPT;  // piece within the operand
+            const int e = pc * 512 + lane * 8;
+            const int row = min(e / D, sk - 1), col = e % D;
+            src = (op ? Vb + (size_t)row * v_rs : Kb + (size_t)row * k_rs) + col;
+            dst = QP * 1024 + op * OPB + pc * 1024;
+        }
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(at_smem + dst), 16, 0, 0);
+    }
+
+    f32x16 o[DB];
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[db][e] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+    const int g16 = (lane >> 4) & 1, q4 = (lane & 15) >> 2, p4 = lane & 3;
+    const int ntiles = (sk + AT_KT - 1) / AT_KT;
+    bf16x8 qf[KS];
+    // this wave's slots issued after its last piece of `tile` (issue order = tile order)
+    for (int tile = 0; tile < ntiles; ++tile) {
+        const int k0 = tile * AT_KT;
+        const int last = QP + (tile + 1) * 2 * PPT;                   // first piece of the next tile
+        const int mine_upto = last > wave ? (last - wave + NW - 1) / NW : 0;
+        attn_wait_vm(PW - mine_upto);
+        // raw barrier: __syncthreads() would add vmcnt(0) and drain the later tiles' DMA
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (tile == 0) {      // Q^T fragments (B operand) from the Q image
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+                qf[ks] = *reinterpret_cast<const bf16x8*>(sQ + (wave * 32 + fr) * D + 16 * ks + 8 * fh);
+        }
+        const u16* kt = sK + k0 * D;
+        const u16* vt = sV + k0 * D;
+        f32x16 s[2];
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                bf16x8 kf = *reinterpret_cast<const bf16x8*>(kt + (sub * 32 + fr) * D + 16 * ks + 8 * fh);
+                s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], ks == 0 ? f32x16{} : s[sub], 0, 0, 0);
+            }
+        }
+        bf16x8 pf[2][2];
+        attn_softmax_tile<DB>(s, k0, sk, fh, scale_log2, m_run, l_run, o, pf);
+        // V^T fragments: transposed reads in inline asm (the builtin makes the compiler drain
+        // every pending LDS-DMA first), retired by an explicit lgkmcnt before their MFMAs
+        typedef unsigned long long u64;
+        const unsigned vbase = (unsigned)(size_t)(__attribute__((address_space(3))) u16*)vt;
+#pragma unroll
+        for (int db = 0; db < DB; ++db) {
+            const int d0 = db * 32 + g16 * 16 + 4 * p4;
+            u64 lo[2][2], hi[2][2];
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+                    const int kb = 32 * sub + 16 * ss + 4 * fh + q4;
+                    const unsigned a0 = vbase + (unsigned)((kb * D + d0) * 2);
+                    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo[sub][ss]) : "v"(a0));
+                    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi[sub][ss]) : "v"(a0), "i"(8 * D * 2));
+                }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+                    asm volatile("" : "+v"(lo[sub][ss]), "+v"(hi[sub][ss]));
+                    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+                    const u64x2 lh = {lo[sub][ss], hi[sub][ss]};
+                    o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, lh),
+                                                                   pf[sub][ss], o[db], 0, 0, 0);
+                }
+        }
+    }
+    if (q < sq) {
+        const float inv = 1.0f / l_run;
+        u16* orow = O + b * o_bs + (size_t)q * o_rs + h * D;
+#pragma unroll
+        for (int db = 0; db < DB; ++db)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int d0 = db * 32 + 8 * g + 4 * fh;
+                if (d0 >= D) continue;
+                V64 w;
+                w.x = (uint32_t)at_f2bf(o[db][4 * g + 0] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 1] * inv) << 16);
+                w.y = (uint32_t)at_f2bf(o[db][4 * g + 2] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 3] * inv) << 16);
+                *reinterpret_cast<V64*>(orow + d0) = w;
+            }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outstanding at exit
+}
+
+template <int D, int NW, int NTILE>
+static void launch_attn_r(dim3 grid, hipStream_t st, const void* q, const void* k, const void* v, void* o,
+                          int sq, int sk, int q_rs, int k_rs, int v_rs, int o_rs, long long q_bs,
+                          long long k_bs, long long v_bs, long long o_bs, float sl2) {
+    constexpr size_t lds = (size_t)NW * 32 * D * 2 + 2 * (size_t)NTILE * AT_KT * D * 2 + 64;
+    static bool attr = false;
+    if (!attr) {
+        hipFuncSetAttribute((const void*)k_attn_r<D, NW, NTILE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_attn_r<D, NW, NTILE>), grid, dim3(NW * 64), lds, st, (const u16*)q,
+                       (const u16*)k, (const u16*)v, (u16*)o, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs,
+                       k_bs, v_bs, o_bs, sl2);
+}
+
+static int g_attn_variant = 1;   // 1/2: k_attn_s, 3: k_attn_r for short sequences, 0: k_attn
+BF_API void bf_attention_set_variant(int v) { g_attn_variant = v; }
+
 BF_API int bf_attention_bf16(const void* q, const void* k, const void* v, void* o, int batch,
                              int heads, int sq, int sk, int head_dim, int q_rs, int k_rs, int v_rs,
                              int o_rs, long long q_bs, long long k_bs, long long v_bs,
@@ -209,6 +621,37 @@ BF_API int bf_attention_bf16(const void* q, const void* k, const void* v, void* 
     // short sequences (CLIP: 257 tokens) run every query of a (batch, head) in ONE workgroup of
     // ceil(sq/32) waves, so K/V are staged once and no 128-query tile is almost empty
     const int nw_one = (sq + 31) / 32;
+    // variant 3: short sequences with all queries in one workgroup, resident K/V filled by
+    // LDS-DMA (measured slower than the streaming ring on CLIP's shape; kept as an alternative)
+    if (g_attn_variant == 3 && nw_one > 4 && nw_one <= 9 && sk <= 5 * AT_KT &&
+        (head_dim == 80 || head_dim == 64)) {
+        const dim3 grid(1, heads, batch);
+        if (head_dim == 80)
+            launch_attn_r<80, 9, 5>(grid, bf_stream(stream), q, k, v, o, sq, sk, q_rs, k_rs, v_rs, o_rs,
+                                    q_bs, k_bs, v_bs, o_bs, sl2);
+        else
+            launch_attn_r<64, 9, 5>(grid, bf_stream(stream), q, k, v, o, sq, sk, q_rs, k_rs, v_rs, o_rs,
+                                    q_bs, k_bs, v_bs, o_bs, sl2);
+        return bf_check_launch();
+    }
+    if (g_attn_variant >= 1) {
+#define LAUNCH_S(DD, NWV)                                                                         \
+    hipLaunchKernelGGL((k_attn_s<DD, NWV>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch),   \
+                       dim3(NWV * 64), 0, bf_stream(stream), (const u16*)q, (const u16*)k,          \
+                       (const u16*)v, (u16*)o, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs,    \
+                       o_bs, sl2)
+#define LAUNCH_SD(DD) if (nw_one > 4 && nw_one <= 9) { LAUNCH_S(DD, 9); } else { LAUNCH_S(DD, 4); }
+        switch (head_dim) {
+            case 32: LAUNCH_SD(32); break;
+            case 64: LAUNCH_SD(64); break;
+            case 80: LAUNCH_SD(80); break;
+            case 128: LAUNCH_S(128, 4); break;     // 9 waves would spill at D = 128
+            default: return BF_ERR_UNSUPPORTED;
+        }
+#undef LAUNCH_SD
+#undef LAUNCH_S
+        return bf_check_launch();
+    }
 #define LAUNCH_NW(DD, NWV, NTV)                                                                   \
     hipLaunchKernelGGL((k_attn<DD, NWV, NTV>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch), \
                        dim3(NWV * 64), 0, bf_stream(stream), (const u16*)q, (const u16*)k,          \

@@ -237,6 +237,10 @@ int bf_attention_bf16(const void* q, const void* k, const void* v, void* o, int 
                       int sq, int sk, int head_dim, int q_rs, int k_rs, int v_rs, int o_rs,
                       long long q_bs, long long k_bs, long long v_bs, long long o_bs, float scale,
                       void* stream);
+/* Attention kernel variant (test/benchmark hook): 1 (default) / 2 = k_attn_s (64-key tiles
+ * through a double-buffered LDS ring), 3 = k_attn_r (resident K/V filled by LDS-DMA when all
+ * queries fit one workgroup and sk <= 320, else k_attn_s), 0 = k_attn (previous kernel). */
+void bf_attention_set_variant(int v);
 
 /* LayerNorm f32[M,C] -> bf16, written to row row_map[r] (NULL = r; < 0 skips). */
 int bf_layernorm(const float* x, int ldx, const float* gamma, const float* beta, float eps,
