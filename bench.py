@@ -69,6 +69,12 @@ def parse():
     p.add_argument("--sync-fusion", action="store_true",
                    help="run the fusion state machine inline instead of on the worker stream")
     p.add_argument("--cpu-detect-frames", type=int, default=1)
+    p.add_argument("--inflight", type=int, default=-1,
+                   help="detect steps in flight per GPU: independent batches replayed on this many "
+                        "streams (each its own DetectStage buffers / graph), so one batch's CLIP "
+                        "phases overlap the next batch's CuTR phases.  -1: 2 when this process fuses "
+                        "only its own frames (N = 1), else 1 (at N > 1 every rank waits for rank 0's "
+                        "fusion of 8N keyframes per step, which needs the CUs a second stream takes)")
     p.add_argument("--cpu-fusion-frames", type=int, default=24)
     return p.parse_args()
 
@@ -241,9 +247,11 @@ def main():
         cutr = make_cubify_transformer(args.dim, True).eval()
         clip_vis = VisionTransformer(224, 14, 1280, args.clip_layers, 16, 1024).eval()
     B = args.batch
-    detect = DetectStage(cutr, clip_vis, CFG, B, 480, 640, SCANNET_K, crops_per_frame=args.crops,
-                         crop_source="top", backproject=True, clip_capacity=B * args.crops,
-                         device=dev, graph=not args.eager)
+    n_inflight = args.inflight if args.inflight > 0 else (2 if world == 1 and args.sim_ranks <= 1 else 1)
+    detects = [DetectStage(cutr, clip_vis, CFG, B, 480, 640, SCANNET_K, crops_per_frame=args.crops,
+                           crop_source="top", backproject=True, clip_capacity=B * args.crops,
+                           device=dev, graph=not args.eager) for _ in range(n_inflight)]
+    detect = detects[0]
     scene = Scene(seed=0)
     N = world
     per_step = B * N
@@ -279,12 +287,16 @@ def main():
             o = s * B
             sl = slice(o, o + B)
             tb = time.perf_counter()
-            detect(rgb_all[sl], depth_all[sl], poses_all[sl], return_instances=False)
+            k = s % n_inflight
+            st_ctx = torch.cuda.stream(det_streams[k])
+            st_ctx.__enter__()      # this step's detect, gather and fusion hand-off on its stream
+            det = detects[k]
+            det(rgb_all[sl], depth_all[sl], poses_all[sl], return_instances=False)
             if args.breakdown:
                 torch.cuda.synchronize()
                 brk["detect"] += time.perf_counter() - tb
                 tb = time.perf_counter()
-            bidx, iidx, cat_idx, feats, sims = detect.last["clip"]
+            bidx, iidx, cat_idx, feats, sims = det.last["clip"]
             recs = rec_all[sl]
             g_rec, g_feat, g_meta = gather_step(recs, feats, (poses_all[sl], cnt_all[sl]), dist, N)
             g_pose, g_cnt = g_meta
@@ -304,6 +316,7 @@ def main():
                     for j in range(g_rec.shape[0]):
                         fusion.submit(base + j - s0 * (g_rec.shape[0]), g_pose[j],
                                       (lambda r=g_rec[j], n=int(g_cnt[j]): unpack_record(r, dev, n)), ev)
+            st_ctx.__exit__(None, None, None)
             if args.breakdown:
                 torch.cuda.synchronize()
                 brk["fusion"] += time.perf_counter() - tb
@@ -318,6 +331,14 @@ def main():
                               else (torch.cuda.current_stream(), None))
     torch.cuda.synchronize()
     torch.cuda.set_stream(det_stream)          # detection (graph replays, gathers) on its CUs
+    det_streams = [det_stream] + [torch.cuda.Stream(device=dev) for _ in range(n_inflight - 1)]
+
+    # capture every DetectStage's graph before the fusion worker exists: a capture must not see
+    # another thread's synchronising calls
+    for k, d in enumerate(detects):
+        with torch.cuda.stream(det_streams[k]):
+            d(rgb_all[:B], depth_all[:B], poses_all[:B], return_instances=False)
+    torch.cuda.synchronize()
 
     def make_fusion():
         st = FusionStage(CFG, SCANNET_K, device=dev)
@@ -377,6 +398,7 @@ def main():
                                    f"CuTR ViT-{ {768: 'B', 384: 'S', 192: 'T'}.get(args.dim, args.dim)} "
                                    f"RGB-D + CLIP ViT-H/14 x{args.crops} crops/frame + fusion",
                        "frames": frames, "global_batch": per_step, "parallelism": f"dp{N}",
+                       "inflight_batches_per_gpu": n_inflight,
                        "fused_boxes": fusion.stats["fused"],
                        "global_boxes": len(fusion.all_pred_box) if fusion.all_pred_box is not None else 0},
             "roofline": {"bound": "mfma", "kernel": "k_gemm256p<true,1> (persistent bf16 GEMM + bias + GELU: MLP up-projections of CLIP ViT-H and CuTR window blocks)",

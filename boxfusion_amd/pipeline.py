@@ -165,7 +165,8 @@ class DetectStage:
                     self._device_forward()
             torch.cuda.current_stream().wait_stream(s)
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
+            # thread-local capture: other threads (the fusion worker) keep running their own work
+            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
                 self._device_forward()
         self.graph.replay()
 
