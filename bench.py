@@ -66,6 +66,9 @@ def parse():
                    help="CUs reserved for the fusion stream (-1: 32 on rank 0 when N > 1, else 0)")
     p.add_argument("--sim-ranks", type=int, default=1,
                    help="stress test at N=1: rank 0 also fuses the frames of R virtual ranks per step")
+    p.add_argument("--mask-cus", type=int, default=-1,
+                   help="1: confine detection and fusion streams to disjoint CU sets (CU-masked "
+                        "streams) when CUs are reserved for fusion; -1: on when fusing for N > 1")
     p.add_argument("--sync-fusion", action="store_true",
                    help="run the fusion state machine inline instead of on the worker stream")
     p.add_argument("--cpu-detect-frames", type=int, default=1)
@@ -118,6 +121,26 @@ def unpack_record(rec, dev, n=None):
     p.scores = rows[:, 0].contiguous()
     p.pred_boxes = rows[:, 1:5].contiguous()
     p.pred_boxes_3d = GeneralInstance3DBoxes(rows[:, 5:11], rows[:, 11:20].reshape(n, 3, 3))
+    p.pred_proj_xy = rows[:, 20:22].contiguous()
+    return p
+
+
+def unpack_records(recs, cnts, dev):
+    """records [nkf, 1 + REC_ROWS*REC_W] of several keyframes -> ONE Instances3D holding every
+    keyframe's detections in order (keyframe j: cnts[j] rows), five gathers in total"""
+    from boxfusion_amd import _lib
+    from boxfusion_amd.boxes import GeneralInstance3DBoxes
+    from boxfusion_amd.instances import Instances3D
+    cnts = np.asarray(cnts, np.int64)
+    idx = np.concatenate([j * REC_ROWS + np.arange(c) for j, c in enumerate(cnts)]) if cnts.sum() else \
+        np.zeros(0, np.int64)
+    rows = recs[:, 1:1 + REC_ROWS * REC_W].reshape(-1, REC_W).index_select(
+        0, _lib.h2d(idx, dev))
+    p = Instances3D((480, 640))
+    p.scores = rows[:, 0].contiguous()
+    p.pred_boxes = rows[:, 1:5].contiguous()
+    p.pred_boxes_3d = GeneralInstance3DBoxes._views(rows[:, 5:11].contiguous(),
+                                                     rows[:, 11:20].reshape(-1, 3, 3).contiguous())
     p.pred_proj_xy = rows[:, 20:22].contiguous()
     return p
 
@@ -313,9 +336,11 @@ def main():
                     ev = torch.cuda.Event()
                     ev.record()
                     g_rec.record_stream(fusion.stream)
-                    for j in range(g_rec.shape[0]):
-                        fusion.submit(base + j - s0 * (g_rec.shape[0]), g_pose[j],
-                                      (lambda r=g_rec[j], n=int(g_cnt[j]): unpack_record(r, dev, n)), ev)
+                    counts = [base + j - s0 * (g_rec.shape[0]) for j in range(g_rec.shape[0])]
+                    # the whole step's keyframes as one job: geometry batched, association serial
+                    fusion.submit_call(
+                        lambda st, r=g_rec, c=np.asarray(g_cnt), p=np.asarray(g_pose), k=counts:
+                        st.keyframes(k, p, unpack_records(r, c, dev), c), ev)
             st_ctx.__exit__(None, None, None)
             if args.breakdown:
                 torch.cuda.synchronize()
@@ -327,11 +352,16 @@ def main():
     fusion_cus = args.fusion_cus
     if fusion_cus < 0:
         fusion_cus = 32 if rank == 0 and (world > 1 or args.sim_ranks > 1) else 0
-    det_stream, fus_stream = (_lib.partition_streams(fusion_cus, local) if fusion_cus > 0
+    masked = args.mask_cus if args.mask_cus >= 0 else int(fusion_cus > 0)
+    det_stream, fus_stream = (_lib.partition_streams(fusion_cus, local, masked=bool(masked)) if fusion_cus > 0
                               else (torch.cuda.current_stream(), None))
     torch.cuda.synchronize()
     torch.cuda.set_stream(det_stream)          # detection (graph replays, gathers) on its CUs
-    det_streams = [det_stream] + [torch.cuda.Stream(device=dev) for _ in range(n_inflight - 1)]
+    if masked and fusion_cus > 0:   # every detect stream on the detection CUs
+        det_streams = [det_stream] + [_lib.partition_streams(fusion_cus, local, masked=True)[0]
+                                      for _ in range(n_inflight - 1)]
+    else:
+        det_streams = [det_stream] + [torch.cuda.Stream(device=dev) for _ in range(n_inflight - 1)]
 
     # capture every DetectStage's graph before the fusion worker exists: a capture must not see
     # another thread's synchronising calls
@@ -358,7 +388,11 @@ def main():
     with timer:       # records every eager GELU-GEMM launch (graph replays launch none from Python)
         run_steps(args.warmup, total_steps, fusion)
         if not args.sync_fusion:
+            worker = fusion
             fusion = fusion.join()
+            if rank == 0:
+                print(f"fusion worker busy {1e3 * worker.busy_s / args.steps:.1f} ms/step "
+                      f"({fusion.stats['keyframes']} keyframes)", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()

@@ -9,6 +9,7 @@ from __future__ import annotations
 import ctypes
 import os
 
+import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -74,6 +75,17 @@ def _stream():
     # the raw handle of the calling thread's current stream (torch.cuda.current_stream() builds a
     # Stream object through several device-index lookups: ~10 us per call on the fusion path)
     return c_void_p(torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice()))
+
+
+def h2d(a, device, dtype=None):
+    """host array -> device tensor without blocking the host: staged through pinned memory (torch's
+    caching host allocator keeps the block until the copy is done) and copied asynchronously on
+    the current stream.  A pageable copy waits until the stream has drained every earlier kernel,
+    which on the fusion path is a hidden synchronisation per upload."""
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.pin_memory().to(device, non_blocking=True)
 
 
 _SYNC_DEBUG = os.environ.get("BF_SYNC_DEBUG", "0") == "1"

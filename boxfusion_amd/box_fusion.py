@@ -102,7 +102,7 @@ class BoxFusion:
         rows = np.array([i for i, _ in jobs], np.int32)
         # one upload: view offsets, view counts, target rows, flattened view indices
         host = np.concatenate([off, nv, rows] + [np.asarray(fl, np.int32) for _, fl in jobs])
-        idx = torch.from_numpy(host).to(dev, non_blocking=True)
+        idx = _lib.h2d(host, dev)
         flat = idx[3 * nj:]
         b3 = per_frame_box.pred_boxes_3d
         out_box, packed, _ = _lib.fusion_fit(

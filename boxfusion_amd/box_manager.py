@@ -129,8 +129,7 @@ class BoxManager:
                                     "box_fusion.list_capacity")
             items[i, :len(row)] = row
             lens[i] = len(row)
-        return (torch.from_numpy(items).to(device, non_blocking=True),
-                torch.from_numpy(lens).to(device, non_blocking=True))
+        return _lib.h2d(items, device), _lib.h2d(lens, device)
 
     def pack_host(self):
         """fusion lists as host arrays (items [n, cap] padded with -1, lengths [n])"""

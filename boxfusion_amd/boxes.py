@@ -66,9 +66,18 @@ class GeneralInstance3DBoxes:
     def translate(self, trans_vector):
         self.tensor[:, :3] += torch.as_tensor(trans_vector, device=self.tensor.device)
 
+    @classmethod
+    def _views(cls, tensor, R):
+        """boxes over existing tensors, no copy (row slices of a larger box set)"""
+        b = cls.__new__(cls)
+        b.tensor, b.R, b.dof, b.box_dim = tensor, R, None, 15
+        return b
+
     def __getitem__(self, item):
         if isinstance(item, int):
             return GeneralInstance3DBoxes(self.tensor[item].view(1, -1), self.R[item].view(1, 3, 3))
+        if isinstance(item, slice) and (item.step is None or item.step == 1):
+            return GeneralInstance3DBoxes._views(self.tensor[item], self.R[item])
         b, r = self.tensor[item], self.R[item]
         assert b.dim() == 2, f"Indexing on Boxes with {item} failed to return a matrix!"
         return GeneralInstance3DBoxes(b, r)

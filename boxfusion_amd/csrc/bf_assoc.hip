@@ -68,6 +68,8 @@ __device__ void block_sort_distinct(int* a, int* tmp, int n) {
 // ------------------------------------------------------------------------------------------
 // NMS scan
 // ------------------------------------------------------------------------------------------
+#define NMS_IOU_LDS_N 120                                   // n <= 120: IoU matrix (<=113 KB) in LDS
+#define NMS_IOU_LDS_MAX (NMS_IOU_LDS_N * NMS_IOU_LDS_N)
 __global__ void __launch_bounds__(SCAN_THREADS) k_nms_scan(
     const double* __restrict__ iou, const float* __restrict__ corners,
     const float* __restrict__ scores, const int32_t* __restrict__ init_id,
@@ -75,17 +77,26 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_nms_scan(
     float* __restrict__ valid_num, int32_t* __restrict__ keep_out, int32_t* __restrict__ n_keep,
     int32_t* __restrict__ succ_out, int32_t* __restrict__ n_succ, int32_t* __restrict__ events,
     int32_t* __restrict__ n_events, int32_t* __restrict__ status, bf_nms_cfg cfg) {
-    extern __shared__ __attribute__((aligned(16))) int smem[];
+    extern __shared__ __attribute__((aligned(16))) double dsmem[];
+    // small problems stage the IoU matrix in LDS: the scan reads one row per kept box
+    const bool iou_lds = (size_t)n * n <= NMS_IOU_LDS_MAX;
+    double* iou_s = dsmem;
+    int* smem = reinterpret_cast<int*>(dsmem + (iou_lds ? (size_t)n * n : 0));
     int* bufA = smem;             // order (ping)
     int* bufB = bufA + n + 1;     // order (pong)
     int* supp = bufB + n + 1;     // suppressed list of the current step
     int* keep = supp + n + 1;     // python-list image of `keep`
     int* succ = keep + n + 2;     // success_nms
+    float* cen = reinterpret_cast<float*>(succ + n + 2);   // box centres [n][3] (nms_3d:49)
     __shared__ int s_wave[SCAN_WAVES];
     __shared__ int s_no, s_nk, s_ns, s_nsupp;
     const int t = threadIdx.x;
     const int cap = cfg.list_capacity;
 
+    for (int i = t; i < n; i += SCAN_THREADS) box_center(corners, i, cen + 3 * i);
+    if (iou_lds)
+        for (int q = t; q < n * n; q += SCAN_THREADS) iou_s[q] = iou[q];
+    const double* I = iou_lds ? iou_s : iou;
     // order = scores.argsort()[::-1]: descending, ties -> higher index first
     for (int i = t; i < n; i += SCAN_THREADS) {
         float si = scores[i];
@@ -111,7 +122,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_nms_scan(
             int q = base + t;
             const bool live = q < no;
             const int j = order[live ? q : no - 1];          // valid index: the load is always safe
-            const double v = live ? iou[(size_t)i * n + j] : 0.0;
+            const double v = live ? I[(size_t)i * n + j] : 0.0;
             bool fr = (q < no) && (v <= cfg.iou_threshold);
             bool fs = (q < no) && (v > cfg.iou_threshold);
             int tr, ts;
@@ -128,12 +139,10 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_nms_scan(
             succ[s_ns++] = i;
             // BoxManager.record(cur=i, fusion_inds=supp)
             const int cur = i;
-            float ccur[3];
-            box_center(corners, cur, ccur);
+            const float* ccur = cen + 3 * cur;
             for (int s = 0; s < nsupp; ++s) {
                 const int idx = supp[s];
-                float cidx[3];
-                box_center(corners, idx, cidx);
+                const float* cidx = cen + 3 * idx;
                 float dx = ccur[0] - cidx[0], dy = ccur[1] - cidx[1], dz = ccur[2] - cidx[2];
                 float cd = sqrtf((dx * dx + dy * dy) + dz * dz);
                 int branch;
@@ -216,7 +225,16 @@ BF_API int bf_nms_scan(const double* iou, const float* corners, const float* sco
     if (!iou || !corners || !scores || !init_id || !cam_poses || !fl_items || !fl_len ||
         !valid_num || !keep || !n_keep || !success || !n_success || !events || !n_events || !status)
         return BF_ERR_ARG;
-    size_t lds = sizeof(int) * (size_t)(5 * n + 8);
+    size_t lds = sizeof(int) * (size_t)(5 * n + 8) + sizeof(float) * 3 * (size_t)n;
+    if ((size_t)n * n <= NMS_IOU_LDS_MAX) lds += sizeof(double) * (size_t)n * n;
+    static bool attr_set = false;
+    if (!attr_set) {
+        const size_t big = sizeof(int) * (5 * BF_MAX_BOXES + 8) + sizeof(float) * 3 * BF_MAX_BOXES;
+        const size_t small = sizeof(double) * NMS_IOU_LDS_MAX + 32 * (size_t)NMS_IOU_LDS_N;
+        hipFuncSetAttribute((const void*)k_nms_scan, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(big > small ? big : small));
+        attr_set = true;
+    }
     hipLaunchKernelGGL(k_nms_scan, dim3(1), dim3(SCAN_THREADS), lds, bf_stream(stream), iou,
                        corners, scores, init_id, cam_poses, n, fl_items, fl_len, valid_num, keep,
                        n_keep, success, n_success, events, n_events, status, *cfg);

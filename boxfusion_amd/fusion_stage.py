@@ -19,12 +19,16 @@ flag, default on as in the reference).
 """
 from __future__ import annotations
 
+import os
 import queue
+import sys
 import threading
+import time
 
 import numpy as np
 import torch
 
+from boxfusion_amd import _lib
 from boxfusion_amd.box_fusion import BoxFusion
 from boxfusion_amd.box_manager import BoxManager
 from boxfusion_amd.instances import Instances3D
@@ -58,9 +62,37 @@ class FusionStage:
         self.box_manager.flush()
         return dict(self._stats, fused=self.fuser.updated_total)
 
-    def keyframe(self, count, pose, pred):
+    def keyframes(self, counts, poses, preds, sizes):
+        """Several keyframes in frame order whose detections arrive as ONE Instances3D `preds`
+        (camera frame, keyframe j's boxes are rows [off_j, off_j + sizes[j])): the per-box
+        geometry (world transform, projection, ids) runs once for all of them, then each keyframe
+        goes through the serial association / fusion exactly like keyframe()."""
+        sizes = np.asarray(sizes, np.int64)
+        n_tot = int(sizes.sum())
+        poses = np.asarray(poses, np.float32)
+        if n_tot:
+            kf = np.repeat(np.arange(len(sizes)), sizes)
+            preds.cam_pose = _lib.h2d(poses[kf], self.dev)
+            ids = np.empty((2, n_tot), np.int64)
+            ids[0] = np.asarray(counts, np.int64)[kf]
+            # init_id of keyframe j = box_count before it + row: box_count grows by n per keyframe
+            ids[1] = self.box_count + np.arange(n_tot)
+            idd = _lib.h2d(ids, self.dev)
+            preds.frame_id, preds.init_id = idd[0], idd[1]
+            preds.valid_num = torch.zeros(n_tot, device=self.dev)
+            preds.pred_boxes_3d.transform2world(preds.cam_pose)
+            preds.project_3d_boxes(self.K_dev, H=self.H, W=self.W)
+        off = 0
+        for j, c in enumerate(counts):
+            n = int(sizes[j])
+            self.keyframe(c, poses[j], preds[off:off + n] if n else None, prepared=True)
+            off += n
+
+    def keyframe(self, count, pose, pred, prepared=False):
         """pred: Instances3D of this keyframe in CAMERA coordinates (after the detection filters
-        and the CLIP step), tensors on the device; it is modified in place like the reference's."""
+        and the CLIP step), tensors on the device; it is modified in place like the reference's.
+        prepared=True: world transform, projection and the id fields were already applied
+        (keyframes())."""
         cfg, bm = self.cfg, self.box_manager
         self.last_pred = pred
         pose = np.asarray(pose, np.float32)
@@ -71,12 +103,13 @@ class FusionStage:
             bm.num_record[count] = self.box_count
             return
         self._stats["keyframes"] += 1
-        pred.cam_pose = torch.from_numpy(pose_np).to(self.dev)
-        pred.frame_id = torch.full((n,), count, dtype=torch.int64, device=self.dev)
-        pred.init_id = self.box_count + torch.arange(n, device=self.dev)
-        pred.valid_num = torch.zeros(n, device=self.dev)
-        pred.pred_boxes_3d.transform2world(pred.cam_pose)
-        pred.project_3d_boxes(self.K_dev, H=self.H, W=self.W)
+        if not prepared:
+            pred.cam_pose = _lib.h2d(pose_np, self.dev)
+            pred.frame_id = torch.full((n,), count, dtype=torch.int64, device=self.dev)
+            pred.init_id = self.box_count + torch.arange(n, device=self.dev)
+            pred.valid_num = torch.zeros(n, device=self.dev)
+            pred.pred_boxes_3d.transform2world(pred.cam_pose)
+            pred.project_3d_boxes(self.K_dev, H=self.H, W=self.W)
         self.box_count += n
         bm.num_record[count] = self.box_count
         if self.all_pred_box is None and (count < self.gap or self.per_frame_ins is None):
@@ -110,7 +143,7 @@ class FusionStage:
             if cfg["box_fusion"].get("use", True):
                 self.fuser.boxfusion(all_pred_box, self.per_frame_ins, bm, defer=True)
         else:
-            all_pred_box = all_pred_box[torch.as_tensor(keep_idx, device=self.dev)]
+            all_pred_box = all_pred_box[_lib.h2d(np.asarray(keep_idx, np.int64), self.dev)]
             all_poses = all_poses[keep_idx]
             bm.update(keep_idx)
         self.all_pred_box, self.all_poses = all_pred_box, all_poses
@@ -143,13 +176,32 @@ class AsyncFusion:
         self.stream = stream if stream is not None else torch.cuda.Stream(device=self.device_index)
         self.q = queue.Queue()
         self.err = None
+        self.busy_s = 0.0      # wall time the worker spent inside keyframe jobs
         self.thread = threading.Thread(target=self._run, name="boxfusion-fusion", daemon=True)
         self.thread.start()
 
     def submit(self, count, pose, make_pred, ready=None):
         self.q.put((count, pose, make_pred, ready))
 
+    def submit_call(self, fn, ready=None):
+        """fn(stage) on the worker (e.g. stage.keyframes for a whole batch of keyframes)"""
+        self.q.put((None, None, fn, ready))
+
     def _run(self):
+        if os.environ.get("BF_PROFILE_FUSION"):      # diagnostic: cProfile of the worker thread
+            import cProfile
+            import pstats
+            pr = cProfile.Profile()
+            pr.enable()
+            try:
+                self._loop()
+            finally:
+                pr.disable()
+                pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(25)
+            return
+        self._loop()
+
+    def _loop(self):
         torch.cuda.set_device(self.device_index)
         with torch.cuda.stream(self.stream):
             while True:
@@ -160,9 +212,14 @@ class AsyncFusion:
                     continue
                 count, pose, make_pred, ready = item
                 try:
+                    t0 = time.perf_counter()
                     if ready is not None:
                         self.stream.wait_event(ready)
-                    self.stage.keyframe(count, pose, make_pred())
+                    if count is None:
+                        make_pred(self.stage)
+                    else:
+                        self.stage.keyframe(count, pose, make_pred())
+                    self.busy_s += time.perf_counter() - t0
                 except BaseException as e:  # noqa: BLE001 - re-raised on join()
                     self.err = e
 

@@ -11,7 +11,6 @@ signatures and return values but run on the GPU:
 from __future__ import annotations
 
 import itertools
-import warnings
 from typing import Any, Dict, List, Tuple
 
 import numpy as np
@@ -38,7 +37,7 @@ class Exchange:
             if isinstance(v, np.ndarray):
                 o, n, _ = self.layout[k]
                 host[o:o + n] = v.reshape(-1)
-        self.buf = torch.from_numpy(host).to(dev)
+        self.buf = _lib.h2d(host, dev)
         self.dev = {k: self.buf[o:o + n].view(*shape) for k, (o, n, shape) in self.layout.items()}
 
     def fetch(self):
@@ -50,6 +49,7 @@ class Instances3D:
     def __init__(self, image_size: Tuple[int, int] = (0, 0), **kwargs: Any):
         self._image_size = image_size
         self._fields: Dict[str, Any] = {}
+        self._len = None
         for k, v in kwargs.items():
             self.set(k, v)
 
@@ -69,17 +69,19 @@ class Instances3D:
         return self._fields[name]
 
     def set(self, name, value):
-        with warnings.catch_warnings(record=True):
-            n = len(value)
-        if len(self._fields):
-            assert len(self) == n, f"Adding a field of length {n} to a Instances3D of length {len(self)}"
+        n = value.shape[0] if isinstance(value, (torch.Tensor, np.ndarray)) else len(value)
+        if self._fields and not (len(self._fields) == 1 and name in self._fields):
+            assert self._len == n, f"Adding a field of length {n} to a Instances3D of length {self._len}"
         self._fields[name] = value
+        self._len = n
 
     def has(self, name):
         return name in self._fields
 
     def remove(self, name):
         del self._fields[name]
+        if not self._fields:
+            self._len = None
 
     def get(self, name):
         return self._fields[name]
@@ -104,7 +106,8 @@ class Instances3D:
 
         def on(device):
             if device not in dev_index:
-                dev_index[device] = torch.as_tensor(item, device=device)
+                dev_index[device] = (_lib.h2d(item, device) if isinstance(item, np.ndarray)
+                                     else torch.as_tensor(item, device=device))
             return dev_index[device]
         for k, v in self._fields.items():
             if isinstance(v, (torch.Tensor, np.ndarray)) or hasattr(v, "tensor"):
@@ -135,9 +138,9 @@ class Instances3D:
         return ret
 
     def __len__(self):
-        for v in self._fields.values():
-            return v.__len__()
-        raise NotImplementedError("Empty Instances3D does not support __len__!")
+        if self._len is None:
+            raise NotImplementedError("Empty Instances3D does not support __len__!")
+        return self._len
 
     def __iter__(self):
         raise NotImplementedError("`Instances3D` object is not iterable!")
@@ -249,7 +252,7 @@ class Instances3D:
                      succ=np.asarray(success_all if success_all else [0], np.int32),
                      counts=np.zeros(3, np.int32), keep=max(1, len(mask_np)), events=3 * (n_all + 1))
         if cur_pose is None:
-            cur_pose = torch.as_tensor(np.asarray(all_kf_pose[frame_id], dtype=np.float32), device=dev)
+            cur_pose = _lib.h2d(np.asarray(all_kf_pose[frame_id], dtype=np.float32), dev)
         K = torch.as_tensor(intrinsic).to(dev, torch.float32)
         succ_dev = x.dev["succ"][:len(success_all)]
         _lib.corr_assoc(

@@ -183,3 +183,29 @@ def test_detect_stage_graph_equals_eager(dev):
         for ra, rb in zip(eager.last["res"], graph.last["res"]):
             torch.testing.assert_close(ra.scores, rb.scores, rtol=1e-4, atol=1e-6)
             torch.testing.assert_close(ra.pred_boxes_3d.tensor, rb.pred_boxes_3d.tensor, rtol=1e-4, atol=1e-4)
+
+
+def test_fusion_stage_batched_keyframes(dev):
+    """FusionStage.keyframes (world transform / projection / ids batched over 8 keyframes, then
+    the serial association) == keyframe() one at a time, bit for bit, over 48 keyframes."""
+    from boxfusion_amd.fusion_stage import FusionStage
+    from boxfusion_amd.instances import Instances3D
+    from boxfusion_amd.pipeline import scene_instances
+    from boxfusion_amd.synthetic import SCANNET_K, Scene
+    cfg = dict(TU.SCANNET_CFG, data=dict(gap=1))
+    scene = Scene(seed=0)
+    one = FusionStage(cfg, SCANNET_K, device=dev)
+    bat = FusionStage(cfg, SCANNET_K, device=dev)
+    for s0 in range(0, 48, 8):
+        fr = list(range(s0, s0 + 8))
+        dets = [scene.detections(f) for f in fr]
+        for f, d in zip(fr, dets):
+            one.keyframe(f, scene.pose(f), scene_instances(d, dev))
+        preds = Instances3D.cat([scene_instances(d, dev) for d in dets])
+        bat.keyframes(fr, np.stack([scene.pose(f) for f in fr]), preds, [len(d["scores"]) for d in dets])
+        assert bat.box_manager.fusion_list == one.box_manager.fusion_list, f"step at {s0}"
+        assert bat.box_manager.already_fusion == one.box_manager.already_fusion, f"step at {s0}"
+        assert bat.box_manager.fusion_flag == one.box_manager.fusion_flag, f"step at {s0}"
+        for a, b in zip(bat.boxes(), one.boxes()):
+            np.testing.assert_array_equal(a, b, err_msg=f"step at {s0}")
+    assert bat.stats == one.stats and bat.stats["fused"] > 5
