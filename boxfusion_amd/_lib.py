@@ -199,6 +199,22 @@ def corr_assoc(corners, dims, scores, boxes2d, init_id, cam_poses, cur_pose, K, 
     return keep, events, counts
 
 
+def corr_assoc_chained(corners, dims, scores, boxes2d, init_id, cam_poses, cur_pose, K, n_glo,
+                       mask, n_mask, success, n_success, fl_items, fl_len, valid_num,
+                       cfg: CorrCfg, out):
+    """bf_corr_assoc_chained: correspondence association on nms_scan's device outputs (mask /
+    n_mask = its keep / counts[0:1], success / n_success = its succ / counts[1:2]); `out` =
+    (keep [n_all], events [n_all + 1, 3], counts [3]) preallocated device views"""
+    keep, events, counts = out
+    _check(lib().bf_corr_assoc_chained(
+        _ptr(corners), _ptr(dims), _ptr(scores), _ptr(boxes2d), _ptr(init_id), _ptr(cam_poses),
+        _ptr(cur_pose), _ptr(K), c_int(scores.shape[0]), c_int(n_glo), _ptr(mask), _ptr(n_mask),
+        _ptr(success), _ptr(n_success), _ptr(fl_items), _ptr(fl_len), _ptr(valid_num), _ptr(keep),
+        _ptr(counts[0:1]), _ptr(events), _ptr(counts[1:2]), _ptr(counts[2:3]), ctypes.byref(cfg),
+        _stream()), "bf_corr_assoc_chained")
+    return keep, events, counts
+
+
 # ------------------------------------------------------------------------------------------
 # fusion
 # ------------------------------------------------------------------------------------------

@@ -78,6 +78,10 @@ class GeneralInstance3DBoxes:
             return GeneralInstance3DBoxes(self.tensor[item].view(1, -1), self.R[item].view(1, 3, 3))
         if isinstance(item, slice) and (item.step is None or item.step == 1):
             return GeneralInstance3DBoxes._views(self.tensor[item], self.R[item])
+        if isinstance(item, torch.Tensor) and item.dtype in (torch.int64, torch.int32) and item.dim() == 1:
+            # a gather makes new tensors already: no second copy
+            return GeneralInstance3DBoxes._views(self.tensor.index_select(0, item),
+                                                 self.R.index_select(0, item))
         b, r = self.tensor[item], self.R[item]
         assert b.dim() == 2, f"Indexing on Boxes with {item} failed to return a matrix!"
         return GeneralInstance3DBoxes(b, r)
@@ -92,7 +96,7 @@ class GeneralInstance3DBoxes:
     def cat(cls, boxes_list):
         if len(boxes_list) == 0:
             return cls.empty()
-        return cls(torch.cat([b.tensor for b in boxes_list], 0), torch.cat([b.R for b in boxes_list], 0))
+        return cls._views(torch.cat([b.tensor for b in boxes_list], 0), torch.cat([b.R for b in boxes_list], 0))
 
     def split(self, sizes):
         return [GeneralInstance3DBoxes(t, r) for t, r in

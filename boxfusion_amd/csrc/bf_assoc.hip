@@ -349,7 +349,15 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_corr_assoc(
     const int32_t* __restrict__ mask, int n_mask, const int32_t* __restrict__ success, int n_success,
     int32_t* __restrict__ fl, int32_t* __restrict__ fl_len, float* __restrict__ valid_num,
     int32_t* __restrict__ keep_out, int32_t* __restrict__ n_keep_out, int32_t* __restrict__ events,
-    int32_t* __restrict__ n_events, int32_t* __restrict__ status, bf_corr_cfg cfg) {
+    int32_t* __restrict__ n_events, int32_t* __restrict__ status, bf_corr_cfg cfg,
+    const int32_t* __restrict__ n_mask_dev, const int32_t* __restrict__ n_success_dev) {
+    // chained after bf_nms_scan: the mask / success counts are that kernel's device outputs
+    // (n_mask is then the capacity the LDS was sized for)
+    if (n_mask_dev) {
+        const int nm = *n_mask_dev;
+        n_mask = nm < n_mask ? nm : n_mask;
+        n_success = *n_success_dev;
+    }
     extern __shared__ __attribute__((aligned(16))) double dsm[];
     double* b2d = dsm;                                  // [ng][4]
     int* keep = reinterpret_cast<int*>(b2d + 4 * (size_t)(n_mask + 1));  // [n_mask]
@@ -461,6 +469,32 @@ BF_API int bf_corr_assoc(const float* corners, const float* dims, const float* s
     hipLaunchKernelGGL(k_corr_assoc, dim3(1), dim3(SCAN_THREADS), lds, bf_stream(stream), corners,
                        dims, scores, boxes2d, init_id, cam_poses, cur_pose, K, n_all, n_glo, mask,
                        n_mask, success, n_success, fl_items, fl_len, valid_num, keep_out,
-                       n_keep_out, events, n_events, status, *cfg);
+                       n_keep_out, events, n_events, status, *cfg, (const int32_t*)nullptr,
+                       (const int32_t*)nullptr);
+    return bf_check_launch();
+}
+
+BF_API int bf_corr_assoc_chained(const float* corners, const float* dims, const float* scores,
+                                 const float* boxes2d, const int32_t* init_id,
+                                 const float* cam_poses, const float* cur_pose, const float* K,
+                                 int n_all, int n_glo, const int32_t* mask,
+                                 const int32_t* n_mask_dev, const int32_t* success,
+                                 const int32_t* n_success_dev, int32_t* fl_items, int32_t* fl_len,
+                                 float* valid_num, int32_t* keep_out, int32_t* n_keep_out,
+                                 int32_t* events, int32_t* n_events, int32_t* status,
+                                 const bf_corr_cfg* cfg, void* stream) {
+    if (!cfg || n_all < 0 || !n_mask_dev || !n_success_dev || !mask || !success) return BF_ERR_ARG;
+    if (n_all > BF_MAX_BOXES) return BF_ERR_CAPACITY;
+    if (n_all == 0) {
+        return hipMemsetAsync(n_keep_out, 0, sizeof(int32_t), bf_stream(stream)) == hipSuccess
+                   ? BF_OK : BF_ERR_LAUNCH;
+    }
+    const int n_mask = n_all;   // nms keep <= n_all
+    size_t lds = sizeof(double) * 4 * (size_t)(n_mask + 1) + sizeof(int) * 2 * (size_t)(n_mask + 1) +
+                 (size_t)n_mask + 16;
+    hipLaunchKernelGGL(k_corr_assoc, dim3(1), dim3(SCAN_THREADS), lds, bf_stream(stream), corners,
+                       dims, scores, boxes2d, init_id, cam_poses, cur_pose, K, n_all, n_glo, mask,
+                       n_mask, success, 0, fl_items, fl_len, valid_num, keep_out, n_keep_out,
+                       events, n_events, status, *cfg, n_mask_dev, n_success_dev);
     return bf_check_launch();
 }

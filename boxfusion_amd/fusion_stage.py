@@ -55,6 +55,9 @@ class FusionStage:
         self.last_pred = None
         self._stats = dict(keyframes=0, suppressed=0)
         self.K_dev = torch.from_numpy(self.K3).to(self.dev)     # uploaded once
+        # nms + correspondence association chained on the device (one host round trip);
+        # False: the reference's two separate calls (same results)
+        self.joint = os.environ.get("BF_JOINT_ASSOC", "1") != "0"
 
     @property
     def stats(self):
@@ -125,18 +128,32 @@ class FusionStage:
         self.per_frame_ins = Instances3D.cat([self.per_frame_ins, pred])
         all_poses = np.concatenate((self.all_poses, pose_np), axis=0)
         corners = all_pred_box.pred_boxes_3d.corners       # shared by both association steps
-        mask, success = Instances3D.spatial_association(all_pred_box, cfg["box_fusion"]["nms_threshold"],
-                                                        bm, self.per_frame_ins.cam_pose, corners=corners)
+        if self.joint and len(all_pred_box) > 1:
+            # nms + correspondence back to back on the device, one read-back
+            mask, success, keep_idx, any_cur = Instances3D.joint_association(
+                all_pred_box, n_before, cfg["box_fusion"]["nms_threshold"],
+                cfg["association"]["small_threshold"], bm, self.per_frame_ins.cam_pose,
+                pred.cam_pose[0], self.K_dev, corners, H=self.H, W=self.W)
+            if any_cur:
+                all_pred_box = all_pred_box[keep_idx]
+                all_poses = all_poses[keep_idx]
+            else:
+                keep_idx = np.asarray(mask)
+        else:
+            mask, success = Instances3D.spatial_association(all_pred_box, cfg["box_fusion"]["nms_threshold"],
+                                                            bm, self.per_frame_ins.cam_pose, corners=corners)
+            cur_keep = [i - n_before for i in mask if i >= n_before]
+            any_cur = bool(cur_keep)
+            keep_idx = np.asarray(mask)
+            if any_cur:
+                cur_success = [i - n_before for i in success if i >= n_before]
+                all_pred_box, all_poses, keep_idx = Instances3D.correspondence_association(
+                    cfg, bm, cur_keep, cur_success, pred, cur_global, all_pred_box, all_poses,
+                    self.per_frame_ins.cam_pose, count, mask, self.K_dev, self.all_kf_pose,
+                    threshold=cfg["association"]["small_threshold"], H=self.H, W=self.W,
+                    corners=corners, cur_pose=pred.cam_pose[0])
         self._stats["suppressed"] += len(success)
-        cur_keep = [i - n_before for i in mask if i >= n_before]
-        cur_success = [i - n_before for i in success if i >= n_before]
-        keep_idx = np.asarray(mask)
-        if cur_keep:
-            all_pred_box, all_poses, keep_idx = Instances3D.correspondence_association(
-                cfg, bm, cur_keep, cur_success, pred, cur_global, all_pred_box, all_poses,
-                self.per_frame_ins.cam_pose, count, mask, self.K_dev, self.all_kf_pose,
-                threshold=cfg["association"]["small_threshold"], H=self.H, W=self.W,
-                corners=corners, cur_pose=pred.cam_pose[0])
+        if any_cur:
             bm.update(keep_idx)
             if cfg["box_fusion"].get("check_valid", False):
                 all_pred_box = bm.check_valid_num(all_pred_box, count, self.gap)

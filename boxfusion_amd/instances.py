@@ -114,7 +114,8 @@ class Instances3D:
                 if isinstance(v, np.ndarray) and isinstance(item, torch.Tensor):
                     ret.set(k, v[item.cpu().numpy()])
                 elif isinstance(v, torch.Tensor) and isinstance(item, np.ndarray):
-                    ret.set(k, v[on(v.device)])
+                    ix = on(v.device)
+                    ret.set(k, v.index_select(0, ix) if ix.dtype == torch.int64 and ix.dim() == 1 else v[ix])
                 elif hasattr(v, "tensor") and isinstance(item, np.ndarray):
                     ret.set(k, v[on(v.tensor.device)])
                 else:
@@ -271,3 +272,52 @@ class Instances3D:
         box_manager.replay_flags(h["events"].reshape(-1, 3)[:c[1]].tolist())
         keep_idx = h["keep"][:c[0]].astype(np.int64)
         return all_pred_box[keep_idx], all_poses[keep_idx], keep_idx
+
+    def joint_association(all_pred_box, n_glo, threshold, small_threshold, box_manager,
+                          per_frame_ins_cam_pose, cur_pose, intrinsic, corners, H=480, W=640):
+        """spatial_association followed by correspondence_association (demo.py:243-262) with ONE
+        host round trip: bf_nms_scan and bf_corr_assoc_chained run back to back on the stream,
+        the second on the first's device outputs.  Returns (mask, success, keep_idx, cur_keep):
+        mask / success as spatial_association's, keep_idx = correspondence_association's keep
+        (equal to mask when no new box survived the NMS, the case where the reference skips the
+        second step), cur_keep = whether a new box (index >= n_glo) is in mask."""
+        boxes = all_pred_box.get("pred_boxes_3d")
+        dev = boxes.device
+        iou = _lib.obb_iou_matrix(corners)
+        scores = all_pred_box.scores.to(dev, torch.float32).contiguous()
+        init_id = all_pred_box.init_id.to(dev, torch.int32).contiguous()
+        poses = per_frame_ins_cam_pose.to(dev, torch.float32).contiguous()
+        vn = all_pred_box.valid_num
+        if not (isinstance(vn, torch.Tensor) and vn.is_cuda and vn.dtype == torch.float32 and vn.is_contiguous()):
+            vn = torch.as_tensor(vn).to(dev, torch.float32).contiguous()
+            all_pred_box.valid_num = vn
+        items, lens = box_manager.pack_host()
+        n = scores.shape[0]
+        x = Exchange(dev, items=items, lens=lens, counts=np.zeros(4, np.int32), keep=n + 1,
+                     succ=n + 1, events=3 * (n + 1), ccounts=np.zeros(3, np.int32), ckeep=n + 1,
+                     cevents=3 * (n + 1))
+        d = x.dev
+        _lib.nms_scan(iou, corners, scores, init_id, poses, d["items"], d["lens"], vn,
+                      box_manager.nms_cfg(threshold),
+                      out=(d["keep"], d["succ"], d["events"].view(-1, 3), d["counts"]))
+        _lib.corr_assoc_chained(
+            corners, boxes.dims.contiguous(), scores,
+            all_pred_box.pred_boxes.to(dev, torch.float32).contiguous(), init_id, poses, cur_pose,
+            torch.as_tensor(intrinsic).to(dev, torch.float32), n_glo, d["keep"], d["counts"][0:1],
+            d["succ"], d["counts"][1:2], d["items"], d["lens"], vn,
+            box_manager.corr_cfg(small_threshold, W, H),
+            out=(d["ckeep"], d["cevents"].view(-1, 3), d["ccounts"]))
+        h = x.fetch()
+        c, cc = h["counts"], h["ccounts"]
+        if c[3]:
+            raise _lib.HipError(f"bf_nms_scan device status {c[3]} (fusion list capacity)")
+        if cc[2]:
+            raise _lib.HipError(f"bf_corr_assoc device status {cc[2]} (fusion list capacity)")
+        box_manager.unpack_host(h["items"], h["lens"])
+        # the NMS events, then the correspondence events, exactly as the two calls replay them
+        box_manager.replay_flags(h["events"].reshape(-1, 3)[:c[2]].tolist())
+        box_manager.replay_flags(h["cevents"].reshape(-1, 3)[:cc[1]].tolist())
+        mask = h["keep"][:c[0]].astype(np.int64)
+        success = h["succ"][:c[1]].astype(np.int64).tolist()
+        keep_idx = h["ckeep"][:cc[0]].astype(np.int64)
+        return mask.tolist(), success, keep_idx, bool((mask >= n_glo).any())

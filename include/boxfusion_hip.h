@@ -132,6 +132,24 @@ int bf_corr_assoc(const float* corners, const float* dims, const float* scores,
                   int32_t* keep_out, int32_t* n_keep_out, int32_t* events, int32_t* n_events,
                   int32_t* status, const bf_corr_cfg* cfg, void* stream);
 
+/* bf_corr_assoc chained on the stream right after bf_nms_scan, without the host round trip the
+ * reference makes between the two steps (demo.py:243-262: spatial_association returns `mask`
+ * and `success` to Python, which slices cur_keep / cur_success and calls
+ * correspondence_association).  mask / n_mask_dev and success / n_success_dev are the NMS
+ * kernel's device outputs (keep / n_keep, success / n_success), fl_items / fl_len / valid_num
+ * the same buffers it updated.  With no new box in `mask` (cur_keep empty: the reference skips
+ * the step) the kernel returns keep_out = mask and no events, so the caller may branch after
+ * reading both results back once. */
+int bf_corr_assoc_chained(const float* corners, const float* dims, const float* scores,
+                          const float* boxes2d, const int32_t* init_id, const float* cam_poses,
+                          const float* cur_pose, const float* K, int n_all, int n_glo,
+                          const int32_t* mask, const int32_t* n_mask_dev,
+                          const int32_t* success, const int32_t* n_success_dev,
+                          int32_t* fl_items, int32_t* fl_len, float* valid_num,
+                          int32_t* keep_out, int32_t* n_keep_out, int32_t* events,
+                          int32_t* n_events, int32_t* status, const bf_corr_cfg* cfg,
+                          void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Multi-view box fusion: particle-swarm refinement
  *   BoxFusion.boxfusion (box_fusion.py:622-724), init_opt_params (:566-600),

@@ -209,3 +209,27 @@ def test_fusion_stage_batched_keyframes(dev):
         for a, b in zip(bat.boxes(), one.boxes()):
             np.testing.assert_array_equal(a, b, err_msg=f"step at {s0}")
     assert bat.stats == one.stats and bat.stats["fused"] > 5
+
+
+@pytest.mark.gpu
+def test_fusion_stage_joint_association(dev):
+    """nms + correspondence association chained on the device (bf_corr_assoc_chained, one read-back)
+    == the reference's two separate calls, bit for bit, over 64 gap=1 keyframes."""
+    from boxfusion_amd.fusion_stage import FusionStage
+    from boxfusion_amd.pipeline import scene_instances
+    from boxfusion_amd.synthetic import SCANNET_K, Scene
+    cfg = dict(TU.SCANNET_CFG, data=dict(gap=1))
+    scene = Scene(seed=3)
+    jnt = FusionStage(cfg, SCANNET_K, device=dev)
+    sep = FusionStage(cfg, SCANNET_K, device=dev)
+    jnt.joint, sep.joint = True, False
+    for f in range(64):
+        d = scene.detections(f)
+        jnt.keyframe(f, scene.pose(f), scene_instances(d, dev))
+        sep.keyframe(f, scene.pose(f), scene_instances(d, dev))
+        assert jnt.box_manager.fusion_list == sep.box_manager.fusion_list, f"keyframe {f}"
+        assert jnt.box_manager.fusion_flag == sep.box_manager.fusion_flag, f"keyframe {f}"
+        for a, b in zip(jnt.boxes(), sep.boxes()):
+            np.testing.assert_array_equal(a, b, err_msg=f"keyframe {f}")
+    assert jnt.box_manager.already_fusion == sep.box_manager.already_fusion
+    assert jnt.stats == sep.stats and jnt.stats["suppressed"] > 50
