@@ -13,7 +13,8 @@ import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libboxfusion_hip.so")
+# BF_LIB_PATH: a diagnostic build of the same sources (e.g. one that forces a rare kernel path)
+LIB_PATH = os.environ.get("BF_LIB_PATH") or os.path.join(HERE, "libboxfusion_hip.so")
 _LIB = None
 
 c_int, c_float, c_double, c_void_p, c_size_t = (ctypes.c_int, ctypes.c_float, ctypes.c_double,

@@ -214,6 +214,199 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_nms_scan(
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Single-wave NMS scan for small problems (n <= NMS_FAST_N and every operand fits in LDS).
+// The IoU matrix, fusion lists, init ids, valid_num, scores and box centres are staged in LDS;
+// the compaction of the remaining candidates is a wave ballot (no workgroup barriers); the
+// pose-disparity tests of one suppression over a fusion list run on the list's lanes at once
+// (record() only counts them: order-free).  The list / keep edits stay on lane 0 in the
+// reference's order, so the results are those of k_nms_scan.
+// ------------------------------------------------------------------------------------------
+#ifndef NMS_FAST_N
+#define NMS_FAST_N 96       // (a diagnostic build sets 0 to run k_nms_scan everywhere)
+#endif
+#define NMS_FAST_LDS_MAX (150 * 1024)
+
+__device__ __forceinline__ unsigned long long lanes_lt_mask() {
+    const int l = threadIdx.x & 63;
+    return l == 0 ? 0ull : ((1ull << l) - 1ull);
+}
+
+// entries q < L of `row` whose pose is far from pose pj (record()'s count, box_manager.py:51-80)
+__device__ __forceinline__ int nms_count_far(const int* row, int L, const float* poses, int pj,
+                                             float cd, const bf_nms_cfg& cfg) {
+    int cnt = 0;
+    for (int base = 0; base < L; base += 64) {
+        const int q = base + (int)threadIdx.x;
+        bool f = false;
+        if (q < L) {
+            float b, a;
+            bf_pose_disparity(poses + 16 * (size_t)row[q], poses + 16 * (size_t)pj, &b, &a);
+            f = (b > cfg.translation_gap || a > cfg.rotation_gap) || (double)cd > cfg.center_gap;
+        }
+        cnt += __popcll(__ballot(f));
+    }
+    return cnt;
+}
+
+static size_t nms_fast_lds(int n, int cap) {
+    return sizeof(double) * (size_t)n * n                       // IoU
+           + sizeof(int) * ((size_t)n * cap + 2 * (size_t)n)     // lists, lengths, init ids
+           + sizeof(float) * 5 * (size_t)n                       // valid_num, scores, centres
+           + sizeof(int) * (5 * (size_t)n + 8);                  // order x2, supp, keep, succ
+}
+
+__global__ void __launch_bounds__(64) k_nms_scan_w(
+    const double* __restrict__ iou, const float* __restrict__ corners,
+    const float* __restrict__ scores, const int32_t* __restrict__ init_id,
+    const float* __restrict__ poses, int n, int32_t* __restrict__ fl, int32_t* __restrict__ fl_len,
+    float* __restrict__ valid_num, int32_t* __restrict__ keep_out, int32_t* __restrict__ n_keep,
+    int32_t* __restrict__ succ_out, int32_t* __restrict__ n_succ, int32_t* __restrict__ events,
+    int32_t* __restrict__ n_events, int32_t* __restrict__ status, bf_nms_cfg cfg) {
+    extern __shared__ __attribute__((aligned(16))) double wsm[];
+    const int cap = cfg.list_capacity;
+    const int t = threadIdx.x;
+    double* I = wsm;
+    int* fls = reinterpret_cast<int*>(I + (size_t)n * n);
+    int* fll = fls + (size_t)n * cap;
+    int* iid = fll + n;
+    float* vn = reinterpret_cast<float*>(iid + n);
+    float* sc = vn + n;
+    float* cen = sc + n;
+    int* bufA = reinterpret_cast<int*>(cen + 3 * n);
+    int* bufB = bufA + n + 1;
+    int* supp = bufB + n + 1;
+    int* keep = supp + n + 1;
+    int* succ = keep + n + 2;
+    for (int q = t; q < n * n; q += 64) I[q] = iou[q];
+    for (int q = t; q < n * cap; q += 64) fls[q] = fl[q];
+    for (int q = t; q < n; q += 64) {
+        fll[q] = fl_len[q];
+        iid[q] = init_id[q];
+        vn[q] = valid_num[q];
+        sc[q] = scores[q];
+        box_center(corners, q, cen + 3 * q);
+    }
+    __syncthreads();
+    // order = scores.argsort()[::-1]: descending, ties -> higher index first
+    for (int i = t; i < n; i += 64) {
+        const float si = sc[i];
+        int r = 0;
+        for (int j = 0; j < n; ++j) {
+            const float sj = sc[j];
+            r += (sj > si) || (sj == si && j > i);
+        }
+        bufA[r] = i;
+    }
+    __syncthreads();
+    int* order = bufA;
+    int* rest = bufB;
+    int no = n, nk = 0, ns = 0, nev = 0, st = 0;   // wave-uniform counters (st: lane 0)
+    while (no > 0) {
+        const int i = order[0];
+        if (t == 0) keep[nk] = i;
+        nk++;
+        int nrest = 0, nsupp = 0;
+        for (int base = 1; base < no; base += 64) {
+            const int q = base + t;
+            const bool live = q < no;
+            const int j = order[live ? q : no - 1];
+            const double v = live ? I[(size_t)i * n + j] : 0.0;
+            const bool fr = live && (v <= cfg.iou_threshold);
+            const bool fs = live && (v > cfg.iou_threshold);
+            const unsigned long long mr = __ballot(fr), ms = __ballot(fs);
+            if (fr) rest[nrest + __popcll(mr & lanes_lt_mask())] = j;
+            if (fs) supp[nsupp + __popcll(ms & lanes_lt_mask())] = j;
+            nrest += __popcll(mr);
+            nsupp += __popcll(ms);
+        }
+        __syncthreads();
+        if (nsupp > 0) {
+            if (t == 0) {
+                vn[i] += 1.0f;
+                succ[ns] = i;
+            }
+            ns++;
+            // BoxManager.record(cur=i, fusion_inds=supp)
+            const int cur = i;
+            const float* ccur = cen + 3 * cur;
+            for (int s = 0; s < nsupp; ++s) {
+                const int idx = supp[s];
+                const float* cidx = cen + 3 * idx;
+                float dx = ccur[0] - cidx[0], dy = ccur[1] - cidx[1], dz = ccur[2] - cidx[2];
+                float cd = sqrtf((dx * dx + dy * dy) + dz * dz);
+                int branch;
+                if (fll[idx] == 1) {
+                    branch = 1;
+                    const int L = fll[cur];
+                    const int cnt = nms_count_far(fls + (size_t)cur * cap, L, poses, iid[idx], cd, cfg);
+                    if (cnt == L && L < cfg.max_list && t == 0) {
+                        int32_t v = iid[idx];
+                        st |= fl_append_sorted(fls + (size_t)cur * cap, fll + cur, cap, &v, 1);
+                    }
+                } else {
+                    branch = 2;
+                    const int L = fll[idx];
+                    const int cnt = nms_count_far(fls + (size_t)idx * cap, L, poses, iid[cur], cd, cfg);
+                    if (cnt == L && L < cfg.max_list) {
+                        // fl[cur] += fl[idx]  (rows are distinct, cur != idx)
+                        if (t == 0)
+                            st |= fl_append_sorted(fls + (size_t)cur * cap, fll + cur, cap,
+                                                   fls + (size_t)idx * cap, L);
+                    } else if (t == 0) {
+                        int pos = -1;
+                        for (int q = 0; q < nk; ++q)
+                            if (keep[q] == cur) { pos = q; break; }
+                        if (pos >= 0) {
+                            for (int q = pos; q + 1 < nk; ++q) keep[q] = keep[q + 1];
+                            keep[nk - 1] = idx;
+                        }
+                    }
+                }
+                if (t == 0) {
+                    events[3 * nev + 0] = cur;
+                    events[3 * nev + 1] = idx;
+                    events[3 * nev + 2] = branch;
+                }
+                nev++;
+                __syncthreads();   // lane 0's LDS edits before the next suppression reads them
+            }
+        }
+        no = nrest;
+        int* tmp = order; order = rest; rest = tmp;
+        if (nrest == 1) {
+            if (t == 0) keep[nk] = order[0];
+            nk++;
+            break;
+        }
+    }
+    __syncthreads();
+    // sort keep / success (distinct indices) by rank into the outputs
+    for (int q = t; q < nk; q += 64) {
+        const int v = keep[q];
+        int r = 0;
+        for (int k = 0; k < nk; ++k) r += keep[k] < v;
+        keep_out[r] = v;
+    }
+    for (int q = t; q < ns; q += 64) {
+        const int v = succ[q];
+        int r = 0;
+        for (int k = 0; k < ns; ++k) r += succ[k] < v;
+        succ_out[r] = v;
+    }
+    for (int q = t; q < n * cap; q += 64) fl[q] = fls[q];
+    for (int q = t; q < n; q += 64) {
+        fl_len[q] = fll[q];
+        valid_num[q] = vn[q];
+    }
+    if (t == 0) {
+        *n_keep = nk;
+        *n_succ = ns;
+        *n_events = nev;
+        *status |= st;
+    }
+}
+
 BF_API int bf_nms_scan(const double* iou, const float* corners, const float* scores,
                        const int32_t* init_id, const float* cam_poses, int n, int32_t* fl_items,
                        int32_t* fl_len, float* valid_num, int32_t* keep, int32_t* n_keep,
@@ -225,6 +418,19 @@ BF_API int bf_nms_scan(const double* iou, const float* corners, const float* sco
     if (!iou || !corners || !scores || !init_id || !cam_poses || !fl_items || !fl_len ||
         !valid_num || !keep || !n_keep || !success || !n_success || !events || !n_events || !status)
         return BF_ERR_ARG;
+    if (n <= NMS_FAST_N && nms_fast_lds(n, cfg->list_capacity) <= NMS_FAST_LDS_MAX) {
+        static bool attr_w = false;
+        if (!attr_w) {
+            hipFuncSetAttribute((const void*)k_nms_scan_w, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                NMS_FAST_LDS_MAX);
+            attr_w = true;
+        }
+        hipLaunchKernelGGL(k_nms_scan_w, dim3(1), dim3(64), nms_fast_lds(n, cfg->list_capacity),
+                           bf_stream(stream), iou, corners, scores, init_id, cam_poses, n, fl_items,
+                           fl_len, valid_num, keep, n_keep, success, n_success, events, n_events,
+                           status, *cfg);
+        return bf_check_launch();
+    }
     size_t lds = sizeof(int) * (size_t)(5 * n + 8) + sizeof(float) * 3 * (size_t)n;
     if ((size_t)n * n <= NMS_IOU_LDS_MAX) lds += sizeof(double) * (size_t)n * n;
     static bool attr_set = false;

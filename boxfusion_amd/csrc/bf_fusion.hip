@@ -142,6 +142,157 @@ __device__ float iou_hulls(P2* c0, P2* ct, int* flags) {
     return iou_hull_pre(c0, ht, nt, polygon_area(ht, nt), flags);
 }
 
+// ------------------------------------------------------------------------------------------
+// LDS form of iou_hull_pre for the refinement loop (same arithmetic, same results).
+// The scratch form keeps ~2 KB of per-thread arrays (hull stacks, 64 candidates) that spill
+// to L2 at this kernel's occupancy; here one wave's stacks live in LDS, element e of lane l
+// at [e * 64 + l], and the 8 projected corners are sorted in registers by a 19-comparator
+// network (any correct sort gives the exchange sort's order: equal keys are equal points).
+// Lanes with more than FAST_CAND candidates (never seen on real boxes: two convex 8-gons give
+// at most 16 vertices + 16 crossings in general position) take the scratch path.
+// ------------------------------------------------------------------------------------------
+#ifndef FAST_CAND
+#define FAST_CAND 32   // (a diagnostic build lowers it to exercise the scratch path)
+#endif
+struct HullLds {
+    P2 cand[FAST_CAND * 64];   // candidates, sorted; then the lower chain in place
+    P2 up[FAST_CAND * 64];     // upper chain of the candidate hull
+    P2 lo0[8 * 64];            // lower chain of hull(c0)
+    P2 up0[8 * 64];            // upper chain of hull(c0)
+};
+
+__device__ __forceinline__ bool p2_greater(P2 a, P2 b) {
+    return a.x > b.x || (a.x == b.x && a.y > b.y);
+}
+
+__device__ __forceinline__ void p2_cswap(P2& a, P2& b) {
+    const bool g = p2_greater(a, b);
+    const P2 lo = g ? b : a, hi = g ? a : b;
+    a = lo;
+    b = hi;
+}
+
+// hull vertex i of a monotone-chain hull stored as lower[0..nl-1) ++ upper[0..nu-1)
+#define HULL_AT(lo, up, nl1, i) ((i) < (nl1) ? (lo)[(i) * 64] : (up)[((i) - (nl1)) * 64])
+
+__device__ float iou_hull_lds(const P2* c0in, const P2* ht, int nt, float at, HullLds& L,
+                              int lane, int* flags) {
+    P2 c[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c[j] = c0in[j];
+    p2_cswap(c[0], c[2]); p2_cswap(c[1], c[3]); p2_cswap(c[4], c[6]); p2_cswap(c[5], c[7]);
+    p2_cswap(c[0], c[4]); p2_cswap(c[1], c[5]); p2_cswap(c[2], c[6]); p2_cswap(c[3], c[7]);
+    p2_cswap(c[0], c[1]); p2_cswap(c[2], c[3]); p2_cswap(c[4], c[5]); p2_cswap(c[6], c[7]);
+    p2_cswap(c[2], c[4]); p2_cswap(c[3], c[5]);
+    p2_cswap(c[1], c[4]); p2_cswap(c[3], c[6]);
+    p2_cswap(c[1], c[2]); p2_cswap(c[3], c[4]); p2_cswap(c[5], c[6]);
+    // hull(c0): convex_hull's two monotone chains
+    P2* lo0 = L.lo0 + lane;
+    P2* up0 = L.up0 + lane;
+    int nl = 0, nu = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        while (nl >= 2 && cross2(lo0[(nl - 2) * 64], lo0[(nl - 1) * 64], c[i]) <= 0) nl--;
+        lo0[(nl++) * 64] = c[i];
+    }
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {
+        while (nu >= 2 && cross2(up0[(nu - 2) * 64], up0[(nu - 1) * 64], c[i]) <= 0) nu--;
+        up0[(nu++) * 64] = c[i];
+    }
+    const int nl1 = nl - 1;
+    const int n0 = nl1 + (nu - 1);
+    // candidates
+    P2* cand = L.cand + lane;
+    int nc = 0;
+    bool slow = false;
+    for (int i = 0; i < n0; ++i) {
+        const P2 p = HULL_AT(lo0, up0, nl1, i);
+        if (point_in_polygon(p, ht, nt)) {
+            if (nc < FAST_CAND) cand[(nc++) * 64] = p;
+            else slow = true;
+        }
+    }
+    for (int i = 0; i < nt; ++i) {
+        // point_in_polygon(ht[i], h0, n0)
+        const P2 p = ht[i];
+        bool in = false;
+        for (int k = 0; k < n0; ++k) {
+            const P2 p1 = HULL_AT(lo0, up0, nl1, k);
+            const P2 p2 = HULL_AT(lo0, up0, nl1, (k + 1) % n0);
+            if ((p1.y > p.y) != (p2.y > p.y)) {
+                float xi = ((p.y - p1.y) * (p2.x - p1.x) / (p2.y - p1.y)) + p1.x;
+                if (p.x < xi) in = !in;
+            }
+        }
+        if (in) {
+            if (nc < FAST_CAND) cand[(nc++) * 64] = p;
+            else slow = true;
+        }
+    }
+    for (int i = 0; i < n0 && !slow; ++i) {
+        const P2 a1 = HULL_AT(lo0, up0, nl1, i);
+        const P2 a2 = HULL_AT(lo0, up0, nl1, (i + 1) % n0);
+        for (int j = 0; j < nt; ++j) {
+            const P2 b1 = ht[j], b2 = ht[(j + 1) % nt];
+            if (seg_boxes_apart(a1, a2, b1, b2)) continue;
+            P2 pt;
+            if (line_intersection(a1, a2, b1, b2, &pt)) {
+                if (nc < FAST_CAND) cand[(nc++) * 64] = pt;
+                else { slow = true; break; }
+            }
+        }
+    }
+    if (slow) {   // scratch path from the original corners (rare)
+        P2 cc[8];
+        for (int j = 0; j < 8; ++j) cc[j] = c0in[j];
+        return iou_hull_pre(cc, ht, nt, at, flags);
+    }
+    float a0 = 0.0f;
+    for (int i = 0; i < n0; ++i) {
+        const P2 p1 = HULL_AT(lo0, up0, nl1, i), p2 = HULL_AT(lo0, up0, nl1, (i + 1) % n0);
+        a0 += p1.x * p2.y - p2.x * p1.y;
+    }
+    a0 = (float)(fabs((double)a0) / 2.0);
+    // hull(cand): sort (insertion: same order as the exchange sort), upper chain into `up`,
+    // then the lower chain in place over the sorted candidates (it writes index <= i only)
+    for (int i = 1; i < nc; ++i) {
+        const P2 x = cand[i * 64];
+        int j = i - 1;
+        while (j >= 0 && p2_greater(cand[j * 64], x)) { cand[(j + 1) * 64] = cand[j * 64]; --j; }
+        cand[(j + 1) * 64] = x;
+    }
+    P2* up = L.up + lane;
+    int ni = 0, cl1 = 0;
+    if (nc > 0) {
+        int mu = 0;
+        for (int i = nc - 1; i >= 0; --i) {
+            const P2 x = cand[i * 64];
+            while (mu >= 2 && cross2(up[(mu - 2) * 64], up[(mu - 1) * 64], x) <= 0) mu--;
+            up[(mu++) * 64] = x;
+        }
+        int ml = 0;
+        for (int i = 0; i < nc; ++i) {
+            const P2 x = cand[i * 64];
+            while (ml >= 2 && cross2(cand[(ml - 2) * 64], cand[(ml - 1) * 64], x) <= 0) ml--;
+            cand[(ml++) * 64] = x;
+        }
+        cl1 = ml - 1;
+        ni = cl1 + (mu - 1);
+    }
+    if (ni > 8) *flags |= BF_DEV_HULL_OVERFLOW;
+    float inter = 0.0f;
+    for (int i = 0; i < ni; ++i) {
+        const P2 p1 = HULL_AT(cand, up, cl1, i), p2 = HULL_AT(cand, up, cl1, (i + 1) % ni);
+        inter += p1.x * p2.y - p2.x * p1.y;
+    }
+    inter = (float)(fabs((double)inter) / 2.0);
+    float uni = a0 + at - inter;
+    float iou = 0;
+    if (uni > 0) iou = (float)((double)inter / ((double)uni + 0.00001));
+    return iou;
+}
+
 struct FuseViews {
     float pose[FUSE_MAX_VIEWS][16];
     float tc[FUSE_MAX_VIEWS][16];
@@ -322,9 +473,33 @@ __global__ void __launch_bounds__(64) k_fuse_init(const int32_t* __restrict__ vi
     for (int k = 0; k < 6; ++k) S.box32[k] = (float)S.x[k];
 }
 
-#define TERM_THREADS 256
+// target hull of every (job, view): fixed over the iterations, built once per call
+struct TargetHull {
+    P2 h[8];
+    int n;
+    float area;
+};
+
+__global__ void __launch_bounds__(64) k_fuse_targets(const float* __restrict__ vtc,
+                                                     const FuseState* __restrict__ states,
+                                                     int max_views, TargetHull* __restrict__ th) {
+    const int job = blockIdx.x, v = threadIdx.x;
+    const FuseState& S = states[job];
+    if (v >= max_views) return;
+    TargetHull& T = th[(size_t)job * max_views + v];
+    if (S.stop || v >= S.nv) { T.n = 0; T.area = 0.f; return; }
+    P2 ct[8], ht[8];
+    const float* tc = vtc + ((size_t)S.off + v) * 16;
+    for (int j = 0; j < 8; ++j) { ct[j].x = tc[2 * j]; ct[j].y = tc[2 * j + 1]; }
+    const int nt = convex_hull<8>(ct, 8, ht);
+    for (int j = 0; j < 8; ++j) T.h[j] = ht[j];
+    T.n = nt;
+    T.area = polygon_area(ht, nt);
+}
+
+#define TERM_THREADS 64   // one wave per workgroup: its hull stacks take 40 KB of LDS
 __global__ void __launch_bounds__(TERM_THREADS) k_fuse_terms(const float* __restrict__ vpose,
-                                                             const float* __restrict__ vtc,
+                                                             const TargetHull* __restrict__ th,
                                                              const float* __restrict__ pst,
                                                              bf_fuse_cfg cfg,
                                                              FuseState* __restrict__ states,
@@ -332,22 +507,26 @@ __global__ void __launch_bounds__(TERM_THREADS) k_fuse_terms(const float* __rest
     const int job = blockIdx.y;
     const FuseState& S = states[job];
     if (S.stop) return;                                   // uniform per workgroup
-    const int P = cfg.pst_size;                           // multiple of TERM_THREADS' divisor 64
+    const int P = cfg.pst_size;                           // multiple of 64
     const int pair = blockIdx.x * TERM_THREADS + threadIdx.x;
     const int v = pair / P, p = pair % P;                 // P % 64 == 0: v is uniform per wave
     if (v >= S.nv) return;
-    __shared__ float s_view[TERM_THREADS / 64][32];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __shared__ float s_pose[16];
+    __shared__ TargetHull s_th;
+    __shared__ HullLds s_hull;
+    const int lane = threadIdx.x;
     const size_t vi = (size_t)S.off + v;
-    if (lane < 16) s_view[w][lane] = vpose[vi * 16 + lane];
-    else if (lane < 32) s_view[w][lane] = vtc[vi * 16 + (lane - 16)];
-    __builtin_amdgcn_wave_barrier();
+    if (lane < 16) s_pose[lane] = vpose[vi * 16 + lane];
+    else if (lane < 16 + 18) reinterpret_cast<float*>(&s_th)[lane - 16] =
+        reinterpret_cast<const float*>(th + (size_t)job * max_views + v)[lane - 16];
+    __syncthreads();
     float b[6], r[9], ss[6], corners[24];
     for (int k = 0; k < 6; ++k) { b[k] = S.box32[k]; ss[k] = S.ss[k]; }
     for (int k = 0; k < 9; ++k) r[k] = S.R[k];
     particle_corners(b, r, pst + 6 * p, ss, corners);
-    const float* Pm = s_view[w];
-    P2 c0[8], ct[8];
+    const float* Pm = s_pose;
+    P2 c0[8];
+#pragma unroll
     for (int j = 0; j < 8; ++j) {
         float vx = corners[3 * j] - Pm[3], vy = corners[3 * j + 1] - Pm[7], vz = corners[3 * j + 2] - Pm[11];
         float cx = Pm[0] * vx + Pm[4] * vy + Pm[8] * vz;
@@ -357,15 +536,9 @@ __global__ void __launch_bounds__(TERM_THREADS) k_fuse_terms(const float* __rest
         float py = ((cy * cfg.K[5]) / cz + cfg.K[6]);
         c0[j].x = (px > cfg.img_w) ? cfg.img_w : (px < 0) ? 0 : px;
         c0[j].y = (py > cfg.img_h) ? cfg.img_h : (py < 0) ? 0 : py;
-        ct[j].x = Pm[16 + 2 * j];
-        ct[j].y = Pm[16 + 2 * j + 1];
     }
-    // the view's target hull is the same for every particle (computed per lane: identical
-    // inputs, identical result, no cross-lane traffic)
-    P2 ht[8];
-    const int nt = convex_hull<8>(ct, 8, ht);
     int flags = 0;
-    const float iou = iou_hull_pre(c0, ht, nt, polygon_area(ht, nt), &flags);
+    const float iou = iou_hull_lds(c0, s_th.h, s_th.n, s_th.area, s_hull, lane, &flags);
     terms[((size_t)job * max_views + v) * P + p] = fabsf(1 - iou);
     if (flags) atomicOr(&states[job].flags, flags);
 }
@@ -384,6 +557,7 @@ __global__ void __launch_bounds__(1024) k_fuse_step(const float* __restrict__ ps
     __shared__ int s_wave[FUSE_MAX_PST / 64];
     __shared__ double s_dsum[8];
     __shared__ float s_fsum[8];
+    __shared__ float s_prod[FUSE_MAX_PST * 8];   // accepted particle k: 6 weighted offsets, w, fit*w
     const int nv = G->nv;
     // ---- fitness: the reference's per-particle loop `val += |1 - iou|; cnt += 1` -------------
     if (t < P) {
@@ -414,16 +588,26 @@ __global__ void __launch_bounds__(1024) k_fuse_step(const float* __restrict__ ps
     const int n_acc = total < cfg.max_accept ? total : cfg.max_accept;
     __syncthreads();
     // ---- cal_transform sums in reference order (8 independent sequential sums) -------------
+    // the f32 products of every accepted particle are formed in parallel into LDS first, so
+    // the 8 sequential sums below only chain adds (not a dependent global load per step)
+    if (t < n_acc) {
+        const int j = s_acc[t];
+        const float fj = s_fit[j];
+        const float w = f0 - fj;
+        const float* pj = pst + 6 * j;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) s_prod[8 * t + c] = pj[c] * w;
+        s_prod[8 * t + 6] = w;
+        s_prod[8 * t + 7] = fj * w;
+    }
+    __syncthreads();
     if (t < 8) {
         double ds = 0.0;
         float fs = 0.0f;
-        for (int k = 0; k < n_acc; ++k) {
-            int j = s_acc[k];
-            float w = f0 - s_fit[j];
-            float prod = (t < 6) ? pst[6 * j + t] * w : (t == 6 ? w : s_fit[j] * w);
-            if (cfg.legacy_promotion) ds += (double)prod;
-            else fs = fs + prod;
-        }
+        if (cfg.legacy_promotion)
+            for (int k = 0; k < n_acc; ++k) ds += (double)s_prod[8 * k + t];
+        else
+            for (int k = 0; k < n_acc; ++k) fs = fs + s_prod[8 * k + t];
         s_dsum[t] = ds;
         s_fsum[t] = fs;
     }
@@ -505,10 +689,17 @@ __global__ void __launch_bounds__(64) k_fuse_final(const FuseState* __restrict__
     if (S.flags) atomicOr(status, S.flags);
 }
 
+static size_t fuse_states_bytes(int n_jobs) {
+    return ((size_t)n_jobs * sizeof(FuseState) + 255) & ~(size_t)255;
+}
+static size_t fuse_targets_bytes(int n_jobs, int max_views) {
+    return ((size_t)n_jobs * max_views * sizeof(TargetHull) + 255) & ~(size_t)255;
+}
+
 BF_API size_t bf_fusion_fit_workspace_size(int n_jobs, int max_views, int pst_size) {
     if (n_jobs <= 0 || max_views <= 0 || pst_size <= 0) return 0;
-    const size_t st = ((size_t)n_jobs * sizeof(FuseState) + 255) & ~(size_t)255;
-    return st + (size_t)n_jobs * max_views * pst_size * sizeof(float);
+    return fuse_states_bytes(n_jobs) + fuse_targets_bytes(n_jobs, max_views) +
+           (size_t)n_jobs * max_views * pst_size * sizeof(float);
 }
 
 BF_API int bf_fusion_fit(const int32_t* view_off, const int32_t* n_views, int n_jobs,
@@ -527,14 +718,16 @@ BF_API int bf_fusion_fit(const int32_t* view_off, const int32_t* n_views, int n_
         return BF_ERR_CAPACITY;
     hipStream_t s = bf_stream(stream);
     FuseState* states = reinterpret_cast<FuseState*>(workspace);
-    const size_t st = ((size_t)n_jobs * sizeof(FuseState) + 255) & ~(size_t)255;
-    float* terms = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + st);
+    char* ws = reinterpret_cast<char*>(workspace) + fuse_states_bytes(n_jobs);
+    TargetHull* th = reinterpret_cast<TargetHull*>(ws);
+    float* terms = reinterpret_cast<float*>(ws + fuse_targets_bytes(n_jobs, max_views));
     const int P = cfg->pst_size;
     hipLaunchKernelGGL(k_fuse_init, dim3(n_jobs), dim3(64), 0, s, view_off, n_views, max_views,
                        view_box, view_R, view_score, *cfg, states);
+    hipLaunchKernelGGL(k_fuse_targets, dim3(n_jobs), dim3(64), 0, s, view_tc, states, max_views, th);
     const dim3 tgrid((unsigned)bf_cdiv(max_views * P, TERM_THREADS), (unsigned)n_jobs);
     for (int it = 0; it < cfg->iters; ++it) {
-        hipLaunchKernelGGL(k_fuse_terms, tgrid, dim3(TERM_THREADS), 0, s, view_pose, view_tc, pst,
+        hipLaunchKernelGGL(k_fuse_terms, tgrid, dim3(TERM_THREADS), 0, s, view_pose, th, pst,
                            *cfg, states, terms, max_views);
         hipLaunchKernelGGL(k_fuse_step, dim3(n_jobs), dim3(P), 0, s, pst, *cfg, states, terms,
                            max_views, it, trace);

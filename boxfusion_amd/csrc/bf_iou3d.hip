@@ -155,14 +155,20 @@ __global__ void __launch_bounds__(IOU_THREADS) k_obb_pairs(const BoxPrep* __rest
     const double ahi0 = A.mx[0] + m, ahi1 = A.mx[1] + m, ahi2 = A.mx[2] + m;
     const double blo0 = B.mn[0] - m, blo1 = B.mn[1] - m, blo2 = B.mn[2] - m;
     const double bhi0 = B.mx[0] + m, bhi1 = B.mx[1] + m, bhi2 = B.mx[2] + m;
+    // both plane sets in registers (96 f64): read from LDS once, not 96 broadcast reads per point
+    double pa[12][4], pb[12][4];
+#pragma unroll
+    for (int k = 0; k < 12; ++k)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) { pa[k][c] = pl[0][k][c]; pb[k][c] = pl[1][k][c]; }
     long long n1 = 0, n2 = 0, n12 = 0;
     for (int p = t; p < 15625; p += IOU_THREADS) {
         int ix = p / 625, iy = (p / 25) % 25, iz = p % 25;
         double x = g[0][ix], y = g[1][iy], z = g[2][iz];
         const bool ina = x >= alo0 && x <= ahi0 && y >= alo1 && y <= ahi1 && z >= alo2 && z <= ahi2;
         const bool inb = x >= blo0 && x <= bhi0 && y >= blo1 && y <= bhi1 && z >= blo2 && z <= bhi2;
-        bool a = ina && inside12(x, y, z, pl[0]);
-        bool b = inb && inside12(x, y, z, pl[1]);
+        bool a = ina && inside12(x, y, z, pa);
+        bool b = inb && inside12(x, y, z, pb);
         n1 += a;
         n2 += b;
         n12 += (a && b);
