@@ -191,12 +191,150 @@ __global__ void __launch_bounds__(IOU_THREADS) k_obb_pairs(const BoxPrep* __rest
     }
 }
 
-__global__ void k_iou_diag(double* iou, int n) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) iou[(size_t)i * n + i] = 1.0;
+// ------------------------------------------------------------------------------------------
+// Split form (default): the gate and the grid count are separate launches, so the grid count
+// only runs for the pairs that pass the gate and spreads each over OBB_SPLIT workgroups.  One
+// workgroup per pair (k_obb_pairs above) leaves most of the chip idle behind a few long
+// workgroups and, on the fusion stream's CU partition, queues thousands of short ones.
+//   k_obb_gate   one wave per pair: 40-lane gate ballot; IoU 0 written for gated-out pairs,
+//                the others appended to a device list (order-free: each pair owns its entries)
+//   k_obb_grid   persistent: item = (gated pair, split), 15625 / OBB_SPLIT grid points each,
+//                integer counts added atomically (exact, order-free)
+//   k_obb_final  IoU = n12 / ((n1 + n2 - n12) + 1e-6) as the single-workgroup form
+// ------------------------------------------------------------------------------------------
+#ifndef OBB_SPLIT
+#define OBB_SPLIT 8         // (a diagnostic build sets 0: one workgroup per pair, k_obb_pairs)
+#endif
+#define OBB_GRID_WGS 512
+
+struct ObbWork {
+    int n_gated;
+    int pad[3];
+};
+
+__global__ void __launch_bounds__(256) k_obb_gate(const BoxPrep* __restrict__ prep, int n,
+                                                  long long pairs, double* __restrict__ iou,
+                                                  ObbWork* __restrict__ w, int* __restrict__ gated,
+                                                  int* __restrict__ cnt) {
+    const long long p = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (p >= pairs) return;                                  // wave-uniform
+    const int t = threadIdx.x & 63;
+    int i, j;
+    pair_of(p, n, &i, &j);
+    const BoxPrep& A = prep[i];
+    const BoxPrep& B = prep[j];
+    bool in = false;
+    if (t < 20) in = inside12(A.pt[t][0], A.pt[t][1], A.pt[t][2], B.pl);
+    else if (t < 40) in = inside12(B.pt[t - 20][0], B.pt[t - 20][1], B.pt[t - 20][2], A.pl);
+    const unsigned long long m = __ballot(in);
+    if (t == 0) {
+        if (m == 0ull) {
+            iou[(size_t)i * n + j] = 0.0;
+            iou[(size_t)j * n + i] = 0.0;
+        } else {
+            const int slot = atomicAdd(&w->n_gated, 1);
+            gated[slot] = (int)p;
+            cnt[3 * slot + 0] = 0;
+            cnt[3 * slot + 1] = 0;
+            cnt[3 * slot + 2] = 0;
+        }
+    }
 }
 
-BF_API size_t bf_obb_iou_workspace_size(int n) { return (size_t)(n > 0 ? n : 0) * sizeof(BoxPrep); }
+__global__ void __launch_bounds__(IOU_THREADS) k_obb_grid(const BoxPrep* __restrict__ prep, int n,
+                                                          const ObbWork* __restrict__ w,
+                                                          const int* __restrict__ gated,
+                                                          int* __restrict__ cnt) {
+    __shared__ double pl[2][12][4];
+    __shared__ double g[3][25];
+    __shared__ int s_red[3][IOU_THREADS / 64];
+    const int t = threadIdx.x;
+    constexpr int SPLIT = OBB_SPLIT > 0 ? OBB_SPLIT : 1;
+    const int items = w->n_gated * SPLIT;
+    constexpr int PER = (15625 + SPLIT - 1) / SPLIT;
+    for (int it = blockIdx.x; it < items; it += gridDim.x) {
+        const int slot = it / SPLIT, part = it % SPLIT;
+        int i, j;
+        pair_of((long long)gated[slot], n, &i, &j);
+        const BoxPrep& A = prep[i];
+        const BoxPrep& B = prep[j];
+        __syncthreads();                                     // previous item's LDS reads done
+        if (t < 48) pl[0][t >> 2][t & 3] = A.pl[t >> 2][t & 3];
+        else if (t < 96) pl[1][(t - 48) >> 2][(t - 48) & 3] = B.pl[(t - 48) >> 2][(t - 48) & 3];
+        else if (t < 96 + 75) {
+            // numpy.linspace(f64(min), f64(max), 25) per axis over the union AABB
+            const int ax = (t - 96) / 25, k = (t - 96) % 25;
+            float lo = fminf(A.mn[ax], B.mn[ax]);
+            float hi = fmaxf(A.mx[ax], B.mx[ax]);
+            double start = lo, stop = hi;
+            double step = (stop - start) / 24.0;
+            g[ax][k] = (k == 24) ? stop : (double)k * step + start;
+        }
+        __syncthreads();
+        // points outside a box's AABB by > 1e-3 skip its plane tests (see k_obb_pairs)
+        const double m = 1e-3;
+        const double alo0 = A.mn[0] - m, alo1 = A.mn[1] - m, alo2 = A.mn[2] - m;
+        const double ahi0 = A.mx[0] + m, ahi1 = A.mx[1] + m, ahi2 = A.mx[2] + m;
+        const double blo0 = B.mn[0] - m, blo1 = B.mn[1] - m, blo2 = B.mn[2] - m;
+        const double bhi0 = B.mx[0] + m, bhi1 = B.mx[1] + m, bhi2 = B.mx[2] + m;
+        int n1 = 0, n2 = 0, n12 = 0;
+        const int p0 = part * PER, p1 = min(p0 + PER, 15625);
+        for (int p = p0 + t; p < p1; p += IOU_THREADS) {
+            int ix = p / 625, iy = (p / 25) % 25, iz = p % 25;
+            double x = g[0][ix], y = g[1][iy], z = g[2][iz];
+            const bool ina = x >= alo0 && x <= ahi0 && y >= alo1 && y <= ahi1 && z >= alo2 && z <= ahi2;
+            const bool inb = x >= blo0 && x <= bhi0 && y >= blo1 && y <= bhi1 && z >= blo2 && z <= bhi2;
+            bool a = ina && inside12(x, y, z, pl[0]);
+            bool b = inb && inside12(x, y, z, pl[1]);
+            n1 += a;
+            n2 += b;
+            n12 += (a && b);
+        }
+        n1 = bf_wave_sum_i32(n1);
+        n2 = bf_wave_sum_i32(n2);
+        n12 = bf_wave_sum_i32(n12);
+        if (bf_lane() == 0) {
+            s_red[0][t >> 6] = n1;
+            s_red[1][t >> 6] = n2;
+            s_red[2][t >> 6] = n12;
+        }
+        __syncthreads();
+        if (t < 3) {
+            int s = 0;
+            for (int q = 0; q < IOU_THREADS / 64; ++q) s += s_red[t][q];
+            atomicAdd(&cnt[3 * slot + t], s);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_obb_final(int n, const ObbWork* __restrict__ w,
+                                                   const int* __restrict__ gated,
+                                                   const int* __restrict__ cnt,
+                                                   double* __restrict__ iou) {
+    const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= w->n_gated) return;
+    int i, j;
+    pair_of((long long)gated[slot], n, &i, &j);
+    const long long a = cnt[3 * slot], b = cnt[3 * slot + 1], c = cnt[3 * slot + 2];
+    const double v = (double)c / ((double)(a + b - c) + 1e-6);
+    iou[(size_t)i * n + j] = v;
+    iou[(size_t)j * n + i] = v;
+}
+
+__global__ void k_iou_diag(double* iou, int n, ObbWork* w) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) iou[(size_t)i * n + i] = 1.0;
+    if (i == 0 && w) w->n_gated = 0;
+}
+
+static size_t obb_prep_bytes(int n) { return ((size_t)n * sizeof(BoxPrep) + 255) & ~(size_t)255; }
+
+BF_API size_t bf_obb_iou_workspace_size(int n) {
+    if (n <= 0) return 0;
+    const size_t pairs = (size_t)n * (n - 1) / 2;
+    // prep | work header | gated pair list | 3 counts per gated pair
+    return obb_prep_bytes(n) + 256 + sizeof(int) * pairs + sizeof(int) * 3 * pairs;
+}
 
 BF_API int bf_obb_iou_matrix(const float* corners, int n, double* iou, void* workspace,
                              void* stream) {
@@ -204,12 +342,26 @@ BF_API int bf_obb_iou_matrix(const float* corners, int n, double* iou, void* wor
     if (n == 0) return BF_OK;
     hipStream_t s = bf_stream(stream);
     BoxPrep* prep = reinterpret_cast<BoxPrep*>(workspace);
-    hipLaunchKernelGGL(k_obb_prep, dim3(bf_cdiv(n, 64)), dim3(64), 0, s, corners, n, prep);
-    hipLaunchKernelGGL(k_iou_diag, dim3(bf_cdiv(n, 256)), dim3(256), 0, s, iou, n);
+    char* ws = reinterpret_cast<char*>(workspace) + obb_prep_bytes(n);
+    ObbWork* w = reinterpret_cast<ObbWork*>(ws);
     long long pairs = (long long)n * (n - 1) / 2;
+    int* gated = reinterpret_cast<int*>(ws + 256);
+    int* cnt = gated + pairs;
+    if (pairs > 0x7fffffffLL / 4) return BF_ERR_CAPACITY;
+    hipLaunchKernelGGL(k_obb_prep, dim3(bf_cdiv(n, 64)), dim3(64), 0, s, corners, n, prep);
+    hipLaunchKernelGGL(k_iou_diag, dim3(bf_cdiv(n, 256)), dim3(256), 0, s, iou, n, w);
     if (pairs > 0) {
-        if (pairs > 0x7fffffffLL) return BF_ERR_CAPACITY;
-        hipLaunchKernelGGL(k_obb_pairs, dim3((unsigned)pairs), dim3(IOU_THREADS), 0, s, prep, n, iou);
+        if (OBB_SPLIT == 0) {
+            hipLaunchKernelGGL(k_obb_pairs, dim3((unsigned)pairs), dim3(IOU_THREADS), 0, s, prep, n, iou);
+        } else {
+            hipLaunchKernelGGL(k_obb_gate, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0, s, prep, n,
+                               pairs, iou, w, gated, cnt);
+            const unsigned gw = (unsigned)(pairs * (OBB_SPLIT > 0 ? OBB_SPLIT : 1) < OBB_GRID_WGS
+                                               ? pairs * (OBB_SPLIT > 0 ? OBB_SPLIT : 1) : OBB_GRID_WGS);
+            hipLaunchKernelGGL(k_obb_grid, dim3(gw), dim3(IOU_THREADS), 0, s, prep, n, w, gated, cnt);
+            hipLaunchKernelGGL(k_obb_final, dim3(bf_cdiv((unsigned)pairs, 256)), dim3(256), 0, s, n, w,
+                               gated, cnt, iou);
+        }
     }
     return bf_check_launch();
 }

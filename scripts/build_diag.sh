@@ -11,6 +11,7 @@ mkdir -p diag
 FL="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -I../../include -Wno-unused-result"
 /opt/rocm/bin/hipcc $FL -DFAST_CAND=4 -c ../csrc/bf_fusion.hip -o diag/bf_fusion.o
 /opt/rocm/bin/hipcc $FL -DNMS_FAST_N=0 -c ../csrc/bf_assoc.hip -o diag/bf_assoc.o
+/opt/rocm/bin/hipcc $FL -DOBB_SPLIT=0 -c ../csrc/bf_iou3d.hip -o diag/bf_iou3d.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o diag/libboxfusion_hip_diag.so \
-    $(ls *.o | grep -v -e '^bf_fusion.o$' -e '^bf_assoc.o$') diag/bf_fusion.o diag/bf_assoc.o
+    $(ls *.o | grep -v -e "^bf_fusion.o$" -e "^bf_assoc.o$" -e "^bf_iou3d.o$") diag/bf_fusion.o diag/bf_assoc.o diag/bf_iou3d.o
 echo "$PWD/diag/libboxfusion_hip_diag.so"
