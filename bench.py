@@ -75,9 +75,9 @@ def parse():
     p.add_argument("--inflight", type=int, default=-1,
                    help="detect steps in flight per GPU: independent batches replayed on this many "
                         "streams (each its own DetectStage buffers / graph), so one batch's CLIP "
-                        "phases overlap the next batch's CuTR phases.  -1: 2 when this process fuses "
-                        "only its own frames (N = 1), else 1 (at N > 1 every rank waits for rank 0's "
-                        "fusion of 8N keyframes per step, which needs the CUs a second stream takes)")
+                        "phases overlap the next batch's CuTR phases (default 2; with 32 CUs "
+                        "reserved for rank 0's fusion at N > 1 the two detect streams run on the "
+                        "other 224)")
     p.add_argument("--cpu-fusion-frames", type=int, default=24)
     return p.parse_args()
 
@@ -270,7 +270,7 @@ def main():
         cutr = make_cubify_transformer(args.dim, True).eval()
         clip_vis = VisionTransformer(224, 14, 1280, args.clip_layers, 16, 1024).eval()
     B = args.batch
-    n_inflight = args.inflight if args.inflight > 0 else (2 if world == 1 and args.sim_ranks <= 1 else 1)
+    n_inflight = args.inflight if args.inflight > 0 else 2
     detects = [DetectStage(cutr, clip_vis, CFG, B, 480, 640, SCANNET_K, crops_per_frame=args.crops,
                            crop_source="top", backproject=True, clip_capacity=B * args.crops,
                            device=dev, graph=not args.eager) for _ in range(n_inflight)]
