@@ -23,6 +23,7 @@ c_int, c_float, c_double, c_void_p, c_size_t = (ctypes.c_int, ctypes.c_float, ct
 BF_DEV_FUSION_LIST_OVERFLOW = 1
 BF_DEV_HULL_OVERFLOW = 2
 BF_DEV_VIEW_OVERFLOW = 4
+BF_DEV_INDEX_RANGE = 8
 
 
 class NmsCfg(ctypes.Structure):
@@ -44,6 +45,14 @@ class FuseCfg(ctypes.Structure):
                 ("center_coef", c_double), ("shape_coef", c_double),
                 ("beta", c_double), ("min_scale", c_double),
                 ("img_h", c_float), ("img_w", c_float), ("K", c_float * 16)]
+
+
+class RowsField(ctypes.Structure):
+    _fields_ = [("a", c_void_p), ("b", c_void_p), ("dst", c_void_p), ("n_a", ctypes.c_int64),
+                ("n_b", ctypes.c_int64), ("row_bytes", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
+ROWS_MAX_FIELDS = 16
 
 
 class HipError(RuntimeError):
@@ -150,6 +159,37 @@ def obb_iou_matrix(corners):
     _check(lib().bf_obb_iou_matrix(_ptr(corners), c_int(n), _ptr(iou), _ptr(ws), _stream()),
            "bf_obb_iou_matrix")
     return iou
+
+
+# ------------------------------------------------------------------------------------------
+# box-set rows (Instances3D.cat / __getitem__ over every field in one launch)
+# ------------------------------------------------------------------------------------------
+_ROWS_DT = np.dtype([("a", np.uint64), ("b", np.uint64), ("dst", np.uint64), ("n_a", np.int64),
+                     ("n_b", np.int64), ("row_bytes", np.int32), ("pad", np.int32)])
+
+
+def rows_gather(pairs, idx=None, n_out=None):
+    """pairs: [(a, b or None)] contiguous device tensors with the same row shape / dtype per pair;
+    returns new tensors with rows idx of cat(a, b) (idx: int64 device tensor; None: the whole
+    concatenation).  One bf_rows_gather launch for up to ROWS_MAX_FIELDS fields."""
+    if idx is not None:
+        n_out = int(idx.shape[0])
+    elif n_out is None:
+        a, b = pairs[0]
+        n_out = a.shape[0] + (0 if b is None else b.shape[0])
+    outs, recs = [], []
+    for a, b in pairs:
+        out = torch.empty((n_out,) + a.shape[1:], dtype=a.dtype, device=a.device)
+        nb = 0 if b is None else b.shape[0]
+        # contiguous tensors: stride(0) = elements per row (also for 0-row tensors)
+        recs.append((a.data_ptr(), b.data_ptr() if nb else 0, out.data_ptr(), a.shape[0], nb,
+                     a.stride(0) * a.element_size() if a.dim() > 1 else a.element_size(), 0))
+        outs.append(out)
+    if pairs and n_out:
+        arr = np.array(recs, dtype=_ROWS_DT)
+        _check(lib().bf_rows_gather(c_void_p(arr.ctypes.data), c_int(len(pairs)), _ptr(idx),
+                                    c_int(n_out), None, _stream()), "bf_rows_gather")
+    return outs
 
 
 # ------------------------------------------------------------------------------------------

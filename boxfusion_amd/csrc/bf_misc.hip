@@ -8,3 +8,53 @@ BF_API int bf_device_count(void) {
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
 }
+
+// ------------------------------------------------------------------------------------------
+// bf_rows_gather: every field of a box set gathered / concatenated in one launch.
+// blockIdx.y = field; threads stride over (row, 4-byte word) of that field's output.
+// ------------------------------------------------------------------------------------------
+struct RowsArgs {
+    bf_rows_field f[BF_ROWS_MAX_FIELDS];
+};
+
+__global__ void __launch_bounds__(256) k_rows_gather(RowsArgs args, const int64_t* __restrict__ idx,
+                                                     int n_out, int32_t* __restrict__ status) {
+    const bf_rows_field& F = args.f[blockIdx.y];
+    const int wpr = F.row_bytes >> 2;                     // 4-byte words per row
+    const long long total = (long long)n_out * wpr;
+    const long long na = F.n_a, nab = F.n_a + F.n_b;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (long long)gridDim.x * blockDim.x) {
+        const long long r = e / wpr, w = e - r * wpr;
+        const long long s = idx ? idx[r] : r;
+        if (s < 0 || s >= nab) {
+            if (status && w == 0) atomicOr(status, BF_DEV_INDEX_RANGE);
+            continue;
+        }
+        const uint32_t* src = s < na ? static_cast<const uint32_t*>(F.a) + s * wpr
+                                     : static_cast<const uint32_t*>(F.b) + (s - na) * wpr;
+        static_cast<uint32_t*>(F.dst)[e] = src[w];
+    }
+}
+
+BF_API int bf_rows_gather(const bf_rows_field* fields, int n_fields, const int64_t* idx, int n_out,
+                          int32_t* status, void* stream) {
+    if (!fields || n_fields < 0 || n_fields > BF_ROWS_MAX_FIELDS || n_out < 0) return BF_ERR_ARG;
+    if (n_fields == 0 || n_out == 0) return BF_OK;
+    RowsArgs args;
+    long long most = 0;
+    for (int k = 0; k < n_fields; ++k) {
+        const bf_rows_field& F = fields[k];
+        if (F.row_bytes <= 0 || (F.row_bytes & 3) || !F.dst || F.n_a < 0 || F.n_b < 0 ||
+            (F.n_a > 0 && !F.a) || (F.n_b > 0 && !F.b))
+            return BF_ERR_ARG;
+        if (!idx && (long long)n_out != F.n_a + F.n_b) return BF_ERR_ARG;
+        args.f[k] = F;
+        const long long words = (long long)n_out * (F.row_bytes >> 2);
+        most = words > most ? words : most;
+    }
+    const unsigned bx = (unsigned)((most + 255) / 256 < 1024 ? (most + 255) / 256 : 1024);
+    hipLaunchKernelGGL(k_rows_gather, dim3(bx, (unsigned)n_fields), dim3(256), 0, bf_stream(stream),
+                       args, idx, n_out, status);
+    return bf_check_launch();
+}

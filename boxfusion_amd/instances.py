@@ -95,7 +95,53 @@ class Instances3D:
             ret.set(k, v.to(*args, **kwargs) if hasattr(v, "to") else v)
         return ret
 
+    def _device_rows(self, others, idx=None):
+        """cat([self] + others) (one other) or self[idx] (idx: int64 device tensor) for instance
+        sets whose fields are all device tensors / boxes: one bf_rows_gather launch.  None when a
+        field needs the generic path."""
+        pairs, plan = [], []
+        for k, v in self._fields.items():
+            w = others[0]._fields.get(k) if others else None
+            if isinstance(v, torch.Tensor):
+                if (v.element_size() * int(np.prod(v.shape[1:], dtype=np.int64))) % 4:
+                    return None
+                if not v.is_cuda or (others and not (isinstance(w, torch.Tensor) and w.dtype == v.dtype
+                                                     and w.shape[1:] == v.shape[1:] and w.is_cuda)):
+                    return None
+                plan.append((k, None))
+                pairs.append((v.contiguous(), w.contiguous() if others else None))
+            elif hasattr(v, "tensor") and hasattr(v, "R") and isinstance(v.tensor, torch.Tensor):
+                if not v.tensor.is_cuda or (others and not hasattr(w, "R")):
+                    return None
+                plan.append((k, type(v)))
+                pairs.append((v.tensor.contiguous(), w.tensor.contiguous() if others else None))
+                pairs.append((v.R.contiguous(), w.R.contiguous() if others else None))
+            else:
+                return None
+        if not pairs or len(pairs) > _lib.ROWS_MAX_FIELDS:
+            return None
+        if others and set(others[0]._fields) != set(self._fields):
+            return None
+        outs = _lib.rows_gather(pairs, idx)
+        ret = Instances3D(self._image_size)
+        o = 0
+        for k, box_type in plan:
+            if box_type is None:
+                ret.set(k, outs[o])
+                o += 1
+            else:
+                ret.set(k, box_type._views(outs[o], outs[o + 1]))
+                o += 2
+        return ret
+
     def __getitem__(self, item):
+        if isinstance(item, np.ndarray) and item.dtype.kind in "iu" and item.ndim == 1 and self._fields:
+            dev = next((v.device if isinstance(v, torch.Tensor) else getattr(getattr(v, "tensor", None), "device", None)
+                        for v in self._fields.values()), None)
+            if dev is not None and dev.type == "cuda":
+                r = self._device_rows([], _lib.h2d(item.astype(np.int64), dev))
+                if r is not None:
+                    return r
         if type(item) == int:
             if item >= len(self) or item < -len(self):
                 raise IndexError("Instances3D index out of range!")
@@ -163,6 +209,10 @@ class Instances3D:
         assert len(instance_lists) > 0
         if len(instance_lists) == 1:
             return instance_lists[0]
+        if len(instance_lists) == 2:
+            r = instance_lists[0]._device_rows([instance_lists[1]])
+            if r is not None:
+                return r
         ret = Instances3D(instance_lists[0]._image_size)
         for k in instance_lists[0]._fields.keys():
             vals = [i.get(k) for i in instance_lists]

@@ -37,6 +37,7 @@ typedef enum {
 #define BF_DEV_FUSION_LIST_OVERFLOW 1   /* a fusion_list row exceeded its capacity */
 #define BF_DEV_HULL_OVERFLOW 2          /* a 2-D hull / clip buffer exceeded its capacity */
 #define BF_DEV_VIEW_OVERFLOW 4          /* a fusion job has 0 or more than 32 views (skipped) */
+#define BF_DEV_INDEX_RANGE 8            /* a gather index outside its source rows (row skipped) */
 
 #define BF_MAX_BOXES 4096               /* NMS / association scan limit per call */
 
@@ -46,6 +47,28 @@ typedef enum {
 const char* bf_version(void);
 /* returns the number of HIP devices visible (>= 0) or a negative bf_status */
 int bf_device_count(void);
+
+/* ------------------------------------------------------------------------------------------
+ * Row gather over the fields of a box set (Instances3D.cat / Instances3D.__getitem__,
+ * instances.py:155-218 of the reference, one torch.cat / index per field there): every field is
+ * a row-major table whose rows are `row_bytes` bytes (a multiple of 4); rows come from the
+ * virtual concatenation [a (n_a rows); b (n_b rows)], dst row r = row idx[r] of it (idx == NULL:
+ * r itself, i.e. the concatenation).  One launch for all fields.  idx values must lie in
+ * [0, n_a + n_b) (checked on the device: out-of-range rows are left unwritten and set
+ * BF_DEV_INDEX_RANGE in *status when status != NULL).
+ * ------------------------------------------------------------------------------------------ */
+#define BF_ROWS_MAX_FIELDS 16
+typedef struct {
+    const void* a;
+    const void* b;           /* may be NULL when n_b == 0 */
+    void* dst;
+    int64_t n_a, n_b;
+    int32_t row_bytes;
+    int32_t pad;
+} bf_rows_field;
+
+int bf_rows_gather(const bf_rows_field* fields, int n_fields, const int64_t* idx, int n_out,
+                   int32_t* status, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * 3-D box geometry  (boxfusion/boxes.py, boxfusion/instances.py)

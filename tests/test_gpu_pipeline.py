@@ -233,3 +233,47 @@ def test_fusion_stage_joint_association(dev):
             np.testing.assert_array_equal(a, b, err_msg=f"keyframe {f}")
     assert jnt.box_manager.already_fusion == sep.box_manager.already_fusion
     assert jnt.stats == sep.stats and jnt.stats["suppressed"] > 50
+
+
+@pytest.mark.gpu
+def test_instances_rows_gather(dev):
+    """Instances3D.cat / integer-array indexing through bf_rows_gather (one launch over every
+    field) == torch.cat / torch indexing per field, including empty sets and 1-row sets."""
+    from boxfusion_amd import _lib
+    from boxfusion_amd.boxes import GeneralInstance3DBoxes
+    from boxfusion_amd.instances import Instances3D
+    g = torch.Generator().manual_seed(5)
+
+    def make(n):
+        p = Instances3D((480, 640))
+        p.scores = torch.rand(n, generator=g).to(dev)
+        p.pred_boxes_3d = GeneralInstance3DBoxes(torch.rand(n, 6, generator=g).to(dev),
+                                                 torch.rand(n, 3, 3, generator=g).to(dev))
+        p.cam_pose = torch.rand(n, 4, 4, generator=g).to(dev)
+        p.init_id = torch.randint(0, 1000, (n,), generator=g).to(dev)
+        return p
+    for na, nb in [(7, 5), (0, 4), (3, 0), (1, 1), (40, 17)]:
+        a, b = make(na), make(nb)
+        c = Instances3D.cat([a, b])
+        for k in ("scores", "cam_pose", "init_id"):
+            torch.testing.assert_close(c.get(k), torch.cat([a.get(k), b.get(k)]), rtol=0, atol=0)
+        torch.testing.assert_close(c.pred_boxes_3d.tensor,
+                                   torch.cat([a.pred_boxes_3d.tensor, b.pred_boxes_3d.tensor]), rtol=0, atol=0)
+        torch.testing.assert_close(c.pred_boxes_3d.R,
+                                   torch.cat([a.pred_boxes_3d.R, b.pred_boxes_3d.R]), rtol=0, atol=0)
+        if na + nb:
+            idx = np.random.default_rng(na).integers(0, na + nb, na + nb + 3)
+            s = c[idx]
+            it = torch.from_numpy(idx).to(dev)
+            for k in ("scores", "cam_pose", "init_id"):
+                torch.testing.assert_close(s.get(k), c.get(k)[it], rtol=0, atol=0)
+            torch.testing.assert_close(s.pred_boxes_3d.R, c.pred_boxes_3d.R[it], rtol=0, atol=0)
+    # an out-of-range row is reported, not written
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    x = torch.arange(4, dtype=torch.float32, device=dev)
+    out = torch.full((2,), -1.0, device=dev)
+    f = (_lib.RowsField * 1)()
+    f[0].a, f[0].b, f[0].dst, f[0].n_a, f[0].n_b, f[0].row_bytes = x.data_ptr(), None, out.data_ptr(), 4, 0, 4
+    idx = torch.tensor([2, 9], dtype=torch.int64, device=dev)
+    assert _lib.lib().bf_rows_gather(f, 1, _lib._ptr(idx), 2, _lib._ptr(st), _lib._stream()) == 0
+    assert out.tolist() == [2.0, -1.0] and int(st.item()) == _lib.BF_DEV_INDEX_RANGE
