@@ -530,3 +530,28 @@ def partition_streams(n_reserved, device=None, masked=False):
     fus = [i for i in range(0, n, step)][:n_reserved]
     det = [i for i in range(n) if i not in set(fus)]
     return cu_masked_stream(det, dev), cu_masked_stream(fus, dev)
+
+
+# ------------------------------------------------------------------------------------------
+# CuTR decoder: cross-attention position bias + clip + softmax
+# ------------------------------------------------------------------------------------------
+def cpb_mlp(ref, pos, axis, w1, b1, w2):
+    """ref f32 [B,nq,4], pos f32 [n] -> f32 [B,nq,n,heads] (GlobalCrossAttention.rpe's MLP)"""
+    ref = _need(ref.contiguous(), torch.float32, "ref")
+    B, nq = ref.shape[0], ref.shape[1]
+    heads, hidden = w2.shape
+    out = torch.empty((B, nq, pos.shape[0], heads), dtype=torch.float32, device=ref.device)
+    _check(lib().bf_cpb_mlp(_ptr(ref), c_int(B), c_int(nq), _ptr(pos.contiguous()), c_int(pos.shape[0]),
+                            c_int(axis), _ptr(w1.contiguous()), _ptr(b1.contiguous()),
+                            _ptr(w2.contiguous()), c_int(hidden), c_int(heads), _ptr(out), _stream()),
+           "bf_cpb_mlp")
+    return out
+
+
+def rpe_softmax(attn, rx, ry, hh, ww, q0):
+    """attn f32 [B,H,Nq,hh*ww] in place: + bias on rows q >= q0, clip, softmax"""
+    _need(attn, torch.float32, "attn")
+    B, H, Nq, N = attn.shape
+    _check(lib().bf_rpe_softmax(_ptr(attn), c_int(B), c_int(H), c_int(Nq), c_int(q0), _ptr(rx),
+                                _ptr(ry), c_int(hh), c_int(ww), _stream()), "bf_rpe_softmax")
+    return attn

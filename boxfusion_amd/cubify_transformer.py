@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import copy
 import math
+import os
 from dataclasses import dataclass
 from functools import partial
 from typing import List, Optional
@@ -127,6 +128,19 @@ class GlobalCrossAttention(nn.Module):
         self.v = nn.Linear(dim, dim)
         self.proj = nn.Linear(dim, dim)
 
+    # the HIP bias/softmax path on device tensors (BF_DECODER_TORCH=1: the torch ops below)
+    fused = os.environ.get("BF_DECODER_TORCH", "0") != "1"
+
+    def _positions(self, h, w, dev):
+        """pos_x / pos_y of rpe() ([w], [h] f32), built by the same torch ops, cached"""
+        key = (h, w, dev)
+        cache = self.__dict__.setdefault("_pos_cache", {})
+        if key not in cache:
+            s = self.feature_stride
+            cache[key] = (torch.linspace(0.5, w - 0.5, w, dtype=torch.float32, device=dev) * s,
+                          torch.linspace(0.5, h - 0.5, h, dtype=torch.float32, device=dev) * s)
+        return cache[key]
+
     @staticmethod
     def _cpb(i, h, o):
         return nn.Sequential(nn.Linear(i, h, bias=True), nn.ReLU(inplace=True), nn.Linear(h, o, bias=False))
@@ -151,9 +165,20 @@ class GlobalCrossAttention(nn.Module):
         B, Nq, C = query.shape
         q = self.q(query).reshape(B, Nq, self.num_heads, C // self.num_heads).permute(0, 2, 1, 3)
         attn = (q * self.scale) @ k.transpose(-2, -1)
-        attn[:, :, box_mask] += self.rpe(reference_2d, h, w)
-        fmin, fmax = torch.finfo(attn.dtype).min, torch.finfo(attn.dtype).max
-        attn = attn.clip(min=fmin, max=fmax).softmax(dim=-1)
+        if (attn.is_cuda and self.fused and isinstance(box_mask, slice) and box_mask.step is None
+                and box_mask.stop is None and attn.dtype == torch.float32 and attn.is_contiguous()):
+            # bf_cpb_mlp + bf_rpe_softmax: the bias tables, then bias + clip + softmax in one pass
+            from boxfusion_amd import _lib
+            pos_x, pos_y = self._positions(h, w, attn.device)
+            ref = reference_2d[:, :, 0].contiguous()
+            m1, m2 = self.cpb_mlp1, self.cpb_mlp2
+            rx = _lib.cpb_mlp(ref, pos_x, 0, m1[0].weight, m1[0].bias, m1[2].weight)
+            ry = _lib.cpb_mlp(ref, pos_y, 1, m2[0].weight, m2[0].bias, m2[2].weight)
+            _lib.rpe_softmax(attn, rx, ry, h, w, box_mask.start or 0)
+        else:
+            attn[:, :, box_mask] += self.rpe(reference_2d, h, w)
+            fmin, fmax = torch.finfo(attn.dtype).min, torch.finfo(attn.dtype).max
+            attn = attn.clip(min=fmin, max=fmax).softmax(dim=-1)
         x = (attn @ v).transpose(1, 2).reshape(B, Nq, C)
         return self.proj(x)
 

@@ -283,6 +283,20 @@ int bf_attention_bf16(const void* q, const void* k, const void* v, void* o, int 
  * queries fit one workgroup and sk <= 320, else k_attn_s), 0 = k_attn (previous kernel). */
 void bf_attention_set_variant(int v);
 
+/* CuTR decoder cross-attention bias (GlobalCrossAttention.rpe + the logits' bias / clip /
+ * softmax, cubify_transformer.py:93-190 of the reference), f32:
+ *   bf_cpb_mlp: out[b,q,p,:] = W2 relu(W1 ((c - s/2, c + s/2) - pos[p]) + b1), where (c, s) =
+ *     (ref[b,q,axis], ref[b,q,2+axis]) of ref f32[B,nq,4] (cx, cy, w, h); W1 f32[hidden,2],
+ *     b1 f32[hidden], W2 f32[heads,hidden]; out f32[B,nq,n,heads].  hidden <= 512, heads <= 16.
+ *   bf_rpe_softmax: attn f32[B,H,Nq,hh*ww] in place: rows q >= q0 get + (rx[b,q-q0,x,h] +
+ *     ry[b,q-q0,y,h]) at column y*ww+x; every row is clipped to the finite f32 range and
+ *     softmax-normalised.  hh*ww % 4 == 0, <= 4096. */
+int bf_cpb_mlp(const float* ref, int B, int nq, const float* pos, int n, int axis,
+               const float* w1, const float* b1, const float* w2, int hidden, int heads,
+               float* out, void* stream);
+int bf_rpe_softmax(float* attn, int B, int H, int Nq, int q0, const float* rx, const float* ry,
+                   int hh, int ww, void* stream);
+
 /* LayerNorm f32[M,C] -> bf16, written to row row_map[r] (NULL = r; < 0 skips). */
 int bf_layernorm(const float* x, int ldx, const float* gamma, const float* beta, float eps,
                  void* out, int ldo, const int32_t* row_map, int M, int C, void* stream);

@@ -95,3 +95,33 @@ def test_clip_engine_vs_fp32(dev):
     err = rel(got, ref)
     print("clip rel err", err)
     assert err < 3e-2
+
+
+def test_decoder_cross_attention_fused_vs_torch(dev):
+    """GlobalCrossAttention with bf_cpb_mlp + bf_rpe_softmax == the torch ops (bias MLP, broadcast
+    bias, index_put, clip, softmax), f32, on decoder-sized inputs (302 queries, 40x40 memory);
+    the HIP sums run in a fixed order, so the bound is f32 rounding."""
+    from boxfusion_amd.cubify_transformer import GlobalCrossAttention
+    torch.manual_seed(3)
+    xa = GlobalCrossAttention(256, 8, 512, 16).to(dev).eval()
+    B, nq, h, w = 2, 300, 40, 40
+    query = torch.randn(B, nq + 2, 256, device=dev)
+    kv = torch.randn(B, h * w, 256, device=dev)
+    cxcy = torch.rand(B, nq, 1, 2, device=dev) * 640
+    wh = torch.rand(B, nq, 1, 2, device=dev) * 200 + 4
+    ref = torch.cat([cxcy, wh], -1)
+    with torch.no_grad():
+        xa.fused = True
+        got = xa(query, ref, kv, kv, (h, w), slice(2, None))
+        xa.fused = False
+        want = xa(query, ref, kv, kv, (h, w), slice(2, None))
+    torch.testing.assert_close(got, want, rtol=1e-4, atol=2e-5)
+    # the bias tables alone
+    from boxfusion_amd import _lib
+    px, _ = xa._positions(h, w, dev)
+    rx = _lib.cpb_mlp(ref[:, :, 0].contiguous(), px, 0, xa.cpb_mlp1[0].weight, xa.cpb_mlp1[0].bias,
+                      xa.cpb_mlp1[2].weight)
+    r4 = torch.cat([ref[..., :2] - ref[..., 2:] / 2, ref[..., :2] + ref[..., 2:] / 2], -1)
+    with torch.no_grad():
+        rx_t = xa.cpb_mlp1(r4[..., 0::2] - px[None, None, :, None])
+    torch.testing.assert_close(rx, rx_t, rtol=1e-4, atol=1e-4)
