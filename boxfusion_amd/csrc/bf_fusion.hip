@@ -22,6 +22,9 @@
 #include "bf_common.h"
 
 #define FUSE_MAX_VIEWS 32
+#ifndef FUSE_SPLIT_ITER
+#define FUSE_SPLIT_ITER 0   // 1 (diagnostic build): separate terms and step launches per iteration
+#endif
 #define FUSE_MAX_PST 1024
 #define CAND_CAP 64
 
@@ -543,62 +546,74 @@ __global__ void __launch_bounds__(TERM_THREADS) k_fuse_terms(const float* __rest
     if (flags) atomicOr(&states[job].flags, flags);
 }
 
-__global__ void __launch_bounds__(1024) k_fuse_step(const float* __restrict__ pst, bf_fuse_cfg cfg,
-                                                    FuseState* __restrict__ states,
-                                                    const float* __restrict__ terms, int max_views,
-                                                    int it, float* __restrict__ trace) {
-    const int job = blockIdx.x;
+// the sequential update of one job after an iteration's terms (any block size, multiple of 64)
+struct StepLds {
+    float fit[FUSE_MAX_PST];
+    int acc[FUSE_MAX_PST];
+    float prod[FUSE_MAX_PST * 8];   // accepted particle k: 6 weighted offsets, w, fit*w
+};
+
+__device__ void fuse_step_body(int job, const float* __restrict__ pst, const bf_fuse_cfg& cfg,
+                               FuseState* __restrict__ states, const float* __restrict__ terms,
+                               int max_views, int it, float* __restrict__ trace, StepLds& L) {
     const int t = threadIdx.x;
     const int P = cfg.pst_size;
     FuseState* G = states + job;
     if (G->stop) return;
-    __shared__ float s_fit[FUSE_MAX_PST];
-    __shared__ int s_acc[FUSE_MAX_PST];
-    __shared__ int s_wave[FUSE_MAX_PST / 64];
+    float* s_fit = L.fit;
+    int* s_acc = L.acc;
+    float* s_prod = L.prod;
+    __shared__ int s_wave[16];
     __shared__ double s_dsum[8];
     __shared__ float s_fsum[8];
-    __shared__ float s_prod[FUSE_MAX_PST * 8];   // accepted particle k: 6 weighted offsets, w, fit*w
     const int nv = G->nv;
+    const int NT = blockDim.x;
     // ---- fitness: the reference's per-particle loop `val += |1 - iou|; cnt += 1` -------------
-    if (t < P) {
+    for (int p = t; p < P; p += NT) {
         float val = 0.0f, cnt = 0.0f;
-        const float* tp = terms + (size_t)job * max_views * P + t;
+        const float* tp = terms + (size_t)job * max_views * P + p;
         for (int v = 0; v < nv; ++v) {
             val += tp[(size_t)v * P];
             cnt += 1.0f;
         }
         const float f = val / (cnt + 1e-6f);
-        s_fit[t] = f;
-        if (trace) trace[((size_t)job * cfg.iters + it) * P + t] = f;
+        s_fit[p] = f;
+        if (trace) trace[((size_t)job * cfg.iters + it) * P + p] = f;
     }
     __syncthreads();
     // ---- accepted particles: j >= 1, fit[j] < fit[0], first max_accept in index order ------
+    // (chunks of NT particles in index order; within a chunk a block ballot prefix)
     const float f0 = s_fit[0];
-    bool flag = (t >= 1) && (t < P) && (s_fit[t] < f0);
-    unsigned long long m = __ballot(flag);
-    if (bf_lane() == 0) s_wave[t >> 6] = __popcll(m);
-    __syncthreads();
-    int before = 0, total = 0;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
-        if (w < (t >> 6)) before += s_wave[w];
-        total += s_wave[w];
+    int base = 0;
+    for (int c0 = 0; c0 < P; c0 += NT) {
+        const int p = c0 + t;
+        const bool flag = (p >= 1) && (p < P) && (s_fit[p] < f0);
+        const unsigned long long m = __ballot(flag);
+        if (bf_lane() == 0) s_wave[t >> 6] = __popcll(m);
+        __syncthreads();
+        int before = 0, tot = 0;
+        for (int w = 0; w < (NT >> 6); ++w) {
+            if (w < (t >> 6)) before += s_wave[w];
+            tot += s_wave[w];
+        }
+        const int rnk = base + before + bf_lanes_below(m);
+        if (flag && rnk < cfg.max_accept) s_acc[rnk] = p;
+        base += tot;
+        __syncthreads();
     }
-    int rnk = before + bf_lanes_below(m);
-    if (flag && rnk < cfg.max_accept) s_acc[rnk] = t;
-    const int n_acc = total < cfg.max_accept ? total : cfg.max_accept;
-    __syncthreads();
+    const int n_acc = base < cfg.max_accept ? base : cfg.max_accept;
     // ---- cal_transform sums in reference order (8 independent sequential sums) -------------
     // the f32 products of every accepted particle are formed in parallel into LDS first, so
     // the 8 sequential sums below only chain adds (not a dependent global load per step)
-    if (t < n_acc) {
-        const int j = s_acc[t];
+    for (int k = t; k < n_acc; k += NT) {
+        const int j = s_acc[k];
         const float fj = s_fit[j];
         const float w = f0 - fj;
         const float* pj = pst + 6 * j;
 #pragma unroll
-        for (int c = 0; c < 6; ++c) s_prod[8 * t + c] = pj[c] * w;
-        s_prod[8 * t + 6] = w;
-        s_prod[8 * t + 7] = fj * w;
+        for (int c = 0; c < 6; ++c) s_prod[8 * k + c] = pj[c] * w;
+        s_prod[8 * k + 6] = w;
+        s_prod[8 * k + 7] = fj * w;
     }
     __syncthreads();
     if (t < 8) {
@@ -673,6 +688,82 @@ __global__ void __launch_bounds__(1024) k_fuse_step(const float* __restrict__ ps
     }
 }
 
+// One launch per iteration: the terms of every (job, view, particle) as k_fuse_terms, then the
+// job's workgroup that finishes last (device-scope counter per job) runs the job's sequential
+// update — half the launches of the terms + step pair, on a path that is launch-latency bound.
+// The step reuses the hull stacks' LDS (dead by then).
+union IterLds {
+    HullLds hull;
+    StepLds step;
+};
+
+__global__ void __launch_bounds__(TERM_THREADS) k_fuse_iter(const float* __restrict__ vpose,
+                                                            const TargetHull* __restrict__ th,
+                                                            const float* __restrict__ pst,
+                                                            bf_fuse_cfg cfg,
+                                                            FuseState* __restrict__ states,
+                                                            float* __restrict__ terms, int max_views,
+                                                            int it, float* __restrict__ trace,
+                                                            int* __restrict__ done) {
+    __shared__ IterLds U;
+    __shared__ float s_pose[16];
+    __shared__ TargetHull s_th;
+    __shared__ int s_last;
+    const int job = blockIdx.y;
+    const FuseState& S = states[job];
+    const int P = cfg.pst_size;                           // multiple of 64
+    const int pair = blockIdx.x * TERM_THREADS + threadIdx.x;
+    const int v = pair / P, p = pair % P;                 // v uniform per (one-wave) workgroup
+    const int lane = threadIdx.x;
+    if (!S.stop && v < S.nv) {
+        const size_t vi = (size_t)S.off + v;
+        if (lane < 16) s_pose[lane] = vpose[vi * 16 + lane];
+        else if (lane < 16 + 18) reinterpret_cast<float*>(&s_th)[lane - 16] =
+            reinterpret_cast<const float*>(th + (size_t)job * max_views + v)[lane - 16];
+        __syncthreads();
+        float b[6], r[9], ss[6], corners[24];
+        for (int k = 0; k < 6; ++k) { b[k] = S.box32[k]; ss[k] = S.ss[k]; }
+        for (int k = 0; k < 9; ++k) r[k] = S.R[k];
+        particle_corners(b, r, pst + 6 * p, ss, corners);
+        const float* Pm = s_pose;
+        P2 c0[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float vx = corners[3 * j] - Pm[3], vy = corners[3 * j + 1] - Pm[7], vz = corners[3 * j + 2] - Pm[11];
+            float cx = Pm[0] * vx + Pm[4] * vy + Pm[8] * vz;
+            float cy = Pm[1] * vx + Pm[5] * vy + Pm[9] * vz;
+            float cz = Pm[2] * vx + Pm[6] * vy + Pm[10] * vz;
+            float px = ((cx * cfg.K[0]) / cz + cfg.K[2]);
+            float py = ((cy * cfg.K[5]) / cz + cfg.K[6]);
+            c0[j].x = (px > cfg.img_w) ? cfg.img_w : (px < 0) ? 0 : px;
+            c0[j].y = (py > cfg.img_h) ? cfg.img_h : (py < 0) ? 0 : py;
+        }
+        int flags = 0;
+        const float iou = iou_hull_lds(c0, s_th.h, s_th.n, s_th.area, U.hull, lane, &flags);
+        terms[((size_t)job * max_views + v) * P + p] = fabsf(1 - iou);
+        if (flags) atomicOr(&states[job].flags, flags);
+    }
+    // the job's last workgroup to finish runs the update
+    __threadfence();
+    __syncthreads();
+    if (lane == 0)
+        s_last = __hip_atomic_fetch_add(&done[job], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+                 (int)gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    if (lane == 0) done[job] = 0;                          // for the next iteration's launch
+    fuse_step_body(job, pst, cfg, states, terms, max_views, it, trace, U.step);
+}
+
+__global__ void __launch_bounds__(1024) k_fuse_step(const float* __restrict__ pst, bf_fuse_cfg cfg,
+                                                    FuseState* __restrict__ states,
+                                                    const float* __restrict__ terms, int max_views,
+                                                    int it, float* __restrict__ trace) {
+    __shared__ StepLds L;
+    fuse_step_body(blockIdx.x, pst, cfg, states, terms, max_views, it, trace, L);
+}
+
 __global__ void __launch_bounds__(64) k_fuse_final(const FuseState* __restrict__ states, int n_jobs,
                                                    float* __restrict__ out_box,
                                                    int32_t* __restrict__ out_updated,
@@ -696,9 +787,11 @@ static size_t fuse_targets_bytes(int n_jobs, int max_views) {
     return ((size_t)n_jobs * max_views * sizeof(TargetHull) + 255) & ~(size_t)255;
 }
 
+static size_t fuse_done_bytes(int n_jobs) { return ((size_t)n_jobs * sizeof(int) + 255) & ~(size_t)255; }
+
 BF_API size_t bf_fusion_fit_workspace_size(int n_jobs, int max_views, int pst_size) {
     if (n_jobs <= 0 || max_views <= 0 || pst_size <= 0) return 0;
-    return fuse_states_bytes(n_jobs) + fuse_targets_bytes(n_jobs, max_views) +
+    return fuse_states_bytes(n_jobs) + fuse_targets_bytes(n_jobs, max_views) + fuse_done_bytes(n_jobs) +
            (size_t)n_jobs * max_views * pst_size * sizeof(float);
 }
 
@@ -720,17 +813,24 @@ BF_API int bf_fusion_fit(const int32_t* view_off, const int32_t* n_views, int n_
     FuseState* states = reinterpret_cast<FuseState*>(workspace);
     char* ws = reinterpret_cast<char*>(workspace) + fuse_states_bytes(n_jobs);
     TargetHull* th = reinterpret_cast<TargetHull*>(ws);
-    float* terms = reinterpret_cast<float*>(ws + fuse_targets_bytes(n_jobs, max_views));
+    int* done = reinterpret_cast<int*>(ws + fuse_targets_bytes(n_jobs, max_views));
+    float* terms = reinterpret_cast<float*>(reinterpret_cast<char*>(done) + fuse_done_bytes(n_jobs));
+    if (hipMemsetAsync(done, 0, sizeof(int) * (size_t)n_jobs, s) != hipSuccess) return BF_ERR_LAUNCH;
     const int P = cfg->pst_size;
     hipLaunchKernelGGL(k_fuse_init, dim3(n_jobs), dim3(64), 0, s, view_off, n_views, max_views,
                        view_box, view_R, view_score, *cfg, states);
     hipLaunchKernelGGL(k_fuse_targets, dim3(n_jobs), dim3(64), 0, s, view_tc, states, max_views, th);
     const dim3 tgrid((unsigned)bf_cdiv(max_views * P, TERM_THREADS), (unsigned)n_jobs);
     for (int it = 0; it < cfg->iters; ++it) {
+#if FUSE_SPLIT_ITER
         hipLaunchKernelGGL(k_fuse_terms, tgrid, dim3(TERM_THREADS), 0, s, view_pose, th, pst,
                            *cfg, states, terms, max_views);
         hipLaunchKernelGGL(k_fuse_step, dim3(n_jobs), dim3(P), 0, s, pst, *cfg, states, terms,
                            max_views, it, trace);
+#else
+        hipLaunchKernelGGL(k_fuse_iter, tgrid, dim3(TERM_THREADS), 0, s, view_pose, th, pst, *cfg,
+                           states, terms, max_views, it, trace, done);
+#endif
     }
     hipLaunchKernelGGL(k_fuse_final, dim3(bf_cdiv(n_jobs, 64)), dim3(64), 0, s, states, n_jobs,
                        out_box, out_updated, out_iters, status);

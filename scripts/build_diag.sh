@@ -9,7 +9,7 @@ cd "$(dirname "$0")/../boxfusion_amd/_build"
 python3 -c "import sys; sys.path.insert(0, '../..'); from boxfusion_amd import build; build.build()"
 mkdir -p diag
 FL="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -I../../include -Wno-unused-result"
-/opt/rocm/bin/hipcc $FL -DFAST_CAND=4 -c ../csrc/bf_fusion.hip -o diag/bf_fusion.o
+/opt/rocm/bin/hipcc $FL -DFAST_CAND=4 -DFUSE_SPLIT_ITER=1 -c ../csrc/bf_fusion.hip -o diag/bf_fusion.o
 /opt/rocm/bin/hipcc $FL -DNMS_FAST_N=0 -c ../csrc/bf_assoc.hip -o diag/bf_assoc.o
 /opt/rocm/bin/hipcc $FL -DOBB_SPLIT=0 -c ../csrc/bf_iou3d.hip -o diag/bf_iou3d.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o diag/libboxfusion_hip_diag.so \
