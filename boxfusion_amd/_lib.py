@@ -171,7 +171,7 @@ _ROWS_DT = np.dtype([("a", np.uint64), ("b", np.uint64), ("dst", np.uint64), ("n
 def rows_gather(pairs, idx=None, n_out=None):
     """pairs: [(a, b or None)] contiguous device tensors with the same row shape / dtype per pair;
     returns new tensors with rows idx of cat(a, b) (idx: int64 device tensor; None: the whole
-    concatenation).  One bf_rows_gather launch for up to ROWS_MAX_FIELDS fields."""
+    concatenation; int32 or int64).  One bf_rows_gather launch for up to ROWS_MAX_FIELDS fields."""
     if idx is not None:
         n_out = int(idx.shape[0])
     elif n_out is None:
@@ -187,7 +187,8 @@ def rows_gather(pairs, idx=None, n_out=None):
         outs.append(out)
     if pairs and n_out:
         arr = np.array(recs, dtype=_ROWS_DT)
-        _check(lib().bf_rows_gather(c_void_p(arr.ctypes.data), c_int(len(pairs)), _ptr(idx),
+        i32 = idx is not None and idx.dtype == torch.int32
+        _check(lib().bf_rows_gather(c_void_p(arr.ctypes.data), c_int(len(pairs)), _ptr(idx), c_int(int(i32)),
                                     c_int(n_out), None, _stream()), "bf_rows_gather")
     return outs
 

@@ -17,8 +17,8 @@ struct RowsArgs {
     bf_rows_field f[BF_ROWS_MAX_FIELDS];
 };
 
-__global__ void __launch_bounds__(256) k_rows_gather(RowsArgs args, const int64_t* __restrict__ idx,
-                                                     int n_out, int32_t* __restrict__ status) {
+__global__ void __launch_bounds__(256) k_rows_gather(RowsArgs args, const void* __restrict__ idx,
+                                                     int idx_i32, int n_out, int32_t* __restrict__ status) {
     const bf_rows_field& F = args.f[blockIdx.y];
     const int wpr = F.row_bytes >> 2;                     // 4-byte words per row
     const long long total = (long long)n_out * wpr;
@@ -26,7 +26,8 @@ __global__ void __launch_bounds__(256) k_rows_gather(RowsArgs args, const int64_
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
          e += (long long)gridDim.x * blockDim.x) {
         const long long r = e / wpr, w = e - r * wpr;
-        const long long s = idx ? idx[r] : r;
+        const long long s = !idx ? r : idx_i32 ? (long long)static_cast<const int32_t*>(idx)[r]
+                                               : static_cast<const int64_t*>(idx)[r];
         if (s < 0 || s >= nab) {
             if (status && w == 0) atomicOr(status, BF_DEV_INDEX_RANGE);
             continue;
@@ -37,8 +38,8 @@ __global__ void __launch_bounds__(256) k_rows_gather(RowsArgs args, const int64_
     }
 }
 
-BF_API int bf_rows_gather(const bf_rows_field* fields, int n_fields, const int64_t* idx, int n_out,
-                          int32_t* status, void* stream) {
+BF_API int bf_rows_gather(const bf_rows_field* fields, int n_fields, const void* idx, int idx_i32,
+                          int n_out, int32_t* status, void* stream) {
     if (!fields || n_fields < 0 || n_fields > BF_ROWS_MAX_FIELDS || n_out < 0) return BF_ERR_ARG;
     if (n_fields == 0 || n_out == 0) return BF_OK;
     RowsArgs args;
@@ -55,6 +56,6 @@ BF_API int bf_rows_gather(const bf_rows_field* fields, int n_fields, const int64
     }
     const unsigned bx = (unsigned)((most + 255) / 256 < 1024 ? (most + 255) / 256 : 1024);
     hipLaunchKernelGGL(k_rows_gather, dim3(bx, (unsigned)n_fields), dim3(256), 0, bf_stream(stream),
-                       args, idx, n_out, status);
+                       args, idx, idx_i32, n_out, status);
     return bf_check_launch();
 }

@@ -130,15 +130,20 @@ class FusionStage:
         corners = all_pred_box.pred_boxes_3d.corners       # shared by both association steps
         if self.joint and len(all_pred_box) > 1:
             # nms + correspondence back to back on the device, one read-back
-            mask, success, keep_idx, any_cur = Instances3D.joint_association(
+            mask, success, keep_idx, any_cur, keep_dev = Instances3D.joint_association(
                 all_pred_box, n_before, cfg["box_fusion"]["nms_threshold"],
                 cfg["association"]["small_threshold"], bm, self.per_frame_ins.cam_pose,
                 pred.cam_pose[0], self.K_dev, corners, H=self.H, W=self.W)
-            if any_cur:
-                all_pred_box = all_pred_box[keep_idx]
-                all_poses = all_poses[keep_idx]
-            else:
+            if not any_cur:
                 keep_idx = np.asarray(mask)
+            kept = all_pred_box._device_rows([], keep_dev)
+            all_pred_box = kept if kept is not None else all_pred_box[keep_idx]
+            all_poses = all_poses[keep_idx]
+            if not any_cur:
+                self._stats["suppressed"] += len(success)
+                bm.update(keep_idx)
+                self.all_pred_box, self.all_poses = all_pred_box, all_poses
+                return
         else:
             mask, success = Instances3D.spatial_association(all_pred_box, cfg["box_fusion"]["nms_threshold"],
                                                             bm, self.per_frame_ins.cam_pose, corners=corners)

@@ -330,7 +330,8 @@ class Instances3D:
         the second on the first's device outputs.  Returns (mask, success, keep_idx, cur_keep):
         mask / success as spatial_association's, keep_idx = correspondence_association's keep
         (equal to mask when no new box survived the NMS, the case where the reference skips the
-        second step), cur_keep = whether a new box (index >= n_glo) is in mask."""
+        second step), cur_keep = whether a new box (index >= n_glo) is in mask, and the kept rows
+        (keep_idx, or mask without cur_keep) as an int32 device tensor."""
         boxes = all_pred_box.get("pred_boxes_3d")
         dev = boxes.device
         iou = _lib.obb_iou_matrix(corners)
@@ -370,4 +371,7 @@ class Instances3D:
         mask = h["keep"][:c[0]].astype(np.int64)
         success = h["succ"][:c[1]].astype(np.int64).tolist()
         keep_idx = h["ckeep"][:cc[0]].astype(np.int64)
-        return mask.tolist(), success, keep_idx, bool((mask >= n_glo).any())
+        any_cur = bool((mask >= n_glo).any())
+        # the row set to keep, still on the device (int32): gather without another upload
+        keep_dev = d["ckeep"][:cc[0]] if any_cur else d["keep"][:c[0]]
+        return mask.tolist(), success, keep_idx, any_cur, keep_dev

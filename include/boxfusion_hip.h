@@ -53,7 +53,7 @@ int bf_device_count(void);
  * instances.py:155-218 of the reference, one torch.cat / index per field there): every field is
  * a row-major table whose rows are `row_bytes` bytes (a multiple of 4); rows come from the
  * virtual concatenation [a (n_a rows); b (n_b rows)], dst row r = row idx[r] of it (idx == NULL:
- * r itself, i.e. the concatenation).  One launch for all fields.  idx values must lie in
+ * r itself, i.e. the concatenation; idx is int32 when idx_i32 != 0, else int64).  One launch for all fields.  idx values must lie in
  * [0, n_a + n_b) (checked on the device: out-of-range rows are left unwritten and set
  * BF_DEV_INDEX_RANGE in *status when status != NULL).
  * ------------------------------------------------------------------------------------------ */
@@ -67,8 +67,8 @@ typedef struct {
     int32_t pad;
 } bf_rows_field;
 
-int bf_rows_gather(const bf_rows_field* fields, int n_fields, const int64_t* idx, int n_out,
-                   int32_t* status, void* stream);
+int bf_rows_gather(const bf_rows_field* fields, int n_fields, const void* idx, int idx_i32,
+                   int n_out, int32_t* status, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * 3-D box geometry  (boxfusion/boxes.py, boxfusion/instances.py)

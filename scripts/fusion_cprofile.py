@@ -25,3 +25,5 @@ torch.cuda.synchronize()
 pr.disable()
 pstats.Stats(pr).sort_stats("tottime").print_stats(25)
 pstats.Stats(pr).sort_stats("cumtime").print_stats(45)
+pstats.Stats(pr).print_callers("index_select")
+pstats.Stats(pr).print_callers("'cpu'")

@@ -268,6 +268,8 @@ def test_instances_rows_gather(dev):
             for k in ("scores", "cam_pose", "init_id"):
                 torch.testing.assert_close(s.get(k), c.get(k)[it], rtol=0, atol=0)
             torch.testing.assert_close(s.pred_boxes_3d.R, c.pred_boxes_3d.R[it], rtol=0, atol=0)
+            s32 = c._device_rows([], it.to(torch.int32))          # int32 device index
+            torch.testing.assert_close(s32.cam_pose, c.cam_pose[it], rtol=0, atol=0)
     # an out-of-range row is reported, not written
     st = torch.zeros(1, dtype=torch.int32, device=dev)
     x = torch.arange(4, dtype=torch.float32, device=dev)
@@ -275,5 +277,5 @@ def test_instances_rows_gather(dev):
     f = (_lib.RowsField * 1)()
     f[0].a, f[0].b, f[0].dst, f[0].n_a, f[0].n_b, f[0].row_bytes = x.data_ptr(), None, out.data_ptr(), 4, 0, 4
     idx = torch.tensor([2, 9], dtype=torch.int64, device=dev)
-    assert _lib.lib().bf_rows_gather(f, 1, _lib._ptr(idx), 2, _lib._ptr(st), _lib._stream()) == 0
+    assert _lib.lib().bf_rows_gather(f, 1, _lib._ptr(idx), 0, 2, _lib._ptr(st), _lib._stream()) == 0
     assert out.tolist() == [2.0, -1.0] and int(st.item()) == _lib.BF_DEV_INDEX_RANGE
