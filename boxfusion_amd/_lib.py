@@ -290,6 +290,16 @@ def fusion_fit(view_off, n_views, view_box, view_R, view_score, view_pose, view_
     return out_box, out_upd, out_it, status, tr
 
 
+def fusion_writeback(out_box, updated, rows, target):
+    """target[rows[j], :6] = out_box[j] where updated[j] (bf_fusion_writeback); rows int32"""
+    _need(target, torch.float32, "target")
+    if not target.is_contiguous():
+        raise HipError("fusion_writeback: target must be contiguous")
+    _check(lib().bf_fusion_writeback(_ptr(out_box), _ptr(updated), _ptr(rows), c_int(rows.shape[0]),
+                                     _ptr(target), c_int(target.shape[1]), _stream()),
+           "bf_fusion_writeback")
+
+
 def fusion_fitness(box, R, view_pose, view_tc, pst, search_size, cfg: FuseCfg):
     nv = view_pose.shape[0]
     out = torch.empty(pst.shape[0], dtype=torch.float32, device=box.device)

@@ -105,19 +105,23 @@ class BoxFusion:
         idx = _lib.h2d(host, dev)
         flat = idx[3 * nj:]
         b3 = per_frame_box.pred_boxes_3d
-        out_box, packed, _ = _lib.fusion_fit(
-            idx[:nj], idx[nj:2 * nj],
-            b3.tensor.index_select(0, flat).contiguous(), b3.R.index_select(0, flat).contiguous(),
-            per_frame_box.scores.to(dev, torch.float32).index_select(0, flat).contiguous(),
-            per_frame_box.cam_pose.to(dev, torch.float32).index_select(0, flat).contiguous(),
-            per_frame_box.projected_boxes.index_select(0, flat).contiguous(),
-            self._pst_dev, self.fuse_cfg(), max_views=min(int(nv.max()), 32), packed_out=True)
+        # every view's box, rotation, score, pose and 2-D hull in one gather launch
+        vb, vr, vs, vp, vt = _lib.rows_gather(
+            [(b3.tensor.contiguous(), None), (b3.R.contiguous(), None),
+             (per_frame_box.scores.to(dev, torch.float32).contiguous(), None),
+             (per_frame_box.cam_pose.to(dev, torch.float32).contiguous(), None),
+             (per_frame_box.projected_boxes.contiguous(), None)], flat)
+        out_box, packed, _ = _lib.fusion_fit(idx[:nj], idx[nj:2 * nj], vb, vr, vs, vp, vt,
+                                             self._pst_dev, self.fuse_cfg(),
+                                             max_views=min(int(nv.max()), 32), packed_out=True)
         # write-back of the updated rows on the device (xyz + lhw; R unchanged, quirk 6)
         target = all_pred_box.pred_boxes_3d.tensor
-        rows_dev = idx[2 * nj:3 * nj].long()
-        upd_dev = packed[:nj]
-        target[rows_dev] = torch.where(upd_dev[:, None] != 0, out_box.to(target.device),
-                                       target.index_select(0, rows_dev))
+        if target.is_contiguous():
+            _lib.fusion_writeback(out_box, packed[:nj], idx[2 * nj:3 * nj], target)
+        else:
+            rows_dev = idx[2 * nj:3 * nj].long()
+            target[rows_dev] = torch.where(packed[:nj, None] != 0, out_box,
+                                           target.index_select(0, rows_dev))
 
         def resolve():
             h = packed.cpu().numpy()

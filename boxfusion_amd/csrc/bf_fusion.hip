@@ -780,6 +780,28 @@ __global__ void __launch_bounds__(64) k_fuse_final(const FuseState* __restrict__
     if (S.flags) atomicOr(status, S.flags);
 }
 
+// BoxFusion.boxfusion's write-back (box_fusion.py:716-724): rows of the refined boxes whose job
+// updated get xyz + lhw (R unchanged); target f32 rows of `ld` floats (xyzlhw first)
+__global__ void __launch_bounds__(64) k_fuse_writeback(const float* __restrict__ out_box,
+                                                       const int32_t* __restrict__ updated,
+                                                       const int32_t* __restrict__ rows, int n_jobs,
+                                                       float* __restrict__ target, int ld) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n_jobs * 6) return;
+    const int job = e / 6, k = e % 6;
+    if (updated[job]) target[(size_t)rows[job] * ld + k] = out_box[6 * job + k];
+}
+
+BF_API int bf_fusion_writeback(const float* out_box, const int32_t* updated, const int32_t* rows,
+                               int n_jobs, float* target, int ld, void* stream) {
+    if (n_jobs < 0 || ld < 6) return BF_ERR_ARG;
+    if (n_jobs == 0) return BF_OK;
+    if (!out_box || !updated || !rows || !target) return BF_ERR_ARG;
+    hipLaunchKernelGGL(k_fuse_writeback, dim3(bf_cdiv(n_jobs * 6, 64)), dim3(64), 0,
+                       bf_stream(stream), out_box, updated, rows, n_jobs, target, ld);
+    return bf_check_launch();
+}
+
 static size_t fuse_states_bytes(int n_jobs) {
     return ((size_t)n_jobs * sizeof(FuseState) + 255) & ~(size_t)255;
 }

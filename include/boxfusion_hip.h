@@ -217,6 +217,12 @@ int bf_fusion_fit(const int32_t* view_off, const int32_t* n_views, int n_jobs, i
 /* Single evaluation of the reference fitness kernel (compute_iou_value + evaluate_iou):
  *   box f32[6], R f32[9], views as above (n_views), search_size f32[6] -> fitness f32[pst_size]
  *   = (sum over views in order of |1 - IoU2D|) / (n_views + 1e-6f). */
+/* The write-back of BoxFusion.boxfusion (box_fusion.py:716-724): for every job j with
+ * updated[j] != 0, target[rows[j]][0..6) = out_box[j] (xyz + lhw; R and any further columns of
+ * the ld-float target rows untouched).  Rows must be distinct. */
+int bf_fusion_writeback(const float* out_box, const int32_t* updated, const int32_t* rows,
+                        int n_jobs, float* target, int ld, void* stream);
+
 int bf_fusion_fitness(const float* box, const float* R, int n_views, const float* view_pose,
                       const float* view_tc, const float* pst, int pst_size,
                       const float* search_size, const bf_fuse_cfg* cfg, float* fitness,
