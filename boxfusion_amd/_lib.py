@@ -169,7 +169,8 @@ _ROWS_DT = np.dtype([("a", np.uint64), ("b", np.uint64), ("dst", np.uint64), ("n
 
 
 def rows_gather(pairs, idx=None, n_out=None):
-    """pairs: [(a, b or None)] contiguous device tensors with the same row shape / dtype per pair;
+    """pairs: [(a, b or None[, narrow])] contiguous device tensors with the same row shape / dtype
+    per pair (narrow=True: int64 rows written as int32);
     returns new tensors with rows idx of cat(a, b) (idx: int64 device tensor; None: the whole
     concatenation; int32 or int64).  One bf_rows_gather launch for up to ROWS_MAX_FIELDS fields."""
     if idx is not None:
@@ -178,12 +179,16 @@ def rows_gather(pairs, idx=None, n_out=None):
         a, b = pairs[0]
         n_out = a.shape[0] + (0 if b is None else b.shape[0])
     outs, recs = [], []
-    for a, b in pairs:
-        out = torch.empty((n_out,) + a.shape[1:], dtype=a.dtype, device=a.device)
+    for pr in pairs:
+        a, b = pr[0], pr[1]
+        narrow = len(pr) > 2 and pr[2]                  # int64 rows -> int32 output
+        out = torch.empty((n_out,) + a.shape[1:], dtype=torch.int32 if narrow else a.dtype,
+                          device=a.device)
         nb = 0 if b is None else b.shape[0]
         # contiguous tensors: stride(0) = elements per row (also for 0-row tensors)
         recs.append((a.data_ptr(), b.data_ptr() if nb else 0, out.data_ptr(), a.shape[0], nb,
-                     a.stride(0) * a.element_size() if a.dim() > 1 else a.element_size(), 0))
+                     a.stride(0) * a.element_size() if a.dim() > 1 else a.element_size(),
+                     1 if narrow else 0))
         outs.append(out)
     if pairs and n_out:
         arr = np.array(recs, dtype=_ROWS_DT)

@@ -23,7 +23,10 @@
 
 #define FUSE_MAX_VIEWS 32
 #ifndef FUSE_SPLIT_ITER
-#define FUSE_SPLIT_ITER 0   // 1 (diagnostic build): separate terms and step launches per iteration
+// 1: terms and step as two launches per iteration (default: measured faster under the detect
+// load — the one-launch form's device-scope fences write back L2 in every workgroup);
+// 0 (diagnostic build): k_fuse_iter, one launch per iteration
+#define FUSE_SPLIT_ITER 1
 #endif
 #define FUSE_MAX_PST 1024
 #define CAND_CAP 64

@@ -28,6 +28,13 @@ struct BoxPrep {
     float pad[2];
 };
 
+// device-side work list of the split form (k_obb_gate / k_obb_grid)
+struct ObbWork {
+    int n_gated;      // pairs that passed the gate
+    int grid_done;    // k_obb_grid workgroups finished (the last one divides)
+    int pad[2];
+};
+
 __device__ void tri_plane(const double* p0, const double* p1, const double* p2, const double* cen,
                           double* pl) {
     double a0 = p1[0] - p0[0], a1 = p1[1] - p0[1], a2 = p1[2] - p0[2];
@@ -43,9 +50,12 @@ __device__ void tri_plane(const double* p0, const double* p1, const double* p2, 
 }
 
 __global__ void __launch_bounds__(64) k_obb_prep(const float* __restrict__ corners, int n,
-                                                 BoxPrep* __restrict__ prep) {
+                                                 BoxPrep* __restrict__ prep, double* __restrict__ iou,
+                                                 ObbWork* __restrict__ w) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0 && w) { w->n_gated = 0; w->grid_done = 0; }
     if (i >= n) return;
+    iou[(size_t)i * n + i] = 1.0;                 // diagonal (pairs fill the rest)
     const float* c = corners + 24 * i;
     double p[8][3], cen[3] = {0, 0, 0};
     for (int q = 0; q < 8; ++q)
@@ -200,17 +210,20 @@ __global__ void __launch_bounds__(IOU_THREADS) k_obb_pairs(const BoxPrep* __rest
 //                the others appended to a device list (order-free: each pair owns its entries)
 //   k_obb_grid   persistent: item = (gated pair, split), 15625 / OBB_SPLIT grid points each,
 //                integer counts added atomically (exact, order-free)
-//   k_obb_final  IoU = n12 / ((n1 + n2 - n12) + 1e-6) as the single-workgroup form
+//                the last workgroup to finish divides: IoU = n12 / ((n1 + n2 - n12) + 1e-6)
+//   (k_obb_prep also writes the diagonal and resets the work list: 3 launches per matrix)
 // ------------------------------------------------------------------------------------------
 #ifndef OBB_SPLIT
 #define OBB_SPLIT 8         // (a diagnostic build sets 0: one workgroup per pair, k_obb_pairs)
 #endif
 #define OBB_GRID_WGS 512
+#ifndef OBB_LAST_BLOCK
+// 0 (default): the division as its own launch (k_obb_final); 1 (diagnostic build): the grid's
+// last workgroup divides (one launch less, but every workgroup's release fence writes back L2,
+// which costs more than the launch under the detect load)
+#define OBB_LAST_BLOCK 0
+#endif
 
-struct ObbWork {
-    int n_gated;
-    int pad[3];
-};
 
 __global__ void __launch_bounds__(256) k_obb_gate(const BoxPrep* __restrict__ prep, int n,
                                                   long long pairs, double* __restrict__ iou,
@@ -242,9 +255,10 @@ __global__ void __launch_bounds__(256) k_obb_gate(const BoxPrep* __restrict__ pr
 }
 
 __global__ void __launch_bounds__(IOU_THREADS) k_obb_grid(const BoxPrep* __restrict__ prep, int n,
-                                                          const ObbWork* __restrict__ w,
+                                                          ObbWork* __restrict__ w,
                                                           const int* __restrict__ gated,
-                                                          int* __restrict__ cnt) {
+                                                          int* __restrict__ cnt,
+                                                          double* __restrict__ iou) {
     __shared__ double pl[2][12][4];
     __shared__ double g[3][25];
     __shared__ int s_red[3][IOU_THREADS / 64];
@@ -305,7 +319,31 @@ __global__ void __launch_bounds__(IOU_THREADS) k_obb_grid(const BoxPrep* __restr
             atomicAdd(&cnt[3 * slot + t], s);
         }
     }
+    if (!OBB_LAST_BLOCK) return;
+    // the last workgroup to finish divides: IoU = n12 / ((n1 + n2 - n12) + 1e-6)
+    __shared__ int s_last;
+    __threadfence();
+    __syncthreads();
+    if (t == 0)
+        s_last = __hip_atomic_fetch_add(&w->grid_done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+                 (int)gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    const int ng = __hip_atomic_load(&w->n_gated, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int slot = t; slot < ng; slot += IOU_THREADS) {
+        int i, j;
+        pair_of((long long)gated[slot], n, &i, &j);
+        const long long a = __hip_atomic_load(&cnt[3 * slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const long long b = __hip_atomic_load(&cnt[3 * slot + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const long long c = __hip_atomic_load(&cnt[3 * slot + 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double v = (double)c / ((double)(a + b - c) + 1e-6);
+        iou[(size_t)i * n + j] = v;
+        iou[(size_t)j * n + i] = v;
+    }
 }
+
+
 
 __global__ void __launch_bounds__(256) k_obb_final(int n, const ObbWork* __restrict__ w,
                                                    const int* __restrict__ gated,
@@ -319,12 +357,6 @@ __global__ void __launch_bounds__(256) k_obb_final(int n, const ObbWork* __restr
     const double v = (double)c / ((double)(a + b - c) + 1e-6);
     iou[(size_t)i * n + j] = v;
     iou[(size_t)j * n + i] = v;
-}
-
-__global__ void k_iou_diag(double* iou, int n, ObbWork* w) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) iou[(size_t)i * n + i] = 1.0;
-    if (i == 0 && w) w->n_gated = 0;
 }
 
 static size_t obb_prep_bytes(int n) { return ((size_t)n * sizeof(BoxPrep) + 255) & ~(size_t)255; }
@@ -348,8 +380,7 @@ BF_API int bf_obb_iou_matrix(const float* corners, int n, double* iou, void* wor
     int* gated = reinterpret_cast<int*>(ws + 256);
     int* cnt = gated + pairs;
     if (pairs > 0x7fffffffLL / 4) return BF_ERR_CAPACITY;
-    hipLaunchKernelGGL(k_obb_prep, dim3(bf_cdiv(n, 64)), dim3(64), 0, s, corners, n, prep);
-    hipLaunchKernelGGL(k_iou_diag, dim3(bf_cdiv(n, 256)), dim3(256), 0, s, iou, n, w);
+    hipLaunchKernelGGL(k_obb_prep, dim3(bf_cdiv(n, 64)), dim3(64), 0, s, corners, n, prep, iou, w);
     if (pairs > 0) {
         if (OBB_SPLIT == 0) {
             hipLaunchKernelGGL(k_obb_pairs, dim3((unsigned)pairs), dim3(IOU_THREADS), 0, s, prep, n, iou);
@@ -358,9 +389,11 @@ BF_API int bf_obb_iou_matrix(const float* corners, int n, double* iou, void* wor
                                pairs, iou, w, gated, cnt);
             const unsigned gw = (unsigned)(pairs * (OBB_SPLIT > 0 ? OBB_SPLIT : 1) < OBB_GRID_WGS
                                                ? pairs * (OBB_SPLIT > 0 ? OBB_SPLIT : 1) : OBB_GRID_WGS);
-            hipLaunchKernelGGL(k_obb_grid, dim3(gw), dim3(IOU_THREADS), 0, s, prep, n, w, gated, cnt);
-            hipLaunchKernelGGL(k_obb_final, dim3(bf_cdiv((unsigned)pairs, 256)), dim3(256), 0, s, n, w,
-                               gated, cnt, iou);
+            hipLaunchKernelGGL(k_obb_grid, dim3(gw), dim3(IOU_THREADS), 0, s, prep, n, w, gated, cnt,
+                               iou);
+            if (!OBB_LAST_BLOCK)
+                hipLaunchKernelGGL(k_obb_final, dim3(bf_cdiv((unsigned)pairs, 256)), dim3(256), 0, s, n,
+                                   w, gated, cnt, iou);
         }
     }
     return bf_check_launch();

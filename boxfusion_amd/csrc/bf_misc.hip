@@ -20,7 +20,8 @@ struct RowsArgs {
 __global__ void __launch_bounds__(256) k_rows_gather(RowsArgs args, const void* __restrict__ idx,
                                                      int idx_i32, int n_out, int32_t* __restrict__ status) {
     const bf_rows_field& F = args.f[blockIdx.y];
-    const int wpr = F.row_bytes >> 2;                     // 4-byte words per row
+    const bool narrow = F.pad == 1;                       // int64 source rows -> int32 output
+    const int wpr = narrow ? F.row_bytes >> 3 : F.row_bytes >> 2;   // output words per row
     const long long total = (long long)n_out * wpr;
     const long long na = F.n_a, nab = F.n_a + F.n_b;
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
@@ -30,6 +31,12 @@ __global__ void __launch_bounds__(256) k_rows_gather(RowsArgs args, const void* 
                                                : static_cast<const int64_t*>(idx)[r];
         if (s < 0 || s >= nab) {
             if (status && w == 0) atomicOr(status, BF_DEV_INDEX_RANGE);
+            continue;
+        }
+        if (narrow) {
+            const int64_t* src = s < na ? static_cast<const int64_t*>(F.a) + s * wpr
+                                        : static_cast<const int64_t*>(F.b) + (s - na) * wpr;
+            static_cast<int32_t*>(F.dst)[e] = (int32_t)src[w];
             continue;
         }
         const uint32_t* src = s < na ? static_cast<const uint32_t*>(F.a) + s * wpr
@@ -46,12 +53,13 @@ BF_API int bf_rows_gather(const bf_rows_field* fields, int n_fields, const void*
     long long most = 0;
     for (int k = 0; k < n_fields; ++k) {
         const bf_rows_field& F = fields[k];
-        if (F.row_bytes <= 0 || (F.row_bytes & 3) || !F.dst || F.n_a < 0 || F.n_b < 0 ||
+        if (F.row_bytes <= 0 || (F.row_bytes & (F.pad == 1 ? 7 : 3)) || (F.pad != 0 && F.pad != 1) ||
+            !F.dst || F.n_a < 0 || F.n_b < 0 ||
             (F.n_a > 0 && !F.a) || (F.n_b > 0 && !F.b))
             return BF_ERR_ARG;
         if (!idx && (long long)n_out != F.n_a + F.n_b) return BF_ERR_ARG;
         args.f[k] = F;
-        const long long words = (long long)n_out * (F.row_bytes >> 2);
+        const long long words = (long long)n_out * (F.row_bytes >> (F.pad == 1 ? 3 : 2));
         most = words > most ? words : most;
     }
     const unsigned bx = (unsigned)((most + 255) / 256 < 1024 ? (most + 255) / 256 : 1024);

@@ -100,10 +100,11 @@ class Instances3D:
         sets whose fields are all device tensors / boxes: one bf_rows_gather launch.  None when a
         field needs the generic path."""
         pairs, plan = [], []
+        narrow_id = None
         for k, v in self._fields.items():
             w = others[0]._fields.get(k) if others else None
             if isinstance(v, torch.Tensor):
-                if (v.element_size() * int(np.prod(v.shape[1:], dtype=np.int64))) % 4:
+                if v.element_size() < 4 and (v.element_size() * int(np.prod(v.shape[1:], dtype=np.int64))) % 4:
                     return None
                 if not v.is_cuda or (others and not (isinstance(w, torch.Tensor) and w.dtype == v.dtype
                                                      and w.shape[1:] == v.shape[1:] and w.is_cuda)):
@@ -118,6 +119,12 @@ class Instances3D:
                 pairs.append((v.R.contiguous(), w.R.contiguous() if others else None))
             else:
                 return None
+        if "init_id" in self._fields and isinstance(self._fields["init_id"], torch.Tensor) \
+                and self._fields["init_id"].dtype == torch.int64 and self._fields["init_id"].dim() == 1:
+            # the association kernels' int32 copy of init_id, produced by the same launch
+            narrow_id = len(pairs)
+            v = self._fields["init_id"]
+            pairs.append((v.contiguous(), others[0]._fields["init_id"].contiguous() if others else None, True))
         if not pairs or len(pairs) > _lib.ROWS_MAX_FIELDS:
             return None
         if others and set(others[0]._fields) != set(self._fields):
@@ -132,6 +139,8 @@ class Instances3D:
             else:
                 ret.set(k, box_type._views(outs[o], outs[o + 1]))
                 o += 2
+        if narrow_id is not None:
+            ret._init_id32 = outs[narrow_id]
         return ret
 
     def __getitem__(self, item):
@@ -336,7 +345,9 @@ class Instances3D:
         dev = boxes.device
         iou = _lib.obb_iou_matrix(corners)
         scores = all_pred_box.scores.to(dev, torch.float32).contiguous()
-        init_id = all_pred_box.init_id.to(dev, torch.int32).contiguous()
+        init_id = getattr(all_pred_box, "_init_id32", None)
+        if init_id is None or init_id.shape[0] != len(all_pred_box):
+            init_id = all_pred_box.init_id.to(dev, torch.int32).contiguous()
         poses = per_frame_ins_cam_pose.to(dev, torch.float32).contiguous()
         vn = all_pred_box.valid_num
         if not (isinstance(vn, torch.Tensor) and vn.is_cuda and vn.dtype == torch.float32 and vn.is_contiguous()):

@@ -63,8 +63,8 @@ typedef struct {
     const void* b;           /* may be NULL when n_b == 0 */
     void* dst;
     int64_t n_a, n_b;
-    int32_t row_bytes;
-    int32_t pad;
+    int32_t row_bytes;       /* bytes of a SOURCE row */
+    int32_t pad;             /* 0: copy; 1: int64 source -> int32 output (row_bytes % 8 == 0) */
 } bf_rows_field;
 
 int bf_rows_gather(const bf_rows_field* fields, int n_fields, const void* idx, int idx_i32,
