@@ -11,37 +11,51 @@
 // In torch that is a [B*nq*w, 512] hidden activation per axis, a broadcast [B,nq,h,w,heads] bias,
 // an index_put add, a clip and a softmax over [B,heads,Nq,h*w] — about 1.6 GB of HBM traffic per
 // decoder layer.  Here:
-//   k_cpb_mlp      one thread per (b, q, position): the 512-wide hidden layer stays in registers
-//                  (weights in LDS, broadcast reads), writes rx / ry [B,nq,n,heads] only
-//   k_rpe_softmax  one wave per attention row: reads the row once, adds the bias built from the
-//                  two small tables, clips, softmax, writes the row once (in place)
+//   k_cpb_mlp      8 lanes per (b, q, position), each over 1/8 of the hidden layer (weights in
+//                  LDS, broadcast reads), xor-shuffle reduction; writes rx / ry [B,nq,n,heads] only
+//   k_rpe_softmax  one wave per attention row: the row's two 1-D bias tables into LDS, the row
+//                  read once, bias + clip + softmax, written once (in place)
 // Numerics: f32 throughout; the sums run in a fixed order (not the BLAS blocking of the torch
 // path), so results match the torch decoder to f32 rounding (tests compare with a tolerance).
 #include "bf_common.h"
 
 #define CPB_MAX_HIDDEN 512
 #define CPB_MAX_HEADS 16
+#define RPE_MAX_SIDE 256
 
 // ------------------------------------------------------------------------------------------
 // rx / ry tables
 // ------------------------------------------------------------------------------------------
+// 8 lanes per output position, each over hidden/8 units of the hidden layer; per unit one
+// 16-B LDS read of (w1[j,0], w1[j,1], b1[j], 0) and the unit's heads-wide column of W2
+// (transposed in LDS); the 8 partial head sums are combined with xor shuffles.
+#define CPB_LANES 8
+#define CPB_W2S (CPB_MAX_HEADS + 4)   // W2^T row stride (floats): 8 adjacent rows hit disjoint banks
+#define CPB_BLOCKS 768                 // persistent (3 x 256 CUs at 41 KB LDS): weights staged once per WG
 __global__ void __launch_bounds__(256) k_cpb_mlp(const float* __restrict__ ref, int B, int nq,
                                                  const float* __restrict__ pos, int n, int axis,
                                                  const float* __restrict__ w1,
                                                  const float* __restrict__ b1,
                                                  const float* __restrict__ w2, int hidden,
                                                  int heads, float* __restrict__ out) {
-    __shared__ float s_w1[2 * CPB_MAX_HIDDEN], s_b1[CPB_MAX_HIDDEN];
-    __shared__ float s_w2[CPB_MAX_HEADS * CPB_MAX_HIDDEN];
-    for (int i = threadIdx.x; i < 2 * hidden; i += blockDim.x) s_w1[i] = w1[i];
-    for (int i = threadIdx.x; i < hidden; i += blockDim.x) s_b1[i] = b1[i];
-    for (int i = threadIdx.x; i < heads * hidden; i += blockDim.x) s_w2[i] = w2[i];
+    __shared__ float4 s_l1[CPB_MAX_HIDDEN];                     // (w1a, w1b, b1, 0) per unit
+    __shared__ float s_w2t[CPB_MAX_HIDDEN * CPB_W2S];           // [unit][head], 80-B rows
+    for (int j = threadIdx.x; j < hidden; j += blockDim.x)
+        s_l1[j] = make_float4(w1[2 * j], w1[2 * j + 1], b1[j], 0.f);
+    for (int i = threadIdx.x; i < heads * hidden; i += blockDim.x) {
+        const int hd = i / hidden, j = i % hidden;
+        s_w2t[j * CPB_W2S + hd] = w2[i];
+    }
     __syncthreads();
     const long long total = (long long)B * nq * n;
-    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= total) return;
-    const int p = (int)(e % n);
-    const long long bq = e / n;
+    const int sub = threadIdx.x % CPB_LANES;
+    const long long step = (long long)gridDim.x * blockDim.x / CPB_LANES;
+    // the 8 lanes of a position share e: the loop and the shuffles are uniform per lane group
+    for (long long e = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / CPB_LANES; e < total;
+         e += step) {
+    const long long ee = e;
+    const int p = (int)(ee % n);
+    const long long bq = ee / n;
     const float* r = ref + bq * 4;
     // (c - wh/2, c + wh/2) on this axis, minus the position
     const float c = r[axis], half = r[2 + axis] / 2;
@@ -50,17 +64,39 @@ __global__ void __launch_bounds__(256) k_cpb_mlp(const float* __restrict__ ref, 
     float acc[CPB_MAX_HEADS];
 #pragma unroll
     for (int hd = 0; hd < CPB_MAX_HEADS; ++hd) acc[hd] = 0.f;
-    for (int j = 0; j < hidden; ++j) {
-        float hv = in0 * s_w1[2 * j] + in1 * s_w1[2 * j + 1] + s_b1[j];
+    const int per = hidden / CPB_LANES;                          // hidden % 8 == 0 (host check)
+#pragma unroll 4
+    for (int jj = 0; jj < per; ++jj) {
+        const int j = jj * CPB_LANES + sub;      // the 8 lanes read 8 adjacent units: no bank conflicts
+        const float4 l1 = s_l1[j];
+        float hv = in0 * l1.x + in1 * l1.y + l1.z;
         hv = hv > 0.f ? hv : 0.f;
+        const float4* w = reinterpret_cast<const float4*>(s_w2t + j * CPB_W2S);
+#pragma unroll
+        for (int q = 0; q < CPB_MAX_HEADS / 4; ++q) {
+            if (4 * q < heads) {
+                const float4 wv = w[q];
+                acc[4 * q + 0] += wv.x * hv;
+                acc[4 * q + 1] += wv.y * hv;
+                acc[4 * q + 2] += wv.z * hv;
+                acc[4 * q + 3] += wv.w * hv;
+            }
+        }
+    }
+#pragma unroll
+    for (int hd = 0; hd < CPB_MAX_HEADS; ++hd) {
+        if (hd < heads) {
+#pragma unroll
+            for (int o = CPB_LANES / 2; o > 0; o >>= 1) acc[hd] += __shfl_xor(acc[hd], o, 64);
+        }
+    }
+    if (sub == 0) {
+        float* o = out + e * heads;
 #pragma unroll
         for (int hd = 0; hd < CPB_MAX_HEADS; ++hd)
-            if (hd < heads) acc[hd] += s_w2[hd * hidden + j] * hv;
+            if (hd < heads) o[hd] = acc[hd];
     }
-    float* o = out + e * heads;
-#pragma unroll
-    for (int hd = 0; hd < CPB_MAX_HEADS; ++hd)
-        if (hd < heads) o[hd] = acc[hd];
+    }
 }
 
 BF_API int bf_cpb_mlp(const float* ref, int B, int nq, const float* pos, int n, int axis,
@@ -68,11 +104,13 @@ BF_API int bf_cpb_mlp(const float* ref, int B, int nq, const float* pos, int n, 
                       float* out, void* stream) {
     if (!ref || !pos || !w1 || !b1 || !w2 || !out || B < 0 || nq < 0 || n <= 0 || (axis != 0 && axis != 1))
         return BF_ERR_ARG;
-    if (hidden <= 0 || hidden > CPB_MAX_HIDDEN || heads <= 0 || heads > CPB_MAX_HEADS)
+    if (hidden <= 0 || hidden > CPB_MAX_HIDDEN || hidden % CPB_LANES || heads <= 0 ||
+        heads > CPB_MAX_HEADS)
         return BF_ERR_CAPACITY;
     const long long total = (long long)B * nq * n;
     if (total == 0) return BF_OK;
-    hipLaunchKernelGGL(k_cpb_mlp, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+    const long long blocks = (total * CPB_LANES + 255) / 256;
+    hipLaunchKernelGGL(k_cpb_mlp, dim3((unsigned)(blocks < CPB_BLOCKS ? blocks : CPB_BLOCKS)), dim3(256), 0,
                        bf_stream(stream), ref, B, nq, pos, n, axis, w1, b1, w2, hidden, heads, out);
     return bf_check_launch();
 }
@@ -104,8 +142,18 @@ __global__ void __launch_bounds__(256) k_rpe_softmax(float* __restrict__ attn, i
     const int hd = bh % H, b = bh / H;
     const bool biased = q >= q0;
     const int nqb = Nq - q0;
-    const float* rxr = biased ? rx + ((size_t)(b * nqb + (q - q0)) * ww) * H + hd : nullptr;
-    const float* ryr = biased ? ry + ((size_t)(b * nqb + (q - q0)) * hh) * H + hd : nullptr;
+    // this row's 1-D bias tables (ww + hh values, stride H in HBM) into LDS once
+    __shared__ float s_bias[4][RPE_MAX_SIDE * 2];
+    float* bx = s_bias[threadIdx.x >> 6];
+    float* by = bx + RPE_MAX_SIDE;
+    if (biased) {
+        const float* rxr = rx + ((size_t)(b * nqb + (q - q0)) * ww) * H + hd;
+        const float* ryr = ry + ((size_t)(b * nqb + (q - q0)) * hh) * H + hd;
+        for (int i = lane; i < ww; i += 64) bx[i] = rxr[(size_t)i * H];
+        for (int i = lane; i < hh; i += 64) by[i] = ryr[(size_t)i * H];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     float* a = attn + (size_t)row * N;
     const float fmax_ = 3.40282347e38f;
     float4 v[NPL];
@@ -120,7 +168,7 @@ __global__ void __launch_bounds__(256) k_rpe_softmax(float* __restrict__ attn, i
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const int nn = c + k, y = nn / ww, xx = nn - y * ww;
-                    xs[k] = xs[k] + (rxr[(size_t)xx * H] + ryr[(size_t)y * H]);
+                    xs[k] = xs[k] + (bx[xx] + by[y]);
                 }
             }
 #pragma unroll
@@ -166,6 +214,7 @@ BF_API int bf_rpe_softmax(float* attn, int B, int H, int Nq, int q0, const float
     if (q0 < Nq && (!rx || !ry)) return BF_ERR_ARG;
     const int N = hh * ww;
     if (N % 4) return BF_ERR_ARG;
+    if (hh > RPE_MAX_SIDE || ww > RPE_MAX_SIDE) return BF_ERR_CAPACITY;
     const int rows = B * H * Nq;
     if (rows == 0) return BF_OK;
     const unsigned grid = (unsigned)((rows + 3) / 4);
