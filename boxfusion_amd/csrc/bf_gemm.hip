@@ -881,12 +881,19 @@ static bool gemm_large_tiles(int M, int N, int K) {
     const long long t1 = (long long)((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N);
     const double e2 = (double)t2 / (double)(((t2 + n_cu - 1) / n_cu) * n_cu);
     const double e1 = (double)t1 / (double)(((t1 + 2 * n_cu - 1) / (2 * n_cu)) * 2 * n_cu);
-    const double adv = 1.0 + 0.2 * (double)(K < 4096 ? K : 4096) / 4096.0;
+    // per-tile advantage of the 256x256 kernel (operand reuse, MFMA density) grows with K;
+    // fitted on the CuTR shapes (scripts/gemm_tiles_probe.py): window qkv K=768 N=2304 and fc2
+    // K=3072 N=768 run faster on 256x256 tiles, proj K=768 N=768 on 128x128
+    const double adv = 1.0 + 0.6 * (double)(K < 4096 ? K : 4096) / 4096.0;
     return N >= 512 && t2 >= n_cu / 2 && e2 * adv >= e1;
 }
 
 // which kernel bf_gemm_bf16 runs for an aligned problem of this shape (1 = 256x256 persistent)
-BF_API int bf_gemm_large_tiles(int M, int N, int K) { return gemm_large_tiles(M, N, K) && !g_force_small ? 1 : 0; }
+static bool gemm_use_large(int M, int N, int K) {
+    return g_force_small < 0 ? true : g_force_small > 0 ? false : gemm_large_tiles(M, N, K);
+}
+
+BF_API int bf_gemm_large_tiles(int M, int N, int K) { return gemm_use_large(M, N, K) ? 1 : 0; }
 
 BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bias,
                         const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
@@ -905,7 +912,7 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
     const int t2m = (M + 255) / 256, t2n = (N + 255) / 256;
     const long long t2 = (long long)t2m * t2n;
     const int n_cu = gemm_cu_count();
-    if (vec_epi && gemm_large_tiles(M, N, K) && !g_force_small) {
+    if (vec_epi && gemm_use_large(M, N, K)) {
         const int grid2 = (int)(t2 < n_cu ? t2 : n_cu);   // persistent: one workgroup per CU
 #define GEMM2(OB, AC) launch_gemm256<OB, AC>(grid2, bf_stream(stream), A, lda, W, ldw, bias, \
                                             resid, ldr, resid_mod, C, ldc, row_map, M, N, K, t2n, t2m)

@@ -260,8 +260,9 @@ int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bi
                  const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
                  const int32_t* row_map, int M, int N, int K, int act, void* stream);
 /* Tile selection: large problems (N >= 512, >= 128 tiles of 256x256, 16-B aligned output rows)
- * run the 256x256 8-wave kernel, the rest the 128x128 4-wave kernel.  Test hook: a non-zero
- * argument forces the 128x128 kernel for every shape (process-wide). */
+ * run the 256x256 8-wave kernel, the rest the 128x128 4-wave kernel.  Test / tuning hook
+ * (process-wide): 1 forces the 128x128 kernel, -1 the 256x256 kernel (aligned shapes), 0 the
+ * heuristic. */
 void bf_gemm_force_small_tiles(int on);
 /* Persistent 256x256 kernel variant: 0 = k_gemm256 (one barrier per K-tile), 1 = k_gemm256p
  * (staggered 4-phase schedule, default).  Test/benchmark hook; results are identical in value. */

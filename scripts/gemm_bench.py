@@ -26,7 +26,11 @@ def bench(fn, iters=10):
     return s.elapsed_time(e) / iters
 
 
-args = sys.argv[1:]
+def main():
+    pass
+
+
+args = sys.argv[1:] if __name__ == "__main__" else ["--only=__none__"]
 only = None
 if args and args[0].startswith("--only="):
     only = args[0][7:].split(",")
