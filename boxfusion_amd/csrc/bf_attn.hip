@@ -346,10 +346,18 @@ __global__ void __launch_bounds__(NW * 64) k_attn_s(const u16* __restrict__ Q, c
         if (more) { ATS_LOAD(k0 + AT_KT); }              // in flight during this tile
         const u16* kt = sK + buf * KTILE;
         const u16* vt = sV + buf * VTILE;
+        // a last tile whose keys all fall in the first 32 (CLIP: 257 = 4*64 + 1) skips the second
+        // sub-tile's MFMAs: its scores would be masked to -inf, its probabilities exactly 0
+        const bool sub1 = k0 + 32 < sk;
         // ---- S^T = K Q^T for two 32-key sub-tiles ------------------------------------------
         f32x16 s[2];
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub) {
+            if (sub == 1 && !sub1) {
+#pragma unroll
+                for (int e = 0; e < 16; ++e) s[1][e] = -INFINITY;
+                continue;
+            }
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
                 bf16x8 kf = *reinterpret_cast<const bf16x8*>(kt + (sub * 32 + fr) * KROW + 16 * ks + 8 * fh);
@@ -367,6 +375,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn_s(const u16* __restrict__ Q, c
             for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
                 for (int ss = 0; ss < 2; ++ss) {
+                    if (sub == 1 && !sub1) continue;
                     const int kb = 32 * sub + 16 * ss + 4 * fh + q4;
                     typedef __attribute__((address_space(3))) s16x4* lds_s4;
                     const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
