@@ -157,11 +157,14 @@ class GlobalCrossAttention(nn.Module):
         ry = self.cpb_mlp2(ref[..., 1::2] - pos_y)
         return (rx[:, :, None] + ry[:, :, :, None]).flatten(2, 3).permute(0, 3, 1, 2)
 
-    def forward(self, query, reference_2d, k_in, v_in, hw, box_mask):
+    def forward(self, query, reference_2d, k_in, v_in, hw, box_mask, kv=None):
+        """kv: this layer's (k(k_in), v(v_in)) when the caller computed every layer's projections
+        of the (layer-invariant) memory in one GEMM each (CubifyTransformer.decode)"""
         h, w = hw
         B, N, C = k_in.shape
-        k = self.k(k_in).reshape(B, N, self.num_heads, C // self.num_heads).permute(0, 2, 1, 3)
-        v = self.v(v_in).reshape(B, N, self.num_heads, C // self.num_heads).permute(0, 2, 1, 3)
+        kp, vp = kv if kv is not None else (self.k(k_in), self.v(v_in))
+        k = kp.reshape(B, N, self.num_heads, C // self.num_heads).permute(0, 2, 1, 3)
+        v = vp.reshape(B, N, self.num_heads, C // self.num_heads).permute(0, 2, 1, 3)
         B, Nq, C = query.shape
         q = self.q(query).reshape(B, Nq, self.num_heads, C // self.num_heads).permute(0, 2, 1, 3)
         attn = (q * self.scale) @ k.transpose(-2, -1)
@@ -194,14 +197,14 @@ class PreNormGlobalDecoderLayer(nn.Module):
         self.linear2 = nn.Linear(d_ffn, d_model)
         self.norm3 = nn.LayerNorm(d_model)
 
-    def forward(self, tgt, query_pos, reference_2d, src, src_pos, hw, self_attn_mask, box_mask):
+    def forward(self, tgt, query_pos, reference_2d, src, src_pos, hw, self_attn_mask, box_mask, kv=None):
         t2 = self.norm2(tgt)
         q = k = t2 + query_pos
         t2 = self.self_attn(q.transpose(0, 1), k.transpose(0, 1), t2.transpose(0, 1),
                             attn_mask=self_attn_mask)[0].transpose(0, 1)
         tgt = tgt + t2
         t2 = self.norm1(tgt)
-        t2 = self.xattn(t2 + query_pos, reference_2d, src + src_pos, src, hw, box_mask)
+        t2 = self.xattn(t2 + query_pos, reference_2d, src + src_pos, src, hw, box_mask, kv=kv)
         tgt = tgt + t2
         t2 = self.linear2(F.relu(self.linear1(self.norm3(tgt))))
         return tgt + t2
@@ -435,6 +438,21 @@ class CubifyTransformer(nn.Module):
         feat = self.backbone.backbone.forward_tensors(batch.image, batch.depth)
         return self.decode(feat, batch)
 
+    def _memory_kv(self, src, pos):
+        """Every decoder layer's cross-attention k(src + pos) and v(src) in one GEMM each (the
+        memory is the same for all layers): [B, N, layers*C] pairs, layer l in columns
+        [l*C, (l+1)*C).  Device only (the CPU path keeps the per-layer linears)."""
+        if not src.is_cuda:
+            return None
+        cache = self.__dict__.setdefault("_kv_cache", {})
+        key = src.device
+        if key not in cache:
+            xs = [layer.xattn for layer in self.decoder.layers]
+            cache[key] = (torch.cat([x.k.weight for x in xs]).detach(), torch.cat([x.k.bias for x in xs]).detach(),
+                          torch.cat([x.v.weight for x in xs]).detach(), torch.cat([x.v.bias for x in xs]).detach())
+        wk, bk, wv, bv = cache[key]
+        return F.linear(src + pos, wk, bk), F.linear(src, wv, bv)
+
     # ---- everything after the backbone (cubify_transformer.py:1172-1227) -------------------------
     def decode(self, feat, batch: FrameBatch, pos=None):
         B, _, h, w = feat.shape
@@ -463,8 +481,12 @@ class CubifyTransformer(nn.Module):
         self_mask[2:, 2:] = False
         box_mask = slice(2, None)      # the nq box queries follow the 2 metric queries
         out = query
+        kv = self._memory_kv(src, pos)
+        C = self.decoder.embed_dim
         for lid, layer in enumerate(self.decoder.layers):
-            out = layer(out, qpos, ref_boxes.detach()[:, :, None], src, pos, (h, w), self_mask, box_mask)
+            kv_l = None if kv is None else (kv[0][..., lid * C:(lid + 1) * C], kv[1][..., lid * C:(lid + 1) * C])
+            out = layer(out, qpos, ref_boxes.detach()[:, :, None], src, pos, (h, w), self_mask, box_mask,
+                        kv=kv_l)
             y = self.decoder.norm(out)
             st = dict(proposal_boxes=ref_boxes, clamp_shape=clamp_shape,
                       depth_params=batch.depth_params if batch.depth is not None else None)

@@ -68,6 +68,16 @@ def test_cutr_engine_end_to_end(dev):
     for r in res:
         assert torch.isfinite(r.scores).all() and torch.isfinite(r.pred_boxes_3d.tensor).all()
         assert (r.scores[:-1] >= r.scores[1:]).all()
+    # the decoder's memory projections of all layers in one GEMM each == the per-layer linears
+    orig = type(model)._memory_kv
+    try:
+        type(model)._memory_kv = lambda self, src, pos: None
+        res2 = eng(rgb, dstd, params, K, Tg, [(480, 640)] * B)
+    finally:
+        type(model)._memory_kv = orig
+    for r, r2 in zip(res, res2):
+        torch.testing.assert_close(r.scores, r2.scores, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(r.pred_boxes_3d.tensor, r2.pred_boxes_3d.tensor, rtol=1e-3, atol=1e-3)
 
 
 def test_clip_engine_vs_fp32(dev):
