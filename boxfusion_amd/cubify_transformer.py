@@ -204,7 +204,8 @@ class PreNormGlobalDecoderLayer(nn.Module):
                             attn_mask=self_attn_mask)[0].transpose(0, 1)
         tgt = tgt + t2
         t2 = self.norm1(tgt)
-        t2 = self.xattn(t2 + query_pos, reference_2d, src + src_pos, src, hw, box_mask, kv=kv)
+        k_in = src + src_pos if kv is None else src        # (only its shape is read with kv)
+        t2 = self.xattn(t2 + query_pos, reference_2d, k_in, src, hw, box_mask, kv=kv)
         tgt = tgt + t2
         t2 = self.linear2(F.relu(self.linear1(self.norm3(tgt))))
         return tgt + t2
@@ -490,7 +491,14 @@ class CubifyTransformer(nn.Module):
             y = self.decoder.norm(out)
             st = dict(proposal_boxes=ref_boxes, clamp_shape=clamp_shape,
                       depth_params=batch.depth_params if batch.depth is not None else None)
+            last = lid == len(self.decoder.layers) - 1
             for p in self.decoder.predictors[lid]:
+                if not last and not isinstance(p, DeltaBox2DPredictor):
+                    # before the last layer only the refined 2-D boxes are read (the next layer's
+                    # reference boxes); the other heads' outputs are overwritten unread
+                    if isinstance(p, ScalePredictor):
+                        y = y[:, 2:]
+                    continue
                 y = p(y, st)
             st["object_desc"] = y
             ref_boxes = st["pred_boxes"]
