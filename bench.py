@@ -46,6 +46,7 @@ CFG = dict(
                                     shape_init_size=0.5, shape_scaling_coefficient=0.5)),
 )
 REC_ROWS, REC_W = 64, 22     # per-frame detection record: rows x (score, xyxy, xyzlhw, R, proj_xy)
+REC_HEAD = 17                # record head: detection count, camera pose (4x4)
 
 
 def parse():
@@ -97,16 +98,26 @@ def gen_frames(frame_ids, dev):
     return rgb, depth
 
 
-def pack_records(dets):
-    """scene detections of a batch of frames -> f32 [b, 1 + REC_ROWS*REC_W] records"""
-    out = np.zeros((len(dets), 1 + REC_ROWS * REC_W), np.float32)
+def pack_records(dets, poses):
+    """scene detections + camera poses of a batch of frames -> f32 [b, REC_HEAD + REC_ROWS*REC_W]
+    records: (count, pose 4x4, rows).  The pose and count travel with the detections, so the
+    exchange is one device all-gather (no host-object collective, which would synchronise the
+    detect stream every step)."""
+    out = np.zeros((len(dets), REC_HEAD + REC_ROWS * REC_W), np.float32)
     for j, d in enumerate(dets):
         n = min(len(d["scores"]), REC_ROWS)
         rows = np.concatenate([d["scores"][:n, None], d["pred_boxes"][:n], d["xyzlhw"][:n],
                                d["R"][:n].reshape(n, 9), d["proj_xy"][:n]], 1)
         out[j, 0] = n
-        out[j, 1:1 + n * REC_W] = rows.reshape(-1)
+        out[j, 1:REC_HEAD] = np.asarray(poses[j], np.float32).reshape(-1)
+        out[j, REC_HEAD:REC_HEAD + n * REC_W] = rows.reshape(-1)
     return out
+
+
+def record_meta(recs):
+    """(poses [k,4,4], counts [k]) on the host from gathered records (one device read)"""
+    h = recs[:, :REC_HEAD].cpu().numpy() if hasattr(recs, "cpu") else np.asarray(recs)[:, :REC_HEAD]
+    return h[:, 1:REC_HEAD].reshape(-1, 4, 4).copy(), h[:, 0].astype(np.int64)
 
 
 def unpack_record(rec, dev, n=None):
@@ -116,7 +127,7 @@ def unpack_record(rec, dev, n=None):
     from boxfusion_amd.instances import Instances3D
     if n is None:
         n = int(rec[0].item())
-    rows = rec[1:1 + n * REC_W].view(n, REC_W)
+    rows = rec[REC_HEAD:REC_HEAD + n * REC_W].view(n, REC_W)
     p = Instances3D((480, 640))
     p.scores = rows[:, 0].contiguous()
     p.pred_boxes = rows[:, 1:5].contiguous()
@@ -126,7 +137,7 @@ def unpack_record(rec, dev, n=None):
 
 
 def unpack_records(recs, cnts, dev):
-    """records [nkf, 1 + REC_ROWS*REC_W] of several keyframes -> ONE Instances3D holding every
+    """records [nkf, REC_HEAD + REC_ROWS*REC_W] of several keyframes -> ONE Instances3D holding every
     keyframe's detections in order (keyframe j: cnts[j] rows), five gathers in total"""
     from boxfusion_amd import _lib
     from boxfusion_amd.boxes import GeneralInstance3DBoxes
@@ -134,7 +145,7 @@ def unpack_records(recs, cnts, dev):
     cnts = np.asarray(cnts, np.int64)
     idx = np.concatenate([j * REC_ROWS + np.arange(c) for j, c in enumerate(cnts)]) if cnts.sum() else \
         np.zeros(0, np.int64)
-    rows = recs[:, 1:1 + REC_ROWS * REC_W].reshape(-1, REC_W).index_select(
+    rows = recs[:, REC_HEAD:REC_HEAD + REC_ROWS * REC_W].reshape(-1, REC_W).index_select(
         0, _lib.h2d(idx, dev))
     p = Instances3D((480, 640))
     p.scores = rows[:, 0].contiguous()
@@ -145,14 +156,14 @@ def unpack_records(recs, cnts, dev):
     return p
 
 
-def gather_step(recs, feats, poses, dist, world):
-    """Exchange of one step: every rank's per-frame records [b, R] and CLIP features
-    [n_crops, 1024] are all-gathered (RCCL over xGMI on the GPU; gloo in the CPU tests) so that
-    the fusion owner sees the step's frames in global frame order (rank-major = frame order, since
-    rank r holds frames step*b*world + r*b ... + b-1).  `poses` is a tuple of small per-frame host
-    arrays (poses, detection counts) gathered as one host object."""
+def gather_step(recs, feats, dist, world):
+    """Exchange of one step: every rank's per-frame records [b, R] (detections, count and camera
+    pose) and CLIP features [n_crops, 1024] are all-gathered (RCCL over xGMI on the GPU; gloo in
+    the CPU tests) so that the fusion owner sees the step's frames in global frame order
+    (rank-major = frame order, since rank r holds frames step*b*world + r*b ... + b-1).  Both
+    collectives are asynchronous device operations: nothing here waits for the detect stream."""
     if dist is None or world == 1:
-        return recs, feats, tuple(np.asarray(x) for x in poses)
+        return recs, feats
     if recs.is_cuda:
         g_rec = torch.empty((world * recs.shape[0],) + recs.shape[1:], dtype=recs.dtype, device=recs.device)
         dist.all_gather_into_tensor(g_rec, recs.contiguous())
@@ -166,9 +177,7 @@ def gather_step(recs, feats, poses, dist, world):
         fparts = [torch.empty_like(feats) for _ in range(world)]
         dist.all_gather(fparts, feats.contiguous())
         g_feat = torch.cat(fparts)
-    g_meta = [None] * world
-    dist.all_gather_object(g_meta, tuple(np.asarray(x) for x in poses))
-    return g_rec, g_feat, tuple(np.concatenate([m[i] for m in g_meta]) for i in range(len(g_meta[0])))
+    return g_rec, g_feat
 
 
 # ------------------------------------------------------------------------------------------------
@@ -287,20 +296,17 @@ def main():
     all_mine = [f for s in range(total_steps) for f in my_frames(s)]
     rgb_all, depth_all = gen_frames(all_mine, dev)
     poses_all = np.stack([scene.pose(f) for f in all_mine]).astype(np.float32)
-    rec_host = pack_records([scene.detections(f) for f in all_mine])
+    rec_host = pack_records([scene.detections(f) for f in all_mine], poses_all)
     rec_all = torch.from_numpy(rec_host).to(dev)
-    cnt_all = rec_host[:, 0].astype(np.int64)
     sim = None
     if args.sim_ranks > 1 and world == 1:
         # what rank 0 of an R-GPU run fuses: R*B frames per step (stress test, not the metric)
         R = args.sim_ranks
-        sim = {"rec": [], "pose": [], "cnt": []}
+        sim = {"rec": []}
         for s_ in range(total_steps):
             fr = [s_ * B * R + j for j in range(B * R)]
-            rh = pack_records([scene.detections(f) for f in fr])
+            rh = pack_records([scene.detections(f) for f in fr], [scene.pose(f) for f in fr])
             sim["rec"].append(torch.from_numpy(rh).to(dev))
-            sim["cnt"].append(rh[:, 0].astype(np.int64))
-            sim["pose"].append(np.stack([scene.pose(f) for f in fr]).astype(np.float32))
     torch.cuda.synchronize()
 
     brk = dict(detect=0.0, fusion=0.0)
@@ -321,13 +327,13 @@ def main():
                 tb = time.perf_counter()
             bidx, iidx, cat_idx, feats, sims = det.last["clip"]
             recs = rec_all[sl]
-            g_rec, g_feat, g_meta = gather_step(recs, feats, (poses_all[sl], cnt_all[sl]), dist, N)
-            g_pose, g_cnt = g_meta
+            g_rec, g_feat = gather_step(recs, feats, dist, N)
             if sim is not None:       # --sim-ranks: rank 0 fuses the frames of R virtual ranks
-                g_rec, g_pose, g_cnt = sim["rec"][s], sim["pose"][s], sim["cnt"][s]
+                g_rec = sim["rec"][s]
             if rank == 0:
                 base = s * (per_step if sim is None else B * args.sim_ranks)
                 if args.sync_fusion:
+                    g_pose, g_cnt = record_meta(g_rec)
                     for j in range(g_rec.shape[0]):
                         fusion.keyframe(base + j - s0 * (g_rec.shape[0]), g_pose[j],
                                         unpack_record(g_rec[j], dev, int(g_cnt[j])))
@@ -338,9 +344,10 @@ def main():
                     g_rec.record_stream(fusion.stream)
                     counts = [base + j - s0 * (g_rec.shape[0]) for j in range(g_rec.shape[0])]
                     # the whole step's keyframes as one job: geometry batched, association serial
-                    fusion.submit_call(
-                        lambda st, r=g_rec, c=np.asarray(g_cnt), p=np.asarray(g_pose), k=counts:
-                        st.keyframes(k, p, unpack_records(r, c, dev), c), ev)
+                    def job(st, r=g_rec, k=counts):
+                        p, c = record_meta(r)       # on the worker's stream, after the gather
+                        st.keyframes(k, p, unpack_records(r, c, dev), c)
+                    fusion.submit_call(job, ev)
             st_ctx.__exit__(None, None, None)
             if args.breakdown:
                 torch.cuda.synchronize()

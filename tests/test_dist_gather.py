@@ -25,16 +25,16 @@ def _worker(rank, world, port, q):
     scene = Scene(seed=0)
     B, step = 4, 3
     frames = [step * B * world + rank * B + j for j in range(B)]
-    recs = torch.from_numpy(bench.pack_records([scene.detections(f) for f in frames]))
-    feats = torch.full((B * 2, 8), float(rank))
     poses = np.stack([scene.pose(f) for f in frames])
-    cnt = recs[:, 0].numpy().astype(np.int64)
-    g_rec, g_feat, (g_pose, g_cnt) = bench.gather_step(recs, feats, (poses, cnt), dist, world)
+    recs = torch.from_numpy(bench.pack_records([scene.detections(f) for f in frames], poses))
+    feats = torch.full((B * 2, 8), float(rank))
+    g_rec, g_feat = bench.gather_step(recs, feats, dist, world)
     if rank == 0:
         want = [step * B * world + j for j in range(B * world)]
-        exp = bench.pack_records([scene.detections(f) for f in want])
+        exp = bench.pack_records([scene.detections(f) for f in want], [scene.pose(f) for f in want])
+        g_pose, g_cnt = bench.record_meta(g_rec)
         ok = (np.array_equal(g_rec.numpy(), exp)
-              and np.array_equal(g_pose, np.stack([scene.pose(f) for f in want]))
+              and np.array_equal(g_pose, np.stack([scene.pose(f) for f in want]).astype(np.float32))
               and np.array_equal(g_cnt, exp[:, 0].astype(np.int64))
               and g_feat[:B * 2].eq(0).all().item() and g_feat[B * 2:].eq(1).all().item())
         unpacked = bench.unpack_record(g_rec[1], "cpu")
