@@ -168,22 +168,27 @@ _ROWS_DT = np.dtype([("a", np.uint64), ("b", np.uint64), ("dst", np.uint64), ("n
                      ("n_b", np.int64), ("row_bytes", np.int32), ("pad", np.int32)])
 
 
-def rows_gather(pairs, idx=None, n_out=None):
+def rows_gather(pairs, idx=None, n_out=None, outs=None):
     """pairs: [(a, b or None[, narrow])] contiguous device tensors with the same row shape / dtype
     per pair (narrow=True: int64 rows written as int32);
     returns new tensors with rows idx of cat(a, b) (idx: int64 device tensor; None: the whole
-    concatenation; int32 or int64).  One bf_rows_gather launch for up to ROWS_MAX_FIELDS fields."""
+    concatenation; int32 or int64); `outs`: write into these contiguous tensors instead (e.g. the
+    tail rows of a preallocated table).  One bf_rows_gather launch for up to ROWS_MAX_FIELDS
+    fields."""
     if idx is not None:
         n_out = int(idx.shape[0])
     elif n_out is None:
         a, b = pairs[0]
         n_out = a.shape[0] + (0 if b is None else b.shape[0])
-    outs, recs = [], []
-    for pr in pairs:
+    given, outs, recs = outs, [], []
+    for k, pr in enumerate(pairs):
         a, b = pr[0], pr[1]
         narrow = len(pr) > 2 and pr[2]                  # int64 rows -> int32 output
-        out = torch.empty((n_out,) + a.shape[1:], dtype=torch.int32 if narrow else a.dtype,
-                          device=a.device)
+        if given is not None:                           # caller's contiguous destinations
+            out = given[k]
+        else:
+            out = torch.empty((n_out,) + a.shape[1:], dtype=torch.int32 if narrow else a.dtype,
+                              device=a.device)
         nb = 0 if b is None else b.shape[0]
         # contiguous tensors: stride(0) = elements per row (also for 0-row tensors)
         recs.append((a.data_ptr(), b.data_ptr() if nb else 0, out.data_ptr(), a.shape[0], nb,

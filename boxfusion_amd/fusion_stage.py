@@ -55,6 +55,7 @@ class FusionStage:
         self.last_pred = None
         self._stats = dict(keyframes=0, suppressed=0)
         self.K_dev = torch.from_numpy(self.K3).to(self.dev)     # uploaded once
+        self._pf_table = None    # append-only device table behind per_frame_ins
         # nms + correspondence association chained on the device (one host round trip);
         # False: the reference's two separate calls (same results)
         self.joint = os.environ.get("BF_JOINT_ASSOC", "1") != "0"
@@ -125,7 +126,7 @@ class FusionStage:
         n_before = len(self.all_pred_box)
         cur_global = self.all_pred_box
         all_pred_box = Instances3D.cat([self.all_pred_box, pred])
-        self.per_frame_ins = Instances3D.cat([self.per_frame_ins, pred])
+        self.per_frame_ins = self._per_frame_append(pred)
         all_poses = np.concatenate((self.all_poses, pose_np), axis=0)
         corners = all_pred_box.pred_boxes_3d.corners       # shared by both association steps
         if self.joint and len(all_pred_box) > 1:
@@ -169,6 +170,55 @@ class FusionStage:
             all_poses = all_poses[keep_idx]
             bm.update(keep_idx)
         self.all_pred_box, self.all_poses = all_pred_box, all_poses
+
+    def _per_frame_append(self, pred):
+        """per_frame_ins = cat(per_frame_ins, pred) on an append-only table: every field lives in a
+        preallocated device buffer (capacity doubling), the new rows are written into its tail by
+        one bf_rows_gather launch and per_frame_ins becomes views of the first n rows.  Rows never
+        change once written, so earlier views stay valid."""
+        cur = self.per_frame_ins
+        n, m = len(cur), len(pred)
+        specs = []   # (key, box_type or None, [tensors of cur], [tensors of pred])
+        for k, v in cur._fields.items():
+            w = pred._fields.get(k)
+            if isinstance(v, torch.Tensor) and isinstance(w, torch.Tensor) and v.is_cuda and \
+                    w.dtype == v.dtype and w.shape[1:] == v.shape[1:]:
+                specs.append((k, None, [v], [w]))
+            elif hasattr(v, "tensor") and hasattr(v, "R") and hasattr(w, "R") and v.tensor.is_cuda:
+                specs.append((k, type(v), [v.tensor, v.R], [w.tensor, w.R]))
+            else:
+                return Instances3D.cat([cur, pred])
+        if set(pred._fields) != set(cur._fields) or \
+                sum(len(t) for _, _, t, _ in specs) > _lib.ROWS_MAX_FIELDS:
+            return Instances3D.cat([cur, pred])
+        tab = self._pf_table
+        flat_cur = [t for _, _, ts, _ in specs for t in ts]
+        if tab is None or tab["n"] != n or tab["keys"] != [k for k, _, _, _ in specs] or \
+                any(t.data_ptr() != b.data_ptr() for t, b in zip(flat_cur, tab["bufs"])):
+            tab = None                                   # (re)build from the current rows
+        if tab is None or n + m > tab["cap"]:
+            cap = max(4096, 2 * (n + m))
+            bufs = [torch.empty((cap,) + t.shape[1:], dtype=t.dtype, device=t.device) for t in flat_cur]
+            if n:
+                _lib.rows_gather([(t.contiguous(), None) for t in flat_cur], n_out=n,
+                                 outs=[b[:n] for b in bufs])
+            tab = dict(cap=cap, bufs=bufs, keys=[k for k, _, _, _ in specs], n=n)
+        bufs = tab["bufs"]
+        flat_new = [t.contiguous() for _, _, _, ts in specs for t in ts]
+        if m:
+            _lib.rows_gather([(t, None) for t in flat_new], n_out=m, outs=[b[n:n + m] for b in bufs])
+        tab["n"] = n + m
+        ret = Instances3D(cur.image_size)
+        o = 0
+        for k, box_type, ts, _ in specs:
+            if box_type is None:
+                ret.set(k, bufs[o][:n + m])
+                o += 1
+            else:
+                ret.set(k, box_type._views(bufs[o][:n + m], bufs[o + 1][:n + m]))
+                o += 2
+        self._pf_table = tab
+        return ret
 
     def finish(self, count, pose, last_was_keyframe):
         """demo.py:200 `count == len(dataset) - 1` re-entry on a non-keyframe last frame."""
