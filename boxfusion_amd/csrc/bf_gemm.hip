@@ -855,6 +855,18 @@ static int g_force_small = 0;
 // test hook: 1 forces the 128x128 kernel for every shape (both kernels stay covered by tests)
 BF_API void bf_gemm_force_small_tiles(int on) { g_force_small = on; }
 
+static int g_balanced = -1;
+// persistent-grid sizing: 1 = balanced (ceil(tiles / rounds) workgroups), 0 = one per CU;
+// default from BF_GEMM_BALANCED (unset: 1)
+BF_API void bf_gemm_set_balanced(int on) { g_balanced = on ? 1 : 0; }
+static int gemm_balanced() {
+    if (g_balanced < 0) {
+        const char* e = getenv("BF_GEMM_BALANCED");
+        g_balanced = (e && e[0] == '0') ? 0 : 1;
+    }
+    return g_balanced;
+}
+
 static int g_cu_budget = 0;
 // CUs the GEMMs may assume (persistent grid size); 0 = every CU of the device.  Set it when the
 // launching stream is CU-masked (e.g. part of the chip is reserved for the fusion stream).
@@ -913,7 +925,17 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
     const long long t2 = (long long)t2m * t2n;
     const int n_cu = gemm_cu_count();
     if (vec_epi && gemm_use_large(M, N, K)) {
-        const int grid2 = (int)(t2 < n_cu ? t2 : n_cu);   // persistent: one workgroup per CU
+        int grid2 = (int)(t2 < n_cu ? t2 : n_cu);   // persistent: one workgroup per CU
+        if (gemm_balanced() && t2 > n_cu && t2 % n_cu >= n_cu / 4) {
+            // as many workgroups as the round count needs (every block walks the same number
+            // of tiles, +-1): the CUs a partial last round would leave idle at the end are free
+            // for the other streams' kernels from the start instead.  Only for a last round at
+            // least a quarter full: a nearly empty one costs little, and a full-width grid runs
+            // the same tiles ~5 % faster alone (measured on CLIP fc1, 2580 tiles)
+            const long long rounds = (t2 + n_cu - 1) / n_cu;
+            const int g = (int)(((t2 + rounds - 1) / rounds + 7) & ~7LL);
+            grid2 = g < n_cu ? g : n_cu;
+        }
 #define GEMM2(OB, AC) launch_gemm256<OB, AC>(grid2, bf_stream(stream), A, lda, W, ldw, bias, \
                                             resid, ldr, resid_mod, C, ldc, row_map, M, N, K, t2n, t2m)
         if (c_bf16) {

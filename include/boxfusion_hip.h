@@ -276,6 +276,12 @@ int bf_gemm_large_tiles(int M, int N, int K);
 /* Number of CUs the GEMM may assume (sizes the persistent grid); 0 = all CUs of the device.
  * Set when GEMMs launch on a CU-masked stream. */
 void bf_gemm_set_cu_budget(int n);
+/* Persistent-grid sizing of the 256x256 kernel: 1 (default; env BF_GEMM_BALANCED=0 turns it
+ * off) launches ceil(tiles / rounds) workgroups so every block walks the same tile count and a
+ * partial last round (when at least a quarter full) leaves its idle CUs to concurrent streams
+ * from the start; 0 = one per CU.
+ * Results are identical in value. */
+void bf_gemm_set_balanced(int on);
 
 /* softmax(Q K^T * scale) V per (batch, head); X(b,h,s,d) at X + b*x_bs + s*x_rs + h*D + d,
  * bf16 in/out, head_dim in {32, 64, 80, 128}.  Replaces vit.py Attention.forward (:170-203,
