@@ -4,6 +4,8 @@
 #   profiles/<r>_bench_under_rocprof.json                      the bench line of that same run
 #   profiles/<r>_pmc_gelu_gemm.json                            HBM bytes per launch of the roofline kernel
 #                                                              (FETCH_SIZE x2 + WRITE_SIZE, separate passes)
+#   profiles/<r>_roofline_kernel_stats.csv / _roofline_bench.json  eager single-stream run: the
+#                                                              bench timer's launches = the trace's
 #   profiles/<r>_bench_default.json / _breakdown.json          plain bench runs
 # usage: scripts/profile_round.sh r01
 set -o pipefail
@@ -22,6 +24,12 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/k
 cp "$(find /tmp/kt_$R -name '*kernel_stats.csv' | head -1)" $P/${R}_bench_kernel_stats.csv
 cp "$(find /tmp/kt_$R -name '*domain_stats.csv' | head -1)" $P/${R}_bench_domain_stats.csv
 grep '"metric"' gpurun_out/prof_$R/kt.log > $P/${R}_bench_under_rocprof.json
+echo "== roofline kernel trace (eager, one detect stream: every launch the bench's HIP-event timer sees)"
+rm -rf /tmp/rk_$R
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/rk_$R -o run -- \
+    python3 -u bench.py --eager --inflight 1 --steps 10 --warmup 1 --no-cpu-baseline > gpurun_out/prof_$R/rk.log 2>&1 || { tail -20 gpurun_out/prof_$R/rk.log; exit 1; }
+cp "$(find /tmp/rk_$R -name '*kernel_stats.csv' | head -1)" $P/${R}_roofline_kernel_stats.csv
+grep '"metric"' gpurun_out/prof_$R/rk.log > $P/${R}_roofline_bench.json
 fi
 
 for ctr in FETCH_SIZE WRITE_SIZE; do
