@@ -452,7 +452,7 @@ def main():
         }
         if args.breakdown:
             line["breakdown_ms_per_step"] = {k: 1e3 * v / args.steps for k, v in brk.items()}
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and N == 1:      # rank 0 at N=1 only (a reported baseline)
             line["cpu_baseline"] = cpu_baseline(cutr, clip_vis, args, scene)
         print(json.dumps(line), flush=True)
     if dist is not None:
