@@ -164,6 +164,9 @@ def gather_step(recs, feats, dist, world):
     collectives are asynchronous device operations: nothing here waits for the detect stream."""
     if dist is None or world == 1:
         return recs, feats
+    if recs.is_cuda and dist.get_backend() == "gloo":     # BF_BENCH_REHEARSE=1 (one-GPU rehearsal)
+        g_rec, g_feat = gather_step(recs.cpu(), feats.cpu(), dist, world)
+        return g_rec.to(recs.device), g_feat.to(feats.device)
     if recs.is_cuda:
         g_rec = torch.empty((world * recs.shape[0],) + recs.shape[1:], dtype=recs.dtype, device=recs.device)
         dist.all_gather_into_tensor(g_rec, recs.contiguous())
@@ -259,11 +262,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # BF_BENCH_REHEARSE=1: every rank on cuda:0 with gloo collectives -- a one-GPU rehearsal of the
+    # N>1 control flow (sharding, exchange, rank-0 fusion, max-over-ranks timing); not a measurement
+    rehearse = os.environ.get("BF_BENCH_REHEARSE", "0") == "1"
+    if rehearse:
+        local = 0
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     from boxfusion_amd import _lib
@@ -405,7 +416,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt], device="cpu" if rehearse else dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ks = timer.summary()
