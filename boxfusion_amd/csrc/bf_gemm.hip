@@ -15,6 +15,15 @@
 // land on the same XCD (shared L2).
 #include "bf_common.h"
 
+// k_gemm256p accumulator layout: 0 (default) = D[m][n] blocks; 1 = transposed (C^T = W A^T on the
+// MFMA: 16-B residual loads, one ds_write_b128 per block in the epilogue, bias + activation after
+// the LDS transpose).  Both pass the same tests; measured on one box the transposed form was no
+// faster (CLIP proj 167.6 vs 165.0 us, bench 130.1 vs 131.2 frames/s): the residual's cost is the
+// lock-step burst at tile boundaries, not the load instruction count.  Kept as a variant.
+#ifndef GEMM_TACC
+#define GEMM_TACC 0
+#endif
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -619,6 +628,26 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
     // start from the residual tile (loaded with 64-B row segments per 16 lanes), so the epilogue
     // has no loads queued behind its own stores.
     const bool acc_init = resid != nullptr && row_map == nullptr && resid_mod <= 0;
+#if GEMM_TACC
+    // transposed accumulators: lane (lr, lq) of block (i, j) holds row m = i*16 + lr, columns
+    // n = j*16 + 4*lq + [0,4) -- one 16-B load per block (N % 4 == 0 for residual GEMMs)
+#define ACC_INIT(m0_, n0_)                                                                         \
+    {                                                                                              \
+        if (acc_init) {                                                                            \
+            _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                       \
+                const float* rp_ = resid + (size_t)min((m0_) + wr * 128 + i * 16 + lr, M - 1) * ldr; \
+                _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                    \
+                    const float4 x_ = *reinterpret_cast<const float4*>(                             \
+                        rp_ + min((n0_) + wc * 64 + j * 16 + 4 * lq, N - 4));                      \
+                    acc[i][j][0] = x_.x; acc[i][j][1] = x_.y; acc[i][j][2] = x_.z; acc[i][j][3] = x_.w; \
+                }                                                                                  \
+            }                                                                                      \
+        } else {                                                                                   \
+            _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 4; ++j) \
+                _Pragma("unroll") for (int e = 0; e < 4; ++e) acc[i][j][e] = 0.f;                  \
+        }                                                                                          \
+    }
+#else
 #define ACC_INIT(m0_, n0_)                                                                         \
     {                                                                                              \
         if (acc_init) {                                                                            \
@@ -632,6 +661,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
                 _Pragma("unroll") for (int e = 0; e < 4; ++e) acc[i][j][e] = 0.f;                  \
         }                                                                                          \
     }
+#endif
 
     bf16x8 fa[8], fb0[4], fb1[4];     // fa: A-half fragments [i*2 + ks]; fb*: [j*2 + ks]
 #define RD_A(stage, mi)                                                                            \
@@ -642,13 +672,17 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
     _Pragma("unroll") for (int j = 0; j < 2; ++j) _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) \
         FB[j * 2 + ks] = *reinterpret_cast<const bf16x8*>(                                         \
             g_smem + (stage) * 65536 + 32768 + (ni) * 16384 + swz(wc * 32 + j * 16 + lr, ks * 4 + lq));
+#if GEMM_TACC
+#define MFMA_OP(FA, FB, C) __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB, FA, C, 0, 0, 0)   // C^T += W A^T
+#else
+#define MFMA_OP(FA, FB, C) __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA, FB, C, 0, 0, 0)
+#endif
 #define MFMA_Q(mi, ni, FB)                                                                         \
     {                                                                                              \
         __builtin_amdgcn_s_setprio(1);                                                             \
         _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i) \
             _Pragma("unroll") for (int j = 0; j < 2; ++j) acc[(mi) * 4 + i][(ni) * 2 + j] =        \
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i * 2 + ks], FB[j * 2 + ks],            \
-                                                        acc[(mi) * 4 + i][(ni) * 2 + j], 0, 0, 0); \
+                MFMA_OP(fa[i * 2 + ks], FB[j * 2 + ks], acc[(mi) * 4 + i][(ni) * 2 + j]);           \
         __builtin_amdgcn_s_setprio(0);                                                             \
     }
 
@@ -674,15 +708,29 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
     constexpr int CW = OUT_BF16 ? 8 : 4;
     constexpr int NIT = 16 * (64 / CW) / 64;      // 16-B stores per lane per 16-row pass
     int stores_pending = 0;   // stores of a full-tile epilogue issued after K-tile g+1's halves
+#if GEMM_TACC
+    // the epilogue adds the bias after the LDS transpose: a lane's CW output columns are fixed
+    const int cl_lane = (lane % (64 / CW)) * CW;
+    float bv[CW];
+#else
     float bv[4];
+#endif
     for (int g = 0; g < total; ++g) {
         const int st = g & 1;
         if (kc.k0 == 0) {     // first K-tile of a tile: its bias columns (loaded well before use)
+#if GEMM_TACC
+#pragma unroll
+            for (int q = 0; q < CW; ++q) {
+                const int n = kc.n0 + wc * 64 + cl_lane + q;
+                bv[q] = bias ? bias[min(n, N - 1)] : 0.f;
+            }
+#else
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int n = kc.n0 + wc * 64 + j * 16 + lr;
                 bv[j] = bias ? bias[min(n, N - 1)] : 0.f;
             }
+#endif
         }
         // ---- P1: quadrant (0,0); reads B0 (retired before the barrier) then A0
         RD_B(fb0, st, 0);
@@ -745,6 +793,14 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
                           n0 + 64 <= N && ablate == 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
+#if GEMM_TACC
+            // row lr of the pass, 16-B slot (4j + lq) ^ lr: the 16 lanes of a write group and
+            // the lanes of a read group hit 16 distinct slots of the 256-B bank row
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                *reinterpret_cast<float4*>(scratch + lr * 64 + (((4 * j + lq) ^ lr) << 2)) =
+                    make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+#else
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 f32x2 v01 = {acc[i][j][0] + bv[j], acc[i][j][1] + bv[j]};
@@ -761,19 +817,36 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
                 scratch[(rl + 2) * 64 + col] = v23.x;
                 scratch[(rl + 3) * 64 + col] = v23.y;
             }
+#endif
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
             for (int it = 0; it < NIT; ++it) {
                 const int id = it * 64 + lane;
                 const int rl = id / (64 / CW), cl = (id % (64 / CW)) * CW;
                 const int m = m0 + i * 16 + rl, n = n0 + cl;
-                const int sw = ((rl >> 2) & 3) << 4;
                 float v[CW];
+#if GEMM_TACC
+#pragma unroll
+                for (int q = 0; q < CW; q += 4) {
+                    const float4 x = *reinterpret_cast<const float4*>(
+                        scratch + rl * 64 + ((((cl + q) >> 2) ^ rl) << 2));
+                    v[q] = x.x; v[q + 1] = x.y; v[q + 2] = x.z; v[q + 3] = x.w;
+                }
+#pragma unroll
+                for (int q = 0; q < CW; q += 2) {
+                    f32x2 p = {v[q] + bv[q], v[q + 1] + bv[q + 1]};
+                    if (ACT == 1) p = gelu_erf2(p);
+                    else if (ACT == 2) { p.x = fmaxf(p.x, 0.f); p.y = fmaxf(p.y, 0.f); }
+                    v[q] = p.x; v[q + 1] = p.y;
+                }
+#else
+                const int sw = ((rl >> 2) & 3) << 4;
 #pragma unroll
                 for (int q = 0; q < CW; q += 4) {
                     const float4 x = *reinterpret_cast<const float4*>(scratch + rl * 64 + ((cl + q) ^ sw));
                     v[q] = x.x; v[q + 1] = x.y; v[q + 2] = x.z; v[q + 3] = x.w;
                 }
+#endif
                 int orow = m;
                 bool keep = true;
                 if (ablate == 2) {   // diagnostic: no global stores
@@ -819,6 +892,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
 #undef RD_A
 #undef RD_B
 #undef MFMA_Q
+#undef MFMA_OP
 #undef STAGE_HALF
 #undef ACC_INIT
 }
