@@ -542,6 +542,35 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict
 #define SB0() __builtin_amdgcn_sched_barrier(0)
 #define PHASE_BARRIER() do { SB0(); CBAR(); __builtin_amdgcn_s_barrier(); CBAR(); SB0(); } while (0)
 
+// k_gemm256p output stores and residual loads, optionally nontemporal (streamed past L2 so the
+// bursts at tile boundaries do not evict the operand panels).  GEMM_NT bits: 1 = bf16 output
+// stores, 2 = f32 output stores, 4 = residual loads.  Default 3 (measured on one box, same run:
+// CLIP fc1 546.8 -> 524.2 us, qkv 295.4 -> 286.5, proj 164.9 -> 151.3, fc2 439.7 -> 429.4, CuTR
+// fc1 164.8 -> 155.3; bench 132.4-132.6 -> 133.6-133.8 frames/s).  Nontemporal residual loads
+// (bit 4) were slower on the residual GEMMs (CuTR global proj 39.5 -> 47.9 us).
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+#ifndef GEMM_NT
+#define GEMM_NT 3
+#endif
+#if GEMM_NT & 4
+#define GEMM_LD_F(p) __builtin_nontemporal_load(p)
+#define GEMM_LD_F4(p) __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(p))
+#else
+#define GEMM_LD_F(p) (*(p))
+#define GEMM_LD_F4(p) (*reinterpret_cast<const f32x4v*>(p))
+#endif
+#if GEMM_NT & 2
+#define GEMM_ST_F4(p, a, b, c, d) __builtin_nontemporal_store((f32x4v){a, b, c, d}, reinterpret_cast<f32x4v*>(p))
+#else
+#define GEMM_ST_F4(p, a, b, c, d) (*reinterpret_cast<f32x4v*>(p) = (f32x4v){a, b, c, d})
+#endif
+#if GEMM_NT & 1
+#define GEMM_ST_U4(p, o) __builtin_nontemporal_store((u32x4v){(o).x, (o).y, (o).z, (o).w}, reinterpret_cast<u32x4v*>(p))
+#else
+#define GEMM_ST_U4(p, o) (*reinterpret_cast<U128*>(p) = (o))
+#endif
+
 template <bool OUT_BF16, int ACT>
 __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restrict__ A, int lda,
                                                             const u16* __restrict__ W, int ldw,
@@ -637,8 +666,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
             _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                       \
                 const float* rp_ = resid + (size_t)min((m0_) + wr * 128 + i * 16 + lr, M - 1) * ldr; \
                 _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                    \
-                    const float4 x_ = *reinterpret_cast<const float4*>(                             \
-                        rp_ + min((n0_) + wc * 64 + j * 16 + 4 * lq, N - 4));                      \
+                    const f32x4v x_ = GEMM_LD_F4(rp_ + min((n0_) + wc * 64 + j * 16 + 4 * lq, N - 4)); \
                     acc[i][j][0] = x_.x; acc[i][j][1] = x_.y; acc[i][j][2] = x_.z; acc[i][j][3] = x_.w; \
                 }                                                                                  \
             }                                                                                      \
@@ -654,7 +682,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
             _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int e = 0; e < 4; ++e) { \
                 const float* rp_ = resid + (size_t)min((m0_) + wr * 128 + i * 16 + 4 * lq + e, M - 1) * ldr; \
                 _Pragma("unroll") for (int j = 0; j < 4; ++j)                                      \
-                    acc[i][j][e] = rp_[min((n0_) + wc * 64 + j * 16 + lr, N - 1)];                 \
+                    acc[i][j][e] = GEMM_LD_F(rp_ + min((n0_) + wc * 64 + j * 16 + lr, N - 1));      \
             }                                                                                      \
         } else {                                                                                   \
             _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 4; ++j) \
@@ -874,10 +902,9 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
                         o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
                         o.z = (uint32_t)f2bf(v[4 % CW]) | ((uint32_t)f2bf(v[5 % CW]) << 16);
                         o.w = (uint32_t)f2bf(v[6 % CW]) | ((uint32_t)f2bf(v[7 % CW]) << 16);
-                        *reinterpret_cast<U128*>(reinterpret_cast<u16*>(Cv) + (size_t)orow * ldc + n) = o;
+                        GEMM_ST_U4(reinterpret_cast<u16*>(Cv) + (size_t)orow * ldc + n, o);
                     } else {
-                        *reinterpret_cast<float4*>(reinterpret_cast<float*>(Cv) + (size_t)orow * ldc + n) =
-                            make_float4(v[0], v[1], v[2], v[3]);
+                        GEMM_ST_F4(reinterpret_cast<float*>(Cv) + (size_t)orow * ldc + n, v[0], v[1], v[2], v[3]);
                     }
                 }
             }
