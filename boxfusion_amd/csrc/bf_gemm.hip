@@ -926,7 +926,12 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
 
 static int g_gemm_variant = 1;   // 0: k_gemm256, 1: k_gemm256p (staggered 4-phase schedule), 2: k_gemm256p unstaggered
 BF_API void bf_gemm_set_variant(int v) { g_gemm_variant = v; }
-static int g_group_m = 8;        // row panels per tile group (tile_coords); 1 = row-major
+// row panels per tile group (tile_coords); 1 = row-major.  Default 8, env BF_GEMM_GROUP_M.
+static int g_group_m = [] {
+    const char* e = getenv("BF_GEMM_GROUP_M");
+    const int g = e ? atoi(e) : 0;
+    return g > 0 ? g : 8;
+}();
 BF_API void bf_gemm_set_group_m(int g) { g_group_m = g; }
 
 template <bool OB, int AC>
