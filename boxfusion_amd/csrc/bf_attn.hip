@@ -617,7 +617,12 @@ static void launch_attn_r(dim3 grid, hipStream_t st, const void* q, const void* 
                        k_bs, v_bs, o_bs, sl2);
 }
 
-static int g_attn_variant = 1;   // 1/2: k_attn_s, 3: k_attn_r for short sequences, 0: k_attn
+// 1/2: k_attn_s, 3: k_attn_r for short sequences, 4/5: k_attn_s with 5/3 waves per workgroup for
+// short sequences, 0: k_attn.  Default 1, env BF_ATTN_VARIANT.
+static int g_attn_variant = [] {
+    const char* e = getenv("BF_ATTN_VARIANT");
+    return e ? atoi(e) : 1;
+}();
 BF_API void bf_attention_set_variant(int v) { g_attn_variant = v; }
 
 BF_API int bf_attention_bf16(const void* q, const void* k, const void* v, void* o, int batch,
@@ -649,7 +654,12 @@ BF_API int bf_attention_bf16(const void* q, const void* k, const void* v, void* 
                        dim3(NWV * 64), 0, bf_stream(stream), (const u16*)q, (const u16*)k,          \
                        (const u16*)v, (u16*)o, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs,    \
                        o_bs, sl2)
-#define LAUNCH_SD(DD) if (nw_one > 4 && nw_one <= 9) { LAUNCH_S(DD, 9); } else { LAUNCH_S(DD, 4); }
+#define LAUNCH_SD(DD)                                                                             \
+    if (nw_one > 4 && nw_one <= 9) {                                                              \
+        if (g_attn_variant == 4) { LAUNCH_S(DD, 5); }                                             \
+        else if (g_attn_variant == 5) { LAUNCH_S(DD, 3); }                                        \
+        else { LAUNCH_S(DD, 9); }                                                                 \
+    } else { LAUNCH_S(DD, 4); }
         switch (head_dim) {
             case 32: LAUNCH_SD(32); break;
             case 64: LAUNCH_SD(64); break;
