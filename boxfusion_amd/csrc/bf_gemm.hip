@@ -47,41 +47,45 @@ __device__ __forceinline__ u16 f2bf(float f) {
 
 // nn.GELU (erf form).  erf by Abramowitz-Stegun 7.1.26 (|error| <= 1.5e-7, far below the bf16
 // output rounding): one v_rcp, one v_exp and a handful of FMAs instead of the library erff.
-__device__ __forceinline__ float erf_as(float x) {
+// With z = x/sqrt(2) and erf(|z|) = 1 - P(t) e^{-z^2}:
+//   GELU(x) = relu(x) - 0.5 |x| P(t) e^{-x^2/2},   t = 1 / (1 + p |x| / sqrt(2))
+// (constants folded; no 1 - (1 - small) cancellation for negative x).
+__device__ __forceinline__ float gelu_erf(float x) {
     const float a = fabsf(x);
-    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.0f));   // v_rcp_f32 (1 ulp)
-    float p = fmaf(1.061405429f, t, -1.453152027f);
-    p = fmaf(p, t, 1.421413741f);
-    p = fmaf(p, t, -0.284496736f);
-    p = fmaf(p, t, 0.254829592f);
-    const float y = 1.0f - p * t * __builtin_amdgcn_exp2f(-a * a * 1.4426950408889634f);
-    return copysignf(y, x);
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, a, 1.0f));
+    float p = fmaf(0.5f * 1.061405429f, t, 0.5f * -1.453152027f);
+    p = fmaf(p, t, 0.5f * 1.421413741f);
+    p = fmaf(p, t, 0.5f * -0.284496736f);
+    p = fmaf(p, t, 0.5f * 0.254829592f);
+    const float e = __builtin_amdgcn_exp2f(a * -0.72134752044448170f * a);
+    return fmaxf(x, 0.f) - a * (p * t) * e;
 }
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_as(x * 0.70710678118654752f)); }
 
 // the same GELU on two values with packed f32 VALU ops (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32
-// on gfx950): identical arithmetic per component, half the issue slots in the epilogue
+// on gfx950), rearranged: with z = x/sqrt(2) and erf(|z|) = 1 - P(t) e^{-z^2} (A&S 7.1.26),
+//   GELU(x) = 0.5 x (1 + erf(z)) = relu(x) - 0.5 |x| P(t) e^{-x^2/2},   t = 1 / (1 + p |x| / sqrt(2))
+// (the 1/sqrt(2), the 0.5 and log2(e) folded into the constants).  18 VALU + 4 transcendental
+// instructions per pair instead of 22 + 4, and no 1 - (1 - small) cancellation for negative x.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
-    const f32x2 z = x * 0.70710678118654752f;
-    const f32x2 a = __builtin_elementwise_abs(z);
-    const f32x2 d = 0.3275911f * a + 1.0f;
+    const f32x2 ax = __builtin_elementwise_abs(x);
+    const f32x2 d = (0.3275911f * 0.70710678118654752f) * ax + 1.0f;
     f32x2 tt;
     tt.x = __builtin_amdgcn_rcpf(d.x);
     tt.y = __builtin_amdgcn_rcpf(d.y);
-    f32x2 p = 1.061405429f * tt - 1.453152027f;
-    p = p * tt + 1.421413741f;
-    p = p * tt - 0.284496736f;
-    p = p * tt + 0.254829592f;
-    const f32x2 q = -a * a * 1.4426950408889634f;
+    f32x2 p = (0.5f * 1.061405429f) * tt + (0.5f * -1.453152027f);     // 0.5 P(t) / t
+    p = p * tt + (0.5f * 1.421413741f);
+    p = p * tt + (0.5f * -0.284496736f);
+    p = p * tt + (0.5f * 0.254829592f);
+    const f32x2 q = (ax * -0.72134752044448170f) * ax;                 // -x^2/2 * log2(e)
     f32x2 ex;
     ex.x = __builtin_amdgcn_exp2f(q.x);
     ex.y = __builtin_amdgcn_exp2f(q.y);
-    const f32x2 y = 1.0f - p * tt * ex;
-    f32x2 er;
-    er.x = copysignf(y.x, z.x);
-    er.y = copysignf(y.y, z.y);
-    return 0.5f * x * (1.0f + er);
+    const f32x2 m = ax * (p * tt) * ex;
+    f32x2 r;
+    r.x = fmaxf(x.x, 0.f);
+    r.y = fmaxf(x.y, 0.f);
+    return r - m;
 }
 
 // byte offset of 16-B chunk `c` (0..7) of row `r` in a [rows][64 bf16] swizzled tile
