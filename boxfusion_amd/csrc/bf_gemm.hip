@@ -88,6 +88,32 @@ __device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
     return r - m;
 }
 
+// two packed pairs at once: the four v_rcp and the four v_exp issue back to back, so their
+// results are not consumed right behind them (fewer trans-use hazard wait states)
+__device__ __forceinline__ void gelu_erf2x2(f32x2& x0, f32x2& x1) {
+    const f32x2 a0 = __builtin_elementwise_abs(x0), a1 = __builtin_elementwise_abs(x1);
+    const f32x2 d0 = (0.3275911f * 0.70710678118654752f) * a0 + 1.0f;
+    const f32x2 d1 = (0.3275911f * 0.70710678118654752f) * a1 + 1.0f;
+    const f32x2 q0 = (a0 * -0.72134752044448170f) * a0;
+    const f32x2 q1 = (a1 * -0.72134752044448170f) * a1;
+    f32x2 t0, t1, e0, e1;
+    t0.x = __builtin_amdgcn_rcpf(d0.x); t0.y = __builtin_amdgcn_rcpf(d0.y);
+    t1.x = __builtin_amdgcn_rcpf(d1.x); t1.y = __builtin_amdgcn_rcpf(d1.y);
+    e0.x = __builtin_amdgcn_exp2f(q0.x); e0.y = __builtin_amdgcn_exp2f(q0.y);
+    e1.x = __builtin_amdgcn_exp2f(q1.x); e1.y = __builtin_amdgcn_exp2f(q1.y);
+    f32x2 p0 = (0.5f * 1.061405429f) * t0 + (0.5f * -1.453152027f);
+    f32x2 p1 = (0.5f * 1.061405429f) * t1 + (0.5f * -1.453152027f);
+    p0 = p0 * t0 + (0.5f * 1.421413741f);      p1 = p1 * t1 + (0.5f * 1.421413741f);
+    p0 = p0 * t0 + (0.5f * -0.284496736f);     p1 = p1 * t1 + (0.5f * -0.284496736f);
+    p0 = p0 * t0 + (0.5f * 0.254829592f);      p1 = p1 * t1 + (0.5f * 0.254829592f);
+    const f32x2 m0 = a0 * (p0 * t0) * e0, m1 = a1 * (p1 * t1) * e1;
+    f32x2 r0, r1;
+    r0.x = fmaxf(x0.x, 0.f); r0.y = fmaxf(x0.y, 0.f);
+    r1.x = fmaxf(x1.x, 0.f); r1.y = fmaxf(x1.y, 0.f);
+    x0 = r0 - m0;
+    x1 = r1 - m1;
+}
+
 // byte offset of 16-B chunk `c` (0..7) of row `r` in a [rows][64 bf16] swizzled tile
 // Two 128-B tile rows share one 256-B LDS bank row, so the XOR key is (r >> 1) & 7: the 16 rows
 // of every ds_read_b128 lane group ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...) then hit 16
@@ -459,7 +485,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict
             for (int j = 0; j < 4; ++j) {
                 f32x2 v01 = {acc[i][j][0] + bv[j], acc[i][j][1] + bv[j]};
                 f32x2 v23 = {acc[i][j][2] + bv[j], acc[i][j][3] + bv[j]};
-                if (ACT == 1) { v01 = gelu_erf2(v01); v23 = gelu_erf2(v23); }
+                if (ACT == 1) gelu_erf2x2(v01, v23);
                 else if (ACT == 2) {
                     v01.x = fmaxf(v01.x, 0.f); v01.y = fmaxf(v01.y, 0.f);
                     v23.x = fmaxf(v23.x, 0.f); v23.y = fmaxf(v23.y, 0.f);
@@ -837,7 +863,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
             for (int j = 0; j < 4; ++j) {
                 f32x2 v01 = {acc[i][j][0] + bv[j], acc[i][j][1] + bv[j]};
                 f32x2 v23 = {acc[i][j][2] + bv[j], acc[i][j][3] + bv[j]};
-                if (ACT == 1) { v01 = gelu_erf2(v01); v23 = gelu_erf2(v23); }
+                if (ACT == 1) gelu_erf2x2(v01, v23);
                 else if (ACT == 2) {
                     v01.x = fmaxf(v01.x, 0.f); v01.y = fmaxf(v01.y, 0.f);
                     v23.x = fmaxf(v23.x, 0.f); v23.y = fmaxf(v23.y, 0.f);
