@@ -213,3 +213,37 @@ def test_crop_resize_im2col(L):
     empty = ((0 - torch.tensor(mean, device="cuda")) / torch.tensor(std, device="cuda"))
     empty = empty.repeat_interleave(196).bfloat16().float()[None]
     assert torch.all(out[3 * 256:, :588].float() == empty)
+
+
+@pytest.mark.parametrize("act,use_resid", [("gelu", False), (None, True)])
+def test_gemm_balanced_grid(L, act, use_resid):
+    """360 tiles of 256x256 (a last round 104/256 full) launch the balanced persistent grid
+    (bf_gemm_set_balanced): every tile is computed the same way whichever workgroup walks it, so
+    the output is bit-identical to the one-block-per-CU grid, and matches the fp32 reference"""
+    from boxfusion_amd._lib import lib
+    g = torch.Generator(device="cuda").manual_seed(23)
+    M, N, K = 10000, 2304, 128
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g)
+    resid = torch.randn(M, N, device="cuda", generator=g) if use_resid else None
+    outs = []
+    try:
+        for bal in (1, 0):
+            lib().bf_gemm_set_balanced(bal)
+            if use_resid:
+                o = resid.clone()
+                L.gemm(a, w, b, resid=o, out=o)
+            else:
+                o = L.gemm(a, w, b, act=act, out_dtype=torch.bfloat16)
+            torch.cuda.synchronize()
+            outs.append(o)
+    finally:
+        lib().bf_gemm_set_balanced(1)
+    assert torch.equal(outs[0], outs[1])
+    y = a.float() @ w.float().T + b
+    if act == "gelu":
+        y = F.gelu(y)
+    if use_resid:
+        y = y + resid
+    assert rel_err(outs[0], y) < (5e-3 if not use_resid else 1e-5)
