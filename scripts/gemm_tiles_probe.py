@@ -10,7 +10,9 @@ from gemm_bench import bench  # noqa: F401  (re-used timing helper)
 
 L = _lib.lib()
 dev = torch.device("cuda")
-extra = [("cutr_proj", 25600, 768, 768, None, False, True), ("cutr_qkv_glb", 25600, 2304, 768, None, True, False)]
+extra = [("cutr_proj", 25600, 768, 768, None, False, True), ("cutr_qkv_glb", 25600, 2304, 768, None, True, False),
+         ("cutr_g_qkv", 12800, 2304, 768, None, True, False), ("cutr_g_proj", 12800, 768, 768, None, False, True),
+         ("cutr_g_fc1", 12800, 3072, 768, "gelu", True, False), ("cutr_g_fc2", 12800, 768, 3072, None, False, True)]
 for name, M, N, K, act, ob, use_resid in SHAPES + extra:
     if not name.startswith("cutr"):
         continue
