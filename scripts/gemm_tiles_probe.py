@@ -14,7 +14,7 @@ extra = [("cutr_proj", 25600, 768, 768, None, False, True), ("cutr_qkv_glb", 256
          ("cutr_g_qkv", 12800, 2304, 768, None, True, False), ("cutr_g_proj", 12800, 768, 768, None, False, True),
          ("cutr_g_fc1", 12800, 3072, 768, "gelu", True, False), ("cutr_g_fc2", 12800, 768, 3072, None, False, True)]
 for name, M, N, K, act, ob, use_resid in SHAPES + extra:
-    if not name.startswith("cutr"):
+    if not name.startswith(("cutr", "clip")):
         continue
     a = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16()
     w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).bfloat16()
