@@ -994,11 +994,11 @@ BF_API void bf_gemm_force_small_tiles(int on) { g_force_small = on; }
 static int g_balanced = -1;
 // persistent-grid sizing: 1 = balanced (ceil(tiles / rounds) workgroups), 0 = one per CU;
 // default from BF_GEMM_BALANCED (unset: 1)
-BF_API void bf_gemm_set_balanced(int on) { g_balanced = on ? 1 : 0; }
+BF_API void bf_gemm_set_balanced(int on) { g_balanced = on == 2 ? 2 : on ? 1 : 0; }
 static int gemm_balanced() {
     if (g_balanced < 0) {
         const char* e = getenv("BF_GEMM_BALANCED");
-        g_balanced = (e && e[0] == '0') ? 0 : 1;
+        g_balanced = (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
     }
     return g_balanced;
 }
@@ -1062,7 +1062,7 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
     const int n_cu = gemm_cu_count();
     if (vec_epi && gemm_use_large(M, N, K)) {
         int grid2 = (int)(t2 < n_cu ? t2 : n_cu);   // persistent: one workgroup per CU
-        if (gemm_balanced() && t2 > n_cu && t2 % n_cu >= n_cu / 4) {
+        if (gemm_balanced() && t2 > n_cu && (gemm_balanced() == 2 || t2 % n_cu >= n_cu / 4)) {
             // as many workgroups as the round count needs (every block walks the same number
             // of tiles, +-1): the CUs a partial last round would leave idle at the end are free
             // for the other streams' kernels from the start instead.  Only for a last round at

@@ -279,7 +279,8 @@ void bf_gemm_set_cu_budget(int n);
 /* Persistent-grid sizing of the 256x256 kernel: 1 (default; env BF_GEMM_BALANCED=0 turns it
  * off) launches ceil(tiles / rounds) workgroups so every block walks the same tile count and a
  * partial last round (when at least a quarter full) leaves its idle CUs to concurrent streams
- * from the start; 0 = one per CU.
+ * from the start; 2 = balanced for every multi-round problem (measured: same bench, CLIP fc1
+ * slower alone); 0 = one per CU.
  * Results are identical in value. */
 void bf_gemm_set_balanced(int on);
 
