@@ -207,7 +207,10 @@ class CLIPEngine:
         M = max_crops * self.S
         bf16, f32 = dict(dtype=torch.bfloat16, device=dev), dict(dtype=torch.float32, device=dev)
         self.A = torch.empty((max_crops * self.np, self.KPAD), **bf16)
-        self.P = torch.empty((max_crops * self.np, W), **f32)
+        # patch row (crop n, patch p) -> token row n*S + 1 + p of X: the patch GEMM writes the
+        # token rows directly and adds the positional embedding in its epilogue
+        self.stem_map = (torch.arange(max_crops, dtype=torch.int32, device=dev)[:, None] * self.S + 1
+                         + torch.arange(self.np, dtype=torch.int32, device=dev)[None]).reshape(-1)
         self.X = torch.empty((M, W), **f32)
         self.LN = torch.empty((M, W), **bf16)
         self.QKV = torch.empty((M, 3 * W), **bf16)
@@ -226,10 +229,10 @@ class CLIPEngine:
         A = self.A[: N * npch]
         _lib.crop_resize_im2col(frames_u8, boxes_i32, frame_idx_i32, self.visual.image_size,
                                 self.visual.patch_size, CLIP_MEAN, CLIP_STD, self.KPAD, out=A)
-        P = _lib.gemm(A, self.patch_w, out=self.P[: N * npch], out_dtype=torch.float32)
         X = self.X[: N * S]
         X3 = X.view(N, S, W)
-        X3[:, 1:] = P.view(N, npch, W) + self.pos[1:]
+        _lib.gemm(A, self.patch_w, resid=self.pos[1:], resid_mod=npch, out=X,
+                  row_map=self.stem_map[: N * npch])
         X3[:, 0] = self.cls + self.pos[0]
         X.copy_(F.layer_norm(X, (W,), self.visual.ln_pre.weight, self.visual.ln_pre.bias,
                              self.visual.ln_pre.eps))
