@@ -4,16 +4,25 @@
 Workload (BASELINE.json configs[2]): synthetic 640x480 RGB-D stream, batch 8 frames
 per step per GPU, every frame a keyframe (gap=1, the per-frame-detect roofline run):
   per frame  depth standardisation + back-projection, CuTR RGB-D ViT-B (dim 768) forward,
-             detection filters, CLIP ViT-H/14 on the top-16 boxes (16 crops/frame), text match
-             against the 473-class vocabulary;
-  per step   all-gather (RCCL) of every rank's per-frame records (scene detections + CLIP
-             features) -> rank 0 runs the fusion state machine (NMS + association + box fusion)
-             over all gathered frames in global frame order.
-Weights are random (no checkpoint offline); the detections feeding fusion come from the seeded
-30-object scene generator (boxfusion_amd/synthetic.py), since random-weight CuTR boxes are noise.
+             detection filters, CLIP ViT-H/14 on the 16 highest-scoring detections of the frame
+             (16 crops/frame), text match against the 473-class vocabulary;
+  per step   all-gather (RCCL) of every rank's per-frame records (detections + camera pose) and
+             CLIP rows (features, best similarity, class) -> rank 0 runs the fusion state machine
+             (NMS + association + box fusion) over all gathered frames in global frame order; the
+             CLIP features ride on the detections through fusion (demo.py:167-171) and the
+             similarity raises their scores by clip_sim_coeff*sim/100.
+Weights are random (no checkpoint offline); the detections come from the seeded 30-object scene
+generator (boxfusion_amd/synthetic.py), since random-weight CuTR boxes are noise.  With random
+CLIP weights every crop would fall below class_sim_thres, so the "" category filter of
+demo.py:171 is not applied (the match itself runs).
 Inputs (frames, scene detections) are resident in HBM before the timed region.
 
-  python bench.py [--gpus N --steps K --warmup W]      (N>1 under torch.distributed.run)
+  python bench.py [--gpus N --steps K --warmup W]
+With --gpus N > 1 and no torch.distributed environment the script starts
+`python -m torch.distributed.run --nproc-per-node N` on itself as a child process (before anything
+touches the GPU) and exits with its status; under torch.distributed.run each rank checks
+WORLD_SIZE == N.  `--cpu-rehearsal` runs the same launch / sharding / all-gather / max-over-ranks
+control flow on CPU with gloo and no kernels (a test harness, not a measurement).
 """
 from __future__ import annotations
 
@@ -47,9 +56,10 @@ CFG = dict(
 )
 REC_ROWS, REC_W = 64, 22     # per-frame detection record: rows x (score, xyxy, xyzlhw, R, proj_xy)
 REC_HEAD = 17                # record head: detection count, camera pose (4x4)
+CLIP_W = 1026                # per-crop CLIP row: feature[1024], best similarity, class index
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=125, help="timed steps (125 x 8 = 1000 frames)")
@@ -80,7 +90,27 @@ def parse():
                         "reserved for rank 0's fusion at N > 1 the two detect streams run on the "
                         "other 224)")
     p.add_argument("--cpu-fusion-frames", type=int, default=24)
-    return p.parse_args()
+    p.add_argument("--cpu-rehearsal", action="store_true",
+                   help="CPU/gloo rehearsal of the N-rank control flow (no kernels; test harness)")
+    return p.parse_args(argv)
+
+
+def launch_ranks(argv, n):
+    """--gpus N > 1 without a torch.distributed environment: run this script under
+    torch.distributed.run as a child process (one rank per GPU, rendezvous on 127.0.0.1) and
+    return its exit status.  Nothing here touches the GPU (no exec from a GPU-initialised
+    process)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    return subprocess.run(cmd, env=env).returncode
 
 
 # ------------------------------------------------------------------------------------------------
@@ -98,13 +128,21 @@ def gen_frames(frame_ids, dev):
     return rgb, depth
 
 
+def sorted_dets(d):
+    """a frame's detections in descending score order, the order CuTR emits them
+    (cubify_transformer.py:945-978: top-k over the sigmoid scores)"""
+    o = np.argsort(-d["scores"], kind="stable")
+    return {k: v[o] for k, v in d.items()}
+
+
 def pack_records(dets, poses):
     """scene detections + camera poses of a batch of frames -> f32 [b, REC_HEAD + REC_ROWS*REC_W]
-    records: (count, pose 4x4, rows).  The pose and count travel with the detections, so the
-    exchange is one device all-gather (no host-object collective, which would synchronise the
-    detect stream every step)."""
+    records: (count, pose 4x4, rows in descending score order).  The pose and count travel with
+    the detections, so the exchange is one device all-gather (no host-object collective, which
+    would synchronise the detect stream every step)."""
     out = np.zeros((len(dets), REC_HEAD + REC_ROWS * REC_W), np.float32)
     for j, d in enumerate(dets):
+        d = sorted_dets(d)
         n = min(len(d["scores"]), REC_ROWS)
         rows = np.concatenate([d["scores"][:n, None], d["pred_boxes"][:n], d["xyzlhw"][:n],
                                d["R"][:n].reshape(n, 9), d["proj_xy"][:n]], 1)
@@ -112,6 +150,23 @@ def pack_records(dets, poses):
         out[j, 1:REC_HEAD] = np.asarray(poses[j], np.float32).reshape(-1)
         out[j, REC_HEAD:REC_HEAD + n * REC_W] = rows.reshape(-1)
     return out
+
+
+def crop_boxes(dets, crops):
+    """f32 [b*crops, 4]: the 2-D boxes of each frame's `crops` highest-scoring detections (the
+    CLIP inputs; a frame with fewer repeats its last box, an empty frame gets zero-size boxes)"""
+    out = np.zeros((len(dets), crops, 4), np.float32)
+    for j, d in enumerate(dets):
+        b = sorted_dets(d)["pred_boxes"][:crops]
+        if len(b):
+            out[j, :len(b)] = b
+            out[j, len(b):] = b[-1]
+    return out.reshape(-1, 4)
+
+
+def clip_rows(feats, sims, cat_idx):
+    """per-crop CLIP rows [n, CLIP_W] = feature, best similarity (x100 scale), class index"""
+    return torch.cat([feats, sims[:, None].to(feats.dtype), cat_idx[:, None].to(feats.dtype)], 1)
 
 
 def record_meta(recs):
@@ -136,15 +191,28 @@ def unpack_record(rec, dev, n=None):
     return p
 
 
-def unpack_records(recs, cnts, dev):
+def record_rows(cnts, crops):
+    """host index maps of a step's keyframes: detection row j*REC_ROWS + r, and its CLIP row
+    j*crops + r (r < crops) or the zero row (len(cnts)*crops) for detections without a crop"""
+    cnts = np.asarray(cnts, np.int64)
+    if not cnts.sum():
+        return np.zeros(0, np.int64), np.zeros(0, np.int64)
+    idx = np.concatenate([j * REC_ROWS + np.arange(c) for j, c in enumerate(cnts)])
+    zero = len(cnts) * crops
+    cidx = np.concatenate([np.where(np.arange(c) < crops, j * crops + np.arange(c), zero)
+                           for j, c in enumerate(cnts)])
+    return idx, cidx
+
+
+def unpack_records(recs, cnts, dev, clip=None, crops=16, clip_coeff=1.0):
     """records [nkf, REC_HEAD + REC_ROWS*REC_W] of several keyframes -> ONE Instances3D holding every
-    keyframe's detections in order (keyframe j: cnts[j] rows), five gathers in total"""
+    keyframe's detections in order (keyframe j: cnts[j] rows).  clip [nkf*crops, CLIP_W]: the
+    CLIP rows of the keyframes' crops; detection r < crops of keyframe j gets feature row
+    j*crops + r and score += clip_coeff * sim / 100 (demo.py:167-170), the others zeros."""
     from boxfusion_amd import _lib
     from boxfusion_amd.boxes import GeneralInstance3DBoxes
     from boxfusion_amd.instances import Instances3D
-    cnts = np.asarray(cnts, np.int64)
-    idx = np.concatenate([j * REC_ROWS + np.arange(c) for j, c in enumerate(cnts)]) if cnts.sum() else \
-        np.zeros(0, np.int64)
+    idx, cidx = record_rows(cnts, crops)
     rows = recs[:, REC_HEAD:REC_HEAD + REC_ROWS * REC_W].reshape(-1, REC_W).index_select(
         0, _lib.h2d(idx, dev))
     p = Instances3D((480, 640))
@@ -153,41 +221,41 @@ def unpack_records(recs, cnts, dev):
     p.pred_boxes_3d = GeneralInstance3DBoxes._views(rows[:, 5:11].contiguous(),
                                                      rows[:, 11:20].reshape(-1, 3, 3).contiguous())
     p.pred_proj_xy = rows[:, 20:22].contiguous()
+    if clip is not None:
+        cz = torch.cat([clip, clip.new_zeros((1, clip.shape[1]))])
+        crow = cz.index_select(0, _lib.h2d(cidx, dev))
+        p.features = crow[:, :1024].contiguous()
+        p.scores = p.scores + clip_coeff * crow[:, 1024] / 100.0
     return p
 
 
-def gather_step(recs, feats, dist, world):
+def gather_step(recs, clip, dist, world):
     """Exchange of one step: every rank's per-frame records [b, R] (detections, count and camera
-    pose) and CLIP features [n_crops, 1024] are all-gathered (RCCL over xGMI on the GPU; gloo in
-    the CPU tests) so that the fusion owner sees the step's frames in global frame order
-    (rank-major = frame order, since rank r holds frames step*b*world + r*b ... + b-1).  Both
-    collectives are asynchronous device operations: nothing here waits for the detect stream."""
+    pose) and CLIP rows [b*crops, CLIP_W] are all-gathered with all_gather_into_tensor (RCCL over
+    xGMI on the GPU; gloo on CPU tensors in the rehearsal and the tests: the same call sequence)
+    so that the fusion owner sees the step's frames in global frame order (rank-major = frame
+    order, since rank r holds frames step*b*world + r*b ... + b-1).  On the GPU both collectives
+    are asynchronous device operations: nothing here waits for the detect stream."""
     if dist is None or world == 1:
-        return recs, feats
+        return recs, clip
     if recs.is_cuda and dist.get_backend() == "gloo":     # BF_BENCH_REHEARSE=1 (one-GPU rehearsal)
-        g_rec, g_feat = gather_step(recs.cpu(), feats.cpu(), dist, world)
-        return g_rec.to(recs.device), g_feat.to(feats.device)
-    if recs.is_cuda:
-        g_rec = torch.empty((world * recs.shape[0],) + recs.shape[1:], dtype=recs.dtype, device=recs.device)
-        dist.all_gather_into_tensor(g_rec, recs.contiguous())
-        g_feat = torch.empty((world * feats.shape[0],) + feats.shape[1:], dtype=feats.dtype,
-                             device=feats.device)
-        dist.all_gather_into_tensor(g_feat, feats.contiguous())
-    else:
-        parts = [torch.empty_like(recs) for _ in range(world)]
-        dist.all_gather(parts, recs.contiguous())
-        g_rec = torch.cat(parts)
-        fparts = [torch.empty_like(feats) for _ in range(world)]
-        dist.all_gather(fparts, feats.contiguous())
-        g_feat = torch.cat(fparts)
-    return g_rec, g_feat
+        g_rec, g_clip = gather_step(recs.cpu(), clip.cpu(), dist, world)
+        return g_rec.to(recs.device), g_clip.to(clip.device)
+    g_rec = recs.new_empty((world * recs.shape[0],) + tuple(recs.shape[1:]))
+    dist.all_gather_into_tensor(g_rec, recs.contiguous())
+    g_clip = clip.new_empty((world * clip.shape[0],) + tuple(clip.shape[1:]))
+    dist.all_gather_into_tensor(g_clip, clip.contiguous())
+    return g_rec, g_clip
 
 
 # ------------------------------------------------------------------------------------------------
 def cpu_baseline(cutr, clip_vis, args, scene):
-    """The parity-checked CPU restatement timed on this host: fp32 torch-CPU CuTR + CLIP on
-    `cpu_detect_frames` frames (16 crops each) and the oracle fusion chain (C restatement,
-    oracle/chain.py) over the first `cpu_fusion_frames` frames of the stream."""
+    """The parity-checked CPU restatement timed on this host, both SURVEY §8(d) configs:
+      per frame  depth standardisation + back-projection (oracle C), RGB normalise + pad
+      keyframe   fp32 torch-CPU CuTR + CLIP on `crops` scene-detection crops (cpu_detect_frames
+                 frames timed) + the oracle fusion chain (oracle/chain.py)
+    gap=1: every frame a keyframe; gap=25: one keyframe per 25 frames (fusion chain timed on
+    keyframes 0, 25, 50, ...)."""
     from oracle.chain import OracleChain
     from boxfusion_amd.box_fusion import load_pst
     from boxfusion_amd.cubify_transformer import FrameBatch
@@ -203,10 +271,12 @@ def cpu_baseline(cutr, clip_vis, args, scene):
     cm = copy.deepcopy(cutr).float().cpu().eval()
     vm = copy.deepcopy(clip_vis).float().cpu().eval()
     nf = args.cpu_detect_frames
-    t0 = time.perf_counter()
+    sb = CFG["detection"]["scale_box"]
+    t_pre = t_model = 0.0
     with torch.no_grad():
         for f in range(nf):
             rgb, depth = frame_rgbd(f)
+            t0 = time.perf_counter()
             mean = torch.tensor(PIXEL_MEAN_U8).view(3, 1, 1)
             std = torch.tensor(PIXEL_STD_U8).view(3, 1, 1)
             img = (torch.from_numpy(np.moveaxis(rgb, -1, 0)).float() - mean) / std
@@ -214,14 +284,17 @@ def cpu_baseline(cutr, clip_vis, args, scene):
             d, params = OR.depth_standardize(depth)
             OR.backproject(depth, SCANNET_K, scene.pose(f))
             d = F.pad(torch.from_numpy(d), (0, 0, 0, 160))[None]
+            t1 = time.perf_counter()
             batch = FrameBatch(image=img, depth=d, depth_params=torch.from_numpy(params)[None],
                                K=torch.from_numpy(SCANNET_K)[None],
                                T_gravity=torch.from_numpy(camera_to_gravity(scene.pose(f)))[None],
                                image_sizes=[(480, 640)])
-            r = cm(batch)[0]
-            boxes = r.pred_boxes[: args.crops].numpy().astype(np.int64)
+            cm(batch)
             crops = []
-            for x1, y1, x2, y2 in boxes:
+            for x1, y1, x2, y2 in crop_boxes([scene.detections(f)], args.crops):
+                cx, cy, w, h = (x1 + x2) / 2, (y1 + y2) / 2, (x2 - x1) * sb, (y2 - y1) * sb
+                x1, x2 = int(np.clip(cx - w / 2, 0, 640)), int(np.clip(cx + w / 2, 0, 640))
+                y1, y2 = int(np.clip(cy - h / 2, 0, 480)), int(np.clip(cy + h / 2, 0, 480))
                 c = torch.from_numpy(rgb[y1:y2, x1:x2]).permute(2, 0, 1).float()[None]
                 c = F.interpolate(c, (224, 224), mode="bilinear", align_corners=False) if c.numel() \
                     else torch.zeros((1, 3, 224, 224))
@@ -229,39 +302,155 @@ def cpu_baseline(cutr, clip_vis, args, scene):
             x = torch.cat(crops) / 255.0
             x = (x - torch.tensor(CLIP_MEAN).view(1, 3, 1, 1)) / torch.tensor(CLIP_STD).view(1, 3, 1, 1)
             vm(x)
-    t_det = (time.perf_counter() - t0) / nf
-    ch = OracleChain(CFG, SCANNET_K, pst=load_pst(), legacy=True)
-    t0 = time.perf_counter()
-    for f in range(args.cpu_fusion_frames):
-        ch.keyframe(f, scene.pose(f), scene.detections(f))
-    t_fuse = (time.perf_counter() - t0) / args.cpu_fusion_frames
-    return {"value": 1.0 / (t_det + t_fuse), "unit": "frames/s", "cores": cores, "kind": "port",
+            t_pre += t1 - t0
+            t_model += time.perf_counter() - t1
+    t_pre, t_model = t_pre / nf, t_model / nf
+    fuse = {}
+    for gap in (1, 25):
+        ch = OracleChain(CFG, SCANNET_K, pst=load_pst(), legacy=True)
+        t0 = time.perf_counter()
+        for k in range(args.cpu_fusion_frames):
+            f = k * gap
+            ch.keyframe(f, scene.pose(f), scene.detections(f))
+        fuse[gap] = (time.perf_counter() - t0) / args.cpu_fusion_frames
+    v1 = 1.0 / (t_pre + t_model + fuse[1])
+    v25 = 25.0 / (25.0 * t_pre + t_model + fuse[25])
+    return {"value": v1, "unit": "frames/s", "cores": cores, "kind": "port", "gap25_value": v25,
             "sample": (f"{nf} frame(s) of fp32 torch-CPU CuTR ViT-B + {args.crops} CLIP ViT-H/14 "
-                       f"crops ({t_det:.2f} s/frame) + oracle fusion chain over frames "
-                       f"0..{args.cpu_fusion_frames - 1} ({1e3 * t_fuse:.1f} ms/frame)")}
+                       f"crops ({t_model:.2f} s/keyframe), per-frame depth standardisation + "
+                       f"back-projection + normalise ({1e3 * t_pre:.1f} ms/frame), oracle fusion "
+                       f"chain over {args.cpu_fusion_frames} keyframes ({1e3 * fuse[1]:.1f} ms/keyframe "
+                       f"at gap 1, {1e3 * fuse[25]:.1f} at gap 25); value = gap 1, gap25_value = "
+                       f"25 frames per keyframe")}
 
 
-def load_pmc_traffic():
-    """HBM-side bytes per launch of the roofline kernel from the committed PMC passes
-    (profiles/*_pmc_gelu_gemm.json, newest round); counters cannot be read from inside the run."""
+def load_pmc_traffic(kernel):
+    """HBM-side bytes per launch of `kernel` from the committed PMC passes (profiles/*_pmc.json,
+    newest round); counters cannot be read from inside the run."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_gelu_gemm.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
     if not files:
         return {}
     with open(files[-1]) as f:
-        d = json.load(f)
-    d["source"] = os.path.relpath(files[-1], ROOT) + " (FETCH_SIZE x2 + WRITE_SIZE, separate --pmc passes)"
+        d = json.load(f).get(kernel)
+    if not d:
+        return {}
+    d = dict(d)
+    d["source"] = (os.path.relpath(files[-1], ROOT) + " (2 x FETCH_SIZE + WRITE_SIZE per launch, "
+                   "separate --pmc passes)")
     return d
 
 
+def roofline_obj(ks, kernel, bound, pmc_key=None):
+    """roofline object of a KernelTimer summary: achieved = algorithmic FLOPs (or bytes) per launch
+    / average launch time (HIP events on the launch stream)"""
+    pmc = load_pmc_traffic(pmc_key or kernel) if ks["launches"] else {}
+    if bound == "hbm":
+        achieved, peak, unit = ks.get("gbs", 0.0), PEAK_HBM_GBS, "GB/s"
+    else:
+        achieved, peak, unit = ks.get("tflops", 0.0), PEAK_BF16_TFLOPS, "TFLOP/s"
+    return {"bound": bound, "kernel": kernel, "achieved": achieved, "peak": peak, "unit": unit,
+            "frac": achieved / peak, "traffic": pmc.get("bytes_per_launch"),
+            "traffic_source": pmc.get("source"), "launches": ks["launches"],
+            "avg_us": ks.get("avg_us", 0.0), "flops_per_launch": ks.get("flops_per_launch", 0.0),
+            "algorithmic_bytes_per_launch": ks.get("bytes_per_launch", 0.0)}
+
+
+def emit(line):
+    print(json.dumps(line), flush=True)
+
+
+def base_line(args, N, frames, dt, per_step, n_inflight):
+    return {
+        "metric": "RGB-D frames/sec (whole node) on 640x480 stream",
+        "value": frames / dt, "unit": "frames/s", "n_gpus": N, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic 640x480 RGB-D stream (seeded), random-init weights, seeded scene detections",
+        "config": {"workload": f"configs[2]: synthetic 640x480 RGB-D, batch {args.batch}/step/GPU, gap=1, "
+                               f"CuTR ViT-{ {768: 'B', 384: 'S', 192: 'T'}.get(args.dim, args.dim)} "
+                               f"RGB-D + CLIP ViT-H/14 x{args.crops} crops/frame + fusion",
+                   "frames": frames, "global_batch": per_step, "parallelism": f"dp{N}",
+                   "inflight_batches_per_gpu": n_inflight},
+    }
+
+
 # ------------------------------------------------------------------------------------------------
-def main():
-    args = parse()
+def rehearse_cpu(args, dist, world, rank):
+    """--cpu-rehearsal: the N-rank control flow of main() on CPU tensors with gloo and no
+    kernels -- frame sharding, per-step records and CLIP rows, gather_step's all_gather_into_tensor
+    sequence, the fusion owner's global frame order check, barrier + max-over-ranks timing and
+    rank 0's JSON line.  CLIP rows are rank/frame-coded stand-ins (no CLIP runs)."""
+    from boxfusion_amd.synthetic import Scene
+    scene = Scene(seed=0)
+    B, N = args.batch, world
+    per_step = B * N
+    total = args.warmup + args.steps
+
+    def my_frames(step):
+        return [step * per_step + rank * B + j for j in range(B)]
+
+    mine = [f for s_ in range(total) for f in my_frames(s_)]
+    dets = [scene.detections(f) for f in mine]
+    rec_all = torch.from_numpy(pack_records(dets, [scene.pose(f) for f in mine]))
+    ok = True
+    fused_frames = 0
+    t0 = None
+    for s_ in range(total):
+        if s_ == args.warmup:            # barrier, then time exactly the --steps steps
+            if dist is not None:
+                dist.barrier()
+            t0 = time.perf_counter()
+        sl = slice(s_ * B, s_ * B + B)
+        fr = torch.tensor(mine[sl], dtype=torch.float32)
+        clip = fr.repeat_interleave(args.crops)[:, None].expand(-1, CLIP_W).contiguous()
+        g_rec, g_clip = gather_step(rec_all[sl], clip, dist, N)
+        if rank == 0:
+            want = [s_ * per_step + j for j in range(per_step)]
+            g_pose, g_cnt = record_meta(g_rec)
+            ok &= bool(np.array_equal(g_pose, np.stack([scene.pose(f) for f in want]).astype(np.float32)))
+            ok &= bool(np.array_equal(g_cnt, [min(len(scene.detections(f)["scores"]), REC_ROWS) for f in want]))
+            ok &= bool(torch.equal(g_clip[:, 0], torch.tensor(want, dtype=torch.float32).repeat_interleave(args.crops)))
+            idx, cidx = record_rows(g_cnt, args.crops)
+            ok &= len(idx) == int(g_cnt.sum()) and int(cidx.max(initial=0)) <= per_step * args.crops
+            fused_frames += len(want)
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    if rank == 0:
+        line = base_line(args, N, per_step * args.steps, dt, per_step, 1)
+        line.update(data="cpu rehearsal of the N-rank control flow (no kernels; not a measurement)",
+                    rehearsal={"frame_order_ok": bool(ok), "frames_received": fused_frames})
+        emit(line)
+
+
+# ------------------------------------------------------------------------------------------------
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(argv, args.gpus)
     if args.breakdown:
         args.sync_fusion = True
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
+    if args.cpu_rehearsal:
+        dist = None
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+        rehearse_cpu(args, dist, world, rank)
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return 0
     # BF_BENCH_REHEARSE=1: every rank on cuda:0 with gloo collectives -- a one-GPU rehearsal of the
     # N>1 control flow (sharding, exchange, rank-0 fusion, max-over-ranks timing); not a measurement
     rehearse = os.environ.get("BF_BENCH_REHEARSE", "0") == "1"
@@ -292,13 +481,14 @@ def main():
     B = args.batch
     n_inflight = args.inflight if args.inflight > 0 else 2
     detects = [DetectStage(cutr, clip_vis, CFG, B, 480, 640, SCANNET_K, crops_per_frame=args.crops,
-                           crop_source="top", backproject=True, clip_capacity=B * args.crops,
+                           crop_source="given", backproject=True, clip_capacity=B * args.crops,
                            device=dev, graph=not args.eager) for _ in range(n_inflight)]
     detect = detects[0]
     scene = Scene(seed=0)
     N = world
     per_step = B * N
     total_steps = args.warmup + args.steps
+    coeff = CFG["box_fusion"]["clip_sim_coeff"]
 
     def my_frames(step):
         return [step * per_step + rank * B + j for j in range(B)]
@@ -307,8 +497,9 @@ def main():
     all_mine = [f for s in range(total_steps) for f in my_frames(s)]
     rgb_all, depth_all = gen_frames(all_mine, dev)
     poses_all = np.stack([scene.pose(f) for f in all_mine]).astype(np.float32)
-    rec_host = pack_records([scene.detections(f) for f in all_mine], poses_all)
-    rec_all = torch.from_numpy(rec_host).to(dev)
+    dets_mine = [scene.detections(f) for f in all_mine]
+    rec_all = torch.from_numpy(pack_records(dets_mine, poses_all)).to(dev)
+    crops_all = torch.from_numpy(crop_boxes(dets_mine, args.crops)).to(dev)
     sim = None
     if args.sim_ranks > 1 and world == 1:
         # what rank 0 of an R-GPU run fuses: R*B frames per step (stress test, not the metric)
@@ -331,33 +522,36 @@ def main():
             st_ctx = torch.cuda.stream(det_streams[k])
             st_ctx.__enter__()      # this step's detect, gather and fusion hand-off on its stream
             det = detects[k]
-            det(rgb_all[sl], depth_all[sl], poses_all[sl], return_instances=False)
+            det(rgb_all[sl], depth_all[sl], poses_all[sl], return_instances=False,
+                crop_boxes=crops_all[s * B * args.crops:(s + 1) * B * args.crops])
             if args.breakdown:
                 torch.cuda.synchronize()
                 brk["detect"] += time.perf_counter() - tb
                 tb = time.perf_counter()
             bidx, iidx, cat_idx, feats, sims = det.last["clip"]
-            recs = rec_all[sl]
-            g_rec, g_feat = gather_step(recs, feats, dist, N)
+            clip = clip_rows(feats, sims, cat_idx)
+            g_rec, g_clip = gather_step(rec_all[sl], clip, dist, N)
             if sim is not None:       # --sim-ranks: rank 0 fuses the frames of R virtual ranks
                 g_rec = sim["rec"][s]
+                g_clip = g_clip.repeat(args.sim_ranks, 1)
             if rank == 0:
                 base = s * (per_step if sim is None else B * args.sim_ranks)
+                counts = [base + j - s0 * (g_rec.shape[0]) for j in range(g_rec.shape[0])]
                 if args.sync_fusion:
                     g_pose, g_cnt = record_meta(g_rec)
-                    for j in range(g_rec.shape[0]):
-                        fusion.keyframe(base + j - s0 * (g_rec.shape[0]), g_pose[j],
-                                        unpack_record(g_rec[j], dev, int(g_cnt[j])))
+                    fusion.keyframes(counts, g_pose, unpack_records(g_rec, g_cnt, dev, g_clip,
+                                                                    args.crops, coeff), g_cnt)
                 else:
                     # hand the step's frames to the fusion worker (side stream), keep detecting
                     ev = torch.cuda.Event()
                     ev.record()
                     g_rec.record_stream(fusion.stream)
-                    counts = [base + j - s0 * (g_rec.shape[0]) for j in range(g_rec.shape[0])]
+                    g_clip.record_stream(fusion.stream)
+
                     # the whole step's keyframes as one job: geometry batched, association serial
-                    def job(st, r=g_rec, k=counts):
+                    def job(st, r=g_rec, c_=g_clip, k_=counts):
                         p, c = record_meta(r)       # on the worker's stream, after the gather
-                        st.keyframes(k, p, unpack_records(r, c, dev), c)
+                        st.keyframes(k_, p, unpack_records(r, c, dev, c_, args.crops, coeff), c)
                     fusion.submit_call(job, ev)
             st_ctx.__exit__(None, None, None)
             if args.breakdown:
@@ -376,8 +570,8 @@ def main():
     torch.cuda.synchronize()
     torch.cuda.set_stream(det_stream)          # detection (graph replays, gathers) on its CUs
     if masked and fusion_cus > 0:   # every detect stream on the detection CUs
-        det_streams = [det_stream] + [_lib.partition_streams(fusion_cus, local, masked=True)[0]
-                                      for _ in range(n_inflight - 1)]
+        det_cus, _ = _lib.partition_cus(fusion_cus, local)
+        det_streams = [det_stream] + [_lib.cu_masked_stream(det_cus, local) for _ in range(n_inflight - 1)]
     else:
         det_streams = [det_stream] + [torch.cuda.Stream(device=dev) for _ in range(n_inflight - 1)]
 
@@ -385,7 +579,8 @@ def main():
     # another thread's synchronising calls
     for k, d in enumerate(detects):
         with torch.cuda.stream(det_streams[k]):
-            d(rgb_all[:B], depth_all[:B], poses_all[:B], return_instances=False)
+            d(rgb_all[:B], depth_all[:B], poses_all[:B], return_instances=False,
+              crop_boxes=crops_all[:B * args.crops])
     torch.cuda.synchronize()
 
     def make_fusion():
@@ -401,9 +596,9 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    timer = _lib.KernelTimer(out_bf16=True, act="gelu", large_tiles=True)
+    timer = _lib.KernelTimer()
     t0 = time.perf_counter()
-    with timer:       # records every eager GELU-GEMM launch (graph replays launch none from Python)
+    with timer:       # records every eager GEMM / attention launch (graph replays launch none from Python)
         run_steps(args.warmup, total_steps, fusion)
         if not args.sync_fusion:
             worker = fusion
@@ -419,57 +614,62 @@ def main():
         t = torch.tensor([dt], device="cpu" if rehearse else dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    ks = timer.summary()
-    if ks["launches"] == 0:
-        # graph mode: time the same kernel launched eagerly on the same inputs, right after the
-        # timed region (HIP events on the launch stream, every GELU-GEMM launch of the steps)
+    source = "timed region"
+    if not timer.records:
+        # graph mode: time the same kernels launched eagerly on the same inputs, right after the
+        # timed region (HIP events on the launch stream, every GEMM / attention launch of the steps)
         detect.use_graph = False
-        timer = _lib.KernelTimer(out_bf16=True, act="gelu", large_tiles=True)
+        timer = _lib.KernelTimer()
         with timer:
             for s in range(args.warmup, min(total_steps, args.warmup + args.roofline_steps)):
                 sl = slice(s * B, s * B + B)
-                detect(rgb_all[sl], depth_all[sl], poses_all[sl], return_instances=False)
+                detect(rgb_all[sl], depth_all[sl], poses_all[sl], return_instances=False,
+                       crop_boxes=crops_all[s * B * args.crops:(s + 1) * B * args.crops])
         torch.cuda.synchronize()
         detect.use_graph = not args.eager
-        ks = timer.summary()
-        ks["source"] = f"eager re-run of {args.roofline_steps} timed steps"
-    else:
-        ks["source"] = "timed region"
+        source = f"eager re-run of {args.roofline_steps} timed steps"
     frames = per_step * args.steps
 
     if rank == 0:
-        achieved = ks["tflops"] if ks["launches"] else 0.0
-        pmc = load_pmc_traffic()
-        line = {
-            "metric": "RGB-D frames/sec (whole node) on 640x480 stream",
-            "value": frames / dt, "unit": "frames/s", "n_gpus": N, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-            "data": "synthetic 640x480 RGB-D stream (seeded), random-init weights, seeded scene detections",
-            "config": {"workload": f"configs[2]: synthetic 640x480 RGB-D, batch {B}/step/GPU, gap=1, "
-                                   f"CuTR ViT-{ {768: 'B', 384: 'S', 192: 'T'}.get(args.dim, args.dim)} "
-                                   f"RGB-D + CLIP ViT-H/14 x{args.crops} crops/frame + fusion",
-                       "frames": frames, "global_batch": per_step, "parallelism": f"dp{N}",
-                       "inflight_batches_per_gpu": n_inflight,
-                       "fused_boxes": fusion.stats["fused"],
-                       "global_boxes": len(fusion.all_pred_box) if fusion.all_pred_box is not None else 0},
-            "roofline": {"bound": "mfma", "kernel": "k_gemm256p<true,1> (persistent bf16 GEMM + bias + GELU: MLP up-projections of CLIP ViT-H and CuTR window blocks)",
-                         "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_BF16_TFLOPS, "traffic": pmc.get("bytes_per_launch"),
-                         "traffic_source": pmc.get("source"),
-                         "launches": ks["launches"], "avg_us": ks.get("avg_us", 0.0),
-                         "flops_per_launch": ks["flops"] / max(ks["launches"], 1),
-                         "measured": ks["source"]},
+        big = lambda t: t["kind"] == "gemm" and t["large"]
+        r_all = roofline_obj(timer.summary(big), "k_gemm256p (persistent bf16 GEMM, every launch: "
+                             "qkv, proj/fc2 + f32 residual, fc1 + GELU of CLIP ViT-H and CuTR)",
+                             "mfma", pmc_key="k_gemm256p")
+        comps = {
+            "resid_gemm": roofline_obj(timer.summary(lambda t: big(t) and t["resid"]),
+                                       "k_gemm256p<false, 0> (proj / fc2 + f32 residual)", "mfma",
+                                       pmc_key="k_gemm256p<false, 0>"),
+            "gelu_gemm": roofline_obj(timer.summary(lambda t: big(t) and t["act"] == 1),
+                                      "k_gemm256p<true, 1> (fc1 + GELU)", "mfma",
+                                      pmc_key="k_gemm256p<true, 1>"),
+            "attention": roofline_obj(timer.summary(lambda t: t["kind"] == "attn"),
+                                      "k_attn_* (every ViT attention launch: CuTR window + global, "
+                                      "CLIP)", "mfma", pmc_key="k_attn"),
+            "attention_clip": roofline_obj(timer.summary(lambda t: t["kind"] == "attn" and t["D"] == 80),
+                                           "CLIP ViT-H/14 attention (S=257, D=80)", "mfma",
+                                           pmc_key="k_attn_clip"),
+            "attention_cutr": roofline_obj(timer.summary(lambda t: t["kind"] == "attn" and t["D"] != 80),
+                                           "CuTR attention (512-key joint windows, 1600-token global)",
+                                           "mfma", pmc_key="k_attn_cutr"),
         }
+        for v in comps.values():
+            v["measured"] = source
+        r_all["measured"] = source
+        line = base_line(args, N, frames, dt, per_step, n_inflight)
+        line["config"].update(fused_boxes=fusion.stats["fused"],
+                              global_boxes=len(fusion.all_pred_box) if fusion.all_pred_box is not None else 0)
+        line["roofline"] = r_all
+        line["roofline_components"] = comps
         if args.breakdown:
             line["breakdown_ms_per_step"] = {k: 1e3 * v / args.steps for k, v in brk.items()}
         if not args.no_cpu_baseline and N == 1:      # rank 0 at N=1 only (a reported baseline)
             line["cpu_baseline"] = cpu_baseline(cutr, clip_vis, args, scene)
-        print(json.dumps(line), flush=True)
+        emit(line)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

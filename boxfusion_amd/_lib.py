@@ -168,13 +168,37 @@ _ROWS_DT = np.dtype([("a", np.uint64), ("b", np.uint64), ("dst", np.uint64), ("n
                      ("n_b", np.int64), ("row_bytes", np.int32), ("pad", np.int32)])
 
 
-def rows_gather(pairs, idx=None, n_out=None, outs=None):
+_STATUS = {}
+
+
+def status_word(device):
+    """persistent int32 device word per device that rows_gather launches without a caller status
+    OR their BF_DEV_* flags into (an out-of-range index skips its row); check_status() reads and
+    clears it -- FusionStage does so at the read-back it already makes per keyframe"""
+    key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+    if key not in _STATUS:
+        _STATUS[key] = torch.zeros(1, dtype=torch.int32, device=torch.device("cuda", key))
+    return _STATUS[key]
+
+
+def check_status(device, what="bf_rows_gather"):
+    w = status_word(device)
+    v = int(w.item())
+    if v:
+        w.zero_()
+        if v & BF_DEV_INDEX_RANGE:
+            raise HipError(f"{what}: index out of range (BF_DEV_INDEX_RANGE)")
+        raise HipError(f"{what}: device status {v:#x}")
+
+
+def rows_gather(pairs, idx=None, n_out=None, outs=None, status=None):
     """pairs: [(a, b or None[, narrow])] contiguous device tensors with the same row shape / dtype
     per pair (narrow=True: int64 rows written as int32);
     returns new tensors with rows idx of cat(a, b) (idx: int64 device tensor; None: the whole
     concatenation; int32 or int64); `outs`: write into these contiguous tensors instead (e.g. the
     tail rows of a preallocated table).  One bf_rows_gather launch for up to ROWS_MAX_FIELDS
-    fields."""
+    fields.  An index outside [0, len(a) + len(b)) sets BF_DEV_INDEX_RANGE in `status` (an int32
+    device word the caller reads back), or else in the device's status_word()."""
     if idx is not None:
         n_out = int(idx.shape[0])
     elif n_out is None:
@@ -198,8 +222,11 @@ def rows_gather(pairs, idx=None, n_out=None, outs=None):
     if pairs and n_out:
         arr = np.array(recs, dtype=_ROWS_DT)
         i32 = idx is not None and idx.dtype == torch.int32
+        if status is None and idx is not None:
+            status = status_word(outs[0].device)
         _check(lib().bf_rows_gather(c_void_p(arr.ctypes.data), c_int(len(pairs)), _ptr(idx), c_int(int(i32)),
-                                    c_int(n_out), None, _stream()), "bf_rows_gather")
+                                    c_int(n_out), _ptr(status) if status is not None else None,
+                                    _stream()), "bf_rows_gather")
     return outs
 
 
@@ -271,15 +298,17 @@ def corr_assoc_chained(corners, dims, scores, boxes2d, init_id, cam_poses, cur_p
 # fusion
 # ------------------------------------------------------------------------------------------
 def fusion_fit(view_off, n_views, view_box, view_R, view_score, view_pose, view_tc, pst,
-               cfg: FuseCfg, trace=False, max_views=None, packed_out=False):
+               cfg: FuseCfg, trace=False, max_views=None, packed_out=False, packed=None):
     """max_views: host-known bound on n_views (avoids a device read when given).
     packed_out: return (out_box, packed, trace) with packed = int32 [updated(n_jobs),
-    iterations(n_jobs), status] (one device->host copy for the caller)."""
+    iterations(n_jobs), status] (one device->host copy for the caller); `packed` may be given
+    (zeroed; its status word may already hold flags of an earlier launch: they are kept)."""
     dev = view_box.device
     n_jobs = view_off.shape[0]
     out_box = torch.empty((n_jobs, 6), dtype=torch.float32, device=dev)
     # updated flags, iteration counts and the status word in one buffer: one read-back
-    packed = torch.zeros(2 * n_jobs + 1, dtype=torch.int32, device=dev)
+    if packed is None:
+        packed = torch.zeros(2 * n_jobs + 1, dtype=torch.int32, device=dev)
     out_upd, out_it, status = packed[:n_jobs], packed[n_jobs:2 * n_jobs], packed[2 * n_jobs:]
     tr = (torch.empty((n_jobs, cfg.iters, cfg.pst_size), dtype=torch.float32, device=dev)
           if trace else None)
@@ -458,15 +487,15 @@ def crop_resize_im2col(img, boxes, img_idx, size, patch, mean, std, kpad, out=No
 
 
 class KernelTimer:
-    """HIP-event timing of selected GEMM launches (used by bench.py for the roofline of the
-    dominant kernel): records (flops, start, end) for every bf_gemm_bf16 launch whose output
-    dtype / activation match while active."""
+    """HIP-event timing of the MFMA tower launches (bench.py's roofline objects): while active,
+    every bf_gemm_bf16 and bf_attention_bf16 launch made from Python is bracketed by two events
+    on the launch stream and recorded with its algorithmic FLOPs and bytes:
+      gemm       2*M*N*K FLOPs; bytes A + W + out (+ the f32 residual read)
+      attention  4*Sq*Sk*D FLOPs per (batch, head); bytes Q + K + V read + O written
+    `summary(pred)` aggregates the records selected by pred(tags)."""
 
-    def __init__(self, out_bf16=True, act="gelu", large_tiles=None):
-        """large_tiles: True / False restricts to launches of k_gemm256 / k_gemm (None: both)."""
-        self.out_bf16, self.act = out_bf16, ACT[act]
-        self.large_tiles = large_tiles
-        self.records = []
+    def __init__(self):
+        self.records = []      # (tags, flops, bytes, start event, end event)
         self.active = False
 
     def __enter__(self):
@@ -480,18 +509,30 @@ class KernelTimer:
         _TIMER = None
         self.active = False
 
-    def summary(self):
+    def record(self, tags, flops, nbytes, fn):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        r = fn()
+        e.record()
+        self.records.append((tags, flops, nbytes, s, e))
+        return r
+
+    def summary(self, pred=lambda tags: True):
         torch.cuda.synchronize()
-        if not self.records:
-            return dict(launches=0, flops=0.0, ms=0.0)
-        ms = sum(s.elapsed_time(e) for _, s, e in self.records)
-        fl = sum(f for f, _, _ in self.records)
-        return dict(launches=len(self.records), flops=fl, ms=ms, avg_us=1e3 * ms / len(self.records),
-                    tflops=fl / (ms * 1e-3) / 1e12)
+        sel = [r for r in self.records if pred(r[0])]
+        if not sel:
+            return dict(launches=0, flops=0.0, bytes=0.0, ms=0.0)
+        ms = sum(s.elapsed_time(e) for _, _, _, s, e in sel)
+        fl = sum(f for _, f, _, _, _ in sel)
+        nb = sum(b for _, _, b, _, _ in sel)
+        return dict(launches=len(sel), flops=fl, bytes=nb, ms=ms, avg_us=1e3 * ms / len(sel),
+                    tflops=fl / (ms * 1e-3) / 1e12, gbs=nb / (ms * 1e-3) / 1e9,
+                    flops_per_launch=fl / len(sel), bytes_per_launch=nb / len(sel))
 
 
 _TIMER = None
 _gemm_untimed = gemm
+_attention_untimed = attention
 
 
 def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype=torch.bfloat16,
@@ -499,19 +540,28 @@ def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype
     t = _TIMER
     if t is None:
         return _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m)
-    ob = (out.dtype if out is not None else out_dtype) == torch.bfloat16
-    if ob != t.out_bf16 or ACT[act] != t.act:
-        return _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m)
     M = a.shape[0] if m is None else m
-    if t.large_tiles is not None and bool(lib().bf_gemm_large_tiles(c_int(M), c_int(w.shape[0]),
-                                                                     c_int(w.shape[1]))) != t.large_tiles:
-        return _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m)
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    r = _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m)
-    e.record()
-    t.records.append((2.0 * M * w.shape[0] * w.shape[1], s, e))
-    return r
+    N, K = w.shape
+    ob = (out.dtype if out is not None else out_dtype) == torch.bfloat16
+    tags = dict(kind="gemm", act=ACT[act], out_bf16=ob, resid=resid is not None, M=M, N=N, K=K,
+                large=bool(lib().bf_gemm_large_tiles(c_int(M), c_int(N), c_int(K))))
+    nbytes = 2.0 * (M * K + N * K) + M * N * (2 if ob else 4)
+    if resid is not None:
+        nbytes += 4.0 * (M * N if not resid_mod else resid_mod * N)
+    return t.record(tags, 2.0 * M * N * K, nbytes,
+                    lambda: _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m))
+
+
+def attention(q, k, v, o, batch, heads, sq, sk, head_dim, scale, q_bs=None, k_bs=None, v_bs=None,
+              o_bs=None):
+    t = _TIMER
+    if t is None:
+        return _attention_untimed(q, k, v, o, batch, heads, sq, sk, head_dim, scale, q_bs, k_bs, v_bs, o_bs)
+    tags = dict(kind="attn", D=head_dim, sq=sq, sk=sk, batch=batch, heads=heads)
+    bh = float(batch * heads)
+    return t.record(tags, 4.0 * bh * sq * sk * head_dim, 2.0 * bh * head_dim * (2 * sq + 2 * sk),
+                    lambda: _attention_untimed(q, k, v, o, batch, heads, sq, sk, head_dim, scale,
+                                               q_bs, k_bs, v_bs, o_bs))
 
 
 # ------------------------------------------------------------------------------------------
@@ -547,10 +597,18 @@ def partition_streams(n_reserved, device=None, masked=False):
     lib().bf_gemm_set_cu_budget(c_int(n - n_reserved))
     if not masked:
         return torch.cuda.current_stream(dev), torch.cuda.Stream(device=dev, priority=-1)
+    det, fus = partition_cus(n_reserved, dev)
+    return cu_masked_stream(det, dev), cu_masked_stream(fus, dev)
+
+
+def partition_cus(n_reserved, device=None):
+    """(detect CUs, fusion CUs): every (n / n_reserved)-th CU goes to the fusion stream"""
+    dev = torch.cuda.current_device() if device is None else device
+    n = torch.cuda.get_device_properties(dev).multi_processor_count
     step = max(1, n // max(1, n_reserved))
     fus = [i for i in range(0, n, step)][:n_reserved]
     det = [i for i in range(n) if i not in set(fus)]
-    return cu_masked_stream(det, dev), cu_masked_stream(fus, dev)
+    return det, fus
 
 
 # ------------------------------------------------------------------------------------------

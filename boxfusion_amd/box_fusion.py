@@ -9,6 +9,7 @@ evaluations of all boxes spread over the whole chip).
 from __future__ import annotations
 
 import os
+import warnings
 
 import numpy as np
 import torch
@@ -54,6 +55,11 @@ class BoxFusion:
         self._pst_dev = torch.from_numpy(self.PST[: self.pst_size]).to(self.device).contiguous()
         self.last_stats = {}
         self.updated_total = 0    # boxes updated over every call (resolved results)
+        # BF_DEV_HULL_OVERFLOW policy: False = count + warn once (the exact hull is used),
+        # True = raise (cfg box_fusion.strict_hull)
+        self.strict_hull = bool(bf.get("strict_hull", False))
+        self.hull_overflow_calls = 0
+        self._warned_hull = False
 
     def update_intrinsics(self, size, K):
         self.H = size[1]
@@ -105,15 +111,19 @@ class BoxFusion:
         idx = _lib.h2d(host, dev)
         flat = idx[3 * nj:]
         b3 = per_frame_box.pred_boxes_3d
+        # updated flags, iteration counts and the status word of the whole call: one read-back
+        # (the view gather's BF_DEV_INDEX_RANGE and the fit's flags land in the same word)
+        packed = torch.zeros(2 * nj + 1, dtype=torch.int32, device=dev)
         # every view's box, rotation, score, pose and 2-D hull in one gather launch
         vb, vr, vs, vp, vt = _lib.rows_gather(
             [(b3.tensor.contiguous(), None), (b3.R.contiguous(), None),
              (per_frame_box.scores.to(dev, torch.float32).contiguous(), None),
              (per_frame_box.cam_pose.to(dev, torch.float32).contiguous(), None),
-             (per_frame_box.projected_boxes.contiguous(), None)], flat)
+             (per_frame_box.projected_boxes.contiguous(), None)], flat, status=packed[2 * nj:])
         out_box, packed, _ = _lib.fusion_fit(idx[:nj], idx[nj:2 * nj], vb, vr, vs, vp, vt,
                                              self._pst_dev, self.fuse_cfg(),
-                                             max_views=min(int(nv.max()), 32), packed_out=True)
+                                             max_views=min(int(nv.max()), 32), packed_out=True,
+                                             packed=packed)
         # write-back of the updated rows on the device (xyz + lhw; R unchanged, quirk 6)
         target = all_pred_box.pred_boxes_3d.tensor
         if target.is_contiguous():
@@ -128,6 +138,23 @@ class BoxFusion:
             upd, iters, st = h[:nj], h[nj:2 * nj], int(h[2 * nj])
             if st & _lib.BF_DEV_VIEW_OVERFLOW:
                 raise _lib.HipError("bf_fusion_fit: a fusion list has more views than the kernel holds")
+            if st & _lib.BF_DEV_INDEX_RANGE:
+                raise _lib.HipError("boxfusion: a fusion list names a per-frame box that does not exist")
+            if st & _lib.BF_DEV_HULL_OVERFLOW:
+                # an intersection polygon with more points than the reference kernel's fixed
+                # buffers hold (convex_inter[8] / corners_i[36], box_fusion.py:378-384; two
+                # overlapping projected hexagons can intersect in up to 12 points): the reference
+                # writes past its array there, the kernel here keeps 64 slots and returns the
+                # intended IoU.  Counted (and warned once) by default; strict_hull raises.
+                self.hull_overflow_calls += 1
+                if self.strict_hull:
+                    raise _lib.HipError("bf_fusion_fit: hull capacity exceeded (BF_DEV_HULL_OVERFLOW): "
+                                        "the reference kernel overruns its fixed buffers on this input")
+                if not self._warned_hull:
+                    self._warned_hull = True
+                    warnings.warn("bf_fusion_fit: an intersection hull exceeded the reference kernel's "
+                                  "8-point buffer (BF_DEV_HULL_OVERFLOW); the exact hull was used",
+                                  RuntimeWarning, stacklevel=2)
             n_upd = 0
             for j, (i, fl) in enumerate(jobs):
                 if upd[j]:

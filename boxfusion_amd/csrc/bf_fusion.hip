@@ -116,9 +116,15 @@ __device__ float iou_hull_pre(P2* c0, const P2* ht, int nt, float at, int* flags
     P2 cand[CAND_CAP];
     int nc = 0;
     for (int i = 0; i < n0; ++i)
-        if (point_in_polygon(h0[i], ht, nt) && nc < CAND_CAP) cand[nc++] = h0[i];
+        if (point_in_polygon(h0[i], ht, nt)) {
+            if (nc < CAND_CAP) cand[nc++] = h0[i];
+            else *flags |= BF_DEV_HULL_OVERFLOW;
+        }
     for (int i = 0; i < nt; ++i)
-        if (point_in_polygon(ht[i], h0, n0) && nc < CAND_CAP) cand[nc++] = ht[i];
+        if (point_in_polygon(ht[i], h0, n0)) {
+            if (nc < CAND_CAP) cand[nc++] = ht[i];
+            else *flags |= BF_DEV_HULL_OVERFLOW;
+        }
     for (int i = 0; i < n0; ++i)
         for (int j = 0; j < nt; ++j) {
             const P2 a1 = h0[i], a2 = h0[(i + 1) % n0], b1 = ht[j], b2 = ht[(j + 1) % nt];

@@ -1049,6 +1049,11 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
     if (!A || !W || !C || M < 0 || N <= 0 || K <= 0) return BF_ERR_ARG;
     if (K % GB_K != 0 || lda % 8 != 0 || ldw % 8 != 0) return BF_ERR_UNSUPPORTED;
     if (M == 0) return BF_OK;
+    // the operand buffer descriptors (num_records) and per-lane row offsets are 32-bit: operands
+    // whose byte extent reaches 2^31 would wrap (split M on the host instead)
+    if ((long long)(M - 1) * lda * 2 + (long long)K * 2 >= (1LL << 31) ||
+        (long long)(N - 1) * ldw * 2 + (long long)K * 2 >= (1LL << 31))
+        return BF_ERR_CAPACITY;
     const int tiles_m = (M + GB_M - 1) / GB_M, tiles_n = (N + GB_N - 1) / GB_N;
     const int nwg = tiles_m * tiles_n;
     const size_t lds = 2 * 32768;

@@ -91,6 +91,7 @@ class FusionStage:
             n = int(sizes[j])
             self.keyframe(c, poses[j], preds[off:off + n] if n else None, prepared=True)
             off += n
+        _lib.check_status(self.dev)     # row gathers of the batch (one read per batch)
 
     def keyframe(self, count, pose, pred, prepared=False):
         """pred: Instances3D of this keyframe in CAMERA coordinates (after the detection filters
@@ -248,7 +249,7 @@ class AsyncFusion:
         self.stream = stream if stream is not None else torch.cuda.Stream(device=self.device_index)
         self.q = queue.Queue()
         self.err = None
-        self.busy_s = 0.0      # wall time the worker spent inside keyframe jobs
+        self.busy_s = 0.0      # wall time the worker spent inside keyframe jobs (after their input was ready)
         self.thread = threading.Thread(target=self._run, name="boxfusion-fusion", daemon=True)
         self.thread.start()
 
@@ -284,9 +285,13 @@ class AsyncFusion:
                     continue
                 count, pose, make_pred, ready = item
                 try:
-                    t0 = time.perf_counter()
                     if ready is not None:
+                        # the job reads the producer's outputs on the host right away (record
+                        # counts), so wait here: busy_s then counts fusion work only, not the wait
+                        # for the detect stream
+                        ready.synchronize()
                         self.stream.wait_event(ready)
+                    t0 = time.perf_counter()
                     if count is None:
                         make_pred(self.stage)
                     else:

@@ -71,9 +71,12 @@ def detection_mask(scores, proj_xy, box3d, cfg, H, W):
 class DetectStage:
     """Everything demo.py does per frame before the fusion step, for a batch of B frames.
 
-    crop_source: "filtered" (reference: CLIP on every instance surviving the filters) or
+    crop_source: "filtered" (reference: CLIP on every instance surviving the filters),
     "top" (throughput runs with random weights: CLIP on the top `crops_per_frame` instances of
-    every frame, so the CLIP tower does the work it would do on real detections).
+    every frame, so the CLIP tower does the work it would do on real detections) or "given"
+    (CLIP on `crops_per_frame` caller-supplied boxes per frame, `crop_boxes` of __call__: the
+    benchmark crops the seeded scene's detections, whose features then travel with them into
+    fusion).
 
     The device work reads fixed input buffers (frames, depth, T_gravity, K, K^-1) and is free of
     host synchronisation; with `graph=True` it is captured once into a HIP graph and replayed
@@ -110,7 +113,10 @@ class DetectStage:
         self.in_pose = torch.zeros((batch, 4, 4), dtype=torch.float32, device=self.dev)
         k = crops_per_frame
         self.top_b = torch.arange(batch, device=self.dev).repeat_interleave(k)
+        self.top_b32 = self.top_b.to(torch.int32)
         self.top_i = torch.arange(k, device=self.dev).repeat(batch)
+        # crop_source "given": the caller supplies k 2-D boxes (xyxy, image pixels) per frame
+        self.in_crops = torch.zeros((batch * k, 4), dtype=torch.float32, device=self.dev)
         self.use_graph = graph
         self.graph = None
         self.out = {}
@@ -146,10 +152,11 @@ class DetectStage:
         box3d = torch.stack([r.pred_boxes_3d.tensor for r in res])
         self.out.update(res=res, keep=detection_mask(scores, proj, box3d, self.cfg, H, W),
                         boxes2d=torch.stack([r.pred_boxes for r in res]))
-        if self.clip is not None and self.crop_source == "top":
+        if self.clip is not None and self.crop_source in ("top", "given"):
             bidx, iidx = self.top_b, self.top_i
-            cat_idx, feats, sims = self.text_prompt(self.in_rgb, self.out["boxes2d"][bidx, iidx].contiguous(),
-                                                    bidx.to(torch.int32))
+            boxes = (self.in_crops if self.crop_source == "given"
+                     else self.out["boxes2d"][bidx, iidx].contiguous())
+            cat_idx, feats, sims = self.text_prompt(self.in_rgb, boxes, self.top_b32)
             self.out["clip"] = (bidx, iidx, cat_idx, feats, sims)
 
     def _run_device(self):
@@ -171,15 +178,20 @@ class DetectStage:
         self.graph.replay()
 
     @torch.no_grad()
-    def __call__(self, rgb_u8, depth, poses, return_instances=True):
+    def __call__(self, rgb_u8, depth, poses, return_instances=True, crop_boxes=None):
         """rgb_u8 [B,H,W,3] u8, depth [B,H,W] f32 (device), poses [B,4,4] host -> list of B
         Instances3D (camera frame, filtered, with categories / features / CLIP-adjusted scores).
         With return_instances=False (throughput runs) nothing is read back: results stay in
-        self.last (device tensors) and the call never waits for the device."""
+        self.last (device tensors) and the call never waits for the device.
+        crop_boxes: f32 device [B*crops_per_frame, 4] (crop_source "given")."""
         B, H, W = self.B, self.H, self.W
         assert rgb_u8.shape == (B, H, W, 3) and depth.shape == (B, H, W)
         self.in_rgb.copy_(rgb_u8, non_blocking=True)
         self.in_depth.copy_(depth, non_blocking=True)
+        if self.crop_source == "given":
+            if crop_boxes is None or tuple(crop_boxes.shape) != tuple(self.in_crops.shape):
+                raise ValueError(f"crop_source='given' needs crop_boxes of shape {tuple(self.in_crops.shape)}")
+            self.in_crops.copy_(crop_boxes, non_blocking=True)
         poses = np.asarray(poses, np.float32)
         self.in_Tg.copy_(torch.from_numpy(np.stack([camera_to_gravity(p) for p in poses])))
         self.in_pose.copy_(torch.from_numpy(poses))
@@ -192,7 +204,7 @@ class DetectStage:
             return None
         res, keep = o["res"], o["keep"]
         out = [r[keep[b]] for b, r in enumerate(res)]
-        if self.clip is None or self.crop_source == "top":
+        if self.clip is None or self.crop_source in ("top", "given"):
             return out
         # reference mode: CLIP on every surviving instance (variable count, eager)
         bidx, iidx = keep.nonzero(as_tuple=True)

@@ -224,3 +224,79 @@ def test_backproject_vs_oracle(L):
     rx, rv = OR.backproject(d, SCANNET_K, RT, 10.0)
     np.testing.assert_array_equal(valid.cpu().numpy(), rv)
     np.testing.assert_allclose(xyz.cpu().numpy(), rx, rtol=1e-5, atol=1e-5)
+
+
+def _hexagon_views(n_views=3, twist_deg=14.0):
+    """a box seen obliquely (projected hull = hexagon) in n views, each view's observed corners =
+    the box's own projection twisted about its centroid: the intersection of the two hexagons has
+    12 vertices, more than the reference kernel's convex_inter[8] (box_fusion.py:381-384)"""
+    from boxfusion_amd.synthetic import SCANNET_K, look_at_pose
+    box = np.array([0.0, 0.0, 0.5, 0.8, 0.6, 0.7], np.float32)
+    R = np.eye(3, dtype=np.float32)
+    poses, tcs = [], []
+    K = SCANNET_K.astype(np.float64)
+    c = OR.box_corners(box[None], R[None])[0].astype(np.float64)
+    for v in range(n_views):
+        a = 0.6 + 0.4 * v
+        P = look_at_pose([2.5 * np.cos(a), 2.5 * np.sin(a), 1.8], [0.0, 0.0, 0.5]).astype(np.float64)
+        cam = (np.linalg.inv(P) @ np.c_[c, np.ones(8)].T).T[:, :3]
+        uv = np.stack([K[0, 0] * cam[:, 0] / cam[:, 2] + K[0, 2], K[1, 1] * cam[:, 1] / cam[:, 2] + K[1, 2]], 1)
+        m = uv.mean(0)
+        t = np.deg2rad(twist_deg)
+        Rt = np.array([[np.cos(t), -np.sin(t)], [np.sin(t), np.cos(t)]])
+        tcs.append(((uv - m) @ Rt.T + m).astype(np.float32))
+        poses.append(P.astype(np.float32))
+    n = n_views
+    return (np.repeat(box[None], n, 0), np.repeat(R[None], n, 0), np.linspace(0.9, 0.7, n).astype(np.float32),
+            np.stack(poses), np.stack(tcs))
+
+
+@pytest.mark.parametrize("legacy", [True, False])
+def test_fusion_hull_overflow_flag_and_exact_hull(L, legacy):
+    """an input whose intersection hull exceeds the reference's 8-point buffer sets
+    BF_DEV_HULL_OVERFLOW, and the kernel still matches the oracle (exact hull) bit for bit"""
+    vb, vr, vs, vp, vt = _hexagon_views()
+    be = HipBackend(L, legacy=legacy)
+    nv = len(vs)
+    off, cnt = _t(np.array([0], np.int32), torch.int32), _t(np.array([nv], np.int32), torch.int32)
+    out, upd, it, status, _ = L.fusion_fit(off, cnt, _t(vb), _t(vr), _t(vs), _t(vp), _t(vt), be.pst,
+                                           be.fcfg, max_views=nv)
+    assert int(status.item()) & L.BF_DEV_HULL_OVERFLOW
+    ocfg = OR.fuse_cfg(TU.SCANNET_CFG, np.array(be.fcfg.K).reshape(4, 4), 480, 640, legacy=legacy)
+    r = OR.fusion_fit(vb, vr, vs, vp, vt, be.pst.cpu().numpy(), ocfg)
+    assert int(upd.item()) == r["updated"]
+    np.testing.assert_array_equal(out.cpu().numpy()[0], r["box"])
+
+
+def test_boxfusion_hull_overflow_policy(L):
+    """BoxFusion counts the overflow (warning once) by default and raises with strict_hull"""
+    import copy
+    import warnings
+    from boxfusion_amd.box_fusion import BoxFusion
+    from boxfusion_amd.box_manager import BoxManager
+    from boxfusion_amd.boxes import GeneralInstance3DBoxes
+    from boxfusion_amd.instances import Instances3D
+    vb, vr, vs, vp, vt = _hexagon_views()
+    for strict in (False, True):
+        cfg = copy.deepcopy(TU.SCANNET_CFG)
+        cfg["box_fusion"]["strict_hull"] = strict
+        pf = Instances3D((480, 640))
+        pf.pred_boxes_3d = GeneralInstance3DBoxes(_t(vb), _t(vr))
+        pf.scores = _t(vs)
+        pf.cam_pose = _t(vp)
+        pf.projected_boxes = _t(vt)
+        allb = Instances3D((480, 640))
+        allb.pred_boxes_3d = GeneralInstance3DBoxes(_t(vb[:1]), _t(vr[:1]))
+        bm = BoxManager(cfg)
+        bm.fusion_list = [[0, 1, 2]]
+        bf = BoxFusion(cfg, device=DEV)
+        bf.update_intrinsics((640, 480), np.array(fuse_cfg(L, True).K).reshape(4, 4)[:3, :3])
+        if strict:
+            with pytest.raises(L.HipError, match="HULL_OVERFLOW"):
+                bf.boxfusion(allb, pf, bm)
+        else:
+            with warnings.catch_warnings(record=True) as w:
+                warnings.simplefilter("always")
+                bf.boxfusion(allb, pf, bm)
+            assert bf.hull_overflow_calls == 1
+            assert any("HULL_OVERFLOW" in str(x.message) for x in w)

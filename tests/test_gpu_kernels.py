@@ -247,3 +247,44 @@ def test_gemm_balanced_grid(L, act, use_resid):
     if use_resid:
         y = y + resid
     assert rel_err(outs[0], y) < (5e-3 if not use_resid else 1e-5)
+
+
+@pytest.mark.parametrize("force", [-1, 1])
+def test_gemm_stem_rowmap_broadcast_resid(L, force):
+    """the CLIP stem GEMM's combination on both tile kernels (forced):
+    row map (patch row n*np + p -> token row n*S + 1 + p), broadcast residual table (pos-embed,
+    resid_mod = np), no bias, f32 out -- against the old formulation P + pos scattered by torch"""
+    from boxfusion_amd._lib import lib
+    g = torch.Generator(device="cuda").manual_seed(29)
+    crops, npch, S, W, K = 128, 256, 257, 1280, 640
+    a = torch.randn(crops * npch, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(W, K, device="cuda", generator=g) / math.sqrt(K)).bfloat16()
+    pos = torch.randn(npch, W, device="cuda", generator=g)
+    row_map = (torch.arange(crops, device="cuda", dtype=torch.int32)[:, None] * S + 1
+               + torch.arange(npch, device="cuda", dtype=torch.int32)[None]).reshape(-1)
+    lib().bf_gemm_force_small_tiles(force)        # -1: the persistent 256x256 kernel, 1: 128x128
+    assert bool(lib().bf_gemm_large_tiles(crops * npch, W, K)) == (force < 0)
+    try:
+        X = torch.full((crops * S, W), 7.0, device="cuda")
+        L.gemm(a, w, resid=pos, resid_mod=npch, out=X, row_map=row_map)
+    finally:
+        lib().bf_gemm_force_small_tiles(0)
+    ref = torch.full((crops * S, W), 7.0, device="cuda")
+    P = a.float() @ w.float().T
+    ref.view(crops, S, W)[:, 1:] = (P.view(crops, npch, W) + pos[None])
+    assert rel_err(X, ref) < 1e-5
+    assert torch.all(X.view(crops, S, W)[:, 0] == 7.0)      # class-token rows untouched
+
+
+def test_gemm_operand_extent_capacity(L):
+    """operands whose byte extent reaches 2^31 are refused (32-bit descriptors), not wrapped"""
+    import ctypes
+    from boxfusion_amd._lib import lib
+    a = torch.empty(1, 64, device="cuda", dtype=torch.bfloat16)
+    w = torch.empty(64, 64, device="cuda", dtype=torch.bfloat16)
+    c = torch.empty(1, 64, device="cuda", dtype=torch.bfloat16)
+    # M = 2^24 rows at lda = 64: (M-1)*lda*2 + K*2 = 2^31 (only the extent is checked; nothing runs)
+    rc = lib().bf_gemm_bf16(ctypes.c_void_p(a.data_ptr()), 64, ctypes.c_void_p(w.data_ptr()), 64,
+                            None, None, 0, 0, ctypes.c_void_p(c.data_ptr()), 64, 1, None, 1 << 24, 64,
+                            64, 0, None)
+    assert rc == -3       # BF_ERR_CAPACITY
