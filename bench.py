@@ -259,7 +259,7 @@ def cpu_baseline(cutr, clip_vis, args, scene):
     from oracle.chain import OracleChain
     from boxfusion_amd.box_fusion import load_pst
     from boxfusion_amd.cubify_transformer import FrameBatch
-    from boxfusion_amd.preprocessor import PIXEL_MEAN_U8, PIXEL_STD_U8
+    from boxfusion_amd.preprocessor import PIXEL_MEAN, PIXEL_STD
     from boxfusion_amd.sensor import camera_to_gravity
     from boxfusion_amd.synthetic import SCANNET_K, frame_rgbd
     from boxfusion_amd.clip import CLIP_MEAN, CLIP_STD
@@ -277,8 +277,8 @@ def cpu_baseline(cutr, clip_vis, args, scene):
         for f in range(nf):
             rgb, depth = frame_rgbd(f)
             t0 = time.perf_counter()
-            mean = torch.tensor(PIXEL_MEAN_U8).view(3, 1, 1)
-            std = torch.tensor(PIXEL_STD_U8).view(3, 1, 1)
+            mean = torch.tensor(PIXEL_MEAN).view(3, 1, 1)
+            std = torch.tensor(PIXEL_STD).view(3, 1, 1)
             img = (torch.from_numpy(np.moveaxis(rgb, -1, 0)).float() - mean) / std
             img = F.pad(img, (0, 0, 0, 160))[None]
             d, params = OR.depth_standardize(depth)

@@ -47,6 +47,13 @@ class FuseCfg(ctypes.Structure):
                 ("img_h", c_float), ("img_w", c_float), ("K", c_float * 16)]
 
 
+class FilterCfg(ctypes.Structure):
+    _fields_ = [("score_thresh", c_float), ("floor_ratio", c_float), ("floor_half", c_float),
+                ("size_max", c_float), ("gap_w", ctypes.c_int32), ("gap_h", ctypes.c_int32),
+                ("W", ctypes.c_int32), ("H", ctypes.c_int32), ("use_score", ctypes.c_int32),
+                ("use_uv", ctypes.c_int32), ("use_floor", ctypes.c_int32), ("use_large", ctypes.c_int32)]
+
+
 class RowsField(ctypes.Structure):
     _fields_ = [("a", c_void_p), ("b", c_void_p), ("dst", c_void_p), ("n_a", ctypes.c_int64),
                 ("n_b", ctypes.c_int64), ("row_bytes", ctypes.c_int32), ("pad", ctypes.c_int32)]
@@ -349,6 +356,37 @@ def fusion_fitness(box, R, view_pose, view_tc, pst, search_size, cfg: FuseCfg):
     return out
 
 
+def filter_cfg(det_cfg, W, H):
+    """FilterCfg from a config's `detection` section (demo.py:138-148 keys)"""
+    c = FilterCfg()
+    c.use_score = 1
+    c.score_thresh = float(np.float32(det_cfg.get("score_thresh", 0.0)))
+    c.use_uv = int(bool(det_cfg.get("uv_bound", False)))
+    ratio = float(det_cfg.get("uv_bound_value", 1.0))
+    c.gap_w, c.gap_h = int((1 - ratio) * W), int((1 - ratio) * H)     # python float, as the reference
+    c.W, c.H = int(W), int(H)
+    c.use_floor = int(bool(det_cfg.get("floor_mask", False)))
+    fr = float(det_cfg.get("floor_ratio", 20))
+    c.floor_ratio, c.floor_half = float(np.float32(fr)), float(np.float32(fr / 2))
+    lg = det_cfg.get("size_max_thres")
+    c.use_large = int(bool(lg))
+    c.size_max = float(np.float32(lg)) if lg else 0.0
+    return c
+
+
+def detection_filter(scores, proj_xy, box3d, cfg: FilterCfg, with_bits=False):
+    """keep mask (bool, shape of scores) of the demo.py:138-148 filters (bf_detection_filter)"""
+    n = scores.numel()
+    keep = torch.empty(scores.shape, dtype=torch.uint8, device=scores.device)
+    bits = torch.empty(scores.shape, dtype=torch.uint8, device=scores.device) if with_bits else None
+    _check(lib().bf_detection_filter(_ptr(_need(scores.contiguous(), torch.float32, "scores")),
+                                     _ptr(_need(proj_xy.contiguous(), torch.float32, "proj_xy")),
+                                     _ptr(_need(box3d.contiguous(), torch.float32, "box3d")),
+                                     c_int(n), ctypes.byref(cfg), _ptr(keep), _ptr(bits), _stream()),
+           "bf_detection_filter")
+    return (keep.bool(), bits) if with_bits else keep.bool()
+
+
 # ------------------------------------------------------------------------------------------
 # per-frame depth
 # ------------------------------------------------------------------------------------------
@@ -410,34 +448,44 @@ def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype
 
 
 def attention(q, k, v, o, batch, heads, sq, sk, head_dim, scale, q_bs=None, k_bs=None, v_bs=None,
-              o_bs=None):
-    """q/k/v/o are 2-D token-major views [batch*S, >= heads*head_dim] (any row stride)."""
+              o_bs=None, o_map=None):
+    """q/k/v/o are 2-D token-major views [batch*S, >= heads*head_dim] (any row stride).
+    o_map: int32 [batch*sq] output row of each query (< 0: not stored)."""
     for x, n in ((q, "q"), (k, "k"), (v, "v"), (o, "o")):
         _need(x, torch.bfloat16, n)
     q_bs = sq * q.stride(0) if q_bs is None else q_bs
     k_bs = sk * k.stride(0) if k_bs is None else k_bs
     v_bs = sk * v.stride(0) if v_bs is None else v_bs
     o_bs = sq * o.stride(0) if o_bs is None else o_bs
+    if o_map is not None:
+        _need(o_map, torch.int32, "o_map")
+        if o_map.numel() < batch * sq:
+            raise HipError(f"o_map has {o_map.numel()} rows < batch*sq = {batch * sq}")
     LL = ctypes.c_longlong
-    _check(lib().bf_attention_bf16(c_void_p(q.data_ptr()), c_void_p(k.data_ptr()),
-                                   c_void_p(v.data_ptr()), c_void_p(o.data_ptr()), c_int(batch),
-                                   c_int(heads), c_int(sq), c_int(sk), c_int(head_dim),
-                                   c_int(q.stride(0)), c_int(k.stride(0)), c_int(v.stride(0)),
-                                   c_int(o.stride(0)), LL(q_bs), LL(k_bs), LL(v_bs), LL(o_bs),
-                                   c_float(scale), _stream()), "bf_attention_bf16")
+    _check(lib().bf_attention_bf16_omap(c_void_p(q.data_ptr()), c_void_p(k.data_ptr()),
+                                        c_void_p(v.data_ptr()), c_void_p(o.data_ptr()), c_int(batch),
+                                        c_int(heads), c_int(sq), c_int(sk), c_int(head_dim),
+                                        c_int(q.stride(0)), c_int(k.stride(0)), c_int(v.stride(0)),
+                                        c_int(o.stride(0)), LL(q_bs), LL(k_bs), LL(v_bs), LL(o_bs),
+                                        c_float(scale), _ptr(o_map) if o_map is not None else None,
+                                        _stream()), "bf_attention_bf16_omap")
     return o
 
 
-def layernorm(x, weight, bias, eps, out=None, row_map=None):
+def layernorm(x, weight, bias, eps, out=None, row_map=None, out_dtype=torch.bfloat16):
+    """x f32 [M, C] (any row stride) -> LayerNorm rows in bf16 (or f32: out / out_dtype), row r
+    written to row_map[r] of out (< 0 skipped)"""
     _need(x, torch.float32, "x")
     M, C = x.shape
     if out is None:
-        out = torch.empty((M, C), dtype=torch.bfloat16, device=x.device)
-    _check(lib().bf_layernorm(c_void_p(x.data_ptr()), c_int(x.stride(0)), _ptr(weight),
-                              _ptr(bias), c_float(eps), c_void_p(out.data_ptr()),
-                              c_int(out.stride(0)),
-                              _ptr(row_map) if row_map is not None else None, c_int(M), c_int(C),
-                              _stream()), "bf_layernorm")
+        out = torch.empty((M, C), dtype=out_dtype, device=x.device)
+    if out.dtype not in (torch.bfloat16, torch.float32) or x.stride(1) != 1 or out.stride(1) != 1:
+        raise HipError("layernorm: f32 in, bf16 / f32 out, unit column stride")
+    _check(lib().bf_layernorm_out(c_void_p(x.data_ptr()), c_int(x.stride(0)), _ptr(weight),
+                                  _ptr(bias), c_float(eps), c_void_p(out.data_ptr()),
+                                  c_int(out.stride(0)), c_int(int(out.dtype == torch.float32)),
+                                  _ptr(row_map) if row_map is not None else None, c_int(M), c_int(C),
+                                  _stream()), "bf_layernorm_out")
     return out
 
 
@@ -445,16 +493,20 @@ def _f3(vals):
     return (c_float * 3)(*[float(v) for v in vals])
 
 
-def im2col_rgb8(img, pad, patch, mean, std, out=None):
-    """img u8 [B,H,W,3] -> bf16 [B*(pad/patch)^2, 3*patch*patch]"""
+def im2col_rgb8(img, pad, patch, mean, std, out=None, chw=False):
+    """img u8 [B,H,W,3] (chw=True: [B,3,H,W]) -> bf16 [B*(pad/patch)^2, 3*patch*patch]"""
     _need(img, torch.uint8, "img")
-    B, H, W, _ = img.shape
+    if chw:
+        B, _, H, W = img.shape
+    else:
+        B, H, W, _ = img.shape
     n = B * (pad // patch) ** 2
     if out is None:
         out = torch.empty((n, 3 * patch * patch), dtype=torch.bfloat16, device=img.device)
-    _check(lib().bf_im2col_rgb8(_ptr(img), c_int(B), c_int(H), c_int(W), c_int(pad), c_int(patch),
-                                _f3(mean), _f3(std), c_void_p(out.data_ptr()),
-                                c_int(out.stride(0)), _stream()), "bf_im2col_rgb8")
+    _check(lib().bf_im2col_rgb8_chw(_ptr(img), c_int(B), c_int(H), c_int(W), c_int(int(chw)),
+                                    c_int(pad), c_int(patch), _f3(mean), _f3(std),
+                                    c_void_p(out.data_ptr()), c_int(out.stride(0)), _stream()),
+           "bf_im2col_rgb8_chw")
     return out
 
 
@@ -553,15 +605,16 @@ def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype
 
 
 def attention(q, k, v, o, batch, heads, sq, sk, head_dim, scale, q_bs=None, k_bs=None, v_bs=None,
-              o_bs=None):
+              o_bs=None, o_map=None):
     t = _TIMER
     if t is None:
-        return _attention_untimed(q, k, v, o, batch, heads, sq, sk, head_dim, scale, q_bs, k_bs, v_bs, o_bs)
+        return _attention_untimed(q, k, v, o, batch, heads, sq, sk, head_dim, scale, q_bs, k_bs, v_bs,
+                                  o_bs, o_map)
     tags = dict(kind="attn", D=head_dim, sq=sq, sk=sk, batch=batch, heads=heads)
     bh = float(batch * heads)
     return t.record(tags, 4.0 * bh * sq * sk * head_dim, 2.0 * bh * head_dim * (2 * sq + 2 * sk),
                     lambda: _attention_untimed(q, k, v, o, batch, heads, sq, sk, head_dim, scale,
-                                               q_bs, k_bs, v_bs, o_bs))
+                                               q_bs, k_bs, v_bs, o_bs, o_map))
 
 
 # ------------------------------------------------------------------------------------------

@@ -1,0 +1,97 @@
+"""Frame packaging of the reference's capture streams (capture_stream.py:185-311 ScanNet,
+:381-529 CA-1M) for frames already in memory, and a synthetic stream in that format.
+
+`make_sample(rgb, depth, K, pose)` builds the sample dict demo.py iterates over: the CHW uint8
+image and the depth map under sample["wide"], a SensorArrayInfo with the `wide` sensor (image /
+depth infos, T_gravity = camera -> gravity rotation, RT = identity) and the `gt` sensor (the
+camera -> world pose), the frame rotated to the upright orientation first (torch.rot90 on
+whatever device the frame is on).  Reading JPEG / PNG files (cv2.imread) is not part of this
+module: the dataset formats are not available offline.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from boxfusion_amd.measurement import DepthMeasurementInfo, ImageMeasurementInfo
+from boxfusion_amd.sensor import (ImageOrientation, PosedSensorInfo, SensorArrayInfo, camera_to_gravity,
+                                  get_orientation)
+
+# image quarter turns to the upright orientation (orientation.py:29-40 ROT_K)
+ROT_K = {ImageOrientation.UPRIGHT: 0, ImageOrientation.LEFT: -1, ImageOrientation.UPSIDE_DOWN: 2,
+         ImageOrientation.RIGHT: 1}
+# camera roll about its optical axis undone by the rotation (orientation.py:17-27 ROT_Z)
+ROT_Z_ANGLE = {ImageOrientation.UPRIGHT: 0.0, ImageOrientation.LEFT: np.pi / 2,
+               ImageOrientation.UPSIDE_DOWN: np.pi, ImageOrientation.RIGHT: -np.pi / 2}
+
+
+def _rot_z4(angle):
+    c, s = np.cos(angle), np.sin(angle)
+    m = np.eye(4, dtype=np.float32)
+    m[:2, :2] = [[c, -s], [s, c]]
+    return m
+
+
+def make_sample(rgb, depth, K, pose, depth_K=None, video_id=0, index=0):
+    """rgb [H,W,3] uint8 (numpy or tensor), depth [Hd,Wd] f32 metres, K [3,3] image intrinsics
+    (depth_K: the depth map's, default K scaled to its width), pose [4,4] camera -> world"""
+    rgb_t = rgb if isinstance(rgb, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(rgb))
+    dep_t = depth if isinstance(depth, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(depth))
+    H, W = rgb_t.shape[:2]
+    Hd, Wd = dep_t.shape[-2:]
+    K = np.asarray(K, np.float32)
+    if depth_K is None:
+        depth_K = K.copy()
+        depth_K[:2] *= Wd / W
+    wide = PosedSensorInfo()
+    wide.image = ImageMeasurementInfo(size=(W, H), K=torch.from_numpy(K)[None])
+    depth_info = DepthMeasurementInfo(size=(Wd, Hd), K=torch.from_numpy(np.asarray(depth_K, np.float32))[None])
+    wide.depth = depth_info
+    pose = np.asarray(pose, np.float32)
+    cur = get_orientation(pose)
+    T_gravity = torch.from_numpy(camera_to_gravity(pose, cur))
+    image = rgb_t.permute(2, 0, 1)[None]
+    dep = dep_t.float()[None]
+    k = ROT_K[cur]
+    if k:
+        image = torch.rot90(image, k, dims=(-2, -1))
+        dep = torch.rot90(dep, k, dims=(-2, -1))
+    up = PosedSensorInfo()
+    up.image = wide.image.orient(cur, ImageOrientation.UPRIGHT)
+    up.depth = wide.depth.orient(cur, ImageOrientation.UPRIGHT)
+    up.RT = torch.eye(4)[None]            # "no need for pose anymore" (capture_stream.py:296)
+    up.T_gravity = T_gravity[None]
+    gt = PosedSensorInfo()
+    gt.RT = torch.from_numpy(pose)[None]
+    gt.depth = depth_info
+    si = SensorArrayInfo()
+    si.wide = up
+    si.gt = gt
+    return {"wide": {"image": image.contiguous(), "depth": dep.contiguous()},
+            "meta": dict(video_id=video_id, timestamp=index), "sensor_info": si}
+
+
+class SyntheticDataset:
+    """the seeded synthetic RGB-D stream (boxfusion_amd.synthetic) as demo.py's dataset:
+    iterable of samples, len() frames"""
+
+    def __init__(self, n_frames=1000, H=480, W=640, K=None, depth_ratio=1, scene=None):
+        from boxfusion_amd.synthetic import SCANNET_K, Scene
+        self.n, self.H, self.W, self.r = n_frames, H, W, depth_ratio
+        self.K = np.asarray(SCANNET_K if K is None else K, np.float32)
+        self.scene = scene if scene is not None else Scene()
+
+    def __len__(self):
+        return self.n
+
+    def frame(self, i):
+        from boxfusion_amd.synthetic import frame_rgbd
+        rgb, depth = frame_rgbd(i, self.H, self.W)
+        if self.r > 1:
+            depth = np.ascontiguousarray(depth[::self.r, ::self.r])
+        return rgb, depth, self.scene.pose(i)
+
+    def __iter__(self):
+        for i in range(self.n):
+            rgb, depth, pose = self.frame(i)
+            yield make_sample(rgb, depth, self.K, pose, index=i)

@@ -39,6 +39,17 @@ __device__ __forceinline__ u16 at_f2bf(float f) {
     return *reinterpret_cast<u16*>(&b);
 }
 
+// element offset of output row (batch b, query q): b*o_bs + q*o_rs, or through o_map (row
+// o_map[b*sq + q] of O, < 0 = not stored): the window attention writes its rows straight back in
+// token order, pad queries dropped, so the proj GEMM runs on the real rows only
+__device__ __forceinline__ long long attn_out_offset(const int32_t* __restrict__ o_map, int b, int q,
+                                                     int sq, long long o_bs, int o_rs) {
+    if (!o_map) return b * o_bs + (long long)q * o_rs;
+    if (q >= sq) return -1;
+    const int r = o_map[(long long)b * sq + q];
+    return r < 0 ? -1 : (long long)r * o_rs;
+}
+
 // NW waves of 32 queries per workgroup; NT key tiles resident in LDS at once: NT == 1 streams
 // the keys tile by tile, NT > 1 (short sequences, sk <= 64*NT) stages every key and V^T column
 // of the (batch, head) once and runs the whole key loop without barriers.
@@ -47,7 +58,8 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const u16* __restrict__ Q, con
                                                      const u16* __restrict__ V, u16* __restrict__ O,
                                                      int sq, int sk, int q_rs, int k_rs, int v_rs,
                                                      int o_rs, long long q_bs, long long k_bs,
-                                                     long long v_bs, long long o_bs, float scale_log2) {
+                                                     long long v_bs, long long o_bs, float scale_log2,
+                                                     const int32_t* __restrict__ o_map) {
     constexpr int KS = D / 16;            // k16 steps over the head dim
     constexpr int DB = (D + 31) / 32;     // 32-row blocks of O^T
     constexpr int DP = DB * 32;           // padded head dim (V^T rows)
@@ -182,9 +194,10 @@ __global__ void __launch_bounds__(NW * 64) k_attn(const u16* __restrict__ Q, con
         }
     }
     // ---- normalise and store O[q][h*D + d] (4 consecutive d per register group) -------------
-    if (q < sq) {
+    const long long o_off = attn_out_offset(o_map, b, q, sq, o_bs, o_rs);
+    if (q < sq && o_off >= 0) {
         const float inv = 1.0f / l_run;
-        u16* orow = O + b * o_bs + (size_t)q * o_rs + h * D;
+        u16* orow = O + o_off + h * D;
 #pragma unroll
         for (int db = 0; db < DB; ++db)
 #pragma unroll
@@ -267,7 +280,8 @@ __global__ void __launch_bounds__(NW * 64) k_attn_s(const u16* __restrict__ Q, c
                                                        const u16* __restrict__ V, u16* __restrict__ O,
                                                        int sq, int sk, int q_rs, int k_rs, int v_rs,
                                                        int o_rs, long long q_bs, long long k_bs,
-                                                       long long v_bs, long long o_bs, float scale_log2) {
+                                                       long long v_bs, long long o_bs, float scale_log2,
+                                                     const int32_t* __restrict__ o_map) {
     constexpr int KS = D / 16;
     constexpr int DB = (D + 31) / 32;
     constexpr int KROW = D + 8;
@@ -391,9 +405,10 @@ __global__ void __launch_bounds__(NW * 64) k_attn_s(const u16* __restrict__ Q, c
         if (more) { ATS_STORE(buf ^ 1); }
         __syncthreads();
     }
-    if (q < sq) {
+    const long long o_off = attn_out_offset(o_map, b, q, sq, o_bs, o_rs);
+    if (q < sq && o_off >= 0) {
         const float inv = 1.0f / l_run;
-        u16* orow = O + b * o_bs + (size_t)q * o_rs + h * D;
+        u16* orow = O + o_off + h * D;
 #pragma unroll
         for (int db = 0; db < DB; ++db)
 #pragma unroll
@@ -462,7 +477,8 @@ __global__ void __launch_bounds__(NW * 64) k_attn_r(const u16* __restrict__ Q, c
                                                        const u16* __restrict__ V, u16* __restrict__ O,
                                                        int sq, int sk, int q_rs, int k_rs, int v_rs,
                                                        int o_rs, long long q_bs, long long k_bs,
-                                                       long long v_bs, long long o_bs, float scale_log2) {
+                                                       long long v_bs, long long o_bs, float scale_log2,
+                                                     const int32_t* __restrict__ o_map) {
     constexpr int KS = D / 16;
     constexpr int DB = (D + 31) / 32;
     constexpr int ROWS = NTILE * AT_KT;
@@ -583,9 +599,10 @@ __global__ void __launch_bounds__(NW * 64) k_attn_r(const u16* __restrict__ Q, c
                 }
         }
     }
-    if (q < sq) {
+    const long long o_off = attn_out_offset(o_map, b, q, sq, o_bs, o_rs);
+    if (q < sq && o_off >= 0) {
         const float inv = 1.0f / l_run;
-        u16* orow = O + b * o_bs + (size_t)q * o_rs + h * D;
+        u16* orow = O + o_off + h * D;
 #pragma unroll
         for (int db = 0; db < DB; ++db)
 #pragma unroll
@@ -604,7 +621,8 @@ __global__ void __launch_bounds__(NW * 64) k_attn_r(const u16* __restrict__ Q, c
 template <int D, int NW, int NTILE>
 static void launch_attn_r(dim3 grid, hipStream_t st, const void* q, const void* k, const void* v, void* o,
                           int sq, int sk, int q_rs, int k_rs, int v_rs, int o_rs, long long q_bs,
-                          long long k_bs, long long v_bs, long long o_bs, float sl2) {
+                          long long k_bs, long long v_bs, long long o_bs, float sl2,
+                          const int32_t* o_map) {
     constexpr size_t lds = (size_t)NW * 32 * D * 2 + 2 * (size_t)NTILE * AT_KT * D * 2 + 64;
     static bool attr = false;
     if (!attr) {
@@ -614,7 +632,7 @@ static void launch_attn_r(dim3 grid, hipStream_t st, const void* q, const void* 
     }
     hipLaunchKernelGGL((k_attn_r<D, NW, NTILE>), grid, dim3(NW * 64), lds, st, (const u16*)q,
                        (const u16*)k, (const u16*)v, (u16*)o, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs,
-                       k_bs, v_bs, o_bs, sl2);
+                       k_bs, v_bs, o_bs, sl2, o_map);
 }
 
 // 1/2: k_attn_s, 3: k_attn_r for short sequences, 4/5: k_attn_s with 5/3 waves per workgroup for
@@ -625,10 +643,10 @@ static int g_attn_variant = [] {
 }();
 BF_API void bf_attention_set_variant(int v) { g_attn_variant = v; }
 
-BF_API int bf_attention_bf16(const void* q, const void* k, const void* v, void* o, int batch,
-                             int heads, int sq, int sk, int head_dim, int q_rs, int k_rs, int v_rs,
-                             int o_rs, long long q_bs, long long k_bs, long long v_bs,
-                             long long o_bs, float scale, void* stream) {
+BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, void* o, int batch,
+                                  int heads, int sq, int sk, int head_dim, int q_rs, int k_rs,
+                                  int v_rs, int o_rs, long long q_bs, long long k_bs, long long v_bs,
+                                  long long o_bs, float scale, const int32_t* o_map, void* stream) {
     if (!q || !k || !v || !o || batch <= 0 || heads <= 0 || sq <= 0 || sk <= 0) return BF_ERR_ARG;
     if ((q_rs | k_rs | v_rs) % 8 != 0 || o_rs % 4 != 0) return BF_ERR_UNSUPPORTED;
     const float sl2 = scale * 1.4426950408889634f;
@@ -642,10 +660,10 @@ BF_API int bf_attention_bf16(const void* q, const void* k, const void* v, void* 
         const dim3 grid(1, heads, batch);
         if (head_dim == 80)
             launch_attn_r<80, 9, 5>(grid, bf_stream(stream), q, k, v, o, sq, sk, q_rs, k_rs, v_rs, o_rs,
-                                    q_bs, k_bs, v_bs, o_bs, sl2);
+                                    q_bs, k_bs, v_bs, o_bs, sl2, o_map);
         else
             launch_attn_r<64, 9, 5>(grid, bf_stream(stream), q, k, v, o, sq, sk, q_rs, k_rs, v_rs, o_rs,
-                                    q_bs, k_bs, v_bs, o_bs, sl2);
+                                    q_bs, k_bs, v_bs, o_bs, sl2, o_map);
         return bf_check_launch();
     }
     if (g_attn_variant >= 1) {
@@ -653,7 +671,7 @@ BF_API int bf_attention_bf16(const void* q, const void* k, const void* v, void* 
     hipLaunchKernelGGL((k_attn_s<DD, NWV>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch),   \
                        dim3(NWV * 64), 0, bf_stream(stream), (const u16*)q, (const u16*)k,          \
                        (const u16*)v, (u16*)o, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs,    \
-                       o_bs, sl2)
+                       o_bs, sl2, o_map)
 #define LAUNCH_SD(DD)                                                                             \
     if (nw_one > 4 && nw_one <= 9) {                                                              \
         if (g_attn_variant == 4) { LAUNCH_S(DD, 5); }                                             \
@@ -675,7 +693,7 @@ BF_API int bf_attention_bf16(const void* q, const void* k, const void* v, void* 
     hipLaunchKernelGGL((k_attn<DD, NWV, NTV>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch), \
                        dim3(NWV * 64), 0, bf_stream(stream), (const u16*)q, (const u16*)k,          \
                        (const u16*)v, (u16*)o, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs,    \
-                       o_bs, sl2)
+                       o_bs, sl2, o_map)
 #define LAUNCH(DD)                                                                                \
     if (nw_one > 4 && nw_one <= 9 && sk <= 5 * AT_KT) { LAUNCH_NW(DD, 9, 5); }                     \
     else if (nw_one > 4 && nw_one <= 9) { LAUNCH_NW(DD, 9, 1); }                                  \
@@ -693,4 +711,12 @@ BF_API int bf_attention_bf16(const void* q, const void* k, const void* v, void* 
 #undef LAUNCH_STREAM
 #undef LAUNCH_NW
     return bf_check_launch();
+}
+
+BF_API int bf_attention_bf16(const void* q, const void* k, const void* v, void* o, int batch,
+                             int heads, int sq, int sk, int head_dim, int q_rs, int k_rs, int v_rs,
+                             int o_rs, long long q_bs, long long k_bs, long long v_bs,
+                             long long o_bs, float scale, void* stream) {
+    return bf_attention_bf16_omap(q, k, v, o, batch, heads, sq, sk, head_dim, q_rs, k_rs, v_rs, o_rs,
+                                  q_bs, k_bs, v_bs, o_bs, scale, nullptr, stream);
 }

@@ -350,3 +350,47 @@ BF_API int bf_depth_standardize(const float* depth, int b, int h, int w, float* 
                        out, params);
     return bf_check_launch();
 }
+
+// ------------------------------------------------------------------------------------------
+// detection filters of demo.py:138-148 (box_manager.py:217-245) over a batch of frames' top-k
+// instances, one thread per instance: keep = score >= thr & uv inside [gap, size - gap] & !floor
+// & !large.  Every comparison in f32 like the reference's torch ops on f32 tensors (a python
+// scalar operand is rounded to f32); bits 1..4 of `bits` record each filter's own mask.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_detection_filter(const float* __restrict__ scores,
+                                                          const float* __restrict__ proj_xy,
+                                                          const float* __restrict__ box3d, int n,
+                                                          bf_filter_cfg cfg, uint8_t* __restrict__ keep,
+                                                          uint8_t* __restrict__ bits) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const bool s_ok = scores[i] >= cfg.score_thresh;
+    const float u = proj_xy[2 * i], v = proj_xy[2 * i + 1];
+    const bool uv_ok = (u > (float)cfg.gap_w) & (u < (float)(cfg.W - cfg.gap_w)) &
+                       (v > (float)cfg.gap_h) & (v < (float)(cfg.H - cfg.gap_h));
+    const float a = box3d[6 * i + 3], b = box3d[6 * i + 4], c = box3d[6 * i + 5];
+    const float mx = fmaxf(fmaxf(a, b), c), mn = fminf(fminf(a, b), c);
+    // second largest of three (torch.sort(descending)[:, 1])
+    const float second = fmaxf(fminf(a, b), fminf(fmaxf(a, b), c));
+    const float q = mx / mn;
+    bool floor_m = q > cfg.floor_ratio;
+    floor_m |= (q > cfg.floor_half) & (mx / second > cfg.floor_half) & (second / mn < 2.0f) &
+               (second < 0.15f) & (mn < 0.15f);
+    const bool large_m = mx > cfg.size_max;
+    bool k = true;
+    if (cfg.use_score) k &= s_ok;
+    if (cfg.use_uv) k &= uv_ok;
+    if (cfg.use_floor) k &= !floor_m;
+    if (cfg.use_large) k &= !large_m;
+    keep[i] = k ? 1 : 0;
+    if (bits) bits[i] = (uint8_t)((s_ok ? 2 : 0) | (uv_ok ? 4 : 0) | (floor_m ? 8 : 0) | (large_m ? 16 : 0));
+}
+
+BF_API int bf_detection_filter(const float* scores, const float* proj_xy, const float* box3d, int n,
+                               const bf_filter_cfg* cfg, uint8_t* keep, uint8_t* bits, void* stream) {
+    if (!scores || !proj_xy || !box3d || !cfg || !keep || n < 0) return BF_ERR_ARG;
+    if (n == 0) return BF_OK;
+    hipLaunchKernelGGL(k_detection_filter, dim3(bf_cdiv(n, 256)), dim3(256), 0, bf_stream(stream),
+                       scores, proj_xy, box3d, n, *cfg, keep, bits);
+    return bf_check_launch();
+}

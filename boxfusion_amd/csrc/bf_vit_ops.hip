@@ -23,11 +23,11 @@ struct alignas(16) W128 {
 // ------------------------------------------------------------------------------------------
 // LayerNorm: one wave per row, C <= 4096, C % 4 == 0
 // ------------------------------------------------------------------------------------------
-template <int NPL>  // float4 per lane
+template <int NPL, bool F32OUT>  // float4 per lane; f32 or bf16 output
 __global__ void __launch_bounds__(256) k_layernorm(const float* __restrict__ x, int ldx,
                                                    const float* __restrict__ g,
                                                    const float* __restrict__ bb, float eps,
-                                                   u16* __restrict__ out, int ldo,
+                                                   void* __restrict__ out_, int ldo,
                                                    const int32_t* __restrict__ row_map, int M,
                                                    int C) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -60,7 +60,22 @@ __global__ void __launch_bounds__(256) k_layernorm(const float* __restrict__ x, 
     const float rstd = rsqrtf(q / (float)C + eps);
     const int orow = row_map ? row_map[row] : row;
     if (orow < 0) return;
-    u16* yr = out + (size_t)orow * ldo;
+    if (F32OUT) {      // (in place allowed: the row is in registers before the first store)
+        float* yr = static_cast<float*>(out_) + (size_t)orow * ldo;
+#pragma unroll
+        for (int i = 0; i < NPL; ++i) {
+            int c = (lane + 64 * i) * 4;
+            if (c < C) {
+                float4 gg = *reinterpret_cast<const float4*>(g + c);
+                float4 be = *reinterpret_cast<const float4*>(bb + c);
+                *reinterpret_cast<float4*>(yr + c) =
+                    make_float4((v[i].x - mean) * rstd * gg.x + be.x, (v[i].y - mean) * rstd * gg.y + be.y,
+                                (v[i].z - mean) * rstd * gg.z + be.z, (v[i].w - mean) * rstd * gg.w + be.w);
+            }
+        }
+        return;
+    }
+    u16* yr = static_cast<u16*>(out_) + (size_t)orow * ldo;
 #pragma unroll
     for (int i = 0; i < NPL; ++i) {
         int c = (lane + 64 * i) * 4;
@@ -76,15 +91,19 @@ __global__ void __launch_bounds__(256) k_layernorm(const float* __restrict__ x, 
     }
 }
 
-BF_API int bf_layernorm(const float* x, int ldx, const float* gamma, const float* beta, float eps,
-                        void* out, int ldo, const int32_t* row_map, int M, int C, void* stream) {
+BF_API int bf_layernorm_out(const float* x, int ldx, const float* gamma, const float* beta, float eps,
+                            void* out, int ldo, int out_f32, const int32_t* row_map, int M, int C,
+                            void* stream) {
     if (!x || !gamma || !beta || !out || M < 0 || C <= 0 || C % 4 || ldx % 4 || ldo % 4)
         return BF_ERR_ARG;
     if (M == 0) return BF_OK;
     dim3 grid((M + 3) / 4), block(256);
     const int npl = (C / 4 + 63) / 64;
-#define LN(N) hipLaunchKernelGGL(k_layernorm<N>, grid, block, 0, bf_stream(stream), x, ldx, gamma, \
-                                 beta, eps, (u16*)out, ldo, row_map, M, C)
+#define LN(N)                                                                                      \
+    if (out_f32) hipLaunchKernelGGL((k_layernorm<N, true>), grid, block, 0, bf_stream(stream), x,  \
+                                    ldx, gamma, beta, eps, out, ldo, row_map, M, C);               \
+    else hipLaunchKernelGGL((k_layernorm<N, false>), grid, block, 0, bf_stream(stream), x, ldx,    \
+                            gamma, beta, eps, out, ldo, row_map, M, C)
     if (npl <= 1) LN(1);
     else if (npl <= 2) LN(2);
     else if (npl <= 3) LN(3);
@@ -97,12 +116,20 @@ BF_API int bf_layernorm(const float* x, int ldx, const float* gamma, const float
     return bf_check_launch();
 }
 
+BF_API int bf_layernorm(const float* x, int ldx, const float* gamma, const float* beta, float eps,
+                        void* out, int ldo, const int32_t* row_map, int M, int C, void* stream) {
+    return bf_layernorm_out(x, ldx, gamma, beta, eps, out, ldo, 0, row_map, M, C, stream);
+}
+
 // ------------------------------------------------------------------------------------------
 // RGB u8 HWC -> normalised, zero-padded to a square of `pad`, patch im2col (K = 3*p*p ordered
 // c, ky, kx like the Conv2d weight), bf16.  One thread per 8 consecutive K elements (same c, ky).
 // ------------------------------------------------------------------------------------------
+// pixel (b, c, y, x) at img[b*sb + c*sc + y*sy + x*sx]: HWC frames (sc = 1, sx = 3) as decoded,
+// or CHW (sx = 1, sc = H*W) as the reference's capture stream hands them over (capture_stream.py:221)
 __global__ void __launch_bounds__(256) k_im2col_rgb8(const uint8_t* __restrict__ img, int B, int H,
-                                                     int W, int pad, int p, float m0, float m1,
+                                                     int W, long long sb, long long sc, long long sy,
+                                                     int sx, int pad, int p, float m0, float m1,
                                                      float m2, float s0, float s1, float s2,
                                                      u16* __restrict__ out, int ldo) {
     const int np = pad / p;
@@ -126,7 +153,7 @@ __global__ void __launch_bounds__(256) k_im2col_rgb8(const uint8_t* __restrict__
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int x = px * p + kx0 + i;
-        const float px_v = (float)img[(((size_t)b * H + min(y, H - 1)) * W + min(x, W - 1)) * 3 + c];
+        const float px_v = (float)img[b * sb + c * sc + min(y, H - 1) * sy + (long long)min(x, W - 1) * sx];
         v[i] = vf2bf((y < H && x < W) ? (px_v - mean) / sd : 0.f);
     }
     W128 w = {(uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2] | ((uint32_t)v[3] << 16),
@@ -134,16 +161,25 @@ __global__ void __launch_bounds__(256) k_im2col_rgb8(const uint8_t* __restrict__
     *reinterpret_cast<W128*>(out + (size_t)prow * ldo + k0) = w;
 }
 
-BF_API int bf_im2col_rgb8(const uint8_t* img, int B, int H, int W, int pad, int patch,
-                          const float* mean3, const float* std3, void* out, int ldo, void* stream) {
-    if (!img || !out || !mean3 || !std3 || B <= 0 || pad % patch || (3 * patch * patch) % 8 || ldo % 8)
+BF_API int bf_im2col_rgb8_chw(const uint8_t* img, int B, int H, int W, int chw, int pad, int patch,
+                              const float* mean3, const float* std3, void* out, int ldo, void* stream) {
+    if (!img || !out || !mean3 || !std3 || B <= 0 || H <= 0 || W <= 0 || pad % patch ||
+        (3 * patch * patch) % 8 || ldo % 8 || H > pad || W > pad)
         return BF_ERR_ARG;
     const int np = pad / patch;
     const long long total = (long long)B * np * np * (3 * patch * patch / 8);
+    const long long hw = (long long)H * W;
+    const long long sb = 3 * hw, sc = chw ? hw : 1, sy = chw ? W : 3 * (long long)W;
+    const int sx = chw ? 1 : 3;
     hipLaunchKernelGGL(k_im2col_rgb8, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                       bf_stream(stream), img, B, H, W, pad, patch, mean3[0], mean3[1], mean3[2],
-                       std3[0], std3[1], std3[2], (u16*)out, ldo);
+                       bf_stream(stream), img, B, H, W, sb, sc, sy, sx, pad, patch, mean3[0],
+                       mean3[1], mean3[2], std3[0], std3[1], std3[2], (u16*)out, ldo);
     return bf_check_launch();
+}
+
+BF_API int bf_im2col_rgb8(const uint8_t* img, int B, int H, int W, int pad, int patch,
+                          const float* mean3, const float* std3, void* out, int ldo, void* stream) {
+    return bf_im2col_rgb8_chw(img, B, H, W, 0, pad, patch, mean3, std3, out, ldo, stream);
 }
 
 // single-channel f32 (standardised depth) -> zero-padded square -> im2col (K = p*p)

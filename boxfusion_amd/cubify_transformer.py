@@ -434,10 +434,36 @@ class CubifyTransformer(nn.Module):
     def device(self):
         return self.pixel_mean.device
 
-    # ---- full fp32 forward ---------------------------------------------------------------------
-    def forward(self, batch: FrameBatch) -> List[Instances3D]:
+    # ---- forward -----------------------------------------------------------------------------
+    def forward(self, batch) -> List[Instances3D]:
+        """`model(packaged)` (demo.py:135): the BatchedSensors dict of Preprocessor.preprocess runs
+        on the MI355X engine (forward_sensors); a FrameBatch of materialised tensors runs the fp32
+        definition of the maths (the parity reference of the tests)."""
+        if isinstance(batch, dict):
+            return self.forward_sensors(batch)
         feat = self.backbone.backbone.forward_tensors(batch.image, batch.depth)
         return self.decode(feat, batch)
+
+    def forward_sensors(self, batched_sensors, sensor_name="wide"):
+        """CubifyTransformer.inference (cubify_transformer.py:1172-1227) for the reference's input
+        structure on the MI355X engine.  One CuTREngine is kept per (batch, frame size, pad,
+        depth ratio, device).  Device tensors only: there is no CPU path."""
+        from boxfusion_amd import _lib
+        from boxfusion_amd.engine import CuTREngine
+        x = sensor_inputs(batched_sensors, sensor_name)
+        raw = x["image_raw"]
+        if not raw.is_cuda:
+            raise _lib.HipError("boxfusion_amd runs on the HIP device: move the inputs with "
+                                "move_input_to_current_device(packaged, model.pixel_mean) first")
+        if self.backbone.backbone.depth_modality and x["depth_std"] is None:
+            raise _lib.HipError("depth model without a depth measurement")
+        B, _, H, W = raw.shape
+        key = (B, H, W, x["pad"], x["ratio"], raw.device)
+        engines = self.__dict__.setdefault("_engines", {})
+        if key not in engines:
+            engines[key] = CuTREngine(self, B, H, W, pad=x["pad"], device=raw.device, depth_ratio=x["ratio"])
+        return engines[key](raw.contiguous(), x["depth_std"], x["depth_params"], x["K"], x["T_gravity"],
+                            x["image_sizes"], chw=True, pixel_mean=x["pixel_mean"], pixel_std=x["pixel_std"])
 
     def _memory_kv(self, src, pos):
         """Every decoder layer's cross-attention k(src + pos) and v(src) in one GEMM each (the
@@ -538,6 +564,47 @@ class CubifyTransformer(nn.Module):
         r.object_desc = st["object_desc"][i][boxes_i]
         r.pred_proj_xy = st["pred_proj_xy"][i][boxes_i]
         return r
+
+
+def sensor_inputs(batched_sensors, sensor_name="wide"):
+    """what the detector reads from Preprocessor.preprocess's BatchedSensors (device agnostic):
+    the unpadded uint8 [B,3,H,W] frames (ImageList.raw) and their normalisation constants, the
+    standardised depth [B,H/r,W/r] + whitening parameters (cubify_transformer.py:568-586), the
+    image K (pos.py:64, :983-986), T_gravity (:991-992), image sizes, square pads and the
+    rgb -> depth ratio"""
+    sensor = batched_sensors[sensor_name]
+    img = sensor["image"]
+    raw = img.data.raw
+    if raw is None or raw.dtype != torch.uint8 or raw.dim() != 4:
+        raise ValueError("expected the uint8 [B,3,H,W] frames of Preprocessor.batch")
+    consts = getattr(img, "normalize_consts", None)
+    if consts is None:
+        raise ValueError("the image measurement was not normalised by Preprocessor.normalize")
+    dev = raw.device
+    dep = sensor.get("depth")
+    sens = img.sensor
+    out = dict(image_raw=raw, image=img.data, pixel_mean=consts[0], pixel_std=consts[1],
+               pad=int(img.data.padded_hw[0]),
+               K=torch.stack([info.K[-1] for info in img.info]).to(dev, torch.float32),
+               T_gravity=(torch.stack([s_.T_gravity[-1] for s_ in sens]).to(dev, torch.float32)
+                          if all(s_.has("T_gravity") for s_ in sens) else None),
+               image_sizes=[tuple(int(v) for v in s_) for s_ in img.data.image_sizes],
+               ratio=int(getattr(dep, "rgb_to_depth_ratio", 1)) if dep is not None else 1,
+               depth=dep.data if dep is not None else None, depth_std=None, depth_params=None)
+    if dep is not None:
+        out["depth_std"] = dep.data.raw.to(torch.float32).contiguous()
+        out["depth_params"] = torch.stack([torch.as_tensor(i.parameters).reshape(-1)[:2]
+                                           for i in dep.info]).to(dev, torch.float32)
+    return out
+
+
+def frame_batch(batched_sensors, sensor_name="wide"):
+    """FrameBatch of the materialised (normalised, zero-padded) tensors -- the fp32 definition's
+    input (tests: the same extraction as the engine path)"""
+    x = sensor_inputs(batched_sensors, sensor_name)
+    return FrameBatch(image=x["image"].tensor, depth=x["depth"].tensor if x["depth"] is not None else None,
+                      depth_params=x["depth_params"], K=x["K"], T_gravity=x["T_gravity"],
+                      image_sizes=x["image_sizes"])
 
 
 def make_cubify_transformer(dimension, depth_model, embed_dim=256):

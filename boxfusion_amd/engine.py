@@ -24,7 +24,7 @@ import torch.nn.functional as F
 from boxfusion_amd import _lib
 from boxfusion_amd.clip import CLIP_MEAN, CLIP_STD
 from boxfusion_amd.cubify_transformer import FrameBatch
-from boxfusion_amd.preprocessor import PIXEL_MEAN_U8, PIXEL_STD_U8
+from boxfusion_amd.preprocessor import PIXEL_MEAN, PIXEL_STD
 from boxfusion_amd.vit import get_abs_pos
 
 
@@ -37,97 +37,157 @@ def _f(w):
 
 
 class CuTREngine:
-    def __init__(self, model, batch, height=480, width=640, pad=640, device="cuda"):
+    """CuTR backbone (+ decode) for a batch of B frames of one size on the MI355X kernels.
+
+    depth_ratio r in {1, 2, 4}: the depth map is (H/r, W/r) and padded to pad/r (preprocessor.py:
+    159-174); its token grid is g/r with windows of ws/r (vit.py:286-300, DEPTH_WINDOW_SIZES), so
+    a joint window holds ws^2 RGB + (ws/r)^2 depth tokens (vit.py:178-199).  A model without depth
+    (depth_model=False) runs RGB-only windows, its layer scales folded into the proj / fc2
+    weights and its encoder_norm on the output (vit.py:303-342, 473)."""
+
+    def __init__(self, model, batch, height=480, width=640, pad=640, device="cuda", depth_ratio=1):
         dev = torch.device(device)
         self.model = model.to(dev).eval()
         vit = model.backbone.backbone
         self.dev, self.B, self.H, self.W, self.P = dev, batch, height, width, pad
         self.C, self.heads = vit.embed_dim, vit.num_heads
         self.D = self.C // self.heads
-        self.g = pad // vit.patch_size
+        p = vit.patch_size
+        if pad % p or height > pad or width > pad:
+            raise ValueError(f"frame {height}x{width} does not fit the {pad} square")
+        self.g = pad // p
         self.ws = vit.window_size
         self.nwx = math.ceil(self.g / self.ws)
         self.nw = self.nwx * self.nwx
         self.T = self.g * self.g
-        self.win_rows = 2 * self.ws * self.ws          # joint rgb+depth tokens per window
-        C, B, T = self.C, self.B, self.T
+        self.has_depth = bool(vit.depth_modality)
+        if self.has_depth:
+            r = int(depth_ratio)
+            if r not in (1, 2, 4) or pad % (p * r) or self.ws % r:
+                raise ValueError(f"unsupported rgb -> depth ratio {depth_ratio} for pad {pad}")
+            self.r = r
+            self.Pd = pad // r
+            self.gd = self.g // r
+            self.wsd = self.ws // r
+            if math.ceil(self.gd / self.wsd) != self.nwx:
+                raise ValueError("depth windows do not pair with the RGB windows")
+            self.Td = self.gd * self.gd
+        else:
+            self.r, self.Pd, self.gd, self.wsd, self.Td = None, 0, 0, 0, 0
+        self.win_rgb = self.ws * self.ws
+        self.win_rows = self.win_rgb + self.wsd * self.wsd      # joint rgb + depth tokens per window
+        C, B, T, Td = self.C, self.B, self.T, self.Td
         # ---- weights ----------------------------------------------------------------------
         self.patch_w = _bf(vit.patch_embed.proj.weight.reshape(C, -1))
         self.patch_b = _f(vit.patch_embed.proj.bias)
-        self.patchd_w = _bf(vit.patch_embed_depth.proj.weight.reshape(C, -1))
-        self.patchd_b = _f(vit.patch_embed_depth.proj.bias)
         with torch.no_grad():
             self.pos = _f(get_abs_pos(vit.pos_embed, vit.pretrain_use_cls_token, (self.g, self.g)).reshape(T, C))
-            self.posd = _f(get_abs_pos(vit.pos_embed_depth, vit.pretrain_use_cls_token, (self.g, self.g)).reshape(T, C))
+            if self.has_depth:
+                self.patchd_w = _bf(vit.patch_embed_depth.proj.weight.reshape(C, -1))
+                self.patchd_b = _f(vit.patch_embed_depth.proj.bias)
+                self.posd = _f(get_abs_pos(vit.pos_embed_depth, vit.pretrain_use_cls_token,
+                                           (self.gd, self.gd)).reshape(Td, C))
         self.blocks = []
-        for i, blk in enumerate(vit.blocks):
+        for blk in vit.blocks:
+            proj_w, proj_b = blk.attn.proj.weight, blk.attn.proj.bias
+            fc2_w, fc2_b = blk.mlp.fc2.weight, blk.mlp.fc2.bias
+            with torch.no_grad():
+                if blk.ls1 is not None:      # x + gamma * (W h + b) = x + (gamma W) h + gamma b
+                    proj_w, proj_b = blk.ls1.gamma[:, None] * proj_w, blk.ls1.gamma * proj_b
+                if blk.ls2 is not None:
+                    fc2_w, fc2_b = blk.ls2.gamma[:, None] * fc2_w, blk.ls2.gamma * fc2_b
             self.blocks.append(dict(
-                window=blk.window_size > 0, depth=blk.depth_modality,
+                window=blk.window_size > 0, depth=bool(blk.depth_modality) and self.has_depth,
                 n1=(_f(blk.norm1.weight), _f(blk.norm1.bias), blk.norm1.eps),
                 n2=(_f(blk.norm2.weight), _f(blk.norm2.bias), blk.norm2.eps),
                 qkv=(_bf(blk.attn.qkv.weight), _f(blk.attn.qkv.bias)),
-                proj=(_bf(blk.attn.proj.weight), _f(blk.attn.proj.bias)),
+                proj=(_bf(proj_w), _f(proj_b)),
                 fc1=(_bf(blk.mlp.fc1.weight), _f(blk.mlp.fc1.bias)),
-                fc2=(_bf(blk.mlp.fc2.weight), _f(blk.mlp.fc2.bias))))
+                fc2=(_bf(fc2_w), _f(fc2_b))))
+        en = vit.encoder_norm
+        self.enc_norm = None if isinstance(en, torch.nn.Identity) else (_f(en.weight), _f(en.bias), en.eps)
         depth_blocks = [i for i, b in enumerate(self.blocks) if b["depth"]]
         self.last_depth = max(depth_blocks) if depth_blocks else -1
         # ---- buffers ----------------------------------------------------------------------
         bf16, f32 = dict(dtype=torch.bfloat16, device=dev), dict(dtype=torch.float32, device=dev)
         nwr = B * self.nw * self.win_rows
-        self.X = torch.zeros((2 * B * T, C), **f32)
-        self.LNW = torch.zeros((nwr, C), **bf16)
-        self.QKV = torch.empty((nwr, 3 * C), **bf16)
-        self.ATT = torch.zeros((nwr, C), **bf16)
-        self.LN2 = torch.empty((2 * B * T, C), **bf16)
-        self.H1 = torch.empty((2 * B * T, 4 * C), **bf16)
-        self.A_rgb = torch.empty((B * T, 3 * 16 * 16), **bf16)
-        self.A_d = torch.empty((B * T, 16 * 16), **bf16)
+        rows = B * T + B * Td                                    # rgb rows, then depth rows
+        self.rows = rows
+        self.X = torch.zeros((rows, C), **f32)
+        self.LNW = torch.zeros((nwr, C), **bf16)                 # pad rows stay zero
+        self.QKV = torch.empty((max(nwr, B * T), 3 * C), **bf16)
+        self.ATT = torch.zeros((rows, C), **bf16)                # token order (window_unpartition)
+        self.LN2 = torch.empty((rows, C), **bf16)
+        self.H1 = torch.empty((rows, 4 * C), **bf16)
+        self.A_rgb = torch.empty((B * T, 3 * p * p), **bf16)
+        self.A_d = torch.empty((B * Td, p * p), **bf16) if self.has_depth else None
+        self.OUT = torch.empty((B * T, C), **f32) if self.enc_norm is not None else None
         self.win_in, self.win_out = self._window_maps()
+        if self.win_out is not None:
+            # queries of the last depth block: rgb rows only (its depth output is never read)
+            w = self.win_out.view(B * self.nw, self.win_rows).clone()
+            self.win_out_rgbq = w[:, :self.win_rgb].contiguous().view(-1)
         self._pos_cache = {}
 
     def _window_maps(self):
+        """win_in: X row -> LNW row (window_partition, vit.py:16-37); win_out: LNW row -> X row or
+        -1 for pad positions (window_unpartition, vit.py:39-58)"""
         B, T, g, ws, nwx = self.B, self.T, self.g, self.ws, self.nwx
-        s, b, y, x = np.meshgrid(np.arange(2), np.arange(B), np.arange(g), np.arange(g), indexing="ij")
+        b, y, x = np.meshgrid(np.arange(B), np.arange(g), np.arange(g), indexing="ij")
         w = (y // ws) * nwx + (x // ws)
-        tw = (y % ws) * ws + (x % ws)
-        win_in = (b * self.nw + w) * self.win_rows + s * ws * ws + tw        # X row -> LNW row
-        nwr = B * self.nw * self.win_rows
-        win_out = -np.ones(nwr, np.int64)
-        xrow = s * B * T + b * T + y * g + x
-        win_out[win_in.reshape(-1)] = xrow.reshape(-1)
-        to = lambda a: torch.as_tensor(a.reshape(-1).astype(np.int32), device=self.dev)
-        return to(win_in), to(win_out)
+        win_in = [((b * self.nw + w) * self.win_rows + (y % ws) * ws + (x % ws)).reshape(-1)]
+        xrow = [(b * T + y * g + x).reshape(-1)]
+        if self.has_depth:
+            gd, wsd = self.gd, self.wsd
+            b, y, x = np.meshgrid(np.arange(B), np.arange(gd), np.arange(gd), indexing="ij")
+            w = (y // wsd) * nwx + (x // wsd)
+            win_in.append(((b * self.nw + w) * self.win_rows + self.win_rgb + (y % wsd) * wsd + (x % wsd)).reshape(-1))
+            xrow.append((B * T + b * self.Td + y * gd + x).reshape(-1))
+        win_in, xrow = np.concatenate(win_in), np.concatenate(xrow)
+        win_out = -np.ones(B * self.nw * self.win_rows, np.int64)
+        win_out[win_in] = xrow
+        to = lambda a: torch.as_tensor(a.astype(np.int32), device=self.dev)
+        order = np.argsort(xrow)
+        return to(win_in[order]), to(win_out)
 
-    def backbone(self, img_u8, depth_std):
-        """img_u8 [B,H,W,3] uint8, depth_std [B,H,W] f32 (standardised) -> features [B,C,g,g] f32"""
+    def backbone(self, img_u8, depth_std, chw=False, pixel_mean=PIXEL_MEAN, pixel_std=PIXEL_STD):
+        """img_u8 [B,H,W,3] (chw: [B,3,H,W]) uint8, depth_std [B,H/r,W/r] f32 (standardised) ->
+        features [B,C,g,g] f32.  pixel_mean / std: the normalisation constants (demo.py's
+        preprocessing divides float frames by (123.675, 116.28, 103.53) / (58.395, 57.12, 57.375))"""
         B, T, C = self.B, self.T, self.C
         X = self.X
         Xr = X[: B * T]
-        _lib.im2col_rgb8(img_u8, self.P, 16, PIXEL_MEAN_U8, PIXEL_STD_U8, out=self.A_rgb)
+        _lib.im2col_rgb8(img_u8, self.P, 16, pixel_mean, pixel_std, out=self.A_rgb, chw=chw)
         _lib.gemm(self.A_rgb, self.patch_w, self.patch_b, resid=self.pos, resid_mod=T, out=Xr)
-        _lib.im2col_f32(depth_std, self.P, 16, out=self.A_d)
-        _lib.gemm(self.A_d, self.patchd_w, self.patchd_b, resid=self.posd, resid_mod=T, out=X[B * T:])
+        if self.has_depth:
+            _lib.im2col_f32(depth_std, self.Pd, 16, out=self.A_d)
+            _lib.gemm(self.A_d, self.patchd_w, self.patchd_b, resid=self.posd, resid_mod=self.Td,
+                      out=X[B * T:])
         scale = self.D ** -0.5
+        nb = B * self.nw
         for i, blk in enumerate(self.blocks):
             g1, b1, e1 = blk["n1"]
             g2, b2, e2 = blk["n2"]
-            if blk["window"] and blk["depth"]:
-                last = i == self.last_depth
-                _lib.layernorm(X, g1, b1, e1, out=self.LNW, row_map=self.win_in)
-                _lib.gemm(self.LNW, *blk["qkv"], out=self.QKV)
-                nb = B * self.nw
+            if blk["window"]:
+                # joint (rgb + depth) or rgb-only windows: LN scattered into the window layout,
+                # qkv over every window row (pad rows give the bias-only keys of vit.py:32),
+                # attention writes the real queries back in token order, proj on those rows only
+                joint = blk["depth"]
+                last = joint and i == self.last_depth
+                src = X if joint else Xr
+                _lib.layernorm(src, g1, b1, e1, out=self.LNW, row_map=self.win_in[: src.shape[0]])
+                _lib.gemm(self.LNW, *blk["qkv"], out=self.QKV[: self.LNW.shape[0]])
                 q = self.QKV[:, :C]
+                rs = self.win_rows * self.QKV.stride(0)
+                sq = self.win_rgb if (last or not joint) else self.win_rows
                 _lib.attention(q, self.QKV[:, C:2 * C], self.QKV[:, 2 * C:], self.ATT, nb, self.heads,
-                               self.ws * self.ws if last else self.win_rows, self.win_rows, self.D,
-                               scale, q_bs=self.win_rows * self.QKV.stride(0),
-                               k_bs=self.win_rows * self.QKV.stride(0),
-                               v_bs=self.win_rows * self.QKV.stride(0),
-                               o_bs=self.win_rows * self.ATT.stride(0))
-                _lib.gemm(self.ATT, *blk["proj"], resid=X, out=X, row_map=self.win_out)
-                rows = B * T if last else 2 * B * T
+                               sq, self.win_rows if joint else self.win_rgb, self.D, scale,
+                               q_bs=rs, k_bs=rs, v_bs=rs, o_bs=0,
+                               o_map=self.win_out_rgbq if sq == self.win_rgb and self.has_depth
+                               else self.win_out)
+                rows = B * T if (last or not joint) else self.rows
                 Xm = X[:rows]
-            elif blk["window"]:
-                raise NotImplementedError("RGB-only window blocks (non-depth CuTR) are not wired yet")
+                _lib.gemm(self.ATT[:rows], *blk["proj"], resid=Xm, out=Xm)
             else:
                 _lib.layernorm(Xr, g1, b1, e1, out=self.LN2[: B * T])
                 qkv = self.QKV[: B * T]
@@ -141,7 +201,10 @@ class CuTREngine:
             _lib.layernorm(Xm, g2, b2, e2, out=self.LN2[:rows])
             _lib.gemm(self.LN2[:rows], *blk["fc1"], act="gelu", out=self.H1[:rows])
             _lib.gemm(self.H1[:rows], *blk["fc2"], resid=Xm, out=Xm)
-        return Xr.view(B, self.g, self.g, C).permute(0, 3, 1, 2)
+        out = Xr
+        if self.enc_norm is not None:
+            out = _lib.layernorm(Xr, self.enc_norm[0], self.enc_norm[1], self.enc_norm[2], out=self.OUT)
+        return out.view(B, self.g, self.g, C).permute(0, 3, 1, 2)
 
     def ray_embedding(self, K_host, size_wh):
         """CameraRayEmbedding depends only on (K, image size): computed once per camera."""
@@ -163,15 +226,16 @@ class CuTREngine:
 
     @torch.no_grad()
     def __call__(self, img_u8, depth_std, depth_params, K, T_gravity, image_sizes, K_host=None,
-                 K_inv=None):
+                 K_inv=None, chw=False, pixel_mean=PIXEL_MEAN, pixel_std=PIXEL_STD):
         """K: device [B,3,3]; K_host (numpy, same values) keys the ray-embedding cache so the call
         never reads device memory (graph-capturable once the cache is warm)."""
         if K_host is None:
             K_host = K.detach().cpu().numpy()
         pos = self.positions(K_host, image_sizes)
-        feat = self.backbone(img_u8, depth_std)
-        batch = FrameBatch(image=None, depth=depth_std, depth_params=depth_params, K=K,
-                           T_gravity=T_gravity, image_sizes=image_sizes, pad=self.P, K_inv=K_inv)
+        feat = self.backbone(img_u8, depth_std, chw=chw, pixel_mean=pixel_mean, pixel_std=pixel_std)
+        batch = FrameBatch(image=None, depth=depth_std if self.has_depth else None,
+                           depth_params=depth_params, K=K, T_gravity=T_gravity,
+                           image_sizes=image_sizes, pad=self.P, K_inv=K_inv)
         return self.model.decode(feat, batch, pos=pos)
 
 
@@ -216,6 +280,11 @@ class CLIPEngine:
         self.QKV = torch.empty((M, 3 * W), **bf16)
         self.ATT = torch.empty((M, W), **bf16)
         self.H1 = torch.empty((M, 4 * W), **bf16)
+        self.ln_pre = (_f(v.ln_pre.weight), _f(v.ln_pre.bias), v.ln_pre.eps)
+        self.ln_post = (_f(v.ln_post.weight), _f(v.ln_post.bias), v.ln_post.eps)
+        self.proj_t = _bf(v.proj.t())                       # [out, width] (nn.Linear layout)
+        self.CLS = torch.empty((max_crops, W), **bf16)
+        self.FEAT = torch.empty((max_crops, v.output_dim), **f32)
 
     @torch.no_grad()
     def __call__(self, frames_u8, boxes_i32, frame_idx_i32):
@@ -234,8 +303,7 @@ class CLIPEngine:
         _lib.gemm(A, self.patch_w, resid=self.pos[1:], resid_mod=npch, out=X,
                   row_map=self.stem_map[: N * npch])
         X3[:, 0] = self.cls + self.pos[0]
-        X.copy_(F.layer_norm(X, (W,), self.visual.ln_pre.weight, self.visual.ln_pre.bias,
-                             self.visual.ln_pre.eps))
+        _lib.layernorm(X, *self.ln_pre, out=X)               # ln_pre in place (f32)
         M = N * S
         LN, QKV, ATT, H1 = self.LN[:M], self.QKV[:M], self.ATT[:M], self.H1[:M]
         scale = self.D ** -0.5
@@ -248,6 +316,6 @@ class CLIPEngine:
             _lib.layernorm(X, *blk["n2"][:2], blk["n2"][2], out=LN)
             _lib.gemm(LN, *blk["fc1"], act="gelu", out=H1)
             _lib.gemm(H1, *blk["fc2"], resid=X, out=X)
-        cls = F.layer_norm(X3[:, 0], (W,), self.visual.ln_post.weight, self.visual.ln_post.bias,
-                           self.visual.ln_post.eps)
-        return cls @ self.visual.proj
+        # ln_post on the class rows (row stride S*W) -> bf16, then the output projection
+        cls = _lib.layernorm(X.view(N, S * W)[:, :W], *self.ln_post, out=self.CLS[:N])
+        return _lib.gemm(cls, self.proj_t, out=self.FEAT[:N])

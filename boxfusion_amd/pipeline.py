@@ -4,7 +4,7 @@
       a1  depth standardisation            bf_depth_standardize          preprocessor.py:97-129
       a13 depth back-projection            bf_backproject                 tools/utils.py:232-287
       a2-a9 CuTR RGB-D forward             CuTREngine (MFMA kernels)      cubify_transformer.py
-      a10 detection filters                torch on device                demo.py:138-148
+      a10 detection filters                bf_detection_filter            demo.py:138-148
       a11 scale_boxes + crop + CLIP        CLIPEngine (fused crop/resize  tools/utils.py:355-495
           + text match                      im2col + MFMA ViT-H/14)       demo.py:162-171
     FusionStage  (serial over keyframes, fusion_stage.py)                demo.py:200-305
@@ -27,6 +27,7 @@ from boxfusion_amd.fusion_stage import FusionStage
 from boxfusion_amd.instances import Instances3D
 from boxfusion_amd.preprocessor import square_pad_size
 from boxfusion_amd.sensor import camera_to_gravity
+from boxfusion_amd.tools_utils import match_features
 
 DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
 
@@ -55,17 +56,10 @@ def scale_boxes(boxes, H, W, scale=1.2):
 
 
 def detection_mask(scores, proj_xy, box3d, cfg, H, W):
-    """demo.py:138-148 filters for a [B,100] batch: score, uv bound, floor, large."""
-    det = cfg["detection"]
-    m = scores >= float(det.get("score_thresh", 0.0))
-    if det.get("uv_bound"):
-        ratio = det["uv_bound_value"]
-        m &= BoxManager.check_uv_bounds(proj_xy.reshape(-1, 2), W, H, ratio).view_as(m)
-    if det.get("floor_mask"):
-        m &= ~BoxManager.check_floor_mask(box3d.reshape(-1, 6), det["floor_ratio"]).view_as(m)
-    if det.get("size_max_thres"):
-        m &= ~BoxManager.check_large_mask(box3d.reshape(-1, 6), det["size_max_thres"]).view_as(m)
-    return m
+    """demo.py:138-148 filters for a [B,100] batch (score, uv bound, floor, large) in one
+    bf_detection_filter launch.  The reference filters sequentially (each mask on the survivors
+    of the previous one); the masks are per-instance, so their conjunction is the same set."""
+    return _lib.detection_filter(scores, proj_xy, box3d, _lib.filter_cfg(cfg["detection"], W, H))
 
 
 class DetectStage:
@@ -131,12 +125,8 @@ class DetectStage:
         for s in range(0, boxes.shape[0], cap):
             feats.append(self.clip(frames_u8, bi[s:s + cap].contiguous(), frame_idx[s:s + cap].contiguous()))
         f = torch.cat(feats, 0) if len(feats) > 1 else feats[0]
-        f = f / f.norm(dim=-1, keepdim=True)
-        self.text /= self.text.norm(dim=-1, keepdim=True)   # in-place renorm every call (quirk 4)
-        probs = 100.0 * f @ self.text.T
-        probs = torch.cat([probs, torch.full_like(probs, self.sim_thres)[..., :1]], dim=-1)
-        mx, idx = torch.max(probs, dim=-1)
-        return idx, f, mx
+        # normalise, in-place text renorm every call (quirk 4), threshold column, argmax
+        return match_features(f, self.text, self.sim_thres)
 
     def _device_forward(self):
         """host-sync-free device work on the input buffers -> self.out"""

@@ -88,6 +88,22 @@ int bf_box_transform2world(float* xyzlhw, float* R, const float* cam_pose, int n
 int bf_project_boxes(const float* corners, const float* cam_pose, const float* K, int n,
                      float W, float H, float* uv, void* stream);
 
+/* Detection filters of demo.py:138-148 (BoxManager.check_uv_bounds / check_floor_mask /
+ * check_large_mask, box_manager.py:217-245, and the score threshold) over n instances:
+ * scores f32[n], proj_xy f32[n,2], box3d f32[n,6] (xyz lhw) -> keep u8[n]; bits u8[n] (may be
+ * NULL): 2 = score >= thr, 4 = uv inside, 8 = floor mask, 16 = large mask.  Thresholds are the
+ * f32 values torch compares with; gap_w / gap_h = int((1 - ratio) * W / H) as in the reference
+ * (63 / 47 at 640 x 480, ratio 0.9). */
+typedef struct {
+    float score_thresh;
+    float floor_ratio, floor_half;   /* ratio and ratio / 2 */
+    float size_max;
+    int32_t gap_w, gap_h, W, H;
+    int32_t use_score, use_uv, use_floor, use_large;
+} bf_filter_cfg;
+int bf_detection_filter(const float* scores, const float* proj_xy, const float* box3d, int n,
+                        const bf_filter_cfg* cfg, uint8_t* keep, uint8_t* bits, void* stream);
+
 /* Sampled 3-D OBB IoU of every pair (instances.py:493-613, Instances3D.obb_iou):
  * vertex/edge-midpoint gate against the 12 hull facets (eps 1e-6), then a 25^3 linspace grid over
  * the union AABB.  corners f32[n,8,3] -> iou f64[n,n] (symmetric, diagonal = 1).
@@ -292,6 +308,13 @@ int bf_attention_bf16(const void* q, const void* k, const void* v, void* o, int 
                       int sq, int sk, int head_dim, int q_rs, int k_rs, int v_rs, int o_rs,
                       long long q_bs, long long k_bs, long long v_bs, long long o_bs, float scale,
                       void* stream);
+/* the same with an output row map: query q of batch b is stored to row o_map[b*sq + q] of o
+ * (o_bs unused; < 0 = not stored).  The window blocks write their outputs back in token order
+ * (window_unpartition, vit.py:39-58) with the pad queries dropped. */
+int bf_attention_bf16_omap(const void* q, const void* k, const void* v, void* o, int batch,
+                           int heads, int sq, int sk, int head_dim, int q_rs, int k_rs, int v_rs,
+                           int o_rs, long long q_bs, long long k_bs, long long v_bs, long long o_bs,
+                           float scale, const int32_t* o_map, void* stream);
 /* Attention kernel variant (test/benchmark hook): 1 (default) / 2 = k_attn_s (64-key tiles
  * through a double-buffered LDS ring), 3 = k_attn_r (resident K/V filled by LDS-DMA when all
  * queries fit one workgroup and sk <= 320, else k_attn_s), 0 = k_attn (previous kernel). */
@@ -314,12 +337,21 @@ int bf_rpe_softmax(float* attn, int B, int H, int Nq, int q0, const float* rx, c
 /* LayerNorm f32[M,C] -> bf16, written to row row_map[r] (NULL = r; < 0 skips). */
 int bf_layernorm(const float* x, int ldx, const float* gamma, const float* beta, float eps,
                  void* out, int ldo, const int32_t* row_map, int M, int C, void* stream);
+/* the same with an f32 output (out_f32 = 1; x == out in place allowed): CLIP ln_pre / ln_post,
+ * CuTR's encoder_norm (vit.py:473) */
+int bf_layernorm_out(const float* x, int ldx, const float* gamma, const float* beta, float eps,
+                     void* out, int ldo, int out_f32, const int32_t* row_map, int M, int C,
+                     void* stream);
 
 /* Preprocessor.normalize + square zero pad + PatchEmbed im2col (preprocessor.py:131-144,
  * imagelist.py:55-115, vit.py:102-128): img u8[B,H,W,3] -> bf16[B*(pad/p)^2, 3*p*p].
  * mean3/std3 are HOST arrays of 3 floats. */
 int bf_im2col_rgb8(const uint8_t* img, int B, int H, int W, int pad, int patch,
                    const float* mean3, const float* std3, void* out, int ldo, void* stream);
+/* the same for CHW frames ([B,3,H,W] u8, chw = 1: the layout of the reference's capture stream,
+ * capture_stream.py:221 `np.moveaxis(image, -1, 0)`) or HWC (chw = 0) */
+int bf_im2col_rgb8_chw(const uint8_t* img, int B, int H, int W, int chw, int pad, int patch,
+                       const float* mean3, const float* std3, void* out, int ldo, void* stream);
 
 /* single-channel f32 [B,H,W] -> zero-padded square -> bf16 im2col [B*(pad/p)^2, p*p] */
 int bf_im2col_f32(const float* x, int B, int H, int W, int pad, int patch, void* out, int ldo,

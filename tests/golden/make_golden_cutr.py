@@ -54,12 +54,16 @@ from boxfusion_amd.synthetic import Scene, frame_rgbd, SCANNET_K  # noqa: E402
 from boxfusion_amd.weights import seeded_state_dict  # noqa: E402
 
 
-def make_sample(rgb, depth, K, pose):
-    """restates ScannetDataset.__iter__ (capture_stream.py:185-311) for one in-memory frame"""
-    H, W = depth.shape
+def make_sample(rgb, depth, K, pose, image_hw=None):
+    """restates ScannetDataset.__iter__ (capture_stream.py:185-311) for one in-memory frame; a
+    depth smaller than the image gets its own info size and K scaled to its resolution"""
+    H, W = image_hw if image_hw is not None else depth.shape
+    Hd, Wd = depth.shape
+    Kd = np.asarray(K, np.float32).copy()
+    Kd[:2] *= Wd / W
     wide = PosedSensorInfo()
     wide.image = ImageMeasurementInfo(size=(W, H), K=torch.tensor(K)[None])
-    depth_info = DepthMeasurementInfo(size=(W, H), K=torch.tensor(K)[None])
+    depth_info = DepthMeasurementInfo(size=(Wd, Hd), K=torch.tensor(Kd)[None])
     wide.depth = depth_info
     result = dict(wide=dict())
     result["wide"]["image"] = torch.tensor(np.moveaxis(rgb, -1, 0))[None]
@@ -84,39 +88,95 @@ def make_sample(rgb, depth, K, pose):
     return result, T_gravity, cur
 
 
-def main(dim=192, frame=7, seed=0):
+FILTER_CFG = dict(  # demo.py:138-148 thresholds: scannet.yaml + cubicle.yaml's size_max_thres
+    scannet=dict(score_thresh=0.5, uv_bound_value=0.9, floor_ratio=15, size_max_thres=0.5),
+    ca1m=dict(score_thresh=0.4, uv_bound_value=0.9, floor_ratio=15, size_max_thres=0.5),
+)
+
+
+def filter_masks(pred, W, H, thr):
+    """the reference's own BoxManager filters (box_manager.py:217-245) on all 100 instances, each
+    mask separately, plus the sequential demo.py:138-148 survivor indices"""
+    from boxfusion.box_manager import BoxManager
+    cfg = dict(association=dict(rotation_gap=30, translation_gap=0.8), box_fusion=dict(small_size=0.35))
+    bm = BoxManager(cfg)
+    score = (pred.scores >= float(thr["score_thresh"])).numpy()
+    uv = bm.check_uv_bounds(pred.pred_proj_xy, W, H, ratio=thr["uv_bound_value"]).numpy()
+    floor = bm.check_floor_mask(pred.pred_boxes_3d.tensor, ratio=thr["floor_ratio"]).numpy()
+    large = bm.check_large_mask(pred.pred_boxes_3d.tensor, thres=thr["size_max_thres"]).numpy()
+    idx = np.arange(len(score))
+    p = pred[pred.scores >= float(thr["score_thresh"])]
+    idx = idx[score]
+    m = bm.check_uv_bounds(p.pred_proj_xy, W, H, ratio=thr["uv_bound_value"])
+    p, idx = p[m], idx[m.numpy()]
+    m = bm.check_floor_mask(p.pred_boxes_3d.tensor, ratio=thr["floor_ratio"])
+    p, idx = p[~m], idx[~m.numpy()]
+    m = bm.check_large_mask(p.pred_boxes_3d.tensor, thres=thr["size_max_thres"])
+    idx = idx[~m.numpy()]
+    return dict(mask_score=score, mask_uv=uv, mask_floor=floor, mask_large=large,
+                kept_sequential=idx.astype(np.int64))
+
+
+def run_case(name, dim, frame, seed, H, W, ratio, K, thr, keep_features=False):
+    """one frame through demo.py:129-136's exact sequence on the reference:
+    augmentor.package -> move_input_to_current_device(., model.pixel_mean) -> preprocess -> model"""
+    from boxfusion.preprocessor import move_input_to_current_device
     torch.set_num_threads(8)
     model = make_cubify_transformer(dimension=dim, depth_model=True).eval()
-    sd = seeded_state_dict(model, seed)
-    model.load_state_dict(sd)
+    model.load_state_dict(seeded_state_dict(model, seed))
     keys = np.array(sorted(f"{k}:{tuple(v.shape)}" for k, v in model.state_dict().items()))
-    rgb, depth = frame_rgbd(frame)
+    rgb, depth = frame_rgbd(frame, H, W)
+    if ratio > 1:           # a lower-resolution depth sensor: every ratio-th pixel
+        depth = np.ascontiguousarray(depth[::ratio, ::ratio])
     pose = Scene().pose(frame)
-    sample, T_gravity, orient = make_sample(rgb, depth, SCANNET_K, pose)
+    sample, T_gravity, orient = make_sample(rgb, depth, K, pose, image_hw=(H, W))
     aug = Augmentor(("wide/image", "wide/depth"))
     pre = Preprocessor()
-    packaged = pre.preprocess([aug.package(sample)])
+    packaged = pre.preprocess([move_input_to_current_device(aug.package(sample), model.pixel_mean)])
     sensor = packaged["wide"]
     with torch.no_grad():
         feats = model.backbone(sensor)[0].tensors
         pred = model(packaged)[0]
     out = dict(
-        dim=np.int32(dim), frame=np.int32(frame), seed=np.int32(seed), keys=keys,
+        dim=np.int32(dim), frame=np.int32(frame), seed=np.int32(seed), H=np.int32(H), W=np.int32(W),
+        ratio=np.int32(ratio), K=np.asarray(K, np.float32), keys=keys,
         orientation=np.int32(orient.value), T_gravity=T_gravity.numpy(),
-        image=sensor["image"].data.tensor.numpy().astype(np.float16),
-        depth=sensor["depth"].data.tensor.numpy(),
         depth_params=np.asarray(sensor["depth"].info[0].parameters, np.float32).reshape(-1),
-        features=feats.numpy().astype(np.float16),
+        image_sum=np.float64(sensor["image"].data.tensor.double().sum()),
+        pad=np.int32(sensor["image"].data.tensor.shape[-1]),
+        depth_pad=np.int32(sensor["depth"].data.tensor.shape[-1]),
         scores=pred.scores.numpy(), pred_classes=pred.pred_classes.numpy(),
         pred_boxes=pred.pred_boxes.numpy(), pred_logits=pred.pred_logits.numpy(),
         boxes3d=pred.pred_boxes_3d.tensor.numpy(), R=pred.pred_boxes_3d.R.numpy(),
         object_desc=pred.object_desc.numpy().astype(np.float16),
         pred_proj_xy=pred.pred_proj_xy.numpy())
-    # the full-size depth/image arrays are regenerable from (frame); keep the fixture small
-    del out["image"], out["depth"]
+    if keep_features:
+        out["features"] = feats.numpy().astype(np.float16)
     out["depth_sum"] = np.float64(sensor["depth"].data.tensor.double().sum())
-    np.savez_compressed(os.path.join(HERE, "cutr_vit_t.npz"), **out)
-    print("cutr golden written", {k: getattr(v, "shape", v) for k, v in out.items() if k != "keys"})
+    out.update(filter_masks(pred, W, H, thr))
+    # random weights put every score / size on one side of the config thresholds: a second set of
+    # thresholds at the medians of this prediction splits each mask (recorded with the masks)
+    dims = pred.pred_boxes_3d.tensor[:, 3:]
+    med = dict(score_thresh=float(pred.scores.median()), uv_bound_value=thr["uv_bound_value"],
+               floor_ratio=float((dims.amax(1) / dims.amin(1)).median()),
+               size_max_thres=float(dims.amax(1).median()))
+    out.update({k + "_med": v for k, v in filter_masks(pred, W, H, med).items()})
+    out["thr"] = np.array([thr[k] for k in ("score_thresh", "uv_bound_value", "floor_ratio", "size_max_thres")])
+    out["thr_med"] = np.array([med[k] for k in ("score_thresh", "uv_bound_value", "floor_ratio", "size_max_thres")])
+    np.savez_compressed(os.path.join(HERE, name), **out)
+    print(name, {k: getattr(v, "shape", v) for k, v in out.items() if k != "keys"})
+
+
+CA1M_K = np.array([[360.0, 0.0, 191.5], [0.0, 360.0, 255.5], [0.0, 0.0, 1.0]], np.float32)
+
+
+def main():
+    # ScanNet-shaped frame (640x480, depth at image resolution): the synthetic stream's camera
+    run_case("cutr_vit_t.npz", 192, 7, 0, 480, 640, 1, SCANNET_K, FILTER_CFG["scannet"], keep_features=True)
+    # CA-1M-shaped portrait frame (384 wide x 512 tall, ca1m.yaml cam) with a half-resolution depth
+    run_case("cutr_ca1m_r2.npz", 192, 11, 1, 512, 384, 2, CA1M_K, FILTER_CFG["ca1m"])
+    # quarter-resolution depth at 640x480
+    run_case("cutr_r4.npz", 192, 3, 2, 480, 640, 4, SCANNET_K, FILTER_CFG["scannet"])
 
 
 if __name__ == "__main__":

@@ -10,37 +10,74 @@ from oracle import oracle as OR
 from tests import trace_util as TU
 
 
+CASES = ["cutr_vit_t.npz", "cutr_ca1m_r2.npz", "cutr_r4.npz"]
+
+
 @pytest.fixture(scope="module")
 def golden():
     return TU.load("cutr_vit_t.npz")
 
 
-def cpu_frame_batch(frame, pad=640):
-    from boxfusion_amd.cubify_transformer import FrameBatch
+def frame_inputs(g):
+    """the golden frame's inputs as demo.py hands them to the model: float frame normalised with
+    the float constants (move_input_to_current_device promotes the uint8 frame first), depth
+    sampled at 1/ratio, standardised (oracle C restatement), both zero padded"""
+    from boxfusion_amd.synthetic import Scene, frame_rgbd
     from boxfusion_amd.sensor import camera_to_gravity
-    from boxfusion_amd.synthetic import Scene, frame_rgbd, SCANNET_K
-    rgb, depth = frame_rgbd(frame)
-    # preprocessor.py:142 casts pixel_mean/std to the uint8 image dtype: (123, 116, 103)/(58, 57, 57)
-    from boxfusion_amd.preprocessor import PIXEL_MEAN_U8, PIXEL_STD_U8
-    mean = torch.tensor(PIXEL_MEAN_U8).view(3, 1, 1)
-    std = torch.tensor(PIXEL_STD_U8).view(3, 1, 1)
+    from boxfusion_amd.preprocessor import PIXEL_MEAN, PIXEL_STD
+    frame, H, W, r = int(g["frame"]), int(g["H"]), int(g["W"]), int(g["ratio"])
+    rgb, depth = frame_rgbd(frame, H, W)
+    depth = np.ascontiguousarray(depth[::r, ::r])
+    d, params = OR.depth_standardize(depth)
+    Tg = camera_to_gravity(Scene().pose(frame))
+    return rgb, depth, d, params, Tg
+
+
+def cpu_frame_batch(g):
+    from boxfusion_amd.cubify_transformer import FrameBatch
+    from boxfusion_amd.preprocessor import PIXEL_MEAN, PIXEL_STD
+    rgb, _, d, params, Tg = frame_inputs(g)
+    pad, dpad = int(g["pad"]), int(g["depth_pad"])
+    mean = torch.tensor(PIXEL_MEAN).view(3, 1, 1)
+    std = torch.tensor(PIXEL_STD).view(3, 1, 1)
     img = (torch.from_numpy(np.moveaxis(rgb, -1, 0)).float() - mean) / std
     img = F.pad(img, (0, pad - img.shape[2], 0, pad - img.shape[1]))[None]
-    d, params = OR.depth_standardize(depth)
-    d = F.pad(torch.from_numpy(d), (0, pad - d.shape[1], 0, pad - d.shape[0]))[None]
+    d = F.pad(torch.from_numpy(d), (0, dpad - d.shape[1], 0, dpad - d.shape[0]))[None]
     return FrameBatch(image=img, depth=d, depth_params=torch.from_numpy(params)[None],
-                      K=torch.from_numpy(SCANNET_K)[None],
-                      T_gravity=torch.from_numpy(camera_to_gravity(Scene().pose(frame)))[None],
-                      image_sizes=[(480, 640)]), params
+                      K=torch.from_numpy(np.asarray(g["K"], np.float32))[None],
+                      T_gravity=torch.from_numpy(Tg)[None],
+                      image_sizes=[(int(g["H"]), int(g["W"]))]), params
+
+
+def model_for(g):
+    from boxfusion_amd.cubify_transformer import make_cubify_transformer
+    from boxfusion_amd.weights import init_seeded
+    torch.manual_seed(0)
+    m = make_cubify_transformer(int(g["dim"]), depth_model=True).eval()
+    return init_seeded(m, int(g["seed"]))
 
 
 @pytest.fixture(scope="module")
 def model(golden):
-    from boxfusion_amd.cubify_transformer import make_cubify_transformer
-    from boxfusion_amd.weights import init_seeded
-    torch.manual_seed(0)
-    m = make_cubify_transformer(int(golden["dim"]), depth_model=True).eval()
-    return init_seeded(m, int(golden["seed"]))
+    return model_for(golden)
+
+
+def assert_instances(r, g, score_tol=(1e-4, 1e-6), box_tol=(1e-4, 1e-3), b3_tol=(1e-4, 1e-4),
+                     R_tol=1e-5, desc_tol=2e-3, min_ok=50):
+    """instances vs a golden: scores everywhere, the rest on instances whose score is separated
+    from its neighbours (the top-k order is only stable there)"""
+    np.testing.assert_allclose(r.scores.cpu().numpy(), g["scores"], rtol=score_tol[0], atol=score_tol[1])
+    s = g["scores"]
+    gap = np.minimum(np.abs(np.diff(s, prepend=np.inf)), np.abs(np.diff(s, append=-np.inf)))
+    ok = gap > max(1e-5, 2 * score_tol[1])
+    assert ok.sum() > min_ok
+    np.testing.assert_array_equal(r.pred_classes.cpu().numpy()[ok], g["pred_classes"][ok])
+    np.testing.assert_allclose(r.pred_boxes.cpu().numpy()[ok], g["pred_boxes"][ok], rtol=box_tol[0], atol=box_tol[1])
+    np.testing.assert_allclose(r.pred_boxes_3d.tensor.cpu().numpy()[ok], g["boxes3d"][ok], rtol=b3_tol[0], atol=b3_tol[1])
+    np.testing.assert_allclose(r.pred_boxes_3d.R.cpu().numpy()[ok], g["R"][ok], atol=R_tol)
+    np.testing.assert_allclose(r.pred_proj_xy.cpu().numpy()[ok], g["pred_proj_xy"][ok], rtol=box_tol[0], atol=box_tol[1])
+    np.testing.assert_allclose(r.object_desc.cpu().numpy()[ok], g["object_desc"][ok].astype(np.float32),
+                               rtol=desc_tol, atol=desc_tol)
 
 
 def test_state_dict_keys_match_reference(model, golden):
@@ -48,27 +85,39 @@ def test_state_dict_keys_match_reference(model, golden):
     assert keys == sorted(golden["keys"].tolist())
 
 
-def test_forward_matches_reference(model, golden):
+@pytest.mark.parametrize("case", CASES)
+def test_forward_matches_reference(case):
+    """the fp32 restatement on each golden frame: ScanNet-shaped (depth at image resolution),
+    CA-1M portrait 384x512 with a half-resolution depth, 640x480 with a quarter-resolution depth"""
     torch.set_num_threads(8)
-    batch, params = cpu_frame_batch(int(golden["frame"]))
-    np.testing.assert_allclose(params, golden["depth_params"], rtol=2e-6)
-    np.testing.assert_allclose(batch.depth.double().sum().item(), golden["depth_sum"], rtol=1e-6)
-    np.testing.assert_allclose(batch.T_gravity[0].numpy(), golden["T_gravity"], atol=1e-6)
+    g = TU.load(case)
+    m = model_for(g)
+    batch, params = cpu_frame_batch(g)
+    np.testing.assert_allclose(params, g["depth_params"], rtol=2e-6)
+    np.testing.assert_allclose(batch.depth.double().sum().item(), g["depth_sum"], rtol=1e-6)
+    np.testing.assert_allclose(batch.image.double().sum().item(), g["image_sum"], rtol=1e-6)
+    np.testing.assert_allclose(batch.T_gravity[0].numpy(), g["T_gravity"], atol=1e-6)
     with torch.no_grad():
-        feat = model.backbone.backbone.forward_tensors(batch.image, batch.depth)
-        ref = torch.from_numpy(golden["features"].astype(np.float32))
-        assert ((feat - ref).norm() / ref.norm()).item() < 2e-3
-        r = model(batch)[0]
-    np.testing.assert_allclose(r.scores.numpy(), golden["scores"], rtol=1e-4, atol=1e-6)
-    # compare instances whose score is separated from its neighbours (stable top-k order)
-    s = golden["scores"]
-    gap = np.minimum(np.abs(np.diff(s, prepend=np.inf)), np.abs(np.diff(s, append=-np.inf)))
-    ok = gap > 1e-5
-    assert ok.sum() > 50
-    np.testing.assert_array_equal(r.pred_classes.numpy()[ok], golden["pred_classes"][ok])
-    np.testing.assert_allclose(r.pred_boxes.numpy()[ok], golden["pred_boxes"][ok], rtol=1e-4, atol=1e-3)
-    np.testing.assert_allclose(r.pred_boxes_3d.tensor.numpy()[ok], golden["boxes3d"][ok], rtol=1e-4, atol=1e-4)
-    np.testing.assert_allclose(r.pred_boxes_3d.R.numpy()[ok], golden["R"][ok], atol=1e-5)
-    np.testing.assert_allclose(r.pred_proj_xy.numpy()[ok], golden["pred_proj_xy"][ok], rtol=1e-4, atol=1e-3)
-    np.testing.assert_allclose(r.object_desc.numpy()[ok], golden["object_desc"][ok].astype(np.float32),
-                               rtol=2e-3, atol=2e-3)
+        if "features" in g:
+            feat = m.backbone.backbone.forward_tensors(batch.image, batch.depth)
+            ref = torch.from_numpy(g["features"].astype(np.float32))
+            assert ((feat - ref).norm() / ref.norm()).item() < 2e-3
+        r = m(batch)[0]
+    assert_instances(r, g)
+
+
+def test_filters_match_reference():
+    """BoxManager.check_uv_bounds / check_floor_mask / check_large_mask + the score threshold
+    (demo.py:138-148) on the golden instances, at the config thresholds and at thresholds that
+    split every mask"""
+    from boxfusion_amd.box_manager import BoxManager
+    for case in CASES:
+        g = TU.load(case)
+        b3 = torch.from_numpy(g["boxes3d"])
+        uv = torch.from_numpy(g["pred_proj_xy"])
+        for suf in ("", "_med"):
+            st, ub, fr, lg = g["thr" + suf]
+            assert np.array_equal((torch.from_numpy(g["scores"]) >= float(st)).numpy(), g["mask_score" + suf])
+            assert np.array_equal(BoxManager.check_uv_bounds(uv, int(g["W"]), int(g["H"]), ub).numpy(), g["mask_uv" + suf])
+            assert np.array_equal(BoxManager.check_floor_mask(b3, fr).numpy(), g["mask_floor" + suf])
+            assert np.array_equal(BoxManager.check_large_mask(b3, lg).numpy(), g["mask_large" + suf])

@@ -1,0 +1,118 @@
+"""demo.py's own per-frame calls against this package (demo.py:121-171):
+
+    packaged = augmentor.package(sample)
+    packaged = move_input_to_current_device(packaged, model.pixel_mean)
+    packaged = preprocessor.preprocess([packaged])
+    pred_instances = model(packaged)[0]
+    ... scale_boxes -> text_prompt(boxes, class_prompt, text_features, image, clip_model, preprocess, thr)
+
+On CPU (no HIP device) the product refuses to run: the depth standardisation kernel and the
+model raise.  These tests inject the oracle's depth standardisation (test-only) to check the
+plumbing: the packaged structure, the normalised / padded tensors the reference would hand its
+model (sums pinned by the reference-run goldens), the inputs the engine reads, and that the fp32
+definition of the model on exactly those tensors reproduces the reference's instances.  The GPU
+tests run the same sequence on the kernels."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as OR
+from tests import trace_util as TU
+from tests.test_cutr_golden import CASES, assert_instances, model_for
+
+
+def oracle_standardize(img, trunc_value=0.1):
+    d, p = OR.depth_standardize(img.cpu().numpy().astype(np.float32))
+    return torch.from_numpy(d), torch.from_numpy(p)
+
+
+def golden_sample(g):
+    from boxfusion_amd.capture_stream import make_sample
+    from boxfusion_amd.synthetic import Scene, frame_rgbd
+    frame, H, W, r = int(g["frame"]), int(g["H"]), int(g["W"]), int(g["ratio"])
+    rgb, depth = frame_rgbd(frame, H, W)
+    depth = np.ascontiguousarray(depth[::r, ::r])
+    return make_sample(rgb, depth, np.asarray(g["K"], np.float32), Scene().pose(frame), index=frame)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_demo_sequence_plumbing(case, monkeypatch):
+    from boxfusion_amd import _lib
+    from boxfusion_amd.cubify_transformer import frame_batch, sensor_inputs
+    from boxfusion_amd.preprocessor import Augmentor, Preprocessor, move_input_to_current_device
+    torch.set_num_threads(8)
+    g = TU.load(case)
+    model = model_for(g)
+    sample = golden_sample(g)
+    aug, pre = Augmentor(("wide/image", "wide/depth")), Preprocessor()
+    packaged = aug.package(sample)
+    assert set(packaged["wide"]) == {"image", "depth"}
+    packaged = move_input_to_current_device(packaged, model.pixel_mean)
+    with pytest.raises(_lib.HipError):          # no CPU path for the depth kernel
+        Preprocessor().preprocess([move_input_to_current_device(aug.package(sample), model.pixel_mean)])
+    monkeypatch.setattr(Preprocessor, "standardize_depth_map", staticmethod(oracle_standardize))
+    packaged = pre.preprocess([packaged])
+    x = sensor_inputs(packaged)
+    assert x["pad"] == int(g["pad"]) and x["ratio"] == int(g["ratio"])
+    assert x["image"].padded_hw == (int(g["pad"]),) * 2 and x["depth"].padded_hw == (int(g["depth_pad"]),) * 2
+    # demo.py's order promotes the frame to float32 first: float normalisation constants
+    assert x["pixel_mean"] == pytest.approx((123.675, 116.28, 103.53))
+    np.testing.assert_allclose(x["depth_params"][0].numpy(), g["depth_params"], rtol=2e-6)
+    np.testing.assert_allclose(x["T_gravity"][0].numpy(), g["T_gravity"], atol=1e-6)
+    np.testing.assert_array_equal(x["K"][0].numpy(), g["K"])
+    fb = frame_batch(packaged)
+    np.testing.assert_allclose(fb.image.double().sum().item(), g["image_sum"], rtol=1e-6)
+    np.testing.assert_allclose(fb.depth.double().sum().item(), g["depth_sum"], rtol=1e-6)
+    with pytest.raises(_lib.HipError):          # the model has no CPU path either
+        model(packaged)
+    with torch.no_grad():
+        r = model(fb)[0]
+    assert_instances(r, g)
+
+
+def test_uint8_frame_without_move_uses_uint8_constants(monkeypatch):
+    """preprocess on a frame still uint8 (no move_input_to_current_device): pixel_mean.to(uint8)
+    = (123, 116, 103) / (58, 57, 57), as the reference computes then"""
+    from boxfusion_amd.cubify_transformer import sensor_inputs
+    from boxfusion_amd.preprocessor import Augmentor, Preprocessor
+    monkeypatch.setattr(Preprocessor, "standardize_depth_map", staticmethod(oracle_standardize))
+    g = TU.load(CASES[0])
+    packaged = Preprocessor().preprocess([Augmentor(("wide/image", "wide/depth")).package(golden_sample(g))])
+    x = sensor_inputs(packaged)
+    assert x["pixel_mean"] == (123.0, 116.0, 103.0) and x["pixel_std"] == (58.0, 57.0, 57.0)
+
+
+def test_scale_boxes_and_crops_match_reference():
+    from boxfusion_amd.tools_utils import crop_boxes_int, scale_boxes
+    u = TU.load("utils.npz")
+    s = scale_boxes(u["boxes"], 480, 640, scale=1.5)
+    np.testing.assert_array_equal(s, u["scaled"])
+    ib = crop_boxes_int(s)
+    hw = np.stack([np.maximum(ib[:, 3] - ib[:, 1], 0), np.maximum(ib[:, 2] - ib[:, 0], 0)], 1)
+    np.testing.assert_array_equal(hw, u["crop_hw"])
+
+
+def test_text_prompt_matches_reference():
+    """text_prompt with the reference's signature and a stand-in CLIP model returning the
+    golden's fixed features: categories, normalised features, max similarities and the in-place
+    text renormalisation all as the reference computed them"""
+    from boxfusion_amd.tools_utils import text_prompt
+    from boxfusion_amd.pipeline import load_class_features, load_class_names
+    from boxfusion_amd.synthetic import frame_rgbd
+    u = TU.load("utils.npz")
+
+    class Stub:
+        def get_batch_images_clip_features(self, images):
+            assert len(images) == len(u["feats"]) and all(i.shape == (224, 224, 3) for i in images)
+            return torch.from_numpy(u["feats"].copy()), None
+
+    names = np.asarray(load_class_names())
+    text = load_class_features() * float(u["text_scale"])
+    rgb, _ = frame_rgbd(int(u["rgb_frame"]))
+    cats, feats, mx = text_prompt(u["scaled"], names, text, rgb, Stub(), None, float(u["sim_thres"]))
+    prompt = np.append(names, "")
+    np.testing.assert_array_equal(cats, prompt[u["cat_idx"]])
+    np.testing.assert_allclose(feats.numpy(), u["img_features"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(mx.numpy(), u["max_values"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(text[:4].numpy(), u["text_after"], rtol=1e-6, atol=1e-7)
+    assert (cats == "").sum() > 0 and (cats != "").sum() > 0

@@ -288,6 +288,7 @@ def test_boxfusion_hull_overflow_policy(L):
         allb = Instances3D((480, 640))
         allb.pred_boxes_3d = GeneralInstance3DBoxes(_t(vb[:1]), _t(vr[:1]))
         bm = BoxManager(cfg)
+        bm.init_new_predictions(1, 0)
         bm.fusion_list = [[0, 1, 2]]
         bf = BoxFusion(cfg, device=DEV)
         bf.update_intrinsics((640, 480), np.array(fuse_cfg(L, True).K).reshape(4, 4)[:3, :3])
