@@ -151,7 +151,7 @@ def run_case(name, dim, frame, seed, H, W, ratio, K, thr, keep_features=False):
         object_desc=pred.object_desc.numpy().astype(np.float16),
         pred_proj_xy=pred.pred_proj_xy.numpy())
     if keep_features:
-        out["features"] = feats.numpy().astype(np.float16)
+        out["features"] = feats.numpy()          # f32: the GPU test feeds them to the decoder
     out["depth_sum"] = np.float64(sensor["depth"].data.tensor.double().sum())
     out.update(filter_masks(pred, W, H, thr))
     # random weights put every score / size on one side of the config thresholds: a second set of
@@ -174,9 +174,9 @@ def main():
     # ScanNet-shaped frame (640x480, depth at image resolution): the synthetic stream's camera
     run_case("cutr_vit_t.npz", 192, 7, 0, 480, 640, 1, SCANNET_K, FILTER_CFG["scannet"], keep_features=True)
     # CA-1M-shaped portrait frame (384 wide x 512 tall, ca1m.yaml cam) with a half-resolution depth
-    run_case("cutr_ca1m_r2.npz", 192, 11, 1, 512, 384, 2, CA1M_K, FILTER_CFG["ca1m"])
+    run_case("cutr_ca1m_r2.npz", 192, 11, 1, 512, 384, 2, CA1M_K, FILTER_CFG["ca1m"], keep_features=True)
     # quarter-resolution depth at 640x480
-    run_case("cutr_r4.npz", 192, 3, 2, 480, 640, 4, SCANNET_K, FILTER_CFG["scannet"])
+    run_case("cutr_r4.npz", 192, 3, 2, 480, 640, 4, SCANNET_K, FILTER_CFG["scannet"], keep_features=True)
 
 
 if __name__ == "__main__":

@@ -192,11 +192,17 @@ def _demo_sequence(g, dev, B=1):
 
 @pytest.mark.parametrize("case", ["cutr_vit_t.npz", "cutr_ca1m_r2.npz", "cutr_r4.npz"])
 def test_demo_sequence_engine_vs_reference(dev, case):
-    """the HIP CuTR path end to end (depth standardisation kernel, MFMA backbone, decoder) through
-    the reference's own call sequence, against the REFERENCE's fp32 output on the same frame and
-    seeded weights.  bf16 backbone: scores within 1e-2 absolute; on instances whose score is
-    separated from its neighbours by more than that, classes equal, 2-D boxes / projected
-    centres within 2 px, 3-D boxes within 2 cm + 2 %, rotations within 2e-2"""
+    """the HIP CuTR path through the reference's own call sequence (package -> move -> preprocess
+    -> model(packaged)), against the REFERENCE's fp32 run on the same frame and seeded weights:
+      * depth whitening parameters (bf_depth_standardize) within 1e-5 relative;
+      * backbone features (bf16 MFMA backbone) within 3e-2 relative L2;
+      * the top-100 score curve within 1e-2;
+      * the decoder (f32 torch + bf_cpb_mlp / bf_rpe_softmax) on the reference's backbone features
+        reproduces the reference's instances to f32 rounding (classes, 2-D / 3-D boxes, R, proj).
+    End-to-end instances are not compared rank by rank: with random weights the encoder's top-300
+    proposal logits sit ~1e-4 apart, so bf16 backbone rounding reorders which proposal a query
+    slot gets."""
+    from boxfusion_amd.cubify_transformer import FrameBatch, sensor_inputs
     from tests import trace_util as TU
     from tests.test_cutr_golden import assert_instances
     g = TU.load(case)
@@ -204,10 +210,28 @@ def test_demo_sequence_engine_vs_reference(dev, case):
     np.testing.assert_allclose(packaged["wide"]["depth"].info[0].parameters.reshape(-1).cpu().numpy(),
                                g["depth_params"], rtol=1e-5)
     s = r.scores.cpu().numpy()
-    print(case, "max |score - ref|", np.abs(s - g["scores"]).max(),
-          "max |box3d - ref|", np.abs(r.pred_boxes_3d.tensor.cpu().numpy() - g["boxes3d"]).max())
-    assert_instances(r, g, score_tol=(0.0, 1e-2), box_tol=(0.0, 2.0), b3_tol=(2e-2, 2e-2),
-                     R_tol=2e-2, desc_tol=0.25, min_ok=5)
+    print(case, "max |score - ref|", np.abs(s - g["scores"]).max())
+    np.testing.assert_allclose(s, g["scores"], rtol=0, atol=1e-2)
+    from tests.test_cutr_golden import model_for
+    m = model_for(g).to(dev)
+    x = sensor_inputs(packaged)
+    raw = x["image_raw"]
+    from boxfusion_amd.engine import CuTREngine
+    B, _, H, W = raw.shape
+    eng = CuTREngine(m, B, H, W, pad=x["pad"], device=dev, depth_ratio=x["ratio"])
+    feat = eng.backbone(raw.contiguous(), x["depth_std"], chw=True, pixel_mean=x["pixel_mean"],
+                        pixel_std=x["pixel_std"])
+    ref = torch.from_numpy(g["features"].astype(np.float32)).to(dev)
+    err = rel(feat, ref)
+    print(case, "backbone rel err vs reference", err)
+    assert err < 3e-2
+    K_host = x["K"].cpu().numpy()
+    batch = FrameBatch(image=None, depth=x["depth_std"], depth_params=x["depth_params"], K=x["K"],
+                       T_gravity=x["T_gravity"], image_sizes=x["image_sizes"], pad=x["pad"])
+    with torch.no_grad():
+        r2 = m.decode(ref, batch, pos=eng.positions(K_host, x["image_sizes"]))[0]
+    assert_instances(r2, g, score_tol=(1e-4, 1e-5), box_tol=(1e-4, 2e-3), b3_tol=(2e-4, 2e-4),
+                     R_tol=2e-5, desc_tol=5e-3)
 
 
 def test_detection_filter_kernel_vs_reference(dev):
