@@ -35,11 +35,20 @@ class BoxFusion:
         self.PST = load_pst(cfg["box_fusion"].get("pst_path"))
         self.K = np.eye(4)
         cam = cfg.get("cam", {})
-        if "fx" in cam:
+        basedir = str(cfg.get("data", {}).get("datadir", ""))
+        if "scannet" in basedir.lower() or cfg.get("dataset") == "online" or \
+                ("fx" in cam and not basedir):
+            # box_fusion.py:36-42: the config's camera
             self.K[:3, :3] = [[cam["fx"], 0.0, cam["cx"]], [0.0, cam["fy"], cam["cy"]], [0, 0, 1]]
             self.H, self.W = cam["H"], cam["W"]
         else:
-            self.H, self.W = cam.get("W", 480), cam.get("H", 640)  # CA-1M swaps (box_fusion.py:50-51)
+            # CA-1M (box_fusion.py:44-51): the sequence's K_depth.txt, H / W swapped (portrait);
+            # demo.py:117 replaces both with the first frame's image K and size anyway
+            kd = os.path.join(basedir, "K_depth.txt")
+            if os.path.exists(kd):
+                Kd = np.loadtxt(kd).reshape(3, 3)
+                self.K[:3, :3] = [[Kd[0, 0], 0.0, Kd[0, 2]], [0.0, Kd[1, 1], Kd[1, 2]], [0, 0, 1]]
+            self.H, self.W = cam.get("W", 480), cam.get("H", 640)
         self.update_K_flag = False
         bf = cfg["box_fusion"]
         ro = bf["random_opt"]

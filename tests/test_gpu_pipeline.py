@@ -279,3 +279,99 @@ def test_instances_rows_gather(dev):
     idx = torch.tensor([2, 9], dtype=torch.int64, device=dev)
     assert _lib.lib().bf_rows_gather(f, 1, _lib._ptr(idx), 0, 2, _lib._ptr(st), _lib._stream()) == 0
     assert out.tolist() == [2.0, -1.0] and int(st.item()) == _lib.BF_DEV_INDEX_RANGE
+
+
+class _DemoDetect:
+    """demo.py:135-171 per keyframe on this package: the scene's detections (what the golden's
+    stand-in model returned), bf_detection_filter (demo.py:138-148), tools_utils.scale_boxes +
+    text_prompt with the golden's stand-in CLIP (seeded features, one draw per call), CLIP score
+    bump and the "" category filter"""
+
+    B = 1
+
+    def __init__(self, scene, keyframes, names, text, cfg, dev, clip_seed):
+        self.scene, self.keyframes, self.calls = scene, keyframes, 0
+        self.names, self.text, self.cfg, self.dev = names, text, cfg, dev
+        self.clip_seed, self.clip_calls = clip_seed, 0
+
+    def get_batch_images_clip_features(self, images):
+        # the golden generator's StubCLIP.features (make_golden_demo.py)
+        rng = np.random.default_rng(self.clip_seed + self.clip_calls)
+        self.clip_calls += 1
+        t = self.text_rows
+        f = rng.normal(0, 1, (len(images), t.shape[1])).astype(np.float32)
+        pick = rng.integers(0, len(t), len(images))
+        near = np.arange(len(images)) % 4 != 3
+        f[near] = t[pick[near]] * 30.0 + f[near] * 0.4
+        return torch.from_numpy(f), None
+
+    def __call__(self, rgb, depth, poses):
+        from boxfusion_amd import _lib
+        from boxfusion_amd.pipeline import scene_instances
+        from boxfusion_amd.tools_utils import scale_boxes, text_prompt
+        f = self.keyframes[self.calls]
+        self.calls += 1
+        det = self.cfg["detection"]
+        p = scene_instances(self.scene.detections(f), self.dev)
+        keep = _lib.detection_filter(p.scores, p.pred_proj_xy, p.pred_boxes_3d.tensor,
+                                     _lib.filter_cfg(det, 640, 480))
+        p = p[keep]
+        if len(p):
+            boxes = scale_boxes(p.pred_boxes.cpu().numpy(), 480, 640, scale=det["scale_box"])
+            cats, feats, sims = text_prompt(boxes, self.names, self.text, rgb[0], self, None,
+                                            det["class_sim_thres"])
+            p.categories = cats
+            p.features = feats
+            p.scores = p.scores + self.cfg["box_fusion"]["clip_sim_coeff"] * sims / 100.0
+            p = p[p.categories != ""]
+        return [p]
+
+
+def test_pipeline_run_vs_reference_demo_gap25(dev, monkeypatch):
+    """Pipeline.run + FusionStage (keyframes every 25 frames, stale re-fusion of the non-keyframe
+    last frame, demo.py:200) against the REFERENCE's own demo.py run() on the same stream
+    (tests/golden/make_golden_demo.py): final fusion lists, fused sets and num_record equal; the
+    global boxes (demo.py:371-379) and the framewise boxes / class indices / CLIP features
+    (demo.py:382-386) equal.  World-space geometry as the reference computed it is injected by
+    init_id (the particle search amplifies the 1-ulp difference of the GPU transform)."""
+    import copy
+    from boxfusion_amd.fusion_stage import FusionStage
+    from boxfusion_amd.pipeline import Pipeline, load_class_features, load_class_names
+    from boxfusion_amd.synthetic import SCANNET_K, Scene, frame_rgbd
+    d = TU.load("demo_gap25.npz")
+    _inject_geometry(monkeypatch, dev, dict(tensor=d["geom_tensor"], R=d["geom_R"], proj=d["geom_proj"]))
+    cfg = copy.deepcopy(TU.SCANNET_CFG)
+    cfg["data"] = dict(gap=int(d["gap"]))
+    cfg["detection"] = dict(score_thresh=0.5, uv_bound=True, uv_bound_value=0.9, floor_mask=True,
+                            floor_ratio=15, scale_box=1.5, class_sim_thres=25.0, size_max_thres=None)
+    cfg["box_fusion"] = dict(cfg["box_fusion"], clip_sim_coeff=1.0)
+    scene = Scene(seed=int(d["scene_seed"]), period=int(d["scene_period"]))
+    n, gap = int(d["n_frames"]), int(d["gap"])
+    names = np.asarray(load_class_names())
+    text = load_class_features()
+    det = _DemoDetect(scene, [f for f in range(n) if f % gap == 0], names, text.to(dev), cfg, dev,
+                      int(d["clip_seed"]))
+    det.text_rows = text.numpy()
+    fusion = FusionStage(cfg, SCANNET_K, device=dev, legacy_promotion=False)
+
+    def frames(ids):
+        rgb = np.stack([frame_rgbd(i)[0] for i in ids])
+        depth = np.stack([frame_rgbd(i)[1] for i in ids])
+        return (torch.from_numpy(rgb).to(dev), torch.from_numpy(depth).to(dev),
+                np.stack([scene.pose(i) for i in ids]))
+
+    Pipeline(det, fusion, gap).run(frames, n)
+    bm = fusion.box_manager
+    ragged = lambda flat, off: [flat[off[i]:off[i + 1]].tolist() for i in range(len(off) - 1)]
+    assert bm.fusion_list == ragged(d["fusion_list_flat"], d["fusion_list_off"])
+    assert bm.already_fusion == ragged(d["already_fusion_flat"], d["already_fusion_off"])
+    assert sorted(bm.num_record) == d["num_record_frames"].tolist()
+    assert [bm.num_record[k] for k in sorted(bm.num_record)] == d["num_record"].tolist()
+    assert n - 1 in bm.num_record and (n - 1) % gap != 0        # the stale re-fusion ran
+    g = fusion.all_pred_box.pred_boxes_3d.corners.cpu().numpy()
+    np.testing.assert_array_equal(g, d["global_corners"])
+    pf = fusion.per_frame_ins
+    cls = np.array([list(names).index(c) for c in pf.categories])
+    np.testing.assert_array_equal(cls, d["fw_class"])
+    np.testing.assert_array_equal(pf.pred_boxes_3d.corners.cpu().numpy(), d["fw_corners"])
+    np.testing.assert_allclose(pf.features.cpu().numpy(), d["fw_features"], rtol=1e-6, atol=1e-7)
