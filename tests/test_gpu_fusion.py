@@ -301,3 +301,39 @@ def test_boxfusion_hull_overflow_policy(L):
                 bf.boxfusion(allb, pf, bm)
             assert bf.hull_overflow_calls == 1
             assert any("HULL_OVERFLOW" in str(x.message) for x in w)
+
+
+@pytest.mark.parametrize("n_glo,n_new", [(150, 25), (97, 0), (300, 40)])
+def test_nms_scan_large_vs_oracle(L, n_glo, n_new):
+    """the greedy scan + record() with more than 96 boxes (the 256-thread k_nms_scan of the
+    default build; <= 96 runs the one-wave form): ~150 global boxes plus a keyframe's new ones,
+    clustered so that suppressions, list merges (up to 5 views) and pose gates all occur;
+    keep / success / events / fusion lists / valid_num bit-exact against the oracle"""
+    from boxfusion_amd.synthetic import Scene
+    rng = np.random.default_rng(n_glo + n_new)
+    n = n_glo + n_new
+    centres = rng.uniform(-2.5, 2.5, (n // 3 + 1, 3))
+    xyz = centres[rng.integers(0, len(centres), n)] + rng.normal(0, 0.04, (n, 3))
+    lhw = rng.uniform(0.2, 0.9, (n, 3))
+    b = np.concatenate([xyz, lhw], 1).astype(np.float32)
+    yaw = rng.uniform(-0.2, 0.2, n)
+    R = np.stack([[[np.cos(a), -np.sin(a), 0], [np.sin(a), np.cos(a), 0], [0, 0, 1]]
+                  for a in yaw]).astype(np.float32)
+    corners = OR.box_corners(b, R)
+    scores = rng.permutation(np.linspace(0.3, 0.99, n)).astype(np.float32)
+    init_id = np.arange(n, dtype=np.int32)
+    scene = Scene(seed=1)
+    cam_poses = np.stack([scene.pose(int(f)) for f in rng.integers(0, 1000, n)]).astype(np.float32)
+    # global boxes carry earlier merges (lists of up to 4 views), the new ones their own id
+    fusion_list = [sorted(set([i] + rng.integers(0, n_glo, rng.integers(0, 4)).tolist())) if i < n_glo
+                   else [i] for i in range(n)]
+    valid_num = rng.integers(0, 3, n).astype(np.float32)
+    iou = L.obb_iou_matrix(_t(corners)).cpu().numpy()
+    assert (iou[np.triu_indices(n, 1)] > 0.1).sum() > n // 4
+    got = HipBackend(L).nms(iou, corners, scores, init_id, cam_poses, fusion_list, valid_num)
+    ref = OR.nms_scan(iou, corners, scores, init_id, cam_poses, fusion_list, valid_num, nms_cfg(L))
+    assert ref["status"] == 0
+    for k in ("keep", "success", "events", "valid_num"):
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    assert got["fusion_list"] == ref["fusion_list"]
+    assert len(ref["success"]) > 10 and len(ref["events"]) > 10
