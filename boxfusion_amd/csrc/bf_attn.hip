@@ -19,6 +19,8 @@
 //   * softmax in f32 with exp2 (scale*log2e folded), O normalised once at the end.
 #include "bf_common.h"
 
+#include <type_traits>
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned short u16;
@@ -269,6 +271,24 @@ __device__ __forceinline__ void attn_softmax_tile(f32x16 (&s)[2], int k0, int sk
         for (int e = 0; e < 16; ++e) o[db][e] *= alpha;
 }
 
+// XCD-aware block order: consecutive workgroup ids land on different XCDs (id % 8 names the
+// XCD group), so the blocks of one XCD are given a contiguous range of (query block, head, batch)
+// -- the query blocks of one head (same K / V) and the neighbouring heads of one token row (the
+// same 128-B lines when 2*D is not a multiple of 128, e.g. CLIP's D = 80) then meet in that XCD's
+// L2 instead of being fetched once per XCD.  Bijective for any grid size.
+struct AttnBlk {
+    int qb, h, b;
+};
+__device__ __forceinline__ AttnBlk attn_block(int remap) {
+    const unsigned nx = gridDim.x, ny = gridDim.y, nz = gridDim.z;
+    if (!remap) return AttnBlk{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+    const unsigned n = nx * ny * nz;
+    const unsigned id = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+    const unsigned xcd = id % 8u, k = id / 8u, q = n / 8u, r = n % 8u;
+    const unsigned lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+    return AttnBlk{(int)(lin % nx), (int)((lin / nx) % ny), (int)(lin / (nx * ny))};
+}
+
 __host__ __device__ constexpr int attn_vrow_bytes(int d) {
     int sb = 2 * d;
     while (sb % 256 != 64 && sb % 256 != 192) sb += 32;
@@ -281,7 +301,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn_s(const u16* __restrict__ Q, c
                                                        int sq, int sk, int q_rs, int k_rs, int v_rs,
                                                        int o_rs, long long q_bs, long long k_bs,
                                                        long long v_bs, long long o_bs, float scale_log2,
-                                                     const int32_t* __restrict__ o_map) {
+                                                     const int32_t* __restrict__ o_map, int remap) {
     constexpr int KS = D / 16;
     constexpr int DB = (D + 31) / 32;
     constexpr int KROW = D + 8;
@@ -295,9 +315,10 @@ __global__ void __launch_bounds__(NW * 64) k_attn_s(const u16* __restrict__ Q, c
     __shared__ __attribute__((aligned(16))) u16 sV[2 * VTILE];
 
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int h = blockIdx.y, b = blockIdx.z;
+    const AttnBlk blk = attn_block(remap);
+    const int h = blk.h, b = blk.b;
     const int fr = lane & 31, fh = lane >> 5;
-    const int q = blockIdx.x * (NW * 32) + wave * 32 + fr;
+    const int q = blk.qb * (NW * 32) + wave * 32 + fr;
     const u16* Qb = Q + b * q_bs + h * D;
     const u16* Kb = K + b * k_bs + h * D;
     const u16* Vb = V + b * v_bs + h * D;
@@ -425,6 +446,235 @@ __global__ void __launch_bounds__(NW * 64) k_attn_s(const u16* __restrict__ Q, c
 
 #undef ATS_LOAD
 #undef ATS_STORE
+
+// ------------------------------------------------------------------------------------------
+// k_attn2: the streaming structure of k_attn_s, restructured for the VALU budget of short heads
+//   * full 64-key tiles run a branch-free body (no masks, both 32-key sub-tiles); only the tail
+//     tile (sk % 64 keys, CLIP: 1 key of 257) runs the masked body, with its empty sub-tile off
+//   * deferred max (RESCALE_THRESHOLD, cdna_hip_programming.md T13): O^T and l are rescaled only
+//     when a row's max grows by more than 2^8 in the exp2 domain (wave-uniform decision, taken
+//     before the tile's P is formed, so everything at the old max is scaled exactly once);
+//     P <= 2^8 then, which bf16 P and f32 O hold with no loss
+//   * D % 32 != 0 (CLIP D = 80): the zero padding rows of V^T become a ones row at d = D, so the
+//     P.V MFMA produces the row sum l in O^T's row D (the sum of the same bf16 P the numerator
+//     uses) and the 32 per-tile adds disappear
+//   * XCD-aware block order (attn_block)
+// ------------------------------------------------------------------------------------------
+#define AT2_THR 8.0f
+
+template <int D, int DB, bool ONES>
+__device__ __forceinline__ void attn2_softmax(f32x16 (&s)[2], bool sub1, bool mask, int k0, int sk,
+                                              int fh, float c, float& m_run, float& l_run,
+                                              f32x16 (&o)[DB], bf16x8 (&pf)[2][2]) {
+    if (mask) {
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int key = k0 + sub * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh;
+                s[sub][e] = (key < sk) ? s[sub][e] : -INFINITY;
+            }
+    }
+    float mt = s[0][0];
+#pragma unroll
+    for (int e = 1; e < 16; ++e) mt = fmaxf(mt, s[0][e]);
+    if (sub1) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) mt = fmaxf(mt, s[1][e]);
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * c;
+    // rescale only when some row's max grew by more than the threshold (wave-uniform)
+    if (__any(mt > m_run + AT2_THR)) {
+        const float m_new = fmaxf(m_run, mt);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);   // m_run = -inf -> 0
+        m_run = m_new;
+        l_run *= alpha;
+#pragma unroll
+        for (int db = 0; db < DB; ++db)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) o[db][e] *= alpha;
+    }
+    float ls = 0.f;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+        if (sub == 1 && !sub1) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) pf[1][e >> 3][e & 7] = (__bf16)0.0f;
+            continue;
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(s[sub][e], c, -m_run));
+            if (!ONES) ls += p;
+            pf[sub][e >> 3][e & 7] = (__bf16)p;
+        }
+    }
+    if (!ONES) l_run += ls;
+}
+
+template <int D, int NW>
+__global__ void __launch_bounds__(NW * 64) k_attn2(const u16* __restrict__ Q, const u16* __restrict__ K,
+                                                      const u16* __restrict__ V, u16* __restrict__ O,
+                                                      int sq, int sk, int q_rs, int k_rs, int v_rs,
+                                                      int o_rs, long long q_bs, long long k_bs,
+                                                      long long v_bs, long long o_bs, float scale_log2,
+                                                      const int32_t* __restrict__ o_map) {
+    constexpr int KS = D / 16;
+    constexpr int DB = (D + 31) / 32;
+    constexpr bool ONES = (D % 32) != 0;                 // a padding row of V^T carries the row sum
+    constexpr int KROW = D + 8;
+    constexpr int VROW = attn_vrow_bytes(D) / 2;
+    constexpr int KTILE = AT_KT * KROW;
+    constexpr int VTILE = AT_KT * VROW;
+    constexpr int CPR = D / 8;
+    constexpr int CH = AT_KT * CPR;
+    constexpr int NT = NW * 64;
+    __shared__ __attribute__((aligned(16))) u16 sK[2 * KTILE];
+    __shared__ __attribute__((aligned(16))) u16 sV[2 * VTILE];
+
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const AttnBlk blk = attn_block(1);
+    const int h = blk.h, b = blk.b;
+    const int fr = lane & 31, fh = lane >> 5;
+    const int q = blk.qb * (NW * 32) + wave * 32 + fr;
+    const u16* Qb = Q + b * q_bs + h * D;
+    const u16* Kb = K + b * k_bs + h * D;
+    const u16* Vb = V + b * v_bs + h * D;
+
+    bf16x8 qf[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+        qf[ks] = *reinterpret_cast<const bf16x8*>(Qb + (size_t)min(q, sq - 1) * q_rs + 16 * ks + 8 * fh);
+    // V padding columns: a ones column at d = D (the row sum), zeros after it
+    if (VROW > D)
+        for (int i = t; i < 2 * AT_KT * (VROW - D); i += NT) {
+            const int r = i / (VROW - D), c = i % (VROW - D);
+            sV[r * VROW + D + c] = (ONES && c == 0) ? (u16)0x3F80 : (u16)0;
+        }
+
+    static_assert(CH % 64 == 0 && NT % 64 == 0, "wave-uniform staging guard");
+    constexpr int NSO = (CH + NT - 1) / NT;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 stk[NSO], stv[NSO];
+    int srow[NSO], scol[NSO];
+#pragma unroll
+    for (int i = 0; i < NSO; ++i) {
+        const int c = min(t + i * NT, CH - 1);
+        srow[i] = c / CPR;
+        scol[i] = (c % CPR) * 8;
+    }
+    auto stage_load = [&](int k0_) {
+#pragma unroll
+        for (int i = 0; i < NSO; ++i) {
+            const int key = min(k0_ + srow[i], sk - 1);
+            stk[i] = *reinterpret_cast<const u32x4*>(Kb + (size_t)key * k_rs + scol[i]);
+            stv[i] = *reinterpret_cast<const u32x4*>(Vb + (size_t)key * v_rs + scol[i]);
+        }
+    };
+    auto stage_store = [&](int buf_) {
+#pragma unroll
+        for (int i = 0; i < NSO; ++i) {
+            if (t + i * NT < CH) {
+                *reinterpret_cast<u32x4*>(sK + buf_ * KTILE + srow[i] * KROW + scol[i]) = stk[i];
+                *reinterpret_cast<u32x4*>(sV + buf_ * VTILE + srow[i] * VROW + scol[i]) = stv[i];
+            }
+        }
+    };
+
+    f32x16 o[DB];
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[db][e] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+    const int g16 = (lane >> 4) & 1, q4 = (lane & 15) >> 2, p4 = lane & 3;
+    const int ntiles = (sk + AT_KT - 1) / AT_KT;
+    const int nfull = sk / AT_KT;
+
+    // one 64-key tile: S^T = K Q^T, softmax, O^T += V^T P^T (MASK: the tail tile)
+    auto tile_body = [&](int tile, auto mask_tag) {
+        constexpr bool MASK = decltype(mask_tag)::value;
+        const int k0 = tile * AT_KT, buf = tile & 1;
+        const u16* kt = sK + buf * KTILE;
+        const u16* vt = sV + buf * VTILE;
+        const bool sub1 = !MASK || (k0 + 32 < sk);
+        f32x16 s[2];
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+            if (MASK && sub == 1 && !sub1) {
+#pragma unroll
+                for (int e = 0; e < 16; ++e) s[1][e] = -INFINITY;
+                continue;
+            }
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                bf16x8 kf = *reinterpret_cast<const bf16x8*>(kt + (sub * 32 + fr) * KROW + 16 * ks + 8 * fh);
+                s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], ks == 0 ? f32x16{} : s[sub], 0, 0, 0);
+            }
+        }
+        bf16x8 pf[2][2];
+        attn2_softmax<D, DB, ONES>(s, sub1, MASK, k0, sk, fh, scale_log2, m_run, l_run, o, pf);
+#pragma unroll
+        for (int db = 0; db < DB; ++db) {
+            const int d0 = db * 32 + g16 * 16 + 4 * p4;
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+                    if (MASK && sub == 1 && !sub1) continue;
+                    const int kb = 32 * sub + 16 * ss + 4 * fh + q4;
+                    typedef __attribute__((address_space(3))) s16x4* lds_s4;
+                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4)(vt + kb * VROW + d0));
+                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4)(vt + (kb + 8) * VROW + d0));
+                    typedef short s16x8 __attribute__((ext_vector_type(8)));
+                    const s16x8 lohi = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                    o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, lohi),
+                                                                   pf[sub][ss], o[db], 0, 0, 0);
+                }
+        }
+    };
+
+    stage_load(0);
+    stage_store(0);
+    __syncthreads();
+    for (int tile = 0; tile < nfull; ++tile) {
+        const bool more = tile + 1 < ntiles;
+        if (more) stage_load((tile + 1) * AT_KT);          // in flight during this tile
+        tile_body(tile, std::false_type{});
+        if (more) stage_store((tile + 1) & 1);
+        __syncthreads();
+    }
+    if (nfull < ntiles) tile_body(nfull, std::true_type{});
+
+    // row sum: the ones row D of O^T (lane half 0, register 8 of block D / 32) or the f32 sum
+    float l;
+    if (ONES) {
+        constexpr int rr = D % 32;   // row within the last block: (e & 3) + 8 (e >> 2) + 4 fh
+        constexpr int e_l = ((rr >> 3) << 2) | (rr & 3);
+        constexpr int fh_l = (rr >> 2) & 1;
+        const float mine = o[DB - 1][e_l];
+        const float other = __shfl_xor(mine, 32, 64);
+        l = (fh == fh_l) ? mine : other;
+    } else {
+        l = l_run + __shfl_xor(l_run, 32, 64);
+    }
+    const long long o_off = attn_out_offset(o_map, b, q, sq, o_bs, o_rs);
+    if (q < sq && o_off >= 0) {
+        const float inv = 1.0f / l;
+        u16* orow = O + o_off + h * D;
+#pragma unroll
+        for (int db = 0; db < DB; ++db)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int d0 = db * 32 + 8 * g + 4 * fh;
+                if (d0 >= D) continue;
+                V64 w;
+                w.x = (uint32_t)at_f2bf(o[db][4 * g + 0] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 1] * inv) << 16);
+                w.y = (uint32_t)at_f2bf(o[db][4 * g + 2] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 3] * inv) << 16);
+                *reinterpret_cast<V64*>(orow + d0) = w;
+            }
+    }
+}
 
 // ------------------------------------------------------------------------------------------
 // Resident variant for short sequences (k_attn_r, sk <= 64*NTILE: CLIP's 257 tokens): the whole
@@ -635,11 +885,14 @@ static void launch_attn_r(dim3 grid, hipStream_t st, const void* q, const void* 
                        k_bs, v_bs, o_bs, sl2, o_map);
 }
 
-// 1/2: k_attn_s, 3: k_attn_r for short sequences, 4/5: k_attn_s with 5/3 waves per workgroup for
-// short sequences, 0: k_attn.  Default 1, env BF_ATTN_VARIANT.
+// 6 (default): k_attn2; 7 / 8: k_attn2 with two 5-wave / three 3-wave workgroups per short head;
+// 1/2: k_attn_s (with / without the XCD block order), 3: k_attn_r for short sequences, 4/5:
+// k_attn_s with 5/3 waves per workgroup for short sequences, 0: k_attn.  Env BF_ATTN_VARIANT.
+// Measured (scripts/attn_bench.py, one MI355X): CLIP 128x16x257x80 k_attn_s 153.7 us -> k_attn2
+// 128.6 us; CuTR windows 72x12x512x64 122.0 -> 109.9; CuTR global 8x12x1600x64 124.8 -> 105.0.
 static int g_attn_variant = [] {
     const char* e = getenv("BF_ATTN_VARIANT");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 6;
 }();
 BF_API void bf_attention_set_variant(int v) { g_attn_variant = v; }
 
@@ -666,12 +919,39 @@ BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, v
                                     q_bs, k_bs, v_bs, o_bs, sl2, o_map);
         return bf_check_launch();
     }
+    if (g_attn_variant >= 6 && g_attn_variant <= 8) {
+#define LAUNCH_2(DD, NWV)                                                                         \
+    hipLaunchKernelGGL((k_attn2<DD, NWV>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch),    \
+                       dim3(NWV * 64), 0, bf_stream(stream), (const u16*)q, (const u16*)k,          \
+                       (const u16*)v, (u16*)o, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs,    \
+                       o_bs, sl2, o_map)
+        // short sequences (<= 288 queries): 6 = one 9-wave workgroup per (batch, head), 7 = two
+        // 5-wave workgroups, 8 = three 3-wave workgroups (several workgroups per CU, independent
+        // barriers; K / V re-read from L2); longer ones: 4-wave workgroups of 128 queries
+        const bool short_s = nw_one > 4 && nw_one <= 9;
+        const int var = g_attn_variant;      // (`v` is the V operand)
+#define LAUNCH_2D(DD)                                                                             \
+    if (!short_s) { LAUNCH_2(DD, 4); }                                                             \
+    else if (var == 7) { LAUNCH_2(DD, 5); }                                                        \
+    else if (var == 8) { LAUNCH_2(DD, 3); }                                                        \
+    else { LAUNCH_2(DD, 9); }
+        switch (head_dim) {
+            case 32: LAUNCH_2D(32); break;
+            case 64: LAUNCH_2D(64); break;
+            case 80: LAUNCH_2D(80); break;
+            case 128: LAUNCH_2(128, 4); break;
+            default: return BF_ERR_UNSUPPORTED;
+        }
+#undef LAUNCH_2D
+#undef LAUNCH_2
+        return bf_check_launch();
+    }
     if (g_attn_variant >= 1) {
 #define LAUNCH_S(DD, NWV)                                                                         \
     hipLaunchKernelGGL((k_attn_s<DD, NWV>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch),   \
                        dim3(NWV * 64), 0, bf_stream(stream), (const u16*)q, (const u16*)k,          \
                        (const u16*)v, (u16*)o, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs,    \
-                       o_bs, sl2, o_map)
+                       o_bs, sl2, o_map, g_attn_variant == 2 ? 0 : 1)
 #define LAUNCH_SD(DD)                                                                             \
     if (nw_one > 4 && nw_one <= 9) {                                                              \
         if (g_attn_variant == 4) { LAUNCH_S(DD, 5); }                                             \

@@ -65,8 +65,8 @@ for name, ctrs in per.items():
 # the bench line's roofline kernels: launch-weighted averages over the matching kernel names
 groups = {"k_gemm256p": ["k_gemm256p"], "k_gemm256p<false, 0>": ["k_gemm256p<false, 0>"],
           "k_gemm256p<true, 1>": ["k_gemm256p<true, 1>"], "k_attn": ["k_attn"],
-          "k_attn_clip": ["k_attn_clip", "k_attn_s<80", "k_attn_r<80"],
-          "k_attn_cutr": ["k_attn_s<64", "k_attn_w", "k_attn_g"]}
+          "k_attn_clip": ["k_attn_clip", "k_attn_s<80", "k_attn_r<80", "k_attn2<80"],
+          "k_attn_cutr": ["k_attn_s<64", "k_attn_w", "k_attn_g", "k_attn2<64"]}
 out = {"round": int(R[1:]), "method": (
     "rocprofv3 --pmc FETCH_SIZE --kernel-trace, a separate --pmc WRITE_SIZE pass and an SQ "
     "instruction-count pass over `bench.py --steps 2 --warmup 1 --eager --inflight 1`; per-dispatch "

@@ -135,26 +135,37 @@ def _attn_ref(q, k, v, B, H, S, D, scale):
     return (p @ vv).transpose(1, 2).reshape(B * S, H * D)
 
 
+@pytest.mark.parametrize("variant", [6, 1])
 @pytest.mark.parametrize("B,H,S,D", [(9, 12, 512, 64), (2, 12, 1600, 64), (3, 16, 257, 80),
                                      (2, 8, 302, 32), (1, 4, 70, 128), (2, 4, 200, 64),
-                                     (2, 4, 288, 80), (2, 2, 257, 128)])
-def test_attention(L, B, H, S, D):
+                                     (2, 4, 288, 80), (2, 2, 257, 128), (3, 12, 320, 64),
+                                     (3, 12, 272, 64), (2, 16, 256, 80), (1, 3, 64, 64)])
+def test_attention(L, B, H, S, D, variant):
     g = torch.Generator(device="cuda").manual_seed(B * S + D)
     qkv = torch.randn(B * S, 3 * H * D, device="cuda", generator=g).bfloat16()
     q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
     o = torch.empty(B * S, H * D, device="cuda", dtype=torch.bfloat16)
     scale = D ** -0.5
-    L.attention(q, k, v, o, B, H, S, S, D, scale)
+    L.lib().bf_attention_set_variant(variant)
+    try:
+        L.attention(q, k, v, o, B, H, S, S, D, scale)
+    finally:
+        L.lib().bf_attention_set_variant(6)
     ref = _attn_ref(q, k, v, B, H, S, D, scale)
     assert rel_err(o, ref) < 1e-2
 
 
-def test_attention_forced_rescale(L):
-    """a spike key late in the sequence forces the online-softmax rescale branch."""
-    B, H, S, D = 1, 2, 300, 64
+@pytest.mark.parametrize("D", [64, 80])
+@pytest.mark.parametrize("spike", [4.0, 1.6, 1.25])
+def test_attention_forced_rescale(L, D, spike):
+    """a spike key late in the sequence forces the online-softmax rescale branch (deferred-max
+    kernel: a max growth beyond the threshold rescales, smaller growth is carried in P <= 2^8);
+    each lane's query meets the spike in a different tile"""
+    B, H, S = 1, 2, 300
     g = torch.Generator(device="cuda").manual_seed(11)
     qkv = torch.randn(B * S, 3 * H * D, device="cuda", generator=g)
-    qkv[250, H * D:2 * H * D] = qkv[0, :H * D] * 4.0
+    qkv[250, H * D:2 * H * D] = qkv[0, :H * D] * spike
+    qkv[130, H * D:2 * H * D] = qkv[1, :H * D] * spike * 0.8
     qkv = qkv.bfloat16()
     q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
     o = torch.empty(B * S, H * D, device="cuda", dtype=torch.bfloat16)
