@@ -41,6 +41,7 @@ sys.path.insert(0, ROOT)
 
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md), no sparsity
 PEAK_HBM_GBS = 8000.0
+PEAK_FP8_TFLOPS = 5000.0    # dense fp8 (block-scaled MFMA) peak, no sparsity
 
 CFG = dict(
     dataset="scannet",
@@ -90,6 +91,11 @@ def parse(argv=None):
                         "reserved for rank 0's fusion at N > 1 the two detect streams run on the "
                         "other 224)")
     p.add_argument("--cpu-fusion-frames", type=int, default=24)
+    p.add_argument("--clip-fp8", action="store_true",
+                   help="configs[4]: CLIP ViT-H qkv / fc1 / fc2 as fp8 e4m3 GEMMs (static per-tensor "
+                        "scales calibrated on the first batch)")
+    p.add_argument("--vocab", type=int, default=0,
+                   help="text-match vocabulary rows (0 = the 473-class table; configs[4]: 200)")
     p.add_argument("--cpu-rehearsal", action="store_true",
                    help="CPU/gloo rehearsal of the N-rank control flow (no kernels; test harness)")
     return p.parse_args(argv)
@@ -329,26 +335,25 @@ def load_pmc_traffic(kernel):
     newest round); counters cannot be read from inside the run."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
-    if not files:
-        return {}
-    with open(files[-1]) as f:
-        d = json.load(f).get(kernel)
-    if not d:
-        return {}
-    d = dict(d)
-    d["source"] = (os.path.relpath(files[-1], ROOT) + " (2 x FETCH_SIZE + WRITE_SIZE per launch, "
-                   "separate --pmc passes)")
-    return d
+    for fn in reversed(files):      # newest round first; a key may live in a workload's own file
+        with open(fn) as f:
+            d = json.load(f).get(kernel)
+        if d:
+            d = dict(d)
+            d["source"] = (os.path.relpath(fn, ROOT) + " (2 x FETCH_SIZE + WRITE_SIZE per launch, "
+                           "separate --pmc passes)")
+            return d
+    return {}
 
 
-def roofline_obj(ks, kernel, bound, pmc_key=None):
+def roofline_obj(ks, kernel, bound, pmc_key=None, peak_tflops=PEAK_BF16_TFLOPS):
     """roofline object of a KernelTimer summary: achieved = algorithmic FLOPs (or bytes) per launch
     / average launch time (HIP events on the launch stream)"""
     pmc = load_pmc_traffic(pmc_key or kernel) if ks["launches"] else {}
     if bound == "hbm":
         achieved, peak, unit = ks.get("gbs", 0.0), PEAK_HBM_GBS, "GB/s"
     else:
-        achieved, peak, unit = ks.get("tflops", 0.0), PEAK_BF16_TFLOPS, "TFLOP/s"
+        achieved, peak, unit = ks.get("tflops", 0.0), peak_tflops, "TFLOP/s"
     return {"bound": bound, "kernel": kernel, "achieved": achieved, "peak": peak, "unit": unit,
             "frac": achieved / peak, "traffic": pmc.get("bytes_per_launch"),
             "traffic_source": pmc.get("source"), "launches": ks["launches"],
@@ -361,6 +366,18 @@ def emit(line):
 
 
 def base_line(args, N, frames, dt, per_step, n_inflight):
+    if getattr(args, "clip_fp8", False):
+        line = base_line_bf16(args, N, frames, dt, per_step, n_inflight)
+        line["dtype"] = "bf16 + fp8 e4m3 (CLIP ViT-H qkv / fc1 / fc2)"
+        line["config"]["workload"] = (
+            f"configs[4]: synthetic 640x480 RGB-D (ScanNetV2 scene0000_00 absent offline), batch "
+            f"{args.batch}/step/GPU, gap=1, CuTR ViT-B RGB-D bf16 + CLIP ViT-H/14 fp8 x{args.crops} "
+            f"crops/frame + {args.vocab or 473}-class text match + fusion")
+        return line
+    return base_line_bf16(args, N, frames, dt, per_step, n_inflight)
+
+
+def base_line_bf16(args, N, frames, dt, per_step, n_inflight):
     return {
         "metric": "RGB-D frames/sec (whole node) on 640x480 stream",
         "value": frames / dt, "unit": "frames/s", "n_gpus": N, "steps": args.steps,
@@ -480,9 +497,18 @@ def main(argv=None):
         clip_vis = VisionTransformer(224, 14, 1280, args.clip_layers, 16, 1024).eval()
     B = args.batch
     n_inflight = args.inflight if args.inflight > 0 else 2
-    detects = [DetectStage(cutr, clip_vis, CFG, B, 480, 640, SCANNET_K, crops_per_frame=args.crops,
+    from boxfusion_amd.pipeline import load_class_features, load_class_names
+    text, names = load_class_features(), load_class_names()
+    if args.vocab:
+        # configs[4]'s 200-class vocabulary: the ScanNet200 names / CLIP text features are not in
+        # the reference; the first `vocab` rows of its 473-class table stand in (same match kernel
+        # path, vocabulary-sized)
+        text, names = text[:args.vocab].clone(), names[:args.vocab]
+    detects = [DetectStage(cutr, clip_vis, CFG, B, 480, 640, SCANNET_K, text_features=text.clone(),
+                           class_names=names, crops_per_frame=args.crops,
                            crop_source="given", backproject=True, clip_capacity=B * args.crops,
-                           device=dev, graph=not args.eager) for _ in range(n_inflight)]
+                           device=dev, graph=not args.eager, clip_fp8=args.clip_fp8)
+               for _ in range(n_inflight)]
     detect = detects[0]
     scene = Scene(seed=0)
     N = world
@@ -500,6 +526,14 @@ def main(argv=None):
     dets_mine = [scene.detections(f) for f in all_mine]
     rec_all = torch.from_numpy(pack_records(dets_mine, poses_all)).to(dev)
     crops_all = torch.from_numpy(crop_boxes(dets_mine, args.crops)).to(dev)
+    if args.clip_fp8:
+        # static fp8 activation scales: calibrated once (bf16 forward of this rank's first batch
+        # of crops, untimed) and shared by every in-flight detect stage
+        from boxfusion_amd.pipeline import scale_boxes
+        bi = scale_boxes(crops_all[:B * args.crops], 480, 640, detect.scale_box).to(torch.int32)
+        scales = detect.clip.calibrate(rgb_all[:B], bi.contiguous(), detect.top_b32)
+        for d in detects[1:]:
+            d.clip.act_scales = scales
     sim = None
     if args.sim_ranks > 1 and world == 1:
         # what rank 0 of an R-GPU run fuses: R*B frames per step (stress test, not the metric)
@@ -658,6 +692,14 @@ def main(argv=None):
         line = base_line(args, N, frames, dt, per_step, n_inflight)
         line["config"].update(fused_boxes=fusion.stats["fused"],
                               global_boxes=len(fusion.all_pred_box) if fusion.all_pred_box is not None else 0)
+        if args.clip_fp8:
+            f8 = roofline_obj(timer.summary(lambda t: t["kind"] == "gemm_fp8"),
+                              "k_gemm256p<*, *, fp8> (CLIP qkv, fc1 + GELU -> fp8, fc2 + f32 residual; "
+                              "block-scaled fp8 MFMA)", "mfma", pmc_key="k_gemm256p_fp8",
+                              peak_tflops=PEAK_FP8_TFLOPS)
+            f8["measured"] = source
+            comps["bf16_gemm"] = r_all
+            r_all = f8
         line["roofline"] = r_all
         line["roofline_components"] = comps
         if args.breakdown:

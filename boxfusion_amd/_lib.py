@@ -489,6 +489,55 @@ def layernorm(x, weight, bias, eps, out=None, row_map=None, out_dtype=torch.bflo
     return out
 
 
+FP8 = torch.float8_e4m3fn      # OCP e4m3 (gfx950's fp8; not the MI300 fnuz variant)
+FP8_MAX = 448.0
+_FP8_OUT = {torch.float32: 0, torch.bfloat16: 1, FP8: 2}
+
+
+def gemm_fp8(a, w, scale, bias=None, act=None, resid=None, out=None, out_dtype=torch.bfloat16,
+             out_qscale=1.0):
+    """out = resid + act(scale * (a @ w.T) + bias); a fp8 e4m3 [M,K], w fp8 [N,K] (per-tensor
+    scales folded into `scale`); out f32 / bf16 / fp8 (fp8: saturate(value * out_qscale))."""
+    _need(a, FP8, "a")
+    _need(w, FP8, "w")
+    M, K = a.shape
+    N = w.shape[0]
+    if w.shape[1] != K:
+        raise HipError(f"gemm_fp8: a K={K} vs w K={w.shape[1]}")
+    if out is None:
+        out = torch.empty((M, N), dtype=out_dtype, device=a.device)
+    if out.dtype not in _FP8_OUT:
+        raise HipError("gemm_fp8 output must be f32, bf16 or fp8")
+    if resid is not None:
+        _need(resid, torch.float32, "resid")
+    if bias is not None:
+        _need(bias, torch.float32, "bias")
+    if a.stride(1) != 1 or w.stride(1) != 1 or out.stride(1) != 1:
+        raise HipError("gemm_fp8 operands need unit column stride")
+    _check(lib().bf_gemm_fp8(c_void_p(a.data_ptr()), c_int(a.stride(0)), c_void_p(w.data_ptr()),
+                             c_int(w.stride(0)), c_float(scale), _ptr(bias) if bias is not None else None,
+                             c_void_p(resid.data_ptr()) if resid is not None else None,
+                             c_int(resid.stride(0) if resid is not None else 0), c_void_p(out.data_ptr()),
+                             c_int(out.stride(0)), c_int(_FP8_OUT[out.dtype]), c_float(out_qscale),
+                             c_int(M), c_int(N), c_int(K), c_int(ACT[act]), _stream()), "bf_gemm_fp8")
+    return out
+
+
+def layernorm_fp8(x, weight, bias, eps, qscale, out=None):
+    """x f32 [M, C] -> fp8 e4m3 saturate(LayerNorm(x) * qscale)"""
+    _need(x, torch.float32, "x")
+    M, C = x.shape
+    if out is None:
+        out = torch.empty((M, C), dtype=FP8, device=x.device)
+    _need(out, FP8, "out")
+    if x.stride(1) != 1 or out.stride(1) != 1:
+        raise HipError("layernorm_fp8: unit column stride")
+    _check(lib().bf_layernorm_fp8(c_void_p(x.data_ptr()), c_int(x.stride(0)), _ptr(weight), _ptr(bias),
+                                  c_float(eps), c_void_p(out.data_ptr()), c_int(out.stride(0)),
+                                  c_float(qscale), c_int(M), c_int(C), _stream()), "bf_layernorm_fp8")
+    return out
+
+
 def _f3(vals):
     return (c_float * 3)(*[float(v) for v in vals])
 
@@ -584,6 +633,7 @@ class KernelTimer:
 
 _TIMER = None
 _gemm_untimed = gemm
+_gemm_fp8_untimed = gemm_fp8
 _attention_untimed = attention
 
 
@@ -602,6 +652,20 @@ def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype
         nbytes += 4.0 * (M * N if not resid_mod else resid_mod * N)
     return t.record(tags, 2.0 * M * N * K, nbytes,
                     lambda: _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m))
+
+
+def gemm_fp8(a, w, scale, bias=None, act=None, resid=None, out=None, out_dtype=torch.bfloat16,
+             out_qscale=1.0):
+    t = _TIMER
+    if t is None:
+        return _gemm_fp8_untimed(a, w, scale, bias, act, resid, out, out_dtype, out_qscale)
+    M, K = a.shape
+    N = w.shape[0]
+    od = out.dtype if out is not None else out_dtype
+    tags = dict(kind="gemm_fp8", act=ACT[act], out=str(od), resid=resid is not None, M=M, N=N, K=K)
+    nbytes = 1.0 * (M * K + N * K) + M * N * od.itemsize + (4.0 * M * N if resid is not None else 0.0)
+    return t.record(tags, 2.0 * M * N * K, nbytes,
+                    lambda: _gemm_fp8_untimed(a, w, scale, bias, act, resid, out, out_dtype, out_qscale))
 
 
 def attention(q, k, v, o, batch, heads, sq, sk, head_dim, scale, q_bs=None, k_bs=None, v_bs=None,

@@ -600,8 +600,28 @@ typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 #else
 #define GEMM_ST_U4(p, o) (*reinterpret_cast<U128*>(p) = (o))
 #endif
+typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
+#if GEMM_NT & 1
+#define GEMM_ST_U2(p, a, b) __builtin_nontemporal_store((u32x2v){(unsigned)(a), (unsigned)(b)}, reinterpret_cast<u32x2v*>(p))
+#else
+#define GEMM_ST_U2(p, a, b) (*reinterpret_cast<u32x2v*>(p) = (u32x2v){(unsigned)(a), (unsigned)(b)})
+#endif
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+// one 32-B fp8 MFMA fragment from two 16-B LDS reads
+__device__ __forceinline__ i32x8 frag32(bf16x8 a, bf16x8 b) {
+    return __builtin_shufflevector(__builtin_bit_cast(i32x4, a), __builtin_bit_cast(i32x4, b), 0, 1, 2, 3, 4, 5, 6, 7);
+}
 
-template <bool OUT_BF16, int ACT>
+// F8 (bit 0): A and W are fp8 e4m3 (OCP) with BK = 128 elements per K-tile (the same 128-B LDS rows),
+// on the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 with unit block scales (E8M0 127): twice
+// the bf16 MFMA rate.  The epilogue then computes acc * csc + bias[n] (csc = activation scale x
+// weight scale, both per tensor: a scalar, no extra VGPRs beside the 246-255 the kernel already
+// holds); an in-place residual initialises the accumulators with resid / csc.  F8 bit 1: fp8 output, v * oqs clamped to +-448 (OUT_BF16 must be set: 8
+// columns per lane, one 8-B store).  The fp8 lane fragment is the bf16 kernel's two k-step
+// fragments (16-B chunks lq and 4+lq of the 128-B row): the MFMA's k order inside a fragment only
+// has to agree between A and B, and the bf16 chunk pattern keeps the LDS reads conflict-free.
+template <bool OUT_BF16, int ACT, int F8 = 0>
 __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restrict__ A, int lda,
                                                             const u16* __restrict__ W, int ldw,
                                                             const float* __restrict__ bias,
@@ -609,8 +629,15 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
                                                             int resid_mod, void* __restrict__ Cv,
                                                             int ldc, const int32_t* __restrict__ row_map,
                                                             int M, int N, int K, int tiles_n,
-                                                            int tiles_m, int stagger, int gm, int ablate) {
+                                                            int tiles_m, int stagger, int gm, int ablate,
+                                                            float csc = 1.f, float oqs = 1.f) {
     extern __shared__ __attribute__((aligned(16))) unsigned char g_smem[];
+#if GEMM_TACC
+    static_assert(F8 == 0, "fp8 operands use the default accumulator layout");
+#endif
+    static_assert(!(F8 & 2) || OUT_BF16, "fp8 output takes the 8-column store path");
+    constexpr int ESZ = (F8 & 1) ? 1 : 2;           // operand bytes
+    constexpr int KTE = GB_K * 2 / ESZ;             // K elements per 128-B K-tile row
     const int t = threadIdx.x;
     const int lane = t & 63, wave = t >> 6;
     const int wr = wave >> 2, wc = wave & 3;
@@ -619,7 +646,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
     const int G = gridDim.x;
     const int slot = (G % 8 == 0) ? ((int)blockIdx.x % 8) * (G / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
     const int my_tiles = ntiles > slot ? (ntiles - slot + G - 1) / G : 0;
-    const int nk = K / GB_K;
+    const int nk = K / KTE;
     const int total = my_tiles * nk;
     if (total == 0) return;
 
@@ -638,8 +665,8 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
             b_row[h][i] = (L >> 5) * 64 + h * 32 + (L & 31);      // tile column of B-half h
         }
     }
-    const int bytesA = (int)(((size_t)(M - 1) * lda + K) * 2);    // < 2^31 (checked on the host)
-    const int bytesW = (int)(((size_t)(N - 1) * ldw + K) * 2);
+    const int bytesA = (int)(((size_t)(M - 1) * lda + K) * ESZ);  // < 2^31 (checked on the host)
+    const int bytesW = (int)(((size_t)(N - 1) * ldw + K) * ESZ);
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
     // K-tile coordinates of the walk, advanced incrementally (a division only at tile boundaries);
     // past the end of the walk the last K-tile is repeated (same bytes into the same stage)
@@ -653,7 +680,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
     int tile_ord = 0;       // tile ordinal (within this block's walk) of the newest KT built
     auto kt_next = [&](KT c) {
         if (c.idx >= total - 1) return c;
-        if (c.k0 + GB_K < K) { c.k0 += GB_K; c.idx += 1; c.buf ^= 1; return c; }
+        if (c.k0 + KTE < K) { c.k0 += KTE; c.idx += 1; c.buf ^= 1; return c; }
         ++tile_ord;
         return kt_at_tile(tile_ord, c.idx + 1);
     };
@@ -665,8 +692,8 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
         for (int h = 0; h < 2; ++h)
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                v.a[h][i] = min(c.m0 + a_row[h][i], M - 1) * lda * 2 + scol[i];
-                v.b[h][i] = min(c.n0 + b_row[h][i], N - 1) * ldw * 2 + scol[i];
+                v.a[h][i] = min(c.m0 + a_row[h][i], M - 1) * lda * ESZ + scol[i];
+                v.b[h][i] = min(c.n0 + b_row[h][i], N - 1) * ldw * ESZ + scol[i];
             }
         return v;
     };
@@ -676,9 +703,9 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
         unsigned char* dst_ = g_smem + (c).buf * 65536 + (which) * 16384 + wave_u * 2048;          \
         _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                         \
             if ((which) < 2)                                                                       \
-                glds_buf16(A, bytesA, dst_ + i_ * 1024, (v).a[(which) & 1][i_], (c).k0 * 2);       \
+                glds_buf16(A, bytesA, dst_ + i_ * 1024, (v).a[(which) & 1][i_], (c).k0 * ESZ);     \
             else                                                                                   \
-                glds_buf16(W, bytesW, dst_ + i_ * 1024, (v).b[(which) & 1][i_], (c).k0 * 2);       \
+                glds_buf16(W, bytesW, dst_ + i_ * 1024, (v).b[(which) & 1][i_], (c).k0 * ESZ);     \
         }                                                                                          \
     }
 
@@ -709,10 +736,13 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
 #define ACC_INIT(m0_, n0_)                                                                         \
     {                                                                                              \
         if (acc_init) {                                                                            \
+            const float rc_ = (F8 & 1) ? 1.f / csc : 1.f;                                         \
             _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int e = 0; e < 4; ++e) { \
                 const float* rp_ = resid + (size_t)min((m0_) + wr * 128 + i * 16 + 4 * lq + e, M - 1) * ldr; \
-                _Pragma("unroll") for (int j = 0; j < 4; ++j)                                      \
+                _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                    \
                     acc[i][j][e] = GEMM_LD_F(rp_ + min((n0_) + wc * 64 + j * 16 + lr, N - 1));      \
+                    if (F8 & 1) acc[i][j][e] *= rc_;                                               \
+                }                                                                                  \
             }                                                                                      \
         } else {                                                                                   \
             _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 4; ++j) \
@@ -722,25 +752,51 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
 #endif
 
     bf16x8 fa[8], fb0[4], fb1[4];     // fa: A-half fragments [i*2 + ks]; fb*: [j*2 + ks]
+    i32x8 ga[4], gb0[2], gb1[2];      // fp8: the two 16-B chunks of a lane as one 32-B fragment
+#define LDS16(off) (*reinterpret_cast<const bf16x8*>(g_smem + (off)))
 #define RD_A(stage, mi)                                                                            \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) \
-        fa[i * 2 + ks] = *reinterpret_cast<const bf16x8*>(                                         \
-            g_smem + (stage) * 65536 + (mi) * 16384 + swz(wr * 64 + i * 16 + lr, ks * 4 + lq));
-#define RD_B(FB, stage, ni)                                                                        \
-    _Pragma("unroll") for (int j = 0; j < 2; ++j) _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) \
-        FB[j * 2 + ks] = *reinterpret_cast<const bf16x8*>(                                         \
-            g_smem + (stage) * 65536 + 32768 + (ni) * 16384 + swz(wc * 32 + j * 16 + lr, ks * 4 + lq));
+    if constexpr ((F8 & 1) != 0) {                                                                 \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                            \
+            const int b_ = (stage) * 65536 + (mi) * 16384;                                         \
+            ga[i] = frag32(LDS16(b_ + swz(wr * 64 + i * 16 + lr, lq)),                             \
+                           LDS16(b_ + swz(wr * 64 + i * 16 + lr, 4 + lq)));                        \
+        }                                                                                          \
+    } else {                                                                                       \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) \
+            fa[i * 2 + ks] = LDS16((stage) * 65536 + (mi) * 16384 + swz(wr * 64 + i * 16 + lr, ks * 4 + lq)); \
+    }
+#define RD_B(FB, GB, stage, ni)                                                                    \
+    if constexpr ((F8 & 1) != 0) {                                                                 \
+        _Pragma("unroll") for (int j = 0; j < 2; ++j) {                                            \
+            const int b_ = (stage) * 65536 + 32768 + (ni) * 16384;                                 \
+            GB[j] = frag32(LDS16(b_ + swz(wc * 32 + j * 16 + lr, lq)),                             \
+                           LDS16(b_ + swz(wc * 32 + j * 16 + lr, 4 + lq)));                        \
+        }                                                                                          \
+    } else {                                                                                       \
+        _Pragma("unroll") for (int j = 0; j < 2; ++j) _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) \
+            FB[j * 2 + ks] = LDS16((stage) * 65536 + 32768 + (ni) * 16384 + swz(wc * 32 + j * 16 + lr, ks * 4 + lq)); \
+    }
 #if GEMM_TACC
 #define MFMA_OP(FA, FB, C) __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB, FA, C, 0, 0, 0)   // C^T += W A^T
 #else
 #define MFMA_OP(FA, FB, C) __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA, FB, C, 0, 0, 0)
 #endif
-#define MFMA_Q(mi, ni, FB)                                                                         \
+#define MFMA_Q(mi, ni, FB, GB)                                                                     \
     {                                                                                              \
         __builtin_amdgcn_s_setprio(1);                                                             \
-        _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i) \
-            _Pragma("unroll") for (int j = 0; j < 2; ++j) acc[(mi) * 4 + i][(ni) * 2 + j] =        \
-                MFMA_OP(fa[i * 2 + ks], FB[j * 2 + ks], acc[(mi) * 4 + i][(ni) * 2 + j]);           \
+        if constexpr ((F8 & 1) != 0) {                                                             \
+            _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) \
+                acc[(mi) * 4 + i][(ni) * 2 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4( \
+                    ga[i], GB[j], acc[(mi) * 4 + i][(ni) * 2 + j], 0, 0, 0, 127, 0, 127);          \
+            /* the scaled MFMA builtin is not convergent: pin the results to this phase, or IR     \
+               sinking moves all four quadrants' MFMAs behind the last barrier */                  \
+            _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) \
+                asm volatile("" : "+v"(acc[(mi) * 4 + i][(ni) * 2 + j]));                          \
+        } else {                                                                                   \
+            _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i) \
+                _Pragma("unroll") for (int j = 0; j < 2; ++j) acc[(mi) * 4 + i][(ni) * 2 + j] =    \
+                    MFMA_OP(fa[i * 2 + ks], FB[j * 2 + ks], acc[(mi) * 4 + i][(ni) * 2 + j]);       \
+        }                                                                                          \
         __builtin_amdgcn_s_setprio(0);                                                             \
     }
 
@@ -791,26 +847,26 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
 #endif
         }
         // ---- P1: quadrant (0,0); reads B0 (retired before the barrier) then A0
-        RD_B(fb0, st, 0);
+        RD_B(fb0, gb0, st, 0);
         SB0();
         RD_A(st, 0);
         asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
         PHASE_BARRIER();
-        MFMA_Q(0, 0, fb0);
+        MFMA_Q(0, 0, fb0, gb0);
         PHASE_BARRIER();
         // ---- P2: quadrant (0,1); reads B1 (retired before the barrier); stage B0 of g+2
-        RD_B(fb1, st, 1);
+        RD_B(fb1, gb1, st, 1);
         STAGE_HALF(k2, v2, 2);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         PHASE_BARRIER();
-        MFMA_Q(0, 1, fb1);
+        MFMA_Q(0, 1, fb1, gb1);
         PHASE_BARRIER();
         // ---- P3: quadrant (1,1); reads A1 (retired before the barrier); stage A0 of g+2
         RD_A(st, 1);
         STAGE_HALF(k2, v2, 0);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         PHASE_BARRIER();
-        MFMA_Q(1, 1, fb1);
+        MFMA_Q(1, 1, fb1, gb1);
         PHASE_BARRIER();
         // ---- P4: quadrant (1,0) from registers; stage B1 and A1 of g+2; retire K-tile g+1 (the
         // stores of an epilogue issued since K-tile g+1 was staged may stay in flight)
@@ -824,7 +880,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         }
         PHASE_BARRIER();
-        MFMA_Q(1, 0, fb0);
+        MFMA_Q(1, 0, fb0, gb0);
         PHASE_BARRIER();
         const KT kd = kc;
         kc = k1; k1 = k2;
@@ -833,7 +889,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
             if (kn.k0 == 0 && kn.idx != k2.idx) v2 = vo_of(kn);   // entered a new tile
             k2 = kn;
         }
-        if (kd.k0 != K - GB_K) continue;
+        if (kd.k0 != K - KTE) continue;
         if (ablate == 1) {          // diagnostic: no epilogue at all (keeps acc live)
 #pragma unroll
             for (int i = 0; i < 8; ++i)
@@ -861,8 +917,14 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
 #else
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                f32x2 v01 = {acc[i][j][0] + bv[j], acc[i][j][1] + bv[j]};
-                f32x2 v23 = {acc[i][j][2] + bv[j], acc[i][j][3] + bv[j]};
+                f32x2 v01, v23;
+                if constexpr ((F8 & 1) != 0) {
+                    v01 = {fmaf(acc[i][j][0], csc, bv[j]), fmaf(acc[i][j][1], csc, bv[j])};
+                    v23 = {fmaf(acc[i][j][2], csc, bv[j]), fmaf(acc[i][j][3], csc, bv[j])};
+                } else {
+                    v01 = {acc[i][j][0] + bv[j], acc[i][j][1] + bv[j]};
+                    v23 = {acc[i][j][2] + bv[j], acc[i][j][3] + bv[j]};
+                }
                 if (ACT == 1) gelu_erf2x2(v01, v23);
                 else if (ACT == 2) {
                     v01.x = fmaxf(v01.x, 0.f); v01.y = fmaxf(v01.y, 0.f);
@@ -926,7 +988,16 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
                     }
                 }
                 if (keep) {
-                    if (OUT_BF16) {
+                    if constexpr ((F8 & 2) != 0) {
+                        int lo = 0, hi = 0;
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) v[q] = fminf(fmaxf(v[q] * oqs, -448.f), 448.f);
+                        lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], lo, false);
+                        lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], lo, true);
+                        hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4], v[5], hi, false);
+                        hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6], v[7], hi, true);
+                        GEMM_ST_U2(reinterpret_cast<unsigned char*>(Cv) + (size_t)orow * ldc + n, lo, hi);
+                    } else if (OUT_BF16) {
                         U128 o;
                         o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
                         o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
@@ -948,6 +1019,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outstanding at exit
 #undef RD_A
 #undef RD_B
+#undef LDS16
 #undef MFMA_Q
 #undef MFMA_OP
 #undef STAGE_HALF
@@ -1105,5 +1177,65 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
         else GEMM_LAUNCH(false, 2);
     }
 #undef GEMM_LAUNCH
+    return bf_check_launch();
+}
+
+// ------------------------------------------------------------------------------------------
+// fp8 e4m3 GEMM (CLIP ViT-H fp8 path, BASELINE configs[4]): C = act(A W^T * scale + bias[n])
+// (+ resid), A [M,K] and W [N,K] fp8 (row strides in elements = bytes), scale = activation scale x
+// weight scale (per-tensor both).  out_kind 0: f32 C (optionally + resid, in place allowed),
+// 1: bf16 C, 2: fp8 C = sat448(value * out_qscale).  The persistent 256x256 kernel only.
+// ------------------------------------------------------------------------------------------
+template <bool OB, int AC, int F8>
+static void launch_gemm256_f8(int grid, hipStream_t st, const void* A, int lda, const void* W, int ldw,
+                              float csc, const float* bias, const float* resid, int ldr, void* C,
+                              int ldc, float oqs, int M, int N, int K, int tiles_n, int tiles_m) {
+    static bool attr = false;
+    if (!attr) {
+        hipFuncSetAttribute((const void*)k_gemm256p<OB, AC, F8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            G2_LDS);
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_gemm256p<OB, AC, F8>), dim3(grid), dim3(G2_THREADS), G2_LDS, st, (const u16*)A,
+                       lda, (const u16*)W, ldw, bias, resid, ldr, 0, C, ldc, (const int32_t*)nullptr, M, N,
+                       K, tiles_n, tiles_m, 1, g_group_m, 0, csc, oqs);
+}
+
+BF_API int bf_gemm_fp8(const void* A, int lda, const void* W, int ldw, float scale,
+                       const float* bias, const float* resid, int ldr, void* C, int ldc, int out_kind,
+                       float out_qscale, int M, int N, int K, int act, void* stream) {
+    if (!A || !W || !C || !(scale > 0.f) || M < 0 || N <= 0 || K <= 0 || act < 0 || act > 1 ||
+        out_kind < 0 || out_kind > 2)
+        return BF_ERR_ARG;
+    if (K % 128 != 0 || lda % 16 != 0 || ldw % 16 != 0) return BF_ERR_UNSUPPORTED;
+    if (resid && (out_kind != 0 || (uintptr_t)resid % 16 != 0 || ldr % 4 != 0)) return BF_ERR_UNSUPPORTED;
+    if (out_kind == 0 && (N % 4 || ldc % 4 || (uintptr_t)C % 16)) return BF_ERR_UNSUPPORTED;
+    if (out_kind == 1 && (N % 8 || ldc % 8 || (uintptr_t)C % 16)) return BF_ERR_UNSUPPORTED;
+    if (out_kind == 2 && (N % 8 || ldc % 8 || (uintptr_t)C % 8)) return BF_ERR_UNSUPPORTED;
+    if (M == 0) return BF_OK;
+    if ((long long)(M - 1) * lda + K >= (1LL << 31) || (long long)(N - 1) * ldw + K >= (1LL << 31))
+        return BF_ERR_CAPACITY;
+    const int t2m = (M + 255) / 256, t2n = (N + 255) / 256;
+    const long long t2 = (long long)t2m * t2n;
+    const int n_cu = gemm_cu_count();
+    int grid = (int)(t2 < n_cu ? t2 : n_cu);
+    if (gemm_balanced() && t2 > n_cu && (gemm_balanced() == 2 || t2 % n_cu >= n_cu / 4)) {
+        const long long rounds = (t2 + n_cu - 1) / n_cu;
+        const int g = (int)(((t2 + rounds - 1) / rounds + 7) & ~7LL);
+        grid = g < n_cu ? g : n_cu;
+    }
+#define GEMM8(OB, AC, F8) launch_gemm256_f8<OB, AC, F8>(grid, bf_stream(stream), A, lda, W, ldw, scale, bias, \
+                                                         resid, ldr, C, ldc, out_qscale, M, N, K, t2n, t2m)
+    if (out_kind == 0) {
+        if (act != 0) return BF_ERR_UNSUPPORTED;   // (f32 GELU output: not on the path)
+        GEMM8(false, 0, 1);
+    } else if (out_kind == 1) {
+        if (act == 0) GEMM8(true, 0, 1);
+        else GEMM8(true, 1, 1);
+    } else {
+        if (act == 0) GEMM8(true, 0, 3);
+        else GEMM8(true, 1, 3);
+    }
+#undef GEMM8
     return bf_check_launch();
 }

@@ -23,13 +23,14 @@ struct alignas(16) W128 {
 // ------------------------------------------------------------------------------------------
 // LayerNorm: one wave per row, C <= 4096, C % 4 == 0
 // ------------------------------------------------------------------------------------------
-template <int NPL, bool F32OUT>  // float4 per lane; f32 or bf16 output
+// OUTK 0: bf16 output, 1: f32, 2: fp8 e4m3 (OCP) = sat448(y * qs) (the CLIP fp8 path's GEMM input)
+template <int NPL, int OUTK>  // float4 per lane
 __global__ void __launch_bounds__(256) k_layernorm(const float* __restrict__ x, int ldx,
                                                    const float* __restrict__ g,
                                                    const float* __restrict__ bb, float eps,
                                                    void* __restrict__ out_, int ldo,
                                                    const int32_t* __restrict__ row_map, int M,
-                                                   int C) {
+                                                   int C, float qs = 1.f) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (row >= M) return;
@@ -60,7 +61,26 @@ __global__ void __launch_bounds__(256) k_layernorm(const float* __restrict__ x, 
     const float rstd = rsqrtf(q / (float)C + eps);
     const int orow = row_map ? row_map[row] : row;
     if (orow < 0) return;
-    if (F32OUT) {      // (in place allowed: the row is in registers before the first store)
+    if (OUTK == 2) {
+        unsigned char* yr = static_cast<unsigned char*>(out_) + (size_t)orow * ldo;
+#pragma unroll
+        for (int i = 0; i < NPL; ++i) {
+            int c = (lane + 64 * i) * 4;
+            if (c < C) {
+                float4 gg = *reinterpret_cast<const float4*>(g + c);
+                float4 be = *reinterpret_cast<const float4*>(bb + c);
+                const float y0 = fminf(fmaxf(((v[i].x - mean) * rstd * gg.x + be.x) * qs, -448.f), 448.f);
+                const float y1 = fminf(fmaxf(((v[i].y - mean) * rstd * gg.y + be.y) * qs, -448.f), 448.f);
+                const float y2 = fminf(fmaxf(((v[i].z - mean) * rstd * gg.z + be.z) * qs, -448.f), 448.f);
+                const float y3 = fminf(fmaxf(((v[i].w - mean) * rstd * gg.w + be.w) * qs, -448.f), 448.f);
+                int p = __builtin_amdgcn_cvt_pk_fp8_f32(y0, y1, 0, false);
+                p = __builtin_amdgcn_cvt_pk_fp8_f32(y2, y3, p, true);
+                *reinterpret_cast<int*>(yr + c) = p;
+            }
+        }
+        return;
+    }
+    if (OUTK == 1) {      // (in place allowed: the row is in registers before the first store)
         float* yr = static_cast<float*>(out_) + (size_t)orow * ldo;
 #pragma unroll
         for (int i = 0; i < NPL; ++i) {
@@ -100,10 +120,10 @@ BF_API int bf_layernorm_out(const float* x, int ldx, const float* gamma, const f
     dim3 grid((M + 3) / 4), block(256);
     const int npl = (C / 4 + 63) / 64;
 #define LN(N)                                                                                      \
-    if (out_f32) hipLaunchKernelGGL((k_layernorm<N, true>), grid, block, 0, bf_stream(stream), x,  \
-                                    ldx, gamma, beta, eps, out, ldo, row_map, M, C);               \
-    else hipLaunchKernelGGL((k_layernorm<N, false>), grid, block, 0, bf_stream(stream), x, ldx,    \
-                            gamma, beta, eps, out, ldo, row_map, M, C)
+    if (out_f32) hipLaunchKernelGGL((k_layernorm<N, 1>), grid, block, 0, bf_stream(stream), x,     \
+                                    ldx, gamma, beta, eps, out, ldo, row_map, M, C, 1.f);          \
+    else hipLaunchKernelGGL((k_layernorm<N, 0>), grid, block, 0, bf_stream(stream), x, ldx,        \
+                            gamma, beta, eps, out, ldo, row_map, M, C, 1.f)
     if (npl <= 1) LN(1);
     else if (npl <= 2) LN(2);
     else if (npl <= 3) LN(3);
@@ -119,6 +139,26 @@ BF_API int bf_layernorm_out(const float* x, int ldx, const float* gamma, const f
 BF_API int bf_layernorm(const float* x, int ldx, const float* gamma, const float* beta, float eps,
                         void* out, int ldo, const int32_t* row_map, int M, int C, void* stream) {
     return bf_layernorm_out(x, ldx, gamma, beta, eps, out, ldo, 0, row_map, M, C, stream);
+}
+
+BF_API int bf_layernorm_fp8(const float* x, int ldx, const float* gamma, const float* beta, float eps,
+                            void* out, int ldo, float qscale, int M, int C, void* stream) {
+    if (!x || !gamma || !beta || !out || M < 0 || C <= 0 || C % 4 || ldx % 4 || ldo % 4 ||
+        !(qscale > 0.f))
+        return BF_ERR_ARG;
+    if (M == 0) return BF_OK;
+    dim3 grid((M + 3) / 4), block(256);
+    const int npl = (C / 4 + 63) / 64;
+#define LN8(N) hipLaunchKernelGGL((k_layernorm<N, 2>), grid, block, 0, bf_stream(stream), x, ldx, gamma, \
+                                  beta, eps, out, ldo, (const int32_t*)nullptr, M, C, qscale)
+    if (npl <= 2) LN8(2);
+    else if (npl <= 4) LN8(4);
+    else if (npl <= 5) LN8(5);
+    else if (npl <= 8) LN8(8);
+    else if (npl <= 16) LN8(16);
+    else return BF_ERR_UNSUPPORTED;
+#undef LN8
+    return bf_check_launch();
 }
 
 // ------------------------------------------------------------------------------------------

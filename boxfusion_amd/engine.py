@@ -239,12 +239,25 @@ class CuTREngine:
         return self.model.decode(feat, batch, pos=pos)
 
 
+def _fp8_weight(w):
+    """per-tensor e4m3 quantisation of a weight: (w / s in fp8, s = amax / 448)"""
+    w = w.detach().to(torch.float32)
+    s = float(w.abs().max().clamp_min(1e-30)) / _lib.FP8_MAX
+    return (w / s).to(_lib.FP8).contiguous(), s
+
+
 class CLIPEngine:
-    """CLIP ViT-H/14 on crops: fused crop+resize+normalise+im2col, 32 MFMA transformer blocks."""
+    """CLIP ViT-H/14 on crops: fused crop+resize+normalise+im2col, 32 MFMA transformer blocks.
+
+    fp8=True (BASELINE configs[4]): in_proj, c_fc and c_proj run as fp8 e4m3 GEMMs on the
+    block-scaled MFMA (bf_gemm_fp8, 2x the bf16 rate): weights per-tensor quantised once; ln_1 /
+    ln_2 write fp8 straight from the LayerNorm kernel and c_fc's GELU epilogue writes fp8 for
+    c_proj, with static per-tensor activation scales calibrated from the bf16 forward of the first
+    batch (or `calibrate()`); attention, out_proj, the stem and the head stay bf16 / f32."""
 
     KPAD = 640  # 3*14*14 = 588 -> 640 (GEMM K multiple of 64)
 
-    def __init__(self, visual, max_crops, device="cuda"):
+    def __init__(self, visual, max_crops, device="cuda", fp8=False):
         dev = torch.device(device)
         self.visual = visual.to(dev).eval()
         v = visual
@@ -285,10 +298,34 @@ class CLIPEngine:
         self.proj_t = _bf(v.proj.t())                       # [out, width] (nn.Linear layout)
         self.CLS = torch.empty((max_crops, W), **bf16)
         self.FEAT = torch.empty((max_crops, v.output_dim), **f32)
+        self.fp8 = bool(fp8)
+        self.act_scales = None          # per block (ln_1 out, ln_2 out, GELU out) amax / 448
+        if self.fp8:
+            for blk, rb in zip(self.blocks, v.transformer.resblocks):
+                blk["qkv8"] = _fp8_weight(rb.attn.in_proj_weight)
+                blk["fc1_8"] = _fp8_weight(rb.mlp.c_fc.weight)
+                blk["fc2_8"] = _fp8_weight(rb.mlp.c_proj.weight)
+            self.LN8 = torch.empty((M, W), dtype=_lib.FP8, device=dev)
+            self.H18 = torch.empty((M, 4 * W), dtype=_lib.FP8, device=dev)
+
+    @torch.no_grad()
+    def calibrate(self, frames_u8, boxes_i32, frame_idx_i32, margin=1.0):
+        """static fp8 activation scales from the bf16 forward of these crops: per block the amax
+        of the ln_1 output, the ln_2 output and the GELU output, / 448 (x margin)"""
+        stats = []
+        self._forward(frames_u8, boxes_i32, frame_idx_i32, fp8=False, stats=stats)
+        a = torch.stack(stats).float().view(len(self.blocks), 3).cpu().numpy()
+        self.act_scales = [tuple(float(max(x, 1e-30)) * margin / _lib.FP8_MAX for x in row) for row in a]
+        return self.act_scales
 
     @torch.no_grad()
     def __call__(self, frames_u8, boxes_i32, frame_idx_i32):
         """frames [F,H,W,3] u8, boxes [N,4] int xyxy, frame index [N] -> features [N, out] f32"""
+        if self.fp8 and self.act_scales is None and boxes_i32.shape[0] > 0:
+            self.calibrate(frames_u8, boxes_i32, frame_idx_i32)
+        return self._forward(frames_u8, boxes_i32, frame_idx_i32, fp8=self.fp8)
+
+    def _forward(self, frames_u8, boxes_i32, frame_idx_i32, fp8=False, stats=None):
         N = boxes_i32.shape[0]
         if N == 0:
             return torch.zeros((0, self.visual.output_dim), device=self.dev)
@@ -307,15 +344,35 @@ class CLIPEngine:
         M = N * S
         LN, QKV, ATT, H1 = self.LN[:M], self.QKV[:M], self.ATT[:M], self.H1[:M]
         scale = self.D ** -0.5
-        for blk in self.blocks:
-            _lib.layernorm(X, *blk["n1"][:2], blk["n1"][2], out=LN)
-            _lib.gemm(LN, *blk["qkv"], out=QKV)
+        if fp8:
+            LN8, H18 = self.LN8[:M], self.H18[:M]
+        for li, blk in enumerate(self.blocks):
+            if fp8:
+                s1, s2, s3 = self.act_scales[li]
+                (q8, wq), (f18, wf1), (f28, wf2) = blk["qkv8"], blk["fc1_8"], blk["fc2_8"]
+                _lib.layernorm_fp8(X, *blk["n1"][:2], blk["n1"][2], 1.0 / s1, out=LN8)
+                _lib.gemm_fp8(LN8, q8, s1 * wq, bias=blk["qkv"][1], out=QKV)
+            else:
+                _lib.layernorm(X, *blk["n1"][:2], blk["n1"][2], out=LN)
+                if stats is not None:
+                    stats.append(LN.abs().amax())
+                _lib.gemm(LN, *blk["qkv"], out=QKV)
             _lib.attention(QKV[:, :W], QKV[:, W:2 * W], QKV[:, 2 * W:], ATT, N, self.heads, S, S,
                            self.D, scale)
             _lib.gemm(ATT, *blk["proj"], resid=X, out=X)
-            _lib.layernorm(X, *blk["n2"][:2], blk["n2"][2], out=LN)
-            _lib.gemm(LN, *blk["fc1"], act="gelu", out=H1)
-            _lib.gemm(H1, *blk["fc2"], resid=X, out=X)
+            if fp8:
+                _lib.layernorm_fp8(X, *blk["n2"][:2], blk["n2"][2], 1.0 / s2, out=LN8)
+                _lib.gemm_fp8(LN8, f18, s2 * wf1, bias=blk["fc1"][1], act="gelu", out=H18,
+                              out_qscale=1.0 / s3)
+                _lib.gemm_fp8(H18, f28, s3 * wf2, bias=blk["fc2"][1], resid=X, out=X)
+            else:
+                _lib.layernorm(X, *blk["n2"][:2], blk["n2"][2], out=LN)
+                if stats is not None:
+                    stats.append(LN.abs().amax())
+                _lib.gemm(LN, *blk["fc1"], act="gelu", out=H1)
+                if stats is not None:
+                    stats.append(H1.abs().amax())
+                _lib.gemm(H1, *blk["fc2"], resid=X, out=X)
         # ln_post on the class rows (row stride S*W) -> bf16, then the output projection
         cls = _lib.layernorm(X.view(N, S * W)[:, :W], *self.ln_post, out=self.CLS[:N])
         return _lib.gemm(cls, self.proj_t, out=self.FEAT[:N])

@@ -79,13 +79,14 @@ class DetectStage:
 
     def __init__(self, cutr_model, clip_visual, cfg, batch, H=480, W=640, K3=None, text_features=None,
                  class_names=None, crops_per_frame=16, crop_source="filtered", backproject=True,
-                 clip_capacity=256, device="cuda", graph=False):
+                 clip_capacity=256, device="cuda", graph=False, clip_fp8=False):
         self.cfg = cfg
         self.dev = torch.device(device)
         self.B, self.H, self.W = batch, H, W
         self.pad = square_pad_size(H, W)
         self.cutr = CuTREngine(cutr_model, batch, H, W, pad=self.pad, device=device)
-        self.clip = CLIPEngine(clip_visual, clip_capacity, device=device) if clip_visual is not None else None
+        self.clip = (CLIPEngine(clip_visual, clip_capacity, device=device, fp8=clip_fp8)
+                     if clip_visual is not None else None)
         self.K3 = np.asarray(K3, np.float32)
         self.K_host = np.stack([self.K3] * batch)
         self.K_dev = torch.from_numpy(self.K_host).to(self.dev)

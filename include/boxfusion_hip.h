@@ -300,6 +300,18 @@ void bf_gemm_set_cu_budget(int n);
  * Results are identical in value. */
 void bf_gemm_set_balanced(int on);
 
+/* fp8 e4m3 (OCP) GEMM of the CLIP ViT-H fp8 path (BASELINE configs[4]; the same open_clip
+ * in_proj / c_fc / c_proj linears as bf_gemm_bf16, tools/utils.py:383-403):
+ *   C[r,n] = (resid ? resid[r,n] : 0) + act(scale * sum_k A[r,k] W[n,k] + bias[n])
+ *   A fp8[M,K] (row stride lda bytes), W fp8[N,K] (stride ldw), scale = activation scale x weight
+ *   scale (per-tensor), bias f32[N] or NULL, act 0 none / 1 GELU(erf);
+ *   out_kind 0: C f32 (+ resid f32, stride ldr, in place allowed; act 0 only), 1: C bf16,
+ *   2: C fp8 = saturate_448(value * out_qscale).  K % 128 == 0, lda/ldw % 16 == 0.
+ * Runs on the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 with unit block scales. */
+int bf_gemm_fp8(const void* A, int lda, const void* W, int ldw, float scale, const float* bias,
+                const float* resid, int ldr, void* C, int ldc, int out_kind, float out_qscale,
+                int M, int N, int K, int act, void* stream);
+
 /* softmax(Q K^T * scale) V per (batch, head); X(b,h,s,d) at X + b*x_bs + s*x_rs + h*D + d,
  * bf16 in/out, head_dim in {32, 64, 80, 128}.  Replaces vit.py Attention.forward (:170-203,
  * joint RGB+depth window attention = plain attention over the concatenated 512 tokens) and the
@@ -315,9 +327,12 @@ int bf_attention_bf16_omap(const void* q, const void* k, const void* v, void* o,
                            int heads, int sq, int sk, int head_dim, int q_rs, int k_rs, int v_rs,
                            int o_rs, long long q_bs, long long k_bs, long long v_bs, long long o_bs,
                            float scale, const int32_t* o_map, void* stream);
-/* Attention kernel variant (test/benchmark hook): 1 (default) / 2 = k_attn_s (64-key tiles
- * through a double-buffered LDS ring), 3 = k_attn_r (resident K/V filled by LDS-DMA when all
- * queries fit one workgroup and sk <= 320, else k_attn_s), 0 = k_attn (previous kernel). */
+/* Attention kernel variant (test/benchmark hook; env BF_ATTN_VARIANT): 6 (default) = k_attn2
+ * (deferred-max softmax, row sums from a ones row of V on the MFMA, 9-wave workgroups for short
+ * heads), 7 / 8 = k_attn2 with 5 / 3 waves per workgroup, 1 / 2 = k_attn_s (64-key tiles through
+ * a double-buffered LDS ring, with / without the XCD block order), 3 = k_attn_r (resident K/V
+ * filled by LDS-DMA when all queries fit one workgroup and sk <= 320, else k_attn_s),
+ * 4 / 5 = k_attn_s with 5 / 3 waves, 0 = k_attn (first kernel). */
 void bf_attention_set_variant(int v);
 
 /* CuTR decoder cross-attention bias (GlobalCrossAttention.rpe + the logits' bias / clip /
@@ -342,6 +357,10 @@ int bf_layernorm(const float* x, int ldx, const float* gamma, const float* beta,
 int bf_layernorm_out(const float* x, int ldx, const float* gamma, const float* beta, float eps,
                      void* out, int ldo, int out_f32, const int32_t* row_map, int M, int C,
                      void* stream);
+/* the same with an fp8 e4m3 output, saturate_448(y * qscale) (ldo in bytes): ln_1 / ln_2 of the
+ * CLIP fp8 path feeding bf_gemm_fp8 */
+int bf_layernorm_fp8(const float* x, int ldx, const float* gamma, const float* beta, float eps,
+                     void* out, int ldo, float qscale, int M, int C, void* stream);
 
 /* Preprocessor.normalize + square zero pad + PatchEmbed im2col (preprocessor.py:131-144,
  * imagelist.py:55-115, vit.py:102-128): img u8[B,H,W,3] -> bf16[B*(pad/p)^2, 3*p*p].

@@ -33,7 +33,8 @@ grep '"metric"' gpurun_out/prof_$R/rk.log > $P/${R}_roofline_bench.json
 fi
 
 if [ "$ONLY" = all ] || [ "$ONLY" = pmc ]; then
-PMC_CMD="python3 -u bench.py --steps 2 --warmup 1 --eager --inflight 1 --no-cpu-baseline --roofline-steps 1"
+# PMC_EXTRA: extra bench flags for a workload's own PMC file (e.g. R=r02_fp8 PMC_EXTRA="--clip-fp8 --vocab 200")
+PMC_CMD="python3 -u bench.py --steps 2 --warmup 1 --eager --inflight 1 --no-cpu-baseline --roofline-steps 1 ${PMC_EXTRA:-}"
 # SQ_PASS: an extra pass of SQ counters (names as `rocprofv3 -L` lists them on the box)
 for pass in FETCH_SIZE WRITE_SIZE ${SQ_PASS:+"$SQ_PASS"}; do
   tag=$(echo $pass | cut -d' ' -f1)
@@ -43,7 +44,7 @@ for pass in FETCH_SIZE WRITE_SIZE ${SQ_PASS:+"$SQ_PASS"}; do
       $PMC_CMD > gpurun_out/prof_$R/pmc_$tag.log 2>&1 || { tail -20 gpurun_out/prof_$R/pmc_$tag.log; exit 1; }
 done
 python3 - "$R" <<'PY'
-import csv, glob, json, sys, collections
+import csv, glob, json, re, sys, collections
 R = sys.argv[1]
 per = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(float)))
 for d in sorted(glob.glob(f"/tmp/pmc_{R}_*")):
@@ -63,8 +64,10 @@ for name, ctrs in per.items():
         k["bytes_per_launch"] = (2 * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024
     kernels[name] = k
 # the bench line's roofline kernels: launch-weighted averages over the matching kernel names
-groups = {"k_gemm256p": ["k_gemm256p"], "k_gemm256p<false, 0>": ["k_gemm256p<false, 0>"],
-          "k_gemm256p<true, 1>": ["k_gemm256p<true, 1>"], "k_attn": ["k_attn"],
+# (regular expressions over the demangled names; k_gemm256p<OUT_BF16, ACT, F8>)
+groups = {"k_gemm256p": [r"k_gemm256p<\w+, \d, 0>"], "k_gemm256p<false, 0>": [r"k_gemm256p<false, 0, 0>"],
+          "k_gemm256p<true, 1>": [r"k_gemm256p<true, 1, 0>"], "k_gemm256p_fp8": [r"k_gemm256p<\w+, \d, [13]>"],
+          "k_attn": ["k_attn"],
           "k_attn_clip": ["k_attn_clip", "k_attn_s<80", "k_attn_r<80", "k_attn2<80"],
           "k_attn_cutr": ["k_attn_s<64", "k_attn_w", "k_attn_g", "k_attn2<64"]}
 out = {"round": int(R[1:]), "method": (
@@ -75,7 +78,7 @@ out = {"round": int(R[1:]), "method": (
     "64 B, MI355X_MICROARCH.md HBM section).  Memory-side L2 traffic, Infinity-Cache hits included."),
     "kernels": kernels}
 for key, pats in groups.items():
-    sel = [(n, k) for n, k in kernels.items() if any(p in n for p in pats) and "bytes_per_launch" in k]
+    sel = [(n, k) for n, k in kernels.items() if any(re.search(p, n) for p in pats) and "bytes_per_launch" in k]
     if not sel:
         continue
     w = sum(k["FETCH_SIZE_dispatches"] for _, k in sel)
