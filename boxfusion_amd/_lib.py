@@ -744,6 +744,30 @@ def cpb_mlp(ref, pos, axis, w1, b1, w2):
     return out
 
 
+def xattn(q, k, v, rx, ry, hh, ww, q0, heads, scale, out=None):
+    """fused global cross-attention (bf_xattn_f32): q f32 [B,Nq,C], k / v f32 [B,hh*ww,C] (any row
+    stride, unit column stride), rx [B,Nq-q0,ww,heads], ry [B,Nq-q0,hh,heads] -> out f32 [B,Nq,C]"""
+    for x, n in ((q, "q"), (k, "k"), (v, "v")):
+        _need(x, torch.float32, n)
+        if x.dim() != 3 or x.stride(2) != 1 or x.stride(0) != x.shape[1] * x.stride(1):
+            raise HipError(f"xattn: {n} must be [B, rows, C] with unit column stride and packed batches")
+    B, Nq, C = q.shape
+    if C != heads * 32 or k.shape != (B, hh * ww, C) or v.shape != k.shape:
+        raise HipError("xattn: head dim 32, k / v [B, hh*ww, C]")
+    if out is None:
+        out = torch.empty((B, Nq, C), dtype=torch.float32, device=q.device)
+    if q0 < Nq:
+        rx = _need(rx.contiguous(), torch.float32, "rx")
+        ry = _need(ry.contiguous(), torch.float32, "ry")
+    _check(lib().bf_xattn_f32(c_void_p(q.data_ptr()), c_int(q.stride(1)), c_void_p(k.data_ptr()),
+                              c_int(k.stride(1)), c_void_p(v.data_ptr()), c_int(v.stride(1)),
+                              _ptr(rx) if q0 < Nq else None, _ptr(ry) if q0 < Nq else None,
+                              c_void_p(out.data_ptr()), c_int(out.stride(1)), c_int(B), c_int(heads),
+                              c_int(Nq), c_int(q0), c_int(hh), c_int(ww), c_float(scale), _stream()),
+           "bf_xattn_f32")
+    return out
+
+
 def rpe_softmax(attn, rx, ry, hh, ww, q0):
     """attn f32 [B,H,Nq,hh*ww] in place: + bias on rows q >= q0, clip, softmax"""
     _need(attn, torch.float32, "attn")

@@ -348,6 +348,16 @@ int bf_cpb_mlp(const float* ref, int B, int nq, const float* pos, int n, int axi
                float* out, void* stream);
 int bf_rpe_softmax(float* attn, int B, int H, int Nq, int q0, const float* rx, const float* ry,
                    int hh, int ww, void* stream);
+/* The whole global cross-attention after the projections (GlobalCrossAttention.forward,
+ * cubify_transformer.py:170-200 of the reference), f32: out[b,q,h*32+d] = sum_j softmax_j(clip(
+ * (scale q[b,q,h]) . k[b,j,h] + bias))[j] v[b,j,h,d] with bias = rx[b,q-q0,x,h] + ry[b,q-q0,y,h]
+ * (j = y*ww + x) for q >= q0, 0 otherwise.  q [B,Nq] rows of stride ldq, k / v [B,hh*ww] rows of
+ * stride ldk / ldv (e.g. one layer's columns of the all-layer memory projections), head dim 32,
+ * hh, ww <= 128.  Replaces the two batched matmuls, bf_rpe_softmax's logits round trip and the
+ * head permutes. */
+int bf_xattn_f32(const float* q, int ldq, const float* k, int ldk, const float* v, int ldv,
+                 const float* rx, const float* ry, float* out, int ldo, int B, int H, int Nq, int q0,
+                 int hh, int ww, float scale, void* stream);
 
 /* LayerNorm f32[M,C] -> bf16, written to row row_map[r] (NULL = r; < 0 skips). */
 int bf_layernorm(const float* x, int ldx, const float* gamma, const float* beta, float eps,

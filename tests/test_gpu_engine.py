@@ -137,6 +137,35 @@ def test_decoder_cross_attention_fused_vs_torch(dev):
     torch.testing.assert_close(rx, rx_t, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("B,Nq,q0,h,w", [(2, 302, 2, 40, 40), (3, 37, 2, 30, 30), (1, 64, 0, 32, 32),
+                                        (2, 33, 33, 7, 9), (1, 300, 2, 24, 32)])
+def test_xattn_kernel_vs_torch(dev, B, Nq, q0, h, w):
+    """bf_xattn_f32 against the torch formula: (scale q) k^T + rx + ry on rows >= q0, clip,
+    softmax, @ v; k / v as one layer's column slice of the all-layer memory projections (row
+    stride 6C), key counts off the 32-key block (900, 63), partial query blocks, no box queries"""
+    from boxfusion_amd import _lib
+    g = torch.Generator(device="cuda").manual_seed(B * Nq + h)
+    C, H = 256, 8
+    N = h * w
+    q = torch.randn(B, Nq, C, device=dev, generator=g)
+    kall = torch.randn(B, N, 6 * C, device=dev, generator=g)
+    vall = torch.randn(B, N, 6 * C, device=dev, generator=g)
+    k, v = kall[..., 2 * C:3 * C], vall[..., 2 * C:3 * C]
+    rx = torch.randn(B, Nq - q0, w, H, device=dev, generator=g)
+    ry = torch.randn(B, Nq - q0, h, H, device=dev, generator=g)
+    scale = 32 ** -0.5
+    got = _lib.xattn(q, k, v, rx, ry, h, w, q0, H, scale)
+    qh = (q * scale).view(B, Nq, H, 32).permute(0, 2, 1, 3)
+    kh = k.reshape(B, N, H, 32).permute(0, 2, 1, 3)
+    vh = v.reshape(B, N, H, 32).permute(0, 2, 1, 3)
+    a = qh @ kh.transpose(-2, -1)
+    bias = (rx[:, :, None] + ry[:, :, :, None]).flatten(2, 3).permute(0, 3, 1, 2)
+    a[:, :, q0:] += bias
+    a = a.clip(torch.finfo(a.dtype).min, torch.finfo(a.dtype).max).softmax(-1)
+    want = (a @ vh).transpose(1, 2).reshape(B, Nq, C)
+    torch.testing.assert_close(got, want, rtol=1e-4, atol=2e-5)
+
+
 @pytest.mark.parametrize("H,W,ratio,depth_model", [(480, 640, 2, True), (480, 640, 4, True),
                                                   (512, 384, 2, True), (512, 384, 1, True),
                                                   (480, 640, 1, False)])
