@@ -930,8 +930,11 @@ BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, v
         // barriers; K / V re-read from L2); longer ones: 4-wave workgroups of 128 queries
         const bool short_s = nw_one > 4 && nw_one <= 9;
         const int var = g_attn_variant;      // (`v` is the V operand)
+        // <= 64 queries per (batch, head) (CLIP's last block: the class token only): 2-wave
+        // workgroups, so no idle waves compute empty query blocks
 #define LAUNCH_2D(DD)                                                                             \
-    if (!short_s) { LAUNCH_2(DD, 4); }                                                             \
+    if (nw_one <= 2) { LAUNCH_2(DD, 2); }                                                          \
+    else if (!short_s) { LAUNCH_2(DD, 4); }                                                        \
     else if (var == 7) { LAUNCH_2(DD, 5); }                                                        \
     else if (var == 8) { LAUNCH_2(DD, 3); }                                                        \
     else { LAUNCH_2(DD, 9); }

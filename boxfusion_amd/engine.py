@@ -257,7 +257,7 @@ class CLIPEngine:
 
     KPAD = 640  # 3*14*14 = 588 -> 640 (GEMM K multiple of 64)
 
-    def __init__(self, visual, max_crops, device="cuda", fp8=False):
+    def __init__(self, visual, max_crops, device="cuda", fp8=False, cls_only_last=True):
         dev = torch.device(device)
         self.visual = visual.to(dev).eval()
         v = visual
@@ -298,6 +298,14 @@ class CLIPEngine:
         self.proj_t = _bf(v.proj.t())                       # [out, width] (nn.Linear layout)
         self.CLS = torch.empty((max_crops, W), **bf16)
         self.FEAT = torch.empty((max_crops, v.output_dim), **f32)
+        # the tower's output reads only the class token of the last block (open_clip's token
+        # pooling: proj(ln_post(x[:, 0]))), so that block's attention runs for the class query
+        # only and its proj / ln_2 / fc1 / fc2 on the N class rows (K / V still from every token)
+        self.cls_only_last = bool(cls_only_last)
+        self.cls_rows = (torch.arange(max_crops, dtype=torch.int32, device=dev) * self.S).contiguous()
+        self.ATTc = torch.empty((max_crops, W), **bf16)
+        self.LNc = torch.empty((max_crops, W), **bf16)
+        self.H1c = torch.empty((max_crops, 4 * W), **bf16)
         self.fp8 = bool(fp8)
         self.act_scales = None          # per block (ln_1 out, ln_2 out, GELU out) amax / 448
         if self.fp8:
@@ -346,7 +354,11 @@ class CLIPEngine:
         scale = self.D ** -0.5
         if fp8:
             LN8, H18 = self.LN8[:M], self.H18[:M]
+        nblk = len(self.blocks)
         for li, blk in enumerate(self.blocks):
+            if li == nblk - 1 and self.cls_only_last and stats is None:
+                self._last_block_cls(blk, X, LN, QKV, N, fp8, li)
+                break
             if fp8:
                 s1, s2, s3 = self.act_scales[li]
                 (q8, wq), (f18, wf1), (f28, wf2) = blk["qkv8"], blk["fc1_8"], blk["fc2_8"]
@@ -373,6 +385,33 @@ class CLIPEngine:
                 if stats is not None:
                     stats.append(H1.abs().amax())
                 _lib.gemm(H1, *blk["fc2"], resid=X, out=X)
+        return self._head(X, N)
+
+    def _last_block_cls(self, blk, X, LN, QKV, N, fp8, li):
+        """the last residual block for the class tokens (rows n*S of X) only; K / V of every token"""
+        W, S = self.width, self.S
+        if fp8:
+            s1 = self.act_scales[li][0]
+            q8, wq = blk["qkv8"]
+            LN8 = self.LN8[:N * S]
+            _lib.layernorm_fp8(X, *blk["n1"][:2], blk["n1"][2], 1.0 / s1, out=LN8)
+            _lib.gemm_fp8(LN8, q8, s1 * wq, bias=blk["qkv"][1], out=QKV)
+        else:
+            _lib.layernorm(X, *blk["n1"][:2], blk["n1"][2], out=LN)
+            _lib.gemm(LN, *blk["qkv"], out=QKV)
+        rs = QKV.stride(0)
+        ATTc, cls = self.ATTc[:N], self.cls_rows[:N]
+        _lib.attention(QKV[:, :W], QKV[:, W:2 * W], QKV[:, 2 * W:], ATTc, N, self.heads, 1, S, self.D,
+                       self.D ** -0.5, q_bs=S * rs, k_bs=S * rs, v_bs=S * rs, o_bs=ATTc.stride(0))
+        _lib.gemm(ATTc, *blk["proj"], resid=X, out=X, row_map=cls)
+        Xc = X.view(-1, S * W)[:N, :W]                      # class rows, row stride S*W
+        LNc, H1c = self.LNc[:N], self.H1c[:N]
+        _lib.layernorm(Xc, *blk["n2"][:2], blk["n2"][2], out=LNc)
+        _lib.gemm(LNc, *blk["fc1"], act="gelu", out=H1c)
+        _lib.gemm(H1c, *blk["fc2"], resid=X, out=X, row_map=cls)
+
+    def _head(self, X, N):
+        W, S = self.width, self.S
         # ln_post on the class rows (row stride S*W) -> bf16, then the output projection
         cls = _lib.layernorm(X.view(N, S * W)[:, :W], *self.ln_post, out=self.CLS[:N])
         return _lib.gemm(cls, self.proj_t, out=self.FEAT[:N])

@@ -107,6 +107,25 @@ def test_clip_engine_vs_fp32(dev):
     assert err < 3e-2
 
 
+def test_clip_last_block_class_rows_only(dev):
+    """the last block on the class tokens only (attention for the class query, proj / ln_2 / fc1 /
+    fc2 on N rows) gives the features of the full last block, bf16 MFMA rounding apart"""
+    from boxfusion_amd.clip import VisionTransformer
+    from boxfusion_amd.engine import CLIPEngine
+    from boxfusion_amd.weights import init_seeded
+    vis = init_seeded(VisionTransformer(224, 14, 1280, 3, 16, 1024).eval(), seed=6).to(dev)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    frames = torch.randint(0, 256, (2, 480, 640, 3), device=dev, dtype=torch.uint8, generator=g)
+    boxes = torch.tensor([[10, 20, 200, 150], [0, 0, 640, 480], [300, 100, 400, 310], [5, 5, 90, 470]],
+                         device=dev, dtype=torch.int32)
+    idx = torch.tensor([0, 1, 1, 0], device=dev, dtype=torch.int32)
+    full = CLIPEngine(vis, 8, cls_only_last=False)(frames, boxes, idx).clone()
+    cls = CLIPEngine(vis, 8)(frames, boxes, idx)
+    err = rel(cls, full)
+    print("class-rows-only last block vs full", err)
+    assert err < 5e-3
+
+
 def test_decoder_cross_attention_fused_vs_torch(dev):
     """GlobalCrossAttention with bf_cpb_mlp + bf_rpe_softmax == the torch ops (bias MLP, broadcast
     bias, index_put, clip, softmax), f32, on decoder-sized inputs (302 queries, 40x40 memory);

@@ -155,6 +155,25 @@ def test_attention(L, B, H, S, D, variant):
     assert rel_err(o, ref) < 1e-2
 
 
+@pytest.mark.parametrize("sq,D", [(1, 80), (1, 64), (40, 80), (64, 32)])
+def test_attention_few_queries(L, sq, D):
+    """<= 64 queries against 257 keys (CLIP's last block: the class token of every crop), the
+    queries a strided subset of the token rows (q_bs = S rows), compact output rows"""
+    B, H, S = 24, 16, 257
+    g = torch.Generator(device="cuda").manual_seed(sq * D)
+    qkv = torch.randn(B * S, 3 * H * D, device="cuda", generator=g).bfloat16()
+    rs = qkv.stride(0)
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    o = torch.empty(B * sq, H * D, device="cuda", dtype=torch.bfloat16)
+    L.attention(q, k, v, o, B, H, sq, S, D, D ** -0.5, q_bs=S * rs, k_bs=S * rs, v_bs=S * rs,
+                o_bs=sq * o.stride(0))
+    qh = q.view(B, S, H, D)[:, :sq].float().transpose(1, 2)
+    kh = k.reshape(B, S, H, D).float().transpose(1, 2)
+    vh = v.reshape(B, S, H, D).float().transpose(1, 2)
+    ref = torch.softmax(qh @ kh.transpose(-2, -1) * D ** -0.5, -1) @ vh
+    assert rel_err(o, ref.transpose(1, 2).reshape(B * sq, H * D)) < 1e-2
+
+
 @pytest.mark.parametrize("D", [64, 80])
 @pytest.mark.parametrize("spike", [4.0, 1.6, 1.25])
 def test_attention_forced_rescale(L, D, spike):
