@@ -472,6 +472,26 @@ def attention(q, k, v, o, batch, heads, sq, sk, head_dim, scale, q_bs=None, k_bs
     return o
 
 
+def attention_fp8out(q, k, v, o, batch, heads, sq, sk, head_dim, scale, out_qscale, q_bs=None,
+                     k_bs=None, v_bs=None, o_bs=None):
+    """attention() with an fp8 e4m3 output o = saturate(softmax(q k^T) v * out_qscale)"""
+    for x, n in ((q, "q"), (k, "k"), (v, "v")):
+        _need(x, torch.bfloat16, n)
+    _need(o, FP8, "o")
+    q_bs = sq * q.stride(0) if q_bs is None else q_bs
+    k_bs = sk * k.stride(0) if k_bs is None else k_bs
+    v_bs = sk * v.stride(0) if v_bs is None else v_bs
+    o_bs = sq * o.stride(0) if o_bs is None else o_bs
+    LL = ctypes.c_longlong
+    _check(lib().bf_attention_fp8out(c_void_p(q.data_ptr()), c_void_p(k.data_ptr()), c_void_p(v.data_ptr()),
+                                     c_void_p(o.data_ptr()), c_int(batch), c_int(heads), c_int(sq),
+                                     c_int(sk), c_int(head_dim), c_int(q.stride(0)), c_int(k.stride(0)),
+                                     c_int(v.stride(0)), c_int(o.stride(0)), LL(q_bs), LL(k_bs), LL(v_bs),
+                                     LL(o_bs), c_float(scale), c_float(out_qscale), _stream()),
+           "bf_attention_fp8out")
+    return o
+
+
 def layernorm(x, weight, bias, eps, out=None, row_map=None, out_dtype=torch.bfloat16):
     """x f32 [M, C] (any row stride) -> LayerNorm rows in bf16 (or f32: out / out_dtype), row r
     written to row_map[r] of out (< 0 skipped)"""
@@ -635,6 +655,7 @@ _TIMER = None
 _gemm_untimed = gemm
 _gemm_fp8_untimed = gemm_fp8
 _attention_untimed = attention
+_attention_fp8out_untimed = attention_fp8out
 
 
 def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype=torch.bfloat16,
@@ -679,6 +700,18 @@ def attention(q, k, v, o, batch, heads, sq, sk, head_dim, scale, q_bs=None, k_bs
     return t.record(tags, 4.0 * bh * sq * sk * head_dim, 2.0 * bh * head_dim * (2 * sq + 2 * sk),
                     lambda: _attention_untimed(q, k, v, o, batch, heads, sq, sk, head_dim, scale,
                                                q_bs, k_bs, v_bs, o_bs, o_map))
+
+
+def attention_fp8out(q, k, v, o, batch, heads, sq, sk, head_dim, scale, out_qscale, q_bs=None,
+                     k_bs=None, v_bs=None, o_bs=None):
+    t = _TIMER
+    fn = lambda: _attention_fp8out_untimed(q, k, v, o, batch, heads, sq, sk, head_dim, scale, out_qscale,
+                                           q_bs, k_bs, v_bs, o_bs)
+    if t is None:
+        return fn()
+    tags = dict(kind="attn", D=head_dim, sq=sq, sk=sk, batch=batch, heads=heads, fp8out=True)
+    bh = float(batch * heads)
+    return t.record(tags, 4.0 * bh * sq * sk * head_dim, bh * head_dim * (2 * sq + 4 * sk + sq), fn)
 
 
 # ------------------------------------------------------------------------------------------

@@ -512,13 +512,14 @@ __device__ __forceinline__ void attn2_softmax(f32x16 (&s)[2], bool sub1, bool ma
     if (!ONES) l_run += ls;
 }
 
-template <int D, int NW>
+// F8O: the output is fp8 e4m3 (OCP), saturate_448(o * oqs) -- the fp8 CLIP path's out_proj input
+template <int D, int NW, bool F8O = false>
 __global__ void __launch_bounds__(NW * 64) k_attn2(const u16* __restrict__ Q, const u16* __restrict__ K,
                                                       const u16* __restrict__ V, u16* __restrict__ O,
                                                       int sq, int sk, int q_rs, int k_rs, int v_rs,
                                                       int o_rs, long long q_bs, long long k_bs,
                                                       long long v_bs, long long o_bs, float scale_log2,
-                                                      const int32_t* __restrict__ o_map) {
+                                                      const int32_t* __restrict__ o_map, float oqs = 1.f) {
     constexpr int KS = D / 16;
     constexpr int DB = (D + 31) / 32;
     constexpr bool ONES = (D % 32) != 0;                 // a padding row of V^T carries the row sum
@@ -661,18 +662,36 @@ __global__ void __launch_bounds__(NW * 64) k_attn2(const u16* __restrict__ Q, co
     const long long o_off = attn_out_offset(o_map, b, q, sq, o_bs, o_rs);
     if (q < sq && o_off >= 0) {
         const float inv = 1.0f / l;
-        u16* orow = O + o_off + h * D;
+        if constexpr (F8O) {
+            unsigned char* orow = reinterpret_cast<unsigned char*>(O) + o_off + h * D;
+            const float sc = inv * oqs;
 #pragma unroll
-        for (int db = 0; db < DB; ++db)
+            for (int db = 0; db < DB; ++db)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int d0 = db * 32 + 8 * g + 4 * fh;
-                if (d0 >= D) continue;
-                V64 w;
-                w.x = (uint32_t)at_f2bf(o[db][4 * g + 0] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 1] * inv) << 16);
-                w.y = (uint32_t)at_f2bf(o[db][4 * g + 2] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 3] * inv) << 16);
-                *reinterpret_cast<V64*>(orow + d0) = w;
-            }
+                for (int g = 0; g < 4; ++g) {
+                    const int d0 = db * 32 + 8 * g + 4 * fh;
+                    if (d0 >= D) continue;
+                    float a[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) a[i] = fminf(fmaxf(o[db][4 * g + i] * sc, -448.f), 448.f);
+                    int pk = __builtin_amdgcn_cvt_pk_fp8_f32(a[0], a[1], 0, false);
+                    pk = __builtin_amdgcn_cvt_pk_fp8_f32(a[2], a[3], pk, true);
+                    *reinterpret_cast<int*>(orow + d0) = pk;
+                }
+        } else {
+            u16* orow = O + o_off + h * D;
+#pragma unroll
+            for (int db = 0; db < DB; ++db)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int d0 = db * 32 + 8 * g + 4 * fh;
+                    if (d0 >= D) continue;
+                    V64 w;
+                    w.x = (uint32_t)at_f2bf(o[db][4 * g + 0] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 1] * inv) << 16);
+                    w.y = (uint32_t)at_f2bf(o[db][4 * g + 2] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 3] * inv) << 16);
+                    *reinterpret_cast<V64*>(orow + d0) = w;
+                }
+        }
     }
 }
 
@@ -1002,4 +1021,32 @@ BF_API int bf_attention_bf16(const void* q, const void* k, const void* v, void* 
                              long long o_bs, float scale, void* stream) {
     return bf_attention_bf16_omap(q, k, v, o, batch, heads, sq, sk, head_dim, q_rs, k_rs, v_rs, o_rs,
                                   q_bs, k_bs, v_bs, o_bs, scale, nullptr, stream);
+}
+
+// the same attention (k_attn2, the default schedule) with an fp8 e4m3 output
+// saturate_448(o * out_qscale); o_rs / o_bs in elements = bytes, o_rs % 4 == 0
+BF_API int bf_attention_fp8out(const void* q, const void* k, const void* v, void* o, int batch,
+                               int heads, int sq, int sk, int head_dim, int q_rs, int k_rs, int v_rs,
+                               int o_rs, long long q_bs, long long k_bs, long long v_bs, long long o_bs,
+                               float scale, float out_qscale, void* stream) {
+    if (!q || !k || !v || !o || batch <= 0 || heads <= 0 || sq <= 0 || sk <= 0 || !(out_qscale > 0.f))
+        return BF_ERR_ARG;
+    if ((q_rs | k_rs | v_rs) % 8 != 0 || o_rs % 4 != 0 || o_bs % 4 != 0) return BF_ERR_UNSUPPORTED;
+    const float sl2 = scale * 1.4426950408889634f;
+    const int nw_one = (sq + 31) / 32;
+#define LAUNCH_8(DD, NWV)                                                                         \
+    hipLaunchKernelGGL((k_attn2<DD, NWV, true>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch), \
+                       dim3(NWV * 64), 0, bf_stream(stream), (const u16*)q, (const u16*)k,          \
+                       (const u16*)v, (u16*)o, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs,    \
+                       o_bs, sl2, (const int32_t*)nullptr, out_qscale)
+#define LAUNCH_8D(DD)                                                                             \
+    if (nw_one > 4 && nw_one <= 9) { LAUNCH_8(DD, 9); } else { LAUNCH_8(DD, 4); }
+    switch (head_dim) {
+        case 64: LAUNCH_8D(64); break;
+        case 80: LAUNCH_8D(80); break;
+        default: return BF_ERR_UNSUPPORTED;
+    }
+#undef LAUNCH_8D
+#undef LAUNCH_8
+    return bf_check_launch();
 }

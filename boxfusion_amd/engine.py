@@ -307,22 +307,25 @@ class CLIPEngine:
         self.LNc = torch.empty((max_crops, W), **bf16)
         self.H1c = torch.empty((max_crops, 4 * W), **bf16)
         self.fp8 = bool(fp8)
-        self.act_scales = None          # per block (ln_1 out, ln_2 out, GELU out) amax / 448
+        self.act_scales = None          # per block (ln_1, attention, ln_2, GELU outputs) amax / 448
         if self.fp8:
             for blk, rb in zip(self.blocks, v.transformer.resblocks):
                 blk["qkv8"] = _fp8_weight(rb.attn.in_proj_weight)
+                blk["proj8"] = _fp8_weight(rb.attn.out_proj.weight)
                 blk["fc1_8"] = _fp8_weight(rb.mlp.c_fc.weight)
                 blk["fc2_8"] = _fp8_weight(rb.mlp.c_proj.weight)
             self.LN8 = torch.empty((M, W), dtype=_lib.FP8, device=dev)
+            self.ATT8 = torch.empty((M, W), dtype=_lib.FP8, device=dev)
             self.H18 = torch.empty((M, 4 * W), dtype=_lib.FP8, device=dev)
 
     @torch.no_grad()
     def calibrate(self, frames_u8, boxes_i32, frame_idx_i32, margin=1.0):
         """static fp8 activation scales from the bf16 forward of these crops: per block the amax
-        of the ln_1 output, the ln_2 output and the GELU output, / 448 (x margin)"""
+        of the ln_1 output, the attention output, the ln_2 output and the GELU output, / 448
+        (x margin)"""
         stats = []
         self._forward(frames_u8, boxes_i32, frame_idx_i32, fp8=False, stats=stats)
-        a = torch.stack(stats).float().view(len(self.blocks), 3).cpu().numpy()
+        a = torch.stack(stats).float().view(len(self.blocks), 4).cpu().numpy()
         self.act_scales = [tuple(float(max(x, 1e-30)) * margin / _lib.FP8_MAX for x in row) for row in a]
         return self.act_scales
 
@@ -360,8 +363,9 @@ class CLIPEngine:
                 self._last_block_cls(blk, X, LN, QKV, N, fp8, li)
                 break
             if fp8:
-                s1, s2, s3 = self.act_scales[li]
+                s1, sa, s2, s3 = self.act_scales[li]
                 (q8, wq), (f18, wf1), (f28, wf2) = blk["qkv8"], blk["fc1_8"], blk["fc2_8"]
+                p8, wp = blk["proj8"]
                 _lib.layernorm_fp8(X, *blk["n1"][:2], blk["n1"][2], 1.0 / s1, out=LN8)
                 _lib.gemm_fp8(LN8, q8, s1 * wq, bias=blk["qkv"][1], out=QKV)
             else:
@@ -369,9 +373,18 @@ class CLIPEngine:
                 if stats is not None:
                     stats.append(LN.abs().amax())
                 _lib.gemm(LN, *blk["qkv"], out=QKV)
-            _lib.attention(QKV[:, :W], QKV[:, W:2 * W], QKV[:, 2 * W:], ATT, N, self.heads, S, S,
-                           self.D, scale)
-            _lib.gemm(ATT, *blk["proj"], resid=X, out=X)
+            if fp8:
+                # attention writes fp8 for the fp8 out_proj
+                ATT8 = self.ATT8[:M]
+                _lib.attention_fp8out(QKV[:, :W], QKV[:, W:2 * W], QKV[:, 2 * W:], ATT8, N, self.heads, S,
+                                      S, self.D, scale, 1.0 / sa)
+                _lib.gemm_fp8(ATT8, p8, sa * wp, bias=blk["proj"][1], resid=X, out=X)
+            else:
+                _lib.attention(QKV[:, :W], QKV[:, W:2 * W], QKV[:, 2 * W:], ATT, N, self.heads, S, S,
+                               self.D, scale)
+                if stats is not None:
+                    stats.append(ATT.abs().amax())
+                _lib.gemm(ATT, *blk["proj"], resid=X, out=X)
             if fp8:
                 _lib.layernorm_fp8(X, *blk["n2"][:2], blk["n2"][2], 1.0 / s2, out=LN8)
                 _lib.gemm_fp8(LN8, f18, s2 * wf1, bias=blk["fc1"][1], act="gelu", out=H18,

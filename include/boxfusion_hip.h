@@ -327,6 +327,12 @@ int bf_attention_bf16_omap(const void* q, const void* k, const void* v, void* o,
                            int heads, int sq, int sk, int head_dim, int q_rs, int k_rs, int v_rs,
                            int o_rs, long long q_bs, long long k_bs, long long v_bs, long long o_bs,
                            float scale, const int32_t* o_map, void* stream);
+/* the same (default kernel) with an fp8 e4m3 output saturate_448(o * out_qscale): the CLIP fp8
+ * path's out_proj input (o_rs, o_bs in bytes; head_dim 64 / 80) */
+int bf_attention_fp8out(const void* q, const void* k, const void* v, void* o, int batch, int heads,
+                        int sq, int sk, int head_dim, int q_rs, int k_rs, int v_rs, int o_rs,
+                        long long q_bs, long long k_bs, long long v_bs, long long o_bs, float scale,
+                        float out_qscale, void* stream);
 /* Attention kernel variant (test/benchmark hook; env BF_ATTN_VARIANT): 6 (default) = k_attn2
  * (deferred-max softmax, row sums from a ones row of V on the MFMA, 9-wave workgroups for short
  * heads), 7 / 8 = k_attn2 with 5 / 3 waves per workgroup, 1 / 2 = k_attn_s (64-key tiles through

@@ -150,3 +150,20 @@ def test_clip_engine_fp8_vs_bf16(L, layers):
     ib, _, mb = match_features(ref, text.clone(), 25.0)
     assert i8.shape == (n,) and int(i8.max()) <= 200
     assert float((m8 - mb).abs().max()) < 2.0     # similarity x100 on unit vectors
+
+
+@pytest.mark.parametrize("B,H,S,D", [(6, 16, 257, 80), (3, 12, 512, 64)])
+def test_attention_fp8_output(L, B, H, S, D):
+    """bf_attention_fp8out == the bf16-output kernel to one e4m3 rounding of its f32 result"""
+    g = torch.Generator(device="cuda").manual_seed(S + D)
+    qkv = torch.randn(B * S, 3 * H * D, device="cuda", generator=g).bfloat16()
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    o16 = torch.empty(B * S, H * D, device="cuda", dtype=torch.bfloat16)
+    L.attention(q, k, v, o16, B, H, S, S, D, D ** -0.5)
+    qs = 448.0 / 3.0
+    o8 = torch.empty(B * S, H * D, device="cuda", dtype=L.FP8)
+    L.attention_fp8out(q, k, v, o8, B, H, S, S, D, D ** -0.5, qs)
+    dec = o8.float() / qs
+    ref = o16.float()
+    tol = ref.abs() * (2.0 ** -3 + 2.0 ** -7) + 2.0 ** -9 / qs
+    assert bool(((dec - ref).abs() <= tol).all())
