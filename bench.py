@@ -96,6 +96,9 @@ def parse(argv=None):
                         "scales calibrated on the first batch)")
     p.add_argument("--vocab", type=int, default=0,
                    help="text-match vocabulary rows (0 = the 473-class table; configs[4]: 200)")
+    p.add_argument("--scene-objects", type=int, default=30,
+                   help="objects in the seeded synthetic scene (150: global box sets past the "
+                        "one-wave NMS scan's 96, so the 256-thread scan runs)")
     p.add_argument("--cpu-rehearsal", action="store_true",
                    help="CPU/gloo rehearsal of the N-rank control flow (no kernels; test harness)")
     return p.parse_args(argv)
@@ -399,7 +402,7 @@ def rehearse_cpu(args, dist, world, rank):
     sequence, the fusion owner's global frame order check, barrier + max-over-ranks timing and
     rank 0's JSON line.  CLIP rows are rank/frame-coded stand-ins (no CLIP runs)."""
     from boxfusion_amd.synthetic import Scene
-    scene = Scene(seed=0)
+    scene = Scene(seed=0, n_objects=args.scene_objects)
     B, N = args.batch, world
     per_step = B * N
     total = args.warmup + args.steps
@@ -510,7 +513,7 @@ def main(argv=None):
                            device=dev, graph=not args.eager, clip_fp8=args.clip_fp8)
                for _ in range(n_inflight)]
     detect = detects[0]
-    scene = Scene(seed=0)
+    scene = Scene(seed=0, n_objects=args.scene_objects)
     N = world
     per_step = B * N
     total_steps = args.warmup + args.steps
@@ -690,7 +693,7 @@ def main(argv=None):
             v["measured"] = source
         r_all["measured"] = source
         line = base_line(args, N, frames, dt, per_step, n_inflight)
-        line["config"].update(fused_boxes=fusion.stats["fused"],
+        line["config"].update(scene_objects=args.scene_objects, fused_boxes=fusion.stats["fused"],
                               global_boxes=len(fusion.all_pred_box) if fusion.all_pred_box is not None else 0)
         if args.clip_fp8:
             f8 = roofline_obj(timer.summary(lambda t: t["kind"] == "gemm_fp8"),
