@@ -49,47 +49,54 @@ __device__ void tri_plane(const double* p0, const double* p1, const double* p2, 
     pl[0] = nx; pl[1] = ny; pl[2] = nz; pl[3] = d;
 }
 
+// 8 lanes per box (the f64 plane fits are long dependent chains: one lane per box left a single
+// latency-bound wave, 30 us at n ~ 60): lanes 0-5 fit face f's two planes, lane 6 writes the gate
+// points, lane 7 the AABB; every value is computed by the same expression sequence as before
 __global__ void __launch_bounds__(64) k_obb_prep(const float* __restrict__ corners, int n,
                                                  BoxPrep* __restrict__ prep, double* __restrict__ iou,
                                                  ObbWork* __restrict__ w) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0 && w) { w->n_gated = 0; w->grid_done = 0; }
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t == 0 && w) { w->n_gated = 0; w->grid_done = 0; }
+    const int i = t >> 3, sub = t & 7;
     if (i >= n) return;
-    iou[(size_t)i * n + i] = 1.0;                 // diagonal (pairs fill the rest)
     const float* c = corners + 24 * i;
-    double p[8][3], cen[3] = {0, 0, 0};
-    for (int q = 0; q < 8; ++q)
-        for (int k = 0; k < 3; ++k) { p[q][k] = c[3 * q + k]; cen[k] += p[q][k]; }
-    for (int k = 0; k < 3; ++k) cen[k] /= 8.0;
     BoxPrep& o = prep[i];
-    for (int f = 0; f < 6; ++f) {
+    if (sub < 6) {
+        if (sub == 0) iou[(size_t)i * n + i] = 1.0;      // diagonal (pairs fill the rest)
+        double p[8][3], cen[3] = {0, 0, 0};
+        for (int q = 0; q < 8; ++q)
+            for (int k = 0; k < 3; ++k) { p[q][k] = c[3 * q + k]; cen[k] += p[q][k]; }
+        for (int k = 0; k < 3; ++k) cen[k] /= 8.0;
+        const int f = sub;
         const double* a = p[c_face[f][0]];
         const double* b = p[c_face[f][1]];
         const double* cc = p[c_face[f][2]];
         const double* d = p[c_face[f][3]];
-        double t[4];
-        tri_plane(a, b, cc, cen, t);
-        if (t[0] * d[0] + t[1] * d[1] + t[2] * d[2] + t[3] <= 0) {
+        double tt[4];
+        tri_plane(a, b, cc, cen, tt);
+        if (tt[0] * d[0] + tt[1] * d[1] + tt[2] * d[2] + tt[3] <= 0) {
             tri_plane(a, b, cc, cen, o.pl[2 * f]);
             tri_plane(a, cc, d, cen, o.pl[2 * f + 1]);
         } else {
             tri_plane(a, b, d, cen, o.pl[2 * f]);
             tri_plane(b, cc, d, cen, o.pl[2 * f + 1]);
         }
-    }
-    for (int q = 0; q < 8; ++q)
-        for (int k = 0; k < 3; ++k) o.pt[q][k] = c[3 * q + k];
-    for (int e = 0; e < 12; ++e)
-        for (int k = 0; k < 3; ++k)
-            o.pt[8 + e][k] = (c[3 * c_edge[e][0] + k] + c[3 * c_edge[e][1] + k]) / 2;
-    for (int k = 0; k < 3; ++k) {
-        float lo = c[k], hi = c[k];
-        for (int q = 1; q < 8; ++q) {
-            lo = fminf(lo, c[3 * q + k]);
-            hi = fmaxf(hi, c[3 * q + k]);
+    } else if (sub == 6) {
+        for (int q = 0; q < 8; ++q)
+            for (int k = 0; k < 3; ++k) o.pt[q][k] = c[3 * q + k];
+        for (int e = 0; e < 12; ++e)
+            for (int k = 0; k < 3; ++k)
+                o.pt[8 + e][k] = (c[3 * c_edge[e][0] + k] + c[3 * c_edge[e][1] + k]) / 2;
+    } else {
+        for (int k = 0; k < 3; ++k) {
+            float lo = c[k], hi = c[k];
+            for (int q = 1; q < 8; ++q) {
+                lo = fminf(lo, c[3 * q + k]);
+                hi = fmaxf(hi, c[3 * q + k]);
+            }
+            o.mn[k] = lo;
+            o.mx[k] = hi;
         }
-        o.mn[k] = lo;
-        o.mx[k] = hi;
     }
 }
 
@@ -380,7 +387,7 @@ BF_API int bf_obb_iou_matrix(const float* corners, int n, double* iou, void* wor
     int* gated = reinterpret_cast<int*>(ws + 256);
     int* cnt = gated + pairs;
     if (pairs > 0x7fffffffLL / 4) return BF_ERR_CAPACITY;
-    hipLaunchKernelGGL(k_obb_prep, dim3(bf_cdiv(n, 64)), dim3(64), 0, s, corners, n, prep, iou, w);
+    hipLaunchKernelGGL(k_obb_prep, dim3(bf_cdiv(8 * n, 64)), dim3(64), 0, s, corners, n, prep, iou, w);
     if (pairs > 0) {
         if (OBB_SPLIT == 0) {
             hipLaunchKernelGGL(k_obb_pairs, dim3((unsigned)pairs), dim3(IOU_THREADS), 0, s, prep, n, iou);
