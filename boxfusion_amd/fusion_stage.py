@@ -270,7 +270,9 @@ class AsyncFusion:
                 self._loop()
             finally:
                 pr.disable()
-                pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(25)
+                st = pstats.Stats(pr, stream=sys.stderr)
+                st.sort_stats("tottime").print_stats(25)
+                st.sort_stats("cumulative").print_stats(40)
             return
         self._loop()
 

@@ -43,3 +43,14 @@ def test_bench_rank_count_mismatch_is_an_error():
                         "--cpu-rehearsal"], cwd=REPO, capture_output=True, text=True, timeout=120,
                        env=env)
     assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_bench_fp8_workload_line():
+    """--clip-fp8 --vocab 200 names BASELINE configs[4] as its workload and its compute dtype"""
+    r, lines = _bench("--gpus", "2", "--cpu-rehearsal", "--no-cpu-baseline", "--steps", "2",
+                      "--warmup", "1", "--batch", "2", "--clip-fp8", "--vocab", "200")
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(lines[0])
+    assert line["config"]["workload"].startswith("configs[4]")
+    assert "200-class" in line["config"]["workload"]
+    assert "fp8" in line["dtype"]
