@@ -1,5 +1,6 @@
 """Stream-K vs tile-parallel persistent GEMM on the path's shapes (bf_gemm_set_streamk).
-python scripts/gemm_streamk_probe.py"""
+The stream-K form was measured slower and removed from bf_gemm.hip; this probe
+needs a build that still has it and exits otherwise.  python scripts/gemm_streamk_probe.py"""
 import torch
 
 from boxfusion_amd import _lib
@@ -19,6 +20,8 @@ def timeit(fn, n=20):
 
 dev = torch.device("cuda")
 L = _lib.lib()
+if not hasattr(L, "bf_gemm_set_streamk"):
+    raise SystemExit("this build has no stream-K GEMM (measured slower and removed, DESIGN.md section 4)")
 SH = [("clip_qkv", 32896, 3840, 1280, None, "bf16"), ("clip_proj", 32896, 1280, 1280, None, "resid"),
       ("clip_fc1", 32896, 5120, 1280, "gelu", "bf16"), ("clip_fc2", 32896, 1280, 5120, None, "resid"),
       ("cutr_qkv", 36864, 2304, 768, None, "bf16"), ("cutr_fc1", 25600, 3072, 768, "gelu", "bf16"),
