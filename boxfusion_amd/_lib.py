@@ -808,3 +808,161 @@ def rpe_softmax(attn, rx, ry, hh, ww, q0):
     _check(lib().bf_rpe_softmax(_ptr(attn), c_int(B), c_int(H), c_int(Nq), c_int(q0), _ptr(rx),
                                 _ptr(ry), c_int(hh), c_int(ww), _stream()), "bf_rpe_softmax")
     return attn
+
+
+# ------------------------------------------------------------------------------------------
+# CuTR decoder tail, f32 (bf_dec_native.hip + bf_self_attn_f32): thin pointer-level wrappers.
+# Views with a row stride and unit column stride are accepted (the row stride is passed on).
+# ------------------------------------------------------------------------------------------
+def _rows(t, name, dtype=torch.float32):
+    """(pointer, row stride) of a 2-D device view with unit column stride"""
+    if t is None:
+        return None, 0
+    if not t.is_cuda:
+        raise HipError("boxfusion_amd kernels need device tensors (no CPU fallback)")
+    _need(t, dtype, name)
+    if t.dim() != 2 or (t.shape[1] > 1 and t.stride(1) != 1):
+        raise HipError(f"{name}: expected a 2-D view with unit column stride")
+    return c_void_p(t.data_ptr()), t.stride(0)
+
+
+def gemm_f32(a, w, bias=None, act=None, resid=None, out=None, a_map=None, c_map=None, m=None):
+    """out[c_map[r]] = resid[c_map[r]] + act(a[a_map[r]] @ w.T + bias) for r < m (f32 MFMA);
+    a_map / c_map int32 (< 0: zero row / dropped row); m defaults to len(a_map) or a.shape[0]"""
+    N, K = w.shape
+    M = m if m is not None else (a_map.shape[0] if a_map is not None else a.shape[0])
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    pa, lda = _rows(a, "a")
+    pw, ldw = _rows(w, "w")
+    pc, ldc = _rows(out, "out")
+    pr, ldr = _rows(resid, "resid")
+    for mp, n in ((a_map, "a_map"), (c_map, "c_map")):
+        if mp is not None:
+            _need(mp, torch.int32, n)
+            if mp.shape[0] < M:
+                raise HipError(f"gemm_f32: {n} shorter than M")
+    if bias is not None:
+        _need(bias, torch.float32, "bias")
+    _check(lib().bf_gemm_f32(pa, c_int(lda), _ptr(a_map), pw, c_int(ldw), _ptr(bias), pr, c_int(ldr),
+                             pc, c_int(ldc), _ptr(c_map), c_int(M), c_int(N), c_int(K), c_int(ACT[act]),
+                             _stream()), "bf_gemm_f32")
+    return out
+
+
+def ln_rows(x, gamma, beta, eps, out=None, pos=None, out2=None, gelu=False):
+    """out = LayerNorm(x rows) [GELU]; out2 = out + pos (optional).  C % 256 == 0, <= 1024"""
+    M, C = x.shape
+    if out is None:
+        out = torch.empty((M, C), dtype=torch.float32, device=x.device)
+    px, ldx = _rows(x, "x")
+    po, ldo = _rows(out, "out")
+    pp, ldp = _rows(pos, "pos")
+    p2, ld2 = _rows(out2, "out2")
+    _check(lib().bf_ln_rows_f32(px, c_int(ldx), _ptr(gamma), _ptr(beta), c_float(eps), po, c_int(ldo),
+                                pp, c_int(ldp), p2, c_int(ld2), c_int(M), c_int(C), c_int(int(gelu)),
+                                _stream()), "bf_ln_rows_f32")
+    return out
+
+
+def groupnorm_cl(x, frames, groups, gamma, beta, eps, out, pos=None, out2=None):
+    """GroupNorm of a channel-last map x [frames*P, C] -> out (and out2 = out + pos)"""
+    px, ldx = _rows(x, "x")
+    po, ldo = _rows(out, "out")
+    pp, ldp = _rows(pos, "pos")
+    p2, ld2 = _rows(out2, "out2")
+    P = x.shape[0] // frames
+    _check(lib().bf_groupnorm_cl_f32(px, c_int(ldx), c_int(frames), c_int(P), c_int(x.shape[1]), c_int(groups),
+                                     _ptr(gamma), _ptr(beta), c_float(eps), po, c_int(ldo), pp, c_int(ldp),
+                                     p2, c_int(ld2), _stream()), "bf_groupnorm_cl_f32")
+    return out
+
+
+def s2d(x, frames, H, W, out=None):
+    """space-to-depth rows (kernel-2 stride-2 conv operand) of a channel-last map [frames*H*W, C]"""
+    C = x.shape[1]
+    if out is None:
+        out = torch.empty((frames * (H // 2) * (W // 2), 4 * C), dtype=torch.float32, device=x.device)
+    px, ldx = _rows(x, "x")
+    _check(lib().bf_s2d_f32(px, c_int(ldx), c_int(frames), c_int(H), c_int(W), c_int(C), _ptr(out), _stream()),
+           "bf_s2d_f32")
+    return out
+
+
+HEAD_MODES = {"class": 0, "box2d": 1, "box3d": 2, "scale": 3}
+
+
+def row_heads(x, in_fs, in_off, rows, nq, w, b, mode, out=None, prop=None, params=None, boxes=None,
+              clamp_wh=(0.0, 0.0), max_ratio=0.0):
+    """the predictors' output linears + transforms (bf_row_heads_f32; see bf_dec_native.hip)"""
+    px, ldx = _rows(x, "x")
+    po, ldo = _rows(out, "out")
+    _check(lib().bf_row_heads_f32(px, c_int(ldx), c_int(in_fs), c_int(in_off), c_int(rows), c_int(nq),
+                                  c_int(w.shape[1]), _ptr(w), _ptr(b), c_int(w.shape[0]), _ptr(prop),
+                                  _ptr(params), po, c_int(ldo), _ptr(boxes), c_float(clamp_wh[0]),
+                                  c_float(clamp_wh[1]), c_float(max_ratio), c_int(HEAD_MODES[mode]),
+                                  _stream()), "bf_row_heads_f32")
+    return out
+
+
+def topk_rows(v, frames, n, k, ldv=1, idx=None, vals=None):
+    """per-frame top-k of v[(f*n + i)*ldv] (descending, ties -> lower index): int32 idx [frames, k]"""
+    if idx is None:
+        idx = torch.empty((frames, k), dtype=torch.int32, device=v.device)
+    _check(lib().bf_topk_rows_f32(c_void_p(v.data_ptr()), c_int(ldv), c_int(frames), c_int(n), c_int(k),
+                                  _ptr(idx), _ptr(vals), _stream()), "bf_topk_rows_f32")
+    return idx
+
+
+def prop_select(boxes, frames, n, k, idx, ref, embs, max_e, qpos, qfs, qoff):
+    """ref[f*k + j] = boxes[f*n + idx[f, j]]; qpos row f*qfs + qoff + j = the 4 box embeddings"""
+    pq, ldq = _rows(qpos, "qpos")
+    ex, ey, ew, eh = embs
+    _check(lib().bf_prop_select_f32(_ptr(boxes), c_int(frames), c_int(n), c_int(k), _ptr(idx), _ptr(ref),
+                                    _ptr(ex), _ptr(ey), _ptr(ew), _ptr(eh), c_int(ex.shape[1]),
+                                    c_float(max_e), pq, c_int(ldq), c_int(qfs), c_int(qoff), _stream()),
+           "bf_prop_select_f32")
+
+
+def infer_select(logits, frames, nq, nc, boxes, b3info, desc, desc_fs, desc_off, Kinv, Tg, img_wh, k, outs):
+    """inference_single_image for every frame (bf_infer_select_f32); outs = dict of output buffers
+    scores [F,k], classes int64 [F,k], logits [F,k,nc], boxes [F,k,4], proj [F,k,2], b3 [F,k,6],
+    R [F,k,3,3], desc [F,k,C]"""
+    pd, ldd = _rows(desc, "desc")
+    _check(lib().bf_infer_select_f32(_ptr(logits), c_int(frames), c_int(nq), c_int(nc), _ptr(boxes),
+                                     _ptr(b3info), pd, c_int(ldd), c_int(desc_fs), c_int(desc_off),
+                                     c_int(desc.shape[1]), _ptr(Kinv), _ptr(Tg), _ptr(img_wh), c_int(k),
+                                     _ptr(outs["scores"]), _ptr(outs["classes"]), _ptr(outs["logits"]),
+                                     _ptr(outs["boxes"]), _ptr(outs["proj"]), _ptr(outs["b3"]),
+                                     _ptr(outs["R"]), _ptr(outs["desc"]), _stream()), "bf_infer_select_f32")
+
+
+def ray_fourier(K3, W, H, feat, stride, scales, out):
+    """CameraRayEmbedding's Fourier features of one camera into out [feat*feat, ld] (ld >= 3 * bands)"""
+    K3 = np.asarray(K3, np.float32).reshape(3, 3)
+    po, ld = _rows(out, "out")
+    _check(lib().bf_ray_fourier_f32(c_float(K3[0, 0]), c_float(K3[1, 1]), c_float(K3[0, 2]), c_float(K3[1, 2]),
+                                    c_int(W), c_int(H), c_int(feat), c_int(stride), _ptr(scales),
+                                    c_int(scales.shape[0]), po, c_int(ld), _stream()), "bf_ray_fourier_f32")
+    return out
+
+
+def self_attn(q, k, v, out, frames, heads, n, q0, scale):
+    """decoder self-attention with the metric / box block mask (bf_self_attn_f32); q / k / v / out
+    [frames*n, heads*32] row views"""
+    pq, ldq = _rows(q, "q")
+    pk, ldk = _rows(k, "k")
+    pv, ldv = _rows(v, "v")
+    po, ldo = _rows(out, "out")
+    _check(lib().bf_self_attn_f32(pq, c_int(ldq), pk, c_int(ldk), pv, c_int(ldv), po, c_int(ldo), c_int(frames),
+                                  c_int(heads), c_int(n), c_int(q0), c_float(scale), _stream()), "bf_self_attn_f32")
+    return out
+
+
+def cpb_mlp_into(ref, pos, axis, w1, b1, w2, out):
+    """cpb_mlp into a preallocated [B, nq, n, heads] buffer"""
+    B, nq = ref.shape[0], ref.shape[1]
+    heads, hidden = w2.shape
+    _check(lib().bf_cpb_mlp(_ptr(ref), c_int(B), c_int(nq), _ptr(pos), c_int(pos.shape[0]), c_int(axis), _ptr(w1),
+                            _ptr(b1), _ptr(w2), c_int(hidden), c_int(heads), _ptr(out), _stream()), "bf_cpb_mlp")
+    return out

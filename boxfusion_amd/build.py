@@ -24,6 +24,7 @@ SOURCES = {
     "bf_iou3d.hip": EXACT,
     "bf_assoc.hip": EXACT,
     "bf_fusion.hip": EXACT,
+    "bf_dec_native.hip": EXACT,
 }
 EXTRA = [s for s in sorted(os.listdir(CSRC)) if s.endswith(".hip") and s not in SOURCES]
 

@@ -249,6 +249,11 @@ BF_API int bf_rpe_softmax(float* attn, int B, int H, int Nq, int q0, const float
 #define XA_WAVES 4
 typedef float xa_f32x16 __attribute__((ext_vector_type(16)));
 
+// SELF: the decoder's masked self-attention (nn.MultiheadAttention with the block mask of
+// CubifyTransformer.decode: the q0 metric queries see only the q0 metric keys, the box queries
+// only the box keys): no bias tables, keys = queries (N = Nq), key j valid for query i iff
+// (j < q0) == (i < q0).
+template <bool SELF>
 __global__ void __launch_bounds__(XA_WAVES * 64) k_xattn(
     const float* __restrict__ q, int ldq, const float* __restrict__ k, int ldk,
     const float* __restrict__ v, int ldv, const float* __restrict__ rx, const float* __restrict__ ry,
@@ -262,13 +267,15 @@ __global__ void __launch_bounds__(XA_WAVES * 64) k_xattn(
     const int qg = qb * 32 + jq;                       // this lane's query
     const int nqb = Nq - q0;
     // bias tables of the 32 queries: [x][query], [y][query] (0 for metric / absent queries)
-    for (int i = t; i < ww * 32; i += XA_WAVES * 64) {
-        const int x = i >> 5, j = i & 31, qq = qb * 32 + j;
-        s_bx[i] = (qq >= q0 && qq < Nq) ? rx[(((size_t)b * nqb + (qq - q0)) * ww + x) * H + hd] : 0.f;
-    }
-    for (int i = t; i < hh * 32; i += XA_WAVES * 64) {
-        const int y = i >> 5, j = i & 31, qq = qb * 32 + j;
-        s_by[i] = (qq >= q0 && qq < Nq) ? ry[(((size_t)b * nqb + (qq - q0)) * hh + y) * H + hd] : 0.f;
+    if (!SELF) {
+        for (int i = t; i < ww * 32; i += XA_WAVES * 64) {
+            const int x = i >> 5, j = i & 31, qq = qb * 32 + j;
+            s_bx[i] = (qq >= q0 && qq < Nq) ? rx[(((size_t)b * nqb + (qq - q0)) * ww + x) * H + hd] : 0.f;
+        }
+        for (int i = t; i < hh * 32; i += XA_WAVES * 64) {
+            const int y = i >> 5, j = i & 31, qq = qb * 32 + j;
+            s_by[i] = (qq >= q0 && qq < Nq) ? ry[(((size_t)b * nqb + (qq - q0)) * hh + y) * H + hd] : 0.f;
+        }
     }
     // Q^T fragments: k-step s of lane half hf is dim 16*hf + s (any order agreeing with K's)
     float qf[16];
@@ -323,6 +330,17 @@ __global__ void __launch_bounds__(XA_WAVES * 64) k_xattn(
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int key0 = kb * 32 + 8 * g + 4 * hf;
+            if (SELF) {
+                const bool qmetric = qg < q0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int r = 4 * g + i, key = key0 + i;
+                    const float sv = (key < N && ((key < q0) == qmetric)) ? sc[r] : -INFINITY;
+                    sc[r] = sv;
+                    mt = fmaxf(mt, sv);
+                }
+                continue;
+            }
             int y = key0 / ww, x = key0 - y * ww;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -343,9 +361,12 @@ __global__ void __launch_bounds__(XA_WAVES * 64) k_xattn(
             for (int r = 0; r < 16; ++r) o[r] *= alpha;
             m_run = mt;
         }
+        // a query with no valid key in this block so far (SELF: the metric queries) keeps
+        // m_run = -inf: its probabilities are 0, not exp(-inf + inf)
+        const float m_ref = m_run == -INFINITY ? 0.f : m_run;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const float p = expf(sc[r] - m_run);
+            const float p = expf(sc[r] - m_ref);
             l_run += p;
             sc[r] = p;
         }
@@ -397,7 +418,22 @@ BF_API int bf_xattn_f32(const float* q, int ldq, const float* k, int ldk, const 
     if (hh > XA_MAX_SIDE || ww > XA_MAX_SIDE || ww < 4) return BF_ERR_CAPACITY;
     if (B == 0 || Nq == 0) return BF_OK;
     const int N = hh * ww;
-    hipLaunchKernelGGL(k_xattn, dim3((Nq + 31) / 32, H, B), dim3(XA_WAVES * 64), 0, bf_stream(stream), q,
+    hipLaunchKernelGGL(k_xattn<false>, dim3((Nq + 31) / 32, H, B), dim3(XA_WAVES * 64), 0, bf_stream(stream), q,
                        ldq, k, ldk, v, ldv, rx, ry, out, ldo, H, Nq, N, q0, hh, ww, scale);
+    return bf_check_launch();
+}
+
+// the decoder self-attention (PreNormGlobalDecoderLayer.self_attn with CubifyTransformer.decode's
+// block mask): q / k / v f32 [B, N, H*32] (row strides ldq / ldk / ldv, batches packed), q0 =
+// number of metric queries, scale = head_dim^-0.5 applied to q (nn.MultiheadAttention)
+BF_API int bf_self_attn_f32(const float* q, int ldq, const float* k, int ldk, const float* v, int ldv,
+                            float* out, int ldo, int B, int H, int N, int q0, float scale, void* stream) {
+    if (!q || !k || !v || !out || B < 0 || H <= 0 || N < 0 || q0 < 0 || q0 > N) return BF_ERR_ARG;
+    if (ldq % 4 || ldo % 4 || ldk % 4 || ldq < H * 32 || ldk < H * 32 || ldv < H * 32 || ldo < H * 32 ||
+        (uintptr_t)q % 16 || (uintptr_t)k % 16 || (uintptr_t)out % 16)
+        return BF_ERR_UNSUPPORTED;
+    if (B == 0 || N == 0) return BF_OK;
+    hipLaunchKernelGGL(k_xattn<true>, dim3((N + 31) / 32, H, B), dim3(XA_WAVES * 64), 0, bf_stream(stream), q,
+                       ldq, k, ldk, v, ldv, nullptr, nullptr, out, ldo, H, N, N, q0, 1, 1, scale);
     return bf_check_launch();
 }

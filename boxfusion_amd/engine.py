@@ -16,6 +16,7 @@ Dead compute skipped: after the last depth window block the depth stream is neve
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -45,8 +46,15 @@ class CuTREngine:
     (depth_model=False) runs RGB-only windows, its layer scales folded into the proj / fc2
     weights and its encoder_norm on the output (vit.py:303-342, 473)."""
 
-    def __init__(self, model, batch, height=480, width=640, pad=640, device="cuda", depth_ratio=1):
+    def __init__(self, model, batch, height=480, width=640, pad=640, device="cuda", depth_ratio=1,
+                 native_decoder=None):
         dev = torch.device(device)
+        # decoder tail: DecoderEngine (f32 HIP kernels) by default; BF_DECODER_TORCH=1 runs the torch
+        # definition (CubifyTransformer.decode, f32 on the device) for comparisons
+        if native_decoder is None:
+            native_decoder = os.environ.get("BF_DECODER_TORCH", "0") != "1"
+        self.native_decoder = bool(native_decoder)
+        self.decoder = None
         self.model = model.to(dev).eval()
         vit = model.backbone.backbone
         self.dev, self.B, self.H, self.W, self.P = dev, batch, height, width, pad
@@ -231,6 +239,18 @@ class CuTREngine:
         never reads device memory (graph-capturable once the cache is warm)."""
         if K_host is None:
             K_host = K.detach().cpu().numpy()
+        if self.native_decoder:
+            # the decoder tail on the f32 HIP kernels (DecoderEngine), fed the channel-last rows
+            if self.decoder is None:
+                from boxfusion_amd.decoder_engine import DecoderEngine
+                self.decoder = DecoderEngine(self.model, self.B, self.g, self.g, device=self.dev)
+            pos = self.decoder.positions(K_host, [(w, h) for h, w in image_sizes])
+            feat = self.backbone(img_u8, depth_std, chw=chw, pixel_mean=pixel_mean, pixel_std=pixel_std)
+            rows = feat.permute(0, 2, 3, 1).reshape(self.B * self.T, self.C)
+            if K_inv is None:
+                K_inv = torch.linalg.inv(K)
+            return self.decoder(rows, pos, depth_params if self.has_depth else None, K_inv, T_gravity,
+                                image_sizes, (self.P, self.P))
         pos = self.positions(K_host, image_sizes)
         feat = self.backbone(img_u8, depth_std, chw=chw, pixel_mean=pixel_mean, pixel_std=pixel_std)
         batch = FrameBatch(image=None, depth=depth_std if self.has_depth else None,

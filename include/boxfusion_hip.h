@@ -364,6 +364,72 @@ int bf_rpe_softmax(float* attn, int B, int H, int Nq, int q0, const float* rx, c
 int bf_xattn_f32(const float* q, int ldq, const float* k, int ldk, const float* v, int ldv,
                  const float* rx, const float* ry, float* out, int ldo, int B, int H, int Nq, int q0,
                  int hh, int ww, float scale, void* stream);
+/* The decoder self-attention (PreNormGlobalDecoderLayer.self_attn, cubify_transformer.py:
+ * 313-352 of the reference, with CubifyTransformer's block mask :1196-1202): q / k / v f32
+ * [B, N] rows (strides ldq / ldk / ldv, batches packed), head dim 32, query i sees key j iff
+ * (j < q0) == (i < q0) (q0 metric queries), scale applied to q. */
+int bf_self_attn_f32(const float* q, int ldq, const float* k, int ldk, const float* v, int ldv,
+                     float* out, int ldo, int B, int H, int N, int q0, float scale, void* stream);
+
+/* ---- the CuTR decoder tail, f32 (bf_dec_native.hip; boxfusion_amd.decoder_engine) ----------
+ * Replaces the torch / hipBLASLt ops of CubifyTransformer.inference after the backbone
+ * (cubify_transformer.py:1172-1227 of the reference).
+ * bf_gemm_f32: C[c_map[m]] = resid[c_map[m]] + act(A[a_map[m]] W^T + bias) for m < M on
+ *   v_mfma_f32_32x32x2_f32 (act 0 none, 1 GELU(erf), 2 ReLU); A [*,K] row stride lda, W [N,K]
+ *   row stride ldw (both % 4, 16-B aligned); a_map / c_map int32 or NULL (identity); a_map < 0
+ *   reads a zero row, c_map < 0 drops the row; resid may alias C.  Every nn.Linear / 1x1 and
+ *   2x2/2 conv of the decoder tail (cubify_transformer.py:93-352, 812-943, 1128-1170). */
+int bf_gemm_f32(const float* A, int lda, const int* a_map, const float* W, int ldw,
+                const float* bias, const float* resid, int ldr, float* C, int ldc,
+                const int* c_map, int M, int N, int K, int act, void* stream);
+/* LayerNorm over rows (C % 256 == 0, <= 1024), optional GELU (LayerNorm2D + GELU of the proposal
+ * levels, :858-862), optional second output out2 = y + pos (the decoder's `norm(tgt) +
+ * query_pos`, :330-341).  out may alias x. */
+int bf_ln_rows_f32(const float* x, int ldx, const float* gamma, const float* beta, float eps,
+                   float* out, int ldo, const float* pos, int ldp, float* out2, int ldo2, int M,
+                   int C, int gelu, void* stream);
+/* GroupNorm(G) of a channel-last map x [B*P, C] (input_proj's GroupNorm, :1131-1136), optional
+ * out2 = y + pos (the memory keys' src + pos). */
+int bf_groupnorm_cl_f32(const float* x, int ldx, int B, int P, int C, int G, const float* gamma,
+                        const float* beta, float eps, float* out, int ldo, const float* pos,
+                        int ldp, float* out2, int ldo2, void* stream);
+/* space-to-depth rows of a channel-last [B,H,W,C] map for a 2x2 stride-2 Conv2d:
+ * out [B*(H/2)*(W/2), 4C], column c*4 + ky*2 + kx (the Conv2d weight order). */
+int bf_s2d_f32(const float* x, int ldx, int B, int H, int W, int C, float* out, void* stream);
+/* The predictors' output linears (K = 256 / 512, nout <= 8) and transforms, one row per
+ * (frame f, query q < nq) of input row f*in_fs + in_off + q: mode 0 ClassPredictor logits
+ * (:396-403), 1 DeltaBox2DPredictor + apply_deltas + cxcywh (:478-541; prop / boxes [rows,4]
+ * cxcywh, may alias), 2 AbsoluteBox3DPredictor (:592-643; 16 floats per row: proj_xy, z,
+ * z_scaled, dims, R_Y(yaw); params [frames,2] = (shift, scale)), 3 ScalePredictor (:545-560;
+ * out [frames,2] = exp of the two tokens' linears).  clamp_w / clamp_h: clamp_xy bounds. */
+int bf_row_heads_f32(const float* x, int ldx, int in_fs, int in_off, int rows, int nq, int K,
+                     const float* w, const float* b, int nout, const float* prop,
+                     const float* params, float* out, int ldo, float* boxes, float clamp_w,
+                     float clamp_h, float max_ratio, int mode, void* stream);
+/* per-frame top-k of v[(f*n + i)*ldv], n <= 4096: idx int32 [frames, k] (and vals), descending,
+ * ties -> lower index (torch.topk, :930 / :967). */
+int bf_topk_rows_f32(const float* v, int ldv, int frames, int n, int k, int* idx, float* vals,
+                     void* stream);
+/* the top-k proposals' boxes (ref [frames*k, 4]) and their learned box prompt embedding
+ * (Box2DPromptEncoderLearned, :706-737: clamp to [0, max_e], int, 4 tables of ed columns) into
+ * qpos row f*qfs + qoff + j. */
+int bf_prop_select_f32(const float* boxes, int frames, int n, int k, const int* idx, float* ref,
+                       const float* ex, const float* ey, const float* ew, const float* eh, int ed,
+                       float max_e, float* qpos, int ldq, int qfs, int qoff, void* stream);
+/* inference_single_image (:945-996) for every frame: sigmoid, top-k over (query, class) (nq*nc
+ * <= 4096), xyxy boxes clamped to img_wh[f], K^-1 (z u, z v, z), dims reversed, T_gravity R
+ * (Tg may be NULL), logits / proj_xy / descriptor rows gathered. */
+int bf_infer_select_f32(const float* logits, int frames, int nq, int nc, const float* boxes,
+                        const float* b3info, const float* desc, int ld_desc, int desc_fs,
+                        int desc_off, int C, const float* Kinv, const float* Tg,
+                        const float* img_wh, int k, float* scores, long long* classes,
+                        float* out_logits, float* out_boxes, float* out_proj, float* out_b3,
+                        float* out_R, float* out_desc, void* stream);
+/* CameraRayEmbedding's ray Fourier features of one camera (pos.py:61-186): rays through
+ * (fx, fy, cx, cy) at pixel centres, square pad feat*stride, nearest sample every stride pixels,
+ * normalised, sin(r_c * scales[k] * pi) -> out [feat*feat, ld] (columns >= 3*nb zeroed). */
+int bf_ray_fourier_f32(float fx, float fy, float cx, float cy, int W, int H, int feat, int stride,
+                       const float* scales, int nb, float* out, int ld, void* stream);
 
 /* LayerNorm f32[M,C] -> bf16, written to row row_map[r] (NULL = r; < 0 skips). */
 int bf_layernorm(const float* x, int ldx, const float* gamma, const float* beta, float eps,
