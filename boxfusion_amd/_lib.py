@@ -509,6 +509,119 @@ def layernorm(x, weight, bias, eps, out=None, row_map=None, out_dtype=torch.bflo
     return out
 
 
+
+def attention_causal(q, k, v, o, batch, heads, s, head_dim, scale):
+    """causal self-attention (CLIP text tower): q/k/v/o token-major 2-D views [batch*s, >= heads*D]"""
+    for x, n in ((q, "q"), (k, "k"), (v, "v"), (o, "o")):
+        _need(x, torch.bfloat16, n)
+    LL = ctypes.c_longlong
+    _check(lib().bf_attention_causal(c_void_p(q.data_ptr()), c_void_p(k.data_ptr()), c_void_p(v.data_ptr()),
+                                     c_void_p(o.data_ptr()), c_int(batch), c_int(heads), c_int(s),
+                                     c_int(head_dim), c_int(q.stride(0)), c_int(k.stride(0)),
+                                     c_int(v.stride(0)), c_int(o.stride(0)), LL(s * q.stride(0)),
+                                     LL(s * k.stride(0)), LL(s * v.stride(0)), LL(s * o.stride(0)),
+                                     c_float(scale), _stream()), "bf_attention_causal")
+    return o
+
+
+def token_embed(ids, table, pos, out=None, status=None):
+    """ids i32 [N, S] -> table[ids] + pos, f32 [N*S, W]; an out-of-range id raises HipError"""
+    _need(ids, torch.int32, "ids")
+    _need(table, torch.float32, "table")
+    _need(pos, torch.float32, "pos")
+    N, S = ids.shape
+    W = table.shape[1]
+    if pos.shape[0] < S or pos.shape[1] != W:
+        raise HipError(f"token_embed: positional table {tuple(pos.shape)} for S={S}, W={W}")
+    if out is None:
+        out = torch.empty((N * S, W), dtype=torch.float32, device=ids.device)
+    _need(out, torch.float32, "out")
+    own = status is None
+    if own:
+        status = torch.zeros(1, dtype=torch.int32, device=ids.device)
+    _check(lib().bf_token_embed(_ptr(ids), c_int(N * S), _ptr(table), c_int(table.shape[0]), _ptr(pos),
+                                c_int(S), c_int(W), _ptr(out), _ptr(status), _stream()), "bf_token_embed")
+    if own and int(status.item()) & BF_DEV_INDEX_RANGE:
+        raise HipError("bf_token_embed: a token id outside the vocabulary (BF_DEV_INDEX_RANGE)")
+    return out
+
+
+def text_pool(ids, x, out=None):
+    """x f32 [N*S, W] -> x[n*S + argmax(ids[n])] f32 [N, W] (open_clip 'argmax' text pooling)"""
+    _need(ids, torch.int32, "ids")
+    _need(x, torch.float32, "x")
+    N, S = ids.shape
+    W = x.shape[1]
+    if out is None:
+        out = torch.empty((N, W), dtype=torch.float32, device=x.device)
+    _need(out, torch.float32, "out")
+    _check(lib().bf_text_pool(_ptr(ids), c_int(N), c_int(S), _ptr(x), c_int(W), _ptr(out), _stream()),
+           "bf_text_pool")
+    return out
+
+
+def l2_normalize_rows(x, out=None):
+    """x f32 [R, W] -> x / ||x||_2 per row (out may be x)"""
+    _need(x, torch.float32, "x")
+    if out is None:
+        out = torch.empty_like(x)
+    _need(out, torch.float32, "out")
+    _check(lib().bf_l2_normalize_rows(_ptr(x), c_int(x.shape[0]), c_int(x.shape[1]), _ptr(out), _stream()),
+           "bf_l2_normalize_rows")
+    return out
+
+
+def ingest_rgbd(bgr, depth_u16, depth_scale, rot_k=0, rgb_out=None, depth_out=None, src_bgr=True):
+    """decoded frames -> sample tensors (capture_stream.py:194-311): bgr u8 [F,Hc,Wc,3], depth
+    int16/uint16 [F,Hd,Wd] (or None) -> rgb u8 [F,3,Ho,Wo] (RGB, cv2-resized to the depth size,
+    rot90 k) and depth f32 [F,Ho,Wo] = depth / depth_scale (rot90 k)"""
+    _need(bgr, torch.uint8, "bgr")
+    if bgr.dim() == 3:
+        bgr = bgr[None]
+    F_, Hc, Wc, C = bgr.shape
+    if C != 3:
+        raise HipError("ingest_rgbd: BGR frames [F,H,W,3]")
+    if depth_u16 is not None:
+        if depth_u16.dtype not in (torch.uint16, torch.int16):
+            raise HipError(f"depth: expected a 16-bit PNG map, got {depth_u16.dtype}")
+        if depth_u16.dim() == 2:
+            depth_u16 = depth_u16[None]
+        if depth_u16.shape[0] != F_:
+            raise HipError("ingest_rgbd: one depth map per frame")
+        Hd, Wd = depth_u16.shape[1:]
+    else:
+        Hd, Wd = Hc, Wc
+    k = rot_k % 4
+    Ho, Wo = (Wd, Hd) if k % 2 else (Hd, Wd)
+    if rgb_out is None:
+        rgb_out = torch.empty((F_, 3, Ho, Wo), dtype=torch.uint8, device=bgr.device)
+    _need(rgb_out, torch.uint8, "rgb_out")
+    if depth_u16 is not None and depth_out is None:
+        depth_out = torch.empty((F_, Ho, Wo), dtype=torch.float32, device=bgr.device)
+    _check(lib().bf_ingest_rgbd(_ptr(bgr), c_int(Hc), c_int(Wc), _ptr(depth_u16), c_int(Hd), c_int(Wd),
+                                c_int(F_), c_float(depth_scale), c_int(k), c_int(int(bool(src_bgr))), _ptr(rgb_out),
+                                _ptr(depth_out) if depth_u16 is not None else None, _stream()),
+           "bf_ingest_rgbd")
+    return rgb_out, depth_out
+
+
+def cv2_resize_u8(src, Wd, Hd, out=None):
+    """cv2.resize(src, (Wd, Hd)) (u8 INTER_LINEAR) of u8 images [H,W], [H,W,cn] or [F,H,W,cn]"""
+    _need(src, torch.uint8, "src")
+    x = src
+    if x.dim() == 2:
+        x = x[None, :, :, None]
+    elif x.dim() == 3:
+        x = x[None]
+    F_, Hs, Ws, cn = x.shape
+    if out is None:
+        out = torch.empty((F_, Hd, Wd, cn), dtype=torch.uint8, device=src.device)
+    _check(lib().bf_cv2_resize_u8(_ptr(x), c_int(Hs), c_int(Ws), c_int(cn), c_int(Hd), c_int(Wd), c_int(F_),
+                                  _ptr(out), _stream()), "bf_cv2_resize_u8")
+    if src.dim() == 2:
+        return out[0, :, :, 0]
+    return out[0] if src.dim() == 3 else out
+
 FP8 = torch.float8_e4m3fn      # OCP e4m3 (gfx950's fp8; not the MI300 fnuz variant)
 FP8_MAX = 448.0
 _FP8_OUT = {torch.float32: 0, torch.bfloat16: 1, FP8: 2}

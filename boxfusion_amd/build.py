@@ -25,6 +25,7 @@ SOURCES = {
     "bf_assoc.hip": EXACT,
     "bf_fusion.hip": EXACT,
     "bf_dec_native.hip": EXACT,
+    "bf_ingest.hip": EXACT,
 }
 EXTRA = [s for s in sorted(os.listdir(CSRC)) if s.endswith(".hip") and s not in SOURCES]
 
@@ -39,7 +40,7 @@ def hipcc():
 def _compile(src, flags):
     obj = os.path.join(BUILD, src.replace(".hip", ".o"))
     path = os.path.join(CSRC, src)
-    deps = [path, os.path.join(CSRC, "bf_common.h"),
+    deps = [path, os.path.join(CSRC, "bf_common.h"), os.path.join(CSRC, "bf_cv2.h"),
             os.path.join(HERE, "..", "include", "boxfusion_hip.h")]
     if os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps
                                    if os.path.exists(d)):

@@ -5,8 +5,9 @@
 image and the depth map under sample["wide"], a SensorArrayInfo with the `wide` sensor (image /
 depth infos, T_gravity = camera -> gravity rotation, RT = identity) and the `gt` sensor (the
 camera -> world pose), the frame rotated to the upright orientation first (torch.rot90 on
-whatever device the frame is on).  Reading JPEG / PNG files (cv2.imread) is not part of this
-module: the dataset formats are not available offline.
+whatever device the frame is on).  `make_sample_decoded` / `DecodedFrameStream` take decoded
+colour + 16-bit depth frames and run the rest of the streams' per-frame work on the GPU
+(bf_ingest_rgbd: cvtColor, cv2.resize, depth scaling, rotation).  Image decode stays on the host.
 """
 from __future__ import annotations
 
@@ -70,6 +71,63 @@ def make_sample(rgb, depth, K, pose, depth_K=None, video_id=0, index=0):
     return {"wide": {"image": image.contiguous(), "depth": dep.contiguous()},
             "meta": dict(video_id=video_id, timestamp=index), "sensor_info": si}
 
+
+def make_sample_decoded(bgr, depth_u16, depth_scale, K, pose, video_id=0, index=0, src_bgr=True):
+    """the reference streams' per-frame work after decode (capture_stream.py:194-311 ScanNet,
+    :402-529 CA-1M) on the GPU: `bgr` u8 [Hc,Wc,3] as cv2.imread returns it (src_bgr=False: RGB,
+    as PIL decodes), `depth_u16` [Hd,Wd] the 16-bit PNG depth, both device tensors.  One
+    bf_ingest_rgbd launch does cvtColor, cv2.resize(color, (Wd, Hd)), astype(f32) / depth_scale,
+    moveaxis and the rotation to the upright orientation; the sensor infos follow make_sample.
+    K: the cfg intrinsics at the depth resolution (the reference uses one K for image and depth)."""
+    from boxfusion_amd import _lib
+    pose = np.asarray(pose, np.float32)
+    cur = get_orientation(pose)
+    rgb, dep = _lib.ingest_rgbd(bgr, depth_u16, depth_scale, ROT_K[cur], src_bgr=src_bgr)
+    Hd, Wd = depth_u16.shape[-2:]
+    K = np.asarray(K, np.float32)
+    wide = PosedSensorInfo()
+    wide.image = ImageMeasurementInfo(size=(Wd, Hd), K=torch.from_numpy(K)[None])
+    depth_info = DepthMeasurementInfo(size=(Wd, Hd), K=torch.from_numpy(K.copy())[None])
+    wide.depth = depth_info
+    up = PosedSensorInfo()
+    up.image = wide.image.orient(cur, ImageOrientation.UPRIGHT)
+    up.depth = wide.depth.orient(cur, ImageOrientation.UPRIGHT)
+    up.RT = torch.eye(4)[None]
+    up.T_gravity = torch.from_numpy(camera_to_gravity(pose, cur))[None]
+    gt = PosedSensorInfo()
+    gt.RT = torch.from_numpy(pose)[None]
+    gt.depth = depth_info
+    si = SensorArrayInfo()
+    si.wide = up
+    si.gt = gt
+    return {"wide": {"image": rgb, "depth": dep},
+            "meta": dict(video_id=video_id, timestamp=index), "sensor_info": si}
+
+
+class DecodedFrameStream:
+    """a ScanNet / CA-1M style frame directory as demo.py's dataset: colour JPEG / PNG and 16-bit
+    depth PNG paths plus camera -> world poses; files are decoded on the host (PIL: the image
+    decoder is not part of the GPU path, and cv2 is absent here) and everything after decode runs
+    in bf_ingest_rgbd on `device`."""
+
+    def __init__(self, color_paths, depth_paths, poses, K, depth_scale, device="cuda", video_id=0):
+        if not (len(color_paths) == len(depth_paths) == len(poses)):
+            raise ValueError("one colour image, depth map and pose per frame")
+        self.color, self.depth, self.poses = list(color_paths), list(depth_paths), list(poses)
+        self.K, self.scale, self.dev, self.video_id = np.asarray(K, np.float32), float(depth_scale), device, video_id
+
+    def __len__(self):
+        return len(self.color)
+
+    def __iter__(self):
+        from PIL import Image
+        for i, (cp, dp) in enumerate(zip(self.color, self.depth)):
+            rgb = np.asarray(Image.open(cp).convert("RGB"))
+            dep = np.asarray(Image.open(dp)).astype(np.uint16)
+            rgb_t = torch.from_numpy(np.ascontiguousarray(rgb)).to(self.dev, non_blocking=True)
+            dep_t = torch.from_numpy(dep.view(np.int16)).to(self.dev, non_blocking=True)
+            yield make_sample_decoded(rgb_t, dep_t, self.scale, self.K, self.poses[i], video_id=self.video_id,
+                                      index=i, src_bgr=False)
 
 class SyntheticDataset:
     """the seeded synthetic RGB-D stream (boxfusion_amd.synthetic) as demo.py's dataset:

@@ -70,3 +70,43 @@ class VisionTransformer(nn.Module):
 
 def vit_h14(**kw):
     return VisionTransformer(224, 14, 1280, 32, 16, 1024, **kw)
+
+
+class TextTransformer(nn.Module):
+    """open_clip TextTransformer ("ViT-H-14" text tower: context 77, vocab 49408, width 1024,
+    16 heads, 24 layers, output 1024), the encode_text of precompute_class_features.py:31-37's
+    commented open_clip path.  Parameter names follow open_clip's CLIP (`token_embedding`,
+    `positional_embedding`, `transformer.resblocks.{i}`, `ln_final`, `text_projection`) so a
+    checkpoint's text entries load unchanged.  fp32 definition; `text_engine.CLIPTextEngine` runs
+    the same weights on the MFMA kernels.  Parity with open_clip is UNPINNED (module and weights
+    absent offline): the architecture is restated from open_clip's published model config."""
+
+    def __init__(self, context_length=77, vocab_size=49408, width=1024, heads=16, layers=24,
+                 output_dim=1024):
+        super().__init__()
+        self.context_length, self.vocab_size = context_length, vocab_size
+        self.width, self.heads, self.layers, self.output_dim = width, heads, layers, output_dim
+        self.token_embedding = nn.Embedding(vocab_size, width)
+        self.positional_embedding = nn.Parameter(0.01 * torch.randn(context_length, width))
+        self.transformer = Transformer(width, layers, heads)
+        self.ln_final = nn.LayerNorm(width)
+        self.text_projection = nn.Parameter(width ** -0.5 * torch.randn(width, output_dim))
+        nn.init.normal_(self.token_embedding.weight, std=0.02)
+        # causal mask (open_clip build_causal_mask: -inf above the diagonal)
+        self.register_buffer("attn_mask", torch.full((context_length, context_length), float("-inf")).triu_(1),
+                             persistent=False)
+
+    def forward(self, text):
+        """text: token ids [N, context_length] (int) -> [N, output_dim] (not normalised)"""
+        x = self.token_embedding(text) + self.positional_embedding
+        for blk in self.transformer.resblocks:
+            y = blk.ln_1(x)
+            x = x + blk.attn(y, y, y, need_weights=False, attn_mask=self.attn_mask)[0]
+            x = x + blk.mlp(blk.ln_2(x))
+        x = self.ln_final(x)
+        x = x[torch.arange(x.shape[0], device=x.device), text.argmax(dim=-1)]
+        return x @ self.text_projection
+
+
+def text_h14(**kw):
+    return TextTransformer(77, 49408, 1024, 16, 24, 1024, **kw)

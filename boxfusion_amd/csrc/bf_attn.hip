@@ -20,6 +20,7 @@
 #include "bf_common.h"
 
 #include <type_traits>
+#include <climits>
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -465,14 +466,16 @@ __global__ void __launch_bounds__(NW * 64) k_attn_s(const u16* __restrict__ Q, c
 template <int D, int DB, bool ONES>
 __device__ __forceinline__ void attn2_softmax(f32x16 (&s)[2], bool sub1, bool mask, int k0, int sk,
                                               int fh, float c, float& m_run, float& l_run,
-                                              f32x16 (&o)[DB], bf16x8 (&pf)[2][2]) {
+                                              f32x16 (&o)[DB], bf16x8 (&pf)[2][2], int kmax = INT_MAX) {
+    // keys past sk (the tail tile) and, for causal attention, keys after the lane's query (kmax)
     if (mask) {
+        const int klim = min(sk - 1, kmax);
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
                 const int key = k0 + sub * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh;
-                s[sub][e] = (key < sk) ? s[sub][e] : -INFINITY;
+                s[sub][e] = (key <= klim) ? s[sub][e] : -INFINITY;
             }
     }
     float mt = s[0][0];
@@ -513,7 +516,9 @@ __device__ __forceinline__ void attn2_softmax(f32x16 (&s)[2], bool sub1, bool ma
 }
 
 // F8O: the output is fp8 e4m3 (OCP), saturate_448(o * oqs) -- the fp8 CLIP path's out_proj input
-template <int D, int NW, bool F8O = false>
+// CAUSAL: query q sees keys 0..q only (the CLIP text tower's attn_mask); every tile runs the masked
+// body, tiles past the workgroup's last query are skipped (sq == sk)
+template <int D, int NW, bool F8O = false, bool CAUSAL = false>
 __global__ void __launch_bounds__(NW * 64) k_attn2(const u16* __restrict__ Q, const u16* __restrict__ K,
                                                       const u16* __restrict__ V, u16* __restrict__ O,
                                                       int sq, int sk, int q_rs, int k_rs, int v_rs,
@@ -614,7 +619,8 @@ __global__ void __launch_bounds__(NW * 64) k_attn2(const u16* __restrict__ Q, co
             }
         }
         bf16x8 pf[2][2];
-        attn2_softmax<D, DB, ONES>(s, sub1, MASK, k0, sk, fh, scale_log2, m_run, l_run, o, pf);
+        attn2_softmax<D, DB, ONES>(s, sub1, MASK, k0, sk, fh, scale_log2, m_run, l_run, o, pf,
+                                   CAUSAL ? q : INT_MAX);
 #pragma unroll
         for (int db = 0; db < DB; ++db) {
             const int d0 = db * 32 + g16 * 16 + 4 * p4;
@@ -638,14 +644,26 @@ __global__ void __launch_bounds__(NW * 64) k_attn2(const u16* __restrict__ Q, co
     stage_load(0);
     stage_store(0);
     __syncthreads();
-    for (int tile = 0; tile < nfull; ++tile) {
-        const bool more = tile + 1 < ntiles;
-        if (more) stage_load((tile + 1) * AT_KT);          // in flight during this tile
-        tile_body(tile, std::false_type{});
-        if (more) stage_store((tile + 1) & 1);
-        __syncthreads();
+    if constexpr (CAUSAL) {
+        // keys beyond the workgroup's last query are masked for every row: stop there
+        const int nt = min(ntiles, (min(blk.qb * (NW * 32) + NW * 32, sq) - 1) / AT_KT + 1);
+        for (int tile = 0; tile < nt; ++tile) {
+            const bool more = tile + 1 < nt;
+            if (more) stage_load((tile + 1) * AT_KT);
+            tile_body(tile, std::true_type{});
+            if (more) stage_store((tile + 1) & 1);
+            __syncthreads();
+        }
+    } else {
+        for (int tile = 0; tile < nfull; ++tile) {
+            const bool more = tile + 1 < ntiles;
+            if (more) stage_load((tile + 1) * AT_KT);          // in flight during this tile
+            tile_body(tile, std::false_type{});
+            if (more) stage_store((tile + 1) & 1);
+            __syncthreads();
+        }
+        if (nfull < ntiles) tile_body(nfull, std::true_type{});
     }
-    if (nfull < ntiles) tile_body(nfull, std::true_type{});
 
     // row sum: the ones row D of O^T (lane half 0, register 8 of block D / 32) or the f32 sum
     float l;
@@ -1048,5 +1066,26 @@ BF_API int bf_attention_fp8out(const void* q, const void* k, const void* v, void
     }
 #undef LAUNCH_8D
 #undef LAUNCH_8
+    return bf_check_launch();
+}
+
+// causal self-attention (sq == sk == s): the CLIP text tower (open_clip TextTransformer's attn_mask,
+// precompute_class_features.py:37 encode_text); same k_attn2 body, keys after the query masked
+BF_API int bf_attention_causal(const void* q, const void* k, const void* v, void* o, int batch, int heads,
+                               int s, int head_dim, int q_rs, int k_rs, int v_rs, int o_rs, long long q_bs,
+                               long long k_bs, long long v_bs, long long o_bs, float scale, void* stream) {
+    if (!q || !k || !v || !o || batch <= 0 || heads <= 0 || s <= 0) return BF_ERR_ARG;
+    if ((q_rs | k_rs | v_rs) % 8 != 0 || o_rs % 4 != 0) return BF_ERR_UNSUPPORTED;
+    const float sl2 = scale * 1.4426950408889634f;
+#define LAUNCH_C(DD)                                                                              \
+    hipLaunchKernelGGL((k_attn2<DD, 4, false, true>), dim3((s + 127) / 128, heads, batch), dim3(256), \
+                       0, bf_stream(stream), (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, s, s, \
+                       q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs, o_bs, sl2, (const int32_t*)nullptr, 1.f)
+    switch (head_dim) {
+        case 64: LAUNCH_C(64); break;
+        case 80: LAUNCH_C(80); break;
+        default: return BF_ERR_UNSUPPORTED;
+    }
+#undef LAUNCH_C
     return bf_check_launch();
 }

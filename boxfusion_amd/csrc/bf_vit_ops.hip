@@ -8,6 +8,7 @@
 //                     14x14 patch im2col (K padded with zeros to a multiple of 64)
 // One wave per LayerNorm row; im2col writes 16-B bf16x8 chunks (coalesced).
 #include "bf_common.h"
+#include "bf_cv2.h"
 
 typedef unsigned short u16;
 
@@ -262,10 +263,11 @@ BF_API int bf_im2col_f32(const float* x, int B, int H, int W, int pad, int patch
 }
 
 // ------------------------------------------------------------------------------------------
-// CLIP crops: for crop n with integer box (x1,y1,x2,y2) of frame img_idx[n] (u8 HWC):
-//   crop = img[y1:y2, x1:x2] (empty -> zeros), bilinear resize to S x S with half-pixel centres
-//   (cv2.INTER_LINEAR mapping), /255, (x - mean_c)/std_c, then p x p patch im2col with K padded
-//   to ldo (zeros).  Output rows: n*(S/p)^2 + patch.
+// CLIP crops: for crop n with integer box (x1,y1,x2,y2) of frame img_idx[n] (u8 HWC RGB):
+//   crop = img[y1:y2, x1:x2] (empty -> zeros, tools/utils.py:385), cv2.resize(crop, (S, S)) with
+//   OpenCV's u8 INTER_LINEAR fixed-point arithmetic (bf_cv2.h; a u8 image, as the reference's),
+//   /255, (x - mean_c)/std_c, then p x p patch im2col with K padded to ldo (zeros).
+//   Output rows: n*(S/p)^2 + patch.
 // ------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_crop_im2col(const uint8_t* __restrict__ img, int H, int W,
                                                      const int32_t* __restrict__ boxes,
@@ -284,17 +286,13 @@ __global__ void __launch_bounds__(256) k_crop_im2col(const uint8_t* __restrict__
     const int pp = (int)(prow % (np * np));
     const int py = pp / np, px = pp % np;
     const int K = 3 * p * p;
-    const int x1 = boxes[4 * n], y1 = boxes[4 * n + 1], x2 = boxes[4 * n + 2], y2 = boxes[4 * n + 3];
+    // numpy slice semantics for the (non-negative) box: clamp into the frame
+    const int x1 = min(max(boxes[4 * n], 0), W), y1 = min(max(boxes[4 * n + 1], 0), H);
+    const int x2 = min(max(boxes[4 * n + 2], x1), W), y2 = min(max(boxes[4 * n + 3], y1), H);
     const int cw = x2 - x1, chh = y2 - y1;
     const bool nonempty = cw > 0 && chh > 0;
-    const uint8_t* im = img + (size_t)max(img_idx ? img_idx[n] : 0, 0) * H * W * 3;
-    // every pixel address is clamped into the frame, so the loads are safe even where the value
-    // is discarded (empty crop, K padding); the sampling itself never leaves the crop
-    auto px_at = [&](int yy, int xx, int c) {
-        const int gy = min(max(y1 + yy, 0), H - 1), gx = min(max(x1 + xx, 0), W - 1);
-        return (float)im[((size_t)gy * W + gx) * 3 + c];
-    };
-    const float fcw = (float)max(cw, 1) / (float)S, fch = (float)max(chh, 1) / (float)S;
+    const uint8_t* crop = img + (size_t)max(img_idx ? img_idx[n] : 0, 0) * H * W * 3 + ((size_t)y1 * W + x1) * 3;
+    const double sxs = nonempty ? cv2_scale(cw, S) : 1.0, sys = nonempty ? cv2_scale(chh, S) : 1.0;
     u16 v[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -302,18 +300,10 @@ __global__ void __launch_bounds__(256) k_crop_im2col(const uint8_t* __restrict__
         const int kk = min(k, K - 1);
         const int c = kk / (p * p), rem = kk % (p * p);
         const int oy = py * p + rem / p, ox = px * p + rem % p;
-        float sy = fmaxf(((float)oy + 0.5f) * fch - 0.5f, 0.f);
-        float sx = fmaxf(((float)ox + 0.5f) * fcw - 0.5f, 0.f);
-        const int iy0 = min((int)sy, max(chh, 1) - 1), ix0 = min((int)sx, max(cw, 1) - 1);
-        const int iy1 = min(iy0 + 1, max(chh, 1) - 1), ix1 = min(ix0 + 1, max(cw, 1) - 1);
-        const float fy = sy - (float)iy0, fx = sx - (float)ix0;
-        const float top = px_at(iy0, ix0, c) * (1.f - fx) + px_at(iy0, ix1, c) * fx;
-        const float bot = px_at(iy1, ix0, c) * (1.f - fx) + px_at(iy1, ix1, c) * fx;
-        // the resized crop is a uint8 image in the reference (cv2.resize of a u8 crop)
-        const float val = nonempty ? rintf(top * (1.f - fy) + bot * fy) : 0.f;
+        const int val = nonempty ? cv2_resize_u8_at(crop, W * 3, chh, cw, 3, c, S, S, oy, ox, c, sxs, sys) : 0;
         const float mean = c == 0 ? m0 : (c == 1 ? m1 : m2);
         const float sd = c == 0 ? s0 : (c == 1 ? s1 : s2);
-        const float f = (val / 255.f - mean) / sd;
+        const float f = ((float)val / 255.f - mean) / sd;
         v[i] = vf2bf(k < K ? f : 0.f);
     }
     W128 w = {(uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2] | ((uint32_t)v[3] << 16),

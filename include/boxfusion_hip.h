@@ -459,12 +459,52 @@ int bf_im2col_f32(const float* x, int B, int H, int W, int pad, int patch, void*
                   void* stream);
 
 /* CLIP crop path (tools/utils.py:405-476 crop_image/segment_image + retriev's 224x224 resize):
- * boxes i32[N,4] integer xyxy on frame img_idx[N] of img u8[*,H,W,3] -> bilinear SxS -> /255 ->
+ * boxes i32[N,4] integer xyxy on frame img_idx[N] of img u8[*,H,W,3] -> cv2.resize(crop, (S, S))
+ * (OpenCV u8 INTER_LINEAR fixed point, bit-exact to oracle/bf_oracle.c or_cv2_resize_u8) -> /255 ->
  * (x-mean)/std -> p x p patch im2col bf16 [N*(S/p)^2, ldo] (K = 3p^2 zero-padded to ldo).
  * mean3/std3 are HOST arrays. */
 int bf_crop_resize_im2col(const uint8_t* img, int H, int W, const int32_t* boxes,
                           const int32_t* img_idx, int N, int size, int patch, const float* mean3,
                           const float* std3, void* out, int ldo, void* stream);
+
+/* ---- CLIP text tower (reference: boxfusion/precompute_class_features.py:31-43, the open_clip
+ * "ViT-H-14" encode_text of its commented path; tools/utils.py:399 renormalises the result) ---- */
+
+/* causal self-attention (open_clip TextTransformer attn_mask: query i sees keys 0..i), sq == sk == s;
+ * operands as bf_attention_bf16; head_dim 64 or 80 */
+int bf_attention_causal(const void* q, const void* k, const void* v, void* o, int batch, int heads,
+                        int s, int head_dim, int q_rs, int k_rs, int v_rs, int o_rs, long long q_bs,
+                        long long k_bs, long long v_bs, long long o_bs, float scale, void* stream);
+
+/* token_embedding(ids) + positional_embedding: ids i32 [n_tok] (token t at position t % S),
+ * table f32 [vocab, W], pos f32 [S, W] -> out f32 [n_tok, W]; W % 4 == 0.  An id outside
+ * [0, vocab) gives a zero embedding row and BF_DEV_INDEX_RANGE in *status (when non-NULL). */
+int bf_token_embed(const int32_t* ids, int n_tok, const float* table, int vocab, const float* pos,
+                   int S, int W, float* out, int32_t* status, void* stream);
+
+/* text_global_pool 'argmax': out[n] = x[n*S + argmax(ids[n, :S])] (first maximum, torch.argmax);
+ * x f32 [N*S, W] -> out f32 [N, W] */
+int bf_text_pool(const int32_t* ids, int N, int S, const float* x, int W, float* out, void* stream);
+
+/* out[r] = x[r] / ||x[r]||_2 (precompute_class_features.py:43); in place allowed */
+int bf_l2_normalize_rows(const float* x, int rows, int W, float* out, void* stream);
+
+/* ---- GPU frame ingestion (reference: capture_stream.py:194-311 ScanNet / :402-529 CA-1M
+ * __iter__ after image decode) ---- */
+
+/* decoded frames -> the sample tensors of the reference's streams, one launch for F frames:
+ * bgr u8 [F,Hc,Wc,3] (cv2.imread order; src_bgr = 0: already RGB) -> cvtColor RGB -> cv2.resize to (Wd, Hd) (u8 INTER_LINEAR,
+ * OpenCV fixed point) -> CHW -> torch.rot90(k=rot_k, dims (-2,-1)) -> rgb_out u8 [F,3,Ho,Wo];
+ * depth u16 [F,Hd,Wd] (PNG, may be NULL) -> f32 / depth_scale -> rot90 -> depth_out f32 [F,Ho,Wo];
+ * (Ho, Wo) = (Hd, Wd) for even rot_k, (Wd, Hd) for odd. */
+int bf_ingest_rgbd(const uint8_t* bgr, int Hc, int Wc, const uint16_t* depth, int Hd, int Wd, int F,
+                   float depth_scale, int rot_k, int src_bgr, uint8_t* rgb_out, float* depth_out,
+                   void* stream);
+
+/* cv2.resize(src, (Wd, Hd)) for u8 HWC images with cn <= 4 channels, F images:
+ * src [F,Hs,Ws,cn] -> dst [F,Hd,Wd,cn] (INTER_LINEAR, OpenCV's fixed-point arithmetic) */
+int bf_cv2_resize_u8(const uint8_t* src, int Hs, int Ws, int cn, int Hd, int Wd, int F, uint8_t* dst,
+                     void* stream);
 
 #ifdef __cplusplus
 }

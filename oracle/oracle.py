@@ -242,3 +242,25 @@ def backproject(depth, K, RT, max_depth=10.0):
     if max_depth is not None and max_depth > 0:
         valid &= d < max_depth
     return world.astype(np.float32), valid
+
+
+def cv2_resize_u8(src, Wd, Hd):
+    """cv2.resize(src, (Wd, Hd)) for a u8 [H, W] or [H, W, cn] image (INTER_LINEAR), restated"""
+    a = np.ascontiguousarray(src, dtype=np.uint8)
+    cn = 1 if a.ndim == 2 else a.shape[2]
+    out = np.empty((Hd, Wd) + (() if a.ndim == 2 else (cn,)), dtype=np.uint8)
+    lib().or_cv2_resize_u8(_p(a), ctypes.c_int(a.shape[0]), ctypes.c_int(a.shape[1]), ctypes.c_int(cn),
+                           _p(out), ctypes.c_int(Hd), ctypes.c_int(Wd))
+    return out
+
+
+def ingest_rgbd(bgr, depth_u16, depth_scale, rot_k):
+    """capture_stream.py:194-311: BGR -> RGB, cv2.resize to the depth size, CHW, rot90; depth
+    u16 -> f32 / scale, rot90 (numpy restatement over or_cv2_resize_u8)"""
+    Hd, Wd = depth_u16.shape
+    rgb = np.ascontiguousarray(bgr[..., ::-1])
+    rgb = cv2_resize_u8(rgb, Wd, Hd)
+    chw = np.moveaxis(rgb, -1, 0)
+    d = depth_u16.astype(np.float32) / np.float32(depth_scale)
+    return (np.ascontiguousarray(np.rot90(chw, rot_k, axes=(-2, -1))),
+            np.ascontiguousarray(np.rot90(d, rot_k, axes=(-2, -1))))
