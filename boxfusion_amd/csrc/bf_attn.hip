@@ -21,6 +21,7 @@
 
 #include <type_traits>
 #include <climits>
+#include <algorithm>
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -518,7 +519,12 @@ __device__ __forceinline__ void attn2_softmax(f32x16 (&s)[2], bool sub1, bool ma
 // F8O: the output is fp8 e4m3 (OCP), saturate_448(o * oqs) -- the fp8 CLIP path's out_proj input
 // CAUSAL: query q sees keys 0..q only (the CLIP text tower's attn_mask); every tile runs the masked
 // body, tiles past the workgroup's last query are skipped (sq == sk)
-template <int D, int NW, bool F8O = false, bool CAUSAL = false>
+// XQ (short heads with sq = 32 NW + 1, CLIP's 257 tokens): NW = 8 waves take queries 0..255 on
+// MFMA (two waves per SIMD instead of a ninth wave holding one real query on one SIMD), and the
+// last query runs beside them in f32 VALU while each K/V tile is in LDS: wave w scores keys
+// 8w..8w+7 of the tile (lane group of 8 = one key, D/8 dims per lane), keeps its own online
+// softmax (m, l, o[D]); the eight partial states merge through LDS after the loop.
+template <int D, int NW, bool F8O = false, bool CAUSAL = false, bool XQ = false>
 __global__ void __launch_bounds__(NW * 64) k_attn2(const u16* __restrict__ Q, const u16* __restrict__ K,
                                                       const u16* __restrict__ V, u16* __restrict__ O,
                                                       int sq, int sk, int q_rs, int k_rs, int v_rs,
@@ -535,8 +541,9 @@ __global__ void __launch_bounds__(NW * 64) k_attn2(const u16* __restrict__ Q, co
     constexpr int CPR = D / 8;
     constexpr int CH = AT_KT * CPR;
     constexpr int NT = NW * 64;
-    __shared__ __attribute__((aligned(16))) u16 sK[2 * KTILE];
-    __shared__ __attribute__((aligned(16))) u16 sV[2 * VTILE];
+    constexpr int NBUF = 2;
+    __shared__ __attribute__((aligned(16))) u16 sK[NBUF * KTILE];
+    __shared__ __attribute__((aligned(16))) u16 sV[NBUF * VTILE];
 
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const AttnBlk blk = attn_block(1);
@@ -553,7 +560,7 @@ __global__ void __launch_bounds__(NW * 64) k_attn2(const u16* __restrict__ Q, co
         qf[ks] = *reinterpret_cast<const bf16x8*>(Qb + (size_t)min(q, sq - 1) * q_rs + 16 * ks + 8 * fh);
     // V padding columns: a ones column at d = D (the row sum), zeros after it
     if (VROW > D)
-        for (int i = t; i < 2 * AT_KT * (VROW - D); i += NT) {
+        for (int i = t; i < NBUF * AT_KT * (VROW - D); i += NT) {
             const int r = i / (VROW - D), c = i % (VROW - D);
             sV[r * VROW + D + c] = (ONES && c == 0) ? (u16)0x3F80 : (u16)0;
         }
@@ -597,17 +604,69 @@ __global__ void __launch_bounds__(NW * 64) k_attn2(const u16* __restrict__ Q, co
     const int ntiles = (sk + AT_KT - 1) / AT_KT;
     const int nfull = sk / AT_KT;
 
-    // one 64-key tile: S^T = K Q^T, softmax, O^T += V^T P^T (MASK: the tail tile)
-    auto tile_body = [&](int tile, auto mask_tag) {
-        constexpr bool MASK = decltype(mask_tag)::value;
-        const int k0 = tile * AT_KT, buf = tile & 1;
-        const u16* kt = sK + buf * KTILE;
-        const u16* vt = sV + buf * VTILE;
-        const bool sub1 = !MASK || (k0 + 32 < sk);
-        f32x16 s[2];
+    // XQ: the last query's state (key group kg = lane / 8, dims dg * DPL .. + DPL)
+    constexpr int DPL = D / 8;
+    static_assert(!XQ || (D % 16 == 0 && NW == 8), "XQ: 8 waves, D a multiple of 16");
+    const int kg = lane >> 3, dg = lane & 7;
+    float xq[XQ ? DPL : 1], xo[XQ ? DPL : 1];
+    float xm = -INFINITY, xl = 0.f;
+    if constexpr (XQ) {
+        const uint32_t* qr = reinterpret_cast<const uint32_t*>(Qb + (size_t)(sq - 1) * q_rs + dg * DPL);
+#pragma unroll
+        for (int j = 0; j < DPL / 2; ++j) {
+            const uint32_t w2 = qr[j];
+            xq[2 * j] = __uint_as_float(w2 << 16) * scale_log2;
+            xq[2 * j + 1] = __uint_as_float(w2 & 0xFFFF0000u) * scale_log2;
+        }
+#pragma unroll
+        for (int j = 0; j < DPL; ++j) xo[j] = 0.f;
+    }
+    auto extra_query = [&](const u16* kt, const u16* vt, int k0) {
+        const int kk = wave * 8 + kg;
+        const uint32_t* kr = reinterpret_cast<const uint32_t*>(kt + kk * KROW + dg * DPL);
+        float sx = 0.f;
+#pragma unroll
+        for (int j = 0; j < DPL / 2; ++j) {
+            const uint32_t w2 = kr[j];
+            sx = fmaf(__uint_as_float(w2 << 16), xq[2 * j], sx);
+            sx = fmaf(__uint_as_float(w2 & 0xFFFF0000u), xq[2 * j + 1], sx);
+        }
+        sx += __shfl_xor(sx, 1, 64);
+        sx += __shfl_xor(sx, 2, 64);
+        sx += __shfl_xor(sx, 4, 64);
+        if (k0 + kk >= sk) sx = -INFINITY;
+        float mt = fmaxf(sx, __shfl_xor(sx, 8, 64));
+        mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+        mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+        if (mt > xm) {                                   // wave-uniform
+            const float alpha = __builtin_amdgcn_exp2f(xm - mt);
+            xm = mt;
+            xl *= alpha;
+#pragma unroll
+            for (int j = 0; j < DPL; ++j) xo[j] *= alpha;
+        }
+        const float pr = __builtin_amdgcn_exp2f(sx - xm);
+        float ps = pr + __shfl_xor(pr, 8, 64);
+        ps += __shfl_xor(ps, 16, 64);
+        ps += __shfl_xor(ps, 32, 64);
+        xl += ps;
+        const uint32_t* vr = reinterpret_cast<const uint32_t*>(vt + kk * VROW + dg * DPL);
+#pragma unroll
+        for (int j = 0; j < DPL / 2; ++j) {
+            const uint32_t w2 = vr[j];
+            xo[2 * j] = fmaf(pr, __uint_as_float(w2 << 16), xo[2 * j]);
+            xo[2 * j + 1] = fmaf(pr, __uint_as_float(w2 & 0xFFFF0000u), xo[2 * j + 1]);
+        }
+    };
+
+    // one 64-key tile: S^T = K Q^T (qk), then softmax and O^T += V^T P^T (sm_pv; MASK: the tail tile)
+    auto qk = [&](int tile, f32x16 (&s)[2], bool maybe_tail) {
+        const int k0 = tile * AT_KT;
+        const u16* kt = sK + (tile % NBUF) * KTILE;
+        const bool sub1 = !maybe_tail || (k0 + 32 < sk);
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub) {
-            if (MASK && sub == 1 && !sub1) {
+            if (sub == 1 && !sub1) {
 #pragma unroll
                 for (int e = 0; e < 16; ++e) s[1][e] = -INFINITY;
                 continue;
@@ -618,6 +677,13 @@ __global__ void __launch_bounds__(NW * 64) k_attn2(const u16* __restrict__ Q, co
                 s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], ks == 0 ? f32x16{} : s[sub], 0, 0, 0);
             }
         }
+    };
+    auto sm_pv = [&](int tile, f32x16 (&s)[2], auto mask_tag) {
+        constexpr bool MASK = decltype(mask_tag)::value;
+        const int k0 = tile * AT_KT;
+        const u16* kt = sK + (tile % NBUF) * KTILE;
+        const u16* vt = sV + (tile % NBUF) * VTILE;
+        const bool sub1 = !MASK || (k0 + 32 < sk);
         bf16x8 pf[2][2];
         attn2_softmax<D, DB, ONES>(s, sub1, MASK, k0, sk, fh, scale_log2, m_run, l_run, o, pf,
                                    CAUSAL ? q : INT_MAX);
@@ -639,6 +705,12 @@ __global__ void __launch_bounds__(NW * 64) k_attn2(const u16* __restrict__ Q, co
                                                                    pf[sub][ss], o[db], 0, 0, 0);
                 }
         }
+        if constexpr (XQ) extra_query(kt, vt, k0);
+    };
+    auto tile_body = [&](int tile, auto mask_tag) {
+        f32x16 s[2];
+        qk(tile, s, decltype(mask_tag)::value);
+        sm_pv(tile, s, mask_tag);
     };
 
     stage_load(0);
@@ -663,6 +735,51 @@ __global__ void __launch_bounds__(NW * 64) k_attn2(const u16* __restrict__ Q, co
             __syncthreads();
         }
         if (nfull < ntiles) tile_body(nfull, std::true_type{});
+    }
+    if constexpr (XQ) {
+        // merge the eight waves' partial states of the last query through LDS (sK is free now)
+#pragma unroll
+        for (int j = 0; j < DPL; ++j) {
+            xo[j] += __shfl_xor(xo[j], 8, 64);
+            xo[j] += __shfl_xor(xo[j], 16, 64);
+            xo[j] += __shfl_xor(xo[j], 32, 64);
+        }
+        __syncthreads();
+        float* scr = reinterpret_cast<float*>(sK);
+        constexpr int SW = D + 2;
+        if (lane < 8) {
+#pragma unroll
+            for (int j = 0; j < DPL; ++j) scr[wave * SW + 2 + dg * DPL + j] = xo[j];
+        }
+        if (lane == 0) { scr[wave * SW] = xm; scr[wave * SW + 1] = xl; }
+        __syncthreads();
+        if (wave == 0) {
+            float M = scr[0];
+#pragma unroll
+            for (int w = 1; w < NW; ++w) M = fmaxf(M, scr[w * SW]);
+            float Ls = 0.f, wt[NW];
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                wt[w] = __builtin_amdgcn_exp2f(scr[w * SW] - M);
+                Ls = fmaf(scr[w * SW + 1], wt[w], Ls);
+            }
+            const float inv = 1.0f / Ls;
+            const long long xoff = attn_out_offset(o_map, b, sq - 1, sq, o_bs, o_rs);
+            if (xoff >= 0) {
+                for (int d = lane; d < D; d += 64) {
+                    float acc = 0.f;
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) acc = fmaf(scr[w * SW + 2 + d], wt[w], acc);
+                    if constexpr (F8O) {
+                        const float a = fminf(fmaxf(acc * inv * oqs, -448.f), 448.f);
+                        const int pk = __builtin_amdgcn_cvt_pk_fp8_f32(a, a, 0, false);
+                        reinterpret_cast<unsigned char*>(O)[xoff + h * D + d] = (unsigned char)(pk & 0xFF);
+                    } else {
+                        O[xoff + h * D + d] = at_f2bf(acc * inv);
+                    }
+                }
+            }
+        }
     }
 
     // row sum: the ones row D of O^T (lane half 0, register 8 of block D / 32) or the f32 sum
@@ -922,11 +1039,292 @@ static void launch_attn_r(dim3 grid, hipStream_t st, const void* q, const void* 
                        k_bs, v_bs, o_bs, sl2, o_map);
 }
 
+// ------------------------------------------------------------------------------------------
+// k_attn_p: persistent short-head attention (CLIP: S = 257, D = 80) on an LDS-DMA ring.
+// The per-(batch, head) workgroup of k_attn2 (one 9-wave workgroup per CU: 164 VGPRs) runs its
+// Q load and first K/V tile with nothing to compute beside them, and keeps only one 20-KB K/V tile
+// in flight per CU.  Here one workgroup per CU walks (batch, head) pairs p = blockIdx.x + j *
+// gridDim.x as one continuous stream of 64-key steps, and every byte arrives by LDS-DMA
+// (global_load_lds, 1-KiB wave pieces, per-lane source rows) three steps ahead:
+//   * ring of 4 step slots: K image [64 keys][10 chunks] x 16 B, chunk order swizzled per row
+//     (atp_pos: conflict-free ds_read_b128 of the S^T = K Q^T A operand, coalesced DMA rows),
+//     V image row-major [64 keys][96] (192-B rows:
+//     conflict-free ds_read_b64_tr_b16; d = 80 is a ones column, 81..95 zeros, both DMA'd from a
+//     32-B constant) -> 22 pieces per step;
+//   * one Q image [288 queries][10 chunks] x 16 B, swizzled like K (45 pieces): pair i+1's Q is issued during
+//     steps 1..2 of pair i (after every wave has read pair i's Q fragments at step 0) and retired
+//     by the step-0 wait of pair i+1;
+//   * batch B_s (issued at step s) = K/V of step s+3 (+ Q pieces); the wait at step s leaves
+//     B_{s-1} and B_{s-2} in flight (counted vmcnt: loads, stores and LDS-DMA retire in issue
+//     order), then a raw s_barrier (no vmcnt(0));
+//   * the tile body is k_attn2's (deferred-max softmax, ones row for l); a pair's output rows are
+//     stored right after its last step, under the next pair's DMA.
+// Requires 193 <= sk <= 320, sq <= 288 (4 or 5 key steps, queries in one workgroup).
+// ------------------------------------------------------------------------------------------
+__device__ const uint16_t g_attn_vpad[16] = {0x3F80, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+
+// K and Q images are dense 160-B rows (so a DMA piece reads whole rows: coalesced) with the 16-B
+// chunk order rotated by one in rows 16..31 of every 32: the ds_read_b128 lane groups of the
+// fragment reads ({0-3,12-15,20-27}, {4-11,16-19,28-31}) then hit 16 distinct 4-bank groups
+__device__ __forceinline__ int atp_pos(int row, int c) { const int p = c + ((row >> 4) & 1); return p >= 10 ? p - 10 : p; }
+__device__ __forceinline__ int atp_chunk(int row, int pos) { const int c = pos - ((row >> 4) & 1); return c < 0 ? c + 10 : c; }
+
+#define ATP_NQ 288
+#define ATP_QPIECES 45                    // 10 chunks x 288 queries x 16 B / 1 KiB
+#define ATP_KPIECES 10
+#define ATP_VPIECES 12
+#define ATP_KV (ATP_KPIECES + ATP_VPIECES)
+#define ATP_SLOT ((ATP_KPIECES + ATP_VPIECES) * 1024)
+#define ATP_LDS (ATP_QPIECES * 1024 + 4 * ATP_SLOT)
+
+template <int NW>
+__global__ void __launch_bounds__(NW * 64) k_attn_p(const u16* __restrict__ Q, const u16* __restrict__ K,
+                                                     const u16* __restrict__ V, u16* __restrict__ O,
+                                                     int heads, int npairs, int sq, int sk, int q_rs,
+                                                     int k_rs, int v_rs, int o_rs, long long q_bs,
+                                                     long long k_bs, long long v_bs, long long o_bs,
+                                                     float scale_log2, const int32_t* __restrict__ o_map) {
+    constexpr int D = 80, KS = 5, DB = 3, VROWB = 192;
+    static_assert(NW * 32 == ATP_NQ, "one workgroup holds every query");
+    extern __shared__ __attribute__((aligned(16))) unsigned char at_smem[];
+    unsigned char* sQ = at_smem;
+    unsigned char* sR = at_smem + ATP_QPIECES * 1024;
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int fr = lane & 31, fh = lane >> 5;
+    const int g16 = (lane >> 4) & 1, q4 = (lane & 15) >> 2, p4 = lane & 3;
+    // pair j of this workgroup = wg + j * G; wg is XCD-major (blockIdx % 8 = XCD) so that the
+    // workgroups of one XCD walk adjacent heads together (their 160-B rows share cache lines)
+    const int G = gridDim.x;
+    const int wg = (G % 8 == 0) ? ((int)blockIdx.x % 8) * (G / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
+    const int nmine = wg < npairs ? (npairs - wg + G - 1) / G : 0;
+    const int NTL = (sk + AT_KT - 1) / AT_KT;
+    const int total = nmine * NTL;
+    const int q = wave * 32 + fr;
+
+    const int n_kv_mine = wave < ATP_KV ? (ATP_KV - wave + NW - 1) / NW : 0;
+    // element offsets of a pair's rows fit in 32 bits (checked on the host): fewer live SGPRs
+    auto pair_off = [&](int j, long long bs) {
+        const int pp = wg + j * G;
+        return (pp / heads) * (int)bs + (pp % heads) * D;
+    };
+    auto issue_kv = [&](int koff, int voff, int k0, int slot) {
+        unsigned char* base = sR + slot * ATP_SLOT;
+        int ln = lane;                                // opaque: keeps the address math in the step
+        asm volatile("" : "+v"(ln));                  // (hoisted, it would pin 20+ VGPRs)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            if (j < n_kv_mine) {
+                const int g = wave + NW * j;          // this wave's pieces: g = wave + 9 j
+                const void* src;
+                if (g < ATP_KPIECES) {                // K rows, swizzled chunk order (atp_pos)
+                    const int sl = g * 64 + ln, r = sl / 10;
+                    src = K + koff + min(k0 + r, sk - 1) * k_rs + atp_chunk(r, sl - r * 10) * 8;
+                } else {                              // V rows: 12 chunks per key, 10..11 padding
+                    const int sl = (g - ATP_KPIECES) * 64 + ln, r = sl / 12, ch = sl - r * 12;
+                    src = ch < 10 ? (const void*)(V + voff + min(k0 + r, sk - 1) * v_rs + ch * 8)
+                                  : (const void*)(g_attn_vpad + (ch - 10) * 8);
+                }
+                __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(base + g * 1024), 16, 0, 0);
+            }
+        }
+        return n_kv_mine;
+    };
+    auto issue_q = [&](int qoff, int ql, int qh) {   // Q pieces [ql, qh): pc = wave mod 9
+        int cnt = 0;
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        for (int pc = ql + ((wave - ql % NW + NW) % NW); pc < qh; pc += NW) {
+            const int sl = pc * 64 + ln, qq = sl / 10;
+            const void* src = Q + qoff + min(qq, sq - 1) * q_rs + atp_chunk(qq, sl - qq * 10) * 8;
+            __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(sQ + pc * 1024), 16, 0, 0);
+            ++cnt;
+        }
+        return cnt;
+    };
+
+    // K/V issue cursor (pair j3, step t3), three steps ahead of the compute cursor (i, tt)
+    int j3 = 0, t3 = 0;
+    int Kb3 = pair_off(0, k_bs), Vb3 = pair_off(0, v_bs);
+    auto advance3 = [&]() {
+        if (++t3 == NTL) {
+            t3 = 0;
+            ++j3;
+            if (j3 < nmine) { Kb3 = pair_off(j3, k_bs); Vb3 = pair_off(j3, v_bs); }
+        }
+    };
+    int c_m2 = 0, c_m1 = 0;
+    if (total > 0) {
+        // B_-3 = Q of pair 0 + K/V of step 0; B_-2, B_-1 = K/V of steps 1, 2
+        int c0 = issue_q(pair_off(0, q_bs), 0, ATP_QPIECES) + issue_kv(Kb3, Vb3, 0, 0);
+        advance3();
+        c_m2 = total > 1 ? issue_kv(Kb3, Vb3, t3 * AT_KT, 1) : 0;
+        if (total > 1) advance3();
+        c_m1 = total > 2 ? issue_kv(Kb3, Vb3, t3 * AT_KT, 2) : 0;
+        if (total > 2) advance3();
+        (void)c0;
+    }
+    int Qn = nmine > 1 ? pair_off(1, q_bs) : 0;     // the next pair's Q rows
+
+    f32x16 o[DB];
+    float m_run = -INFINITY, l_run = 0.f;
+    bf16x8 qf[KS];
+    int i = 0, tt = 0;
+    for (int s = 0; s < total; ++s) {
+        attn_wait_vm(c_m2 + c_m1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        int c_now = 0;
+        if (s + 3 < total) {
+            c_now += issue_kv(Kb3, Vb3, t3 * AT_KT, (s + 3) & 3);
+            advance3();
+        }
+        if (i + 1 < nmine) {
+            if (NTL == 5 && tt == 1) c_now += issue_q(Qn, 0, 23);
+            else if (NTL == 5 && tt == 2) c_now += issue_q(Qn, 23, ATP_QPIECES);
+            else if (NTL == 4 && tt == 1) c_now += issue_q(Qn, 0, ATP_QPIECES);
+        }
+        c_m2 = c_m1;
+        c_m1 = c_now;
+        if (tt == 0) {
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+                qf[ks] = *reinterpret_cast<const bf16x8*>(sQ + (q * 10 + atp_pos(q, 2 * ks + fh)) * 16);
+#pragma unroll
+            for (int db = 0; db < DB; ++db)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) o[db][e] = 0.f;
+            m_run = -INFINITY;
+            l_run = 0.f;
+        }
+        const unsigned char* kt = sR + (s & 3) * ATP_SLOT;
+        const unsigned char* vt = kt + ATP_KPIECES * 1024;
+        const int k0 = tt * AT_KT;
+        const bool mask = k0 + AT_KT > sk;
+        const bool sub1 = k0 + 32 < sk;
+        f32x16 sc[2];
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+            if (sub == 1 && !sub1) {
+#pragma unroll
+                for (int e = 0; e < 16; ++e) sc[1][e] = -INFINITY;
+                continue;
+            }
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const int kr = sub * 32 + fr;
+                const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kt + (kr * 10 + atp_pos(kr, 2 * ks + fh)) * 16);
+                sc[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], ks == 0 ? f32x16{} : sc[sub], 0, 0, 0);
+            }
+        }
+        bf16x8 pf[2][2];
+        attn2_softmax<D, DB, true>(sc, sub1, mask, k0, sk, fh, scale_log2, m_run, l_run, o, pf);
+        typedef unsigned long long u64;
+        const unsigned vbase = (unsigned)(size_t)(__attribute__((address_space(3))) const unsigned char*)vt;
+#pragma unroll
+        for (int db = 0; db < DB; ++db) {
+            const int d0 = db * 32 + g16 * 16 + 4 * p4;
+            u64 lo[2][2], hi[2][2];
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+                    const int kb = 32 * sub + 16 * ss + 4 * fh + q4;
+                    const unsigned a0 = vbase + (unsigned)(kb * VROWB + d0 * 2);
+                    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo[sub][ss]) : "v"(a0));
+                    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi[sub][ss]) : "v"(a0), "i"(8 * VROWB));
+                }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+                    if (sub == 1 && !sub1) continue;
+                    asm volatile("" : "+v"(lo[sub][ss]), "+v"(hi[sub][ss]));
+                    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+                    const u64x2 lh = {lo[sub][ss], hi[sub][ss]};
+                    o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, lh), pf[sub][ss],
+                                                                   o[db], 0, 0, 0);
+                }
+        }
+        if (tt == NTL - 1) {
+            // row sum from the ones row d = 80 of O^T: block 2, row 16 -> register 8 of lane half 0
+            const float mine_l = o[DB - 1][8];
+            const float other = __shfl_xor(mine_l, 32, 64);
+            const float l = fh == 0 ? mine_l : other;
+            const int p = wg + i * G;
+            const int b = p / heads, h = p % heads;
+            const long long o_off = attn_out_offset(o_map, b, q, sq, o_bs, o_rs);
+            if (q < sq && o_off >= 0) {
+                const float inv = 1.0f / l;
+                u16* orow = O + o_off + h * D;
+#pragma unroll
+                for (int db = 0; db < DB; ++db)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const int d0 = db * 32 + 8 * g + 4 * fh;
+                        if (db * 32 + 8 * g >= D) continue;
+                        V64 w;
+                        w.x = (uint32_t)at_f2bf(o[db][4 * g + 0] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 1] * inv) << 16);
+                        w.y = (uint32_t)at_f2bf(o[db][4 * g + 2] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 3] * inv) << 16);
+                        *reinterpret_cast<V64*>(orow + d0) = w;
+                    }
+            }
+        }
+        if (++tt == NTL) {
+            tt = 0;
+            ++i;
+            if (i + 1 < nmine) Qn = pair_off(i + 1, q_bs);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outstanding at exit
+}
+
+static int attn_num_cus() {
+    static int n = [] {
+        int dev = 0, c = 0;
+        hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+        return c;
+    }();
+    return n;
+}
+
+static int launch_attn_p(hipStream_t st, const void* q, const void* k, const void* v, void* o, int batch,
+                         int heads, int sq, int sk, int q_rs, int k_rs, int v_rs, int o_rs, long long q_bs,
+                         long long k_bs, long long v_bs, long long o_bs, float sl2, const int32_t* o_map) {
+    static bool attr = false;
+    if (!attr) {
+        hipFuncSetAttribute((const void*)k_attn_p<9>, hipFuncAttributeMaxDynamicSharedMemorySize, ATP_LDS);
+        attr = true;
+    }
+    const int npairs = batch * heads;
+    const long long span = (long long)(batch - 1) * std::max(std::max(q_bs, k_bs), v_bs) + (long long)heads * 80 +
+                           (long long)ATP_NQ * std::max(std::max(q_rs, k_rs), v_rs);
+    if (span >= (1ll << 31)) return BF_ERR_UNSUPPORTED;      // 32-bit element offsets in the kernel
+    const int grid = npairs < attn_num_cus() ? npairs : attn_num_cus();
+    hipLaunchKernelGGL((k_attn_p<9>), dim3(grid), dim3(9 * 64), ATP_LDS, st, (const u16*)q, (const u16*)k,
+                       (const u16*)v, (u16*)o, heads, npairs, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs,
+                       o_bs, sl2, o_map);
+    return bf_check_launch();
+}
+
 // 6 (default): k_attn2; 7 / 8: k_attn2 with two 5-wave / three 3-wave workgroups per short head;
 // 1/2: k_attn_s (with / without the XCD block order), 3: k_attn_r for short sequences, 4/5:
 // k_attn_s with 5/3 waves per workgroup for short sequences, 0: k_attn.  Env BF_ATTN_VARIANT.
+// 9: k_attn_p (persistent, LDS-DMA ring 3 steps deep, next head's Q prefetched), 10: k_attn2 XQ
+// (8 MFMA waves + the 257th query in VALU).
 // Measured (scripts/attn_bench.py, one MI355X): CLIP 128x16x257x80 k_attn_s 153.7 us -> k_attn2
 // 128.6 us; CuTR windows 72x12x512x64 122.0 -> 109.9; CuTR global 8x12x1600x64 124.8 -> 105.0.
+// CLIP, this round: v6 130.9-132.5 us, v9 131.0 (equal: same FETCH, +9 M SALU / +7 M VALU for
+// the DMA address math), v10 146.9 (8 waves hide less latency than 9: 41 % of wave cycles at
+// waitcnt / barrier, 32 % issue-stalled; a 3-slot ring issuing tile t+1's S^T MFMAs beside tile
+// t's softmax on top of it: 149.7, dropped).  scripts/attn_rounds.py: 17 us per round of 256
+// (batch, head) workgroups from 1 to 16 rounds, also with every operand MALL-resident -- the
+// per-workgroup chain, not HBM, sets the time.
 static int g_attn_variant = [] {
     const char* e = getenv("BF_ATTN_VARIANT");
     return e ? atoi(e) : 6;
@@ -956,7 +1354,26 @@ BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, v
                                     q_bs, k_bs, v_bs, o_bs, sl2, o_map);
         return bf_check_launch();
     }
-    if (g_attn_variant >= 6 && g_attn_variant <= 8) {
+    // variant 9: the persistent LDS-DMA ring (k_attn_p) for D = 80 heads of 193..320 keys and
+    // <= 288 queries (CLIP ViT-H: 257); other shapes take k_attn2
+    if (g_attn_variant == 9 && head_dim == 80 && sq <= ATP_NQ && sk >= 193 && sk <= 5 * AT_KT &&
+        batch * heads < (1 << 30))
+        return launch_attn_p(bf_stream(stream), q, k, v, o, batch, heads, sq, sk, q_rs, k_rs, v_rs, o_rs,
+                             q_bs, k_bs, v_bs, o_bs, sl2, o_map);
+    // variant 10: short heads with sq = 257-like (32*8 + 1): 8 MFMA waves + the last query in
+    // VALU beside them (k_attn2 XQ), one workgroup per (batch, head)
+    if (g_attn_variant == 10 && nw_one == 9 && sq % 32 == 1 && (head_dim == 80 || head_dim == 64)) {
+        if (head_dim == 80)
+            hipLaunchKernelGGL((k_attn2<80, 8, false, false, true>), dim3(1, heads, batch), dim3(512), 0,
+                               bf_stream(stream), (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, sq, sk,
+                               q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs, o_bs, sl2, o_map, 1.f);
+        else
+            hipLaunchKernelGGL((k_attn2<64, 8, false, false, true>), dim3(1, heads, batch), dim3(512), 0,
+                               bf_stream(stream), (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, sq, sk,
+                               q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs, o_bs, sl2, o_map, 1.f);
+        return bf_check_launch();
+    }
+    if (g_attn_variant >= 6 && g_attn_variant <= 10) {
 #define LAUNCH_2(DD, NWV)                                                                         \
     hipLaunchKernelGGL((k_attn2<DD, NWV>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch),    \
                        dim3(NWV * 64), 0, bf_stream(stream), (const u16*)q, (const u16*)k,          \
@@ -1058,7 +1475,12 @@ BF_API int bf_attention_fp8out(const void* q, const void* k, const void* v, void
                        (const u16*)v, (u16*)o, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs,    \
                        o_bs, sl2, (const int32_t*)nullptr, out_qscale)
 #define LAUNCH_8D(DD)                                                                             \
-    if (nw_one > 4 && nw_one <= 9) { LAUNCH_8(DD, 9); } else { LAUNCH_8(DD, 4); }
+    if (g_attn_variant == 10 && nw_one == 9 && sq % 32 == 1) {                                    \
+        hipLaunchKernelGGL((k_attn2<DD, 8, true, false, true>), dim3(1, heads, batch), dim3(512), 0,  \
+                           bf_stream(stream), (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, sq, \
+                           sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs, o_bs, sl2,                 \
+                           (const int32_t*)nullptr, out_qscale);                                    \
+    } else if (nw_one > 4 && nw_one <= 9) { LAUNCH_8(DD, 9); } else { LAUNCH_8(DD, 4); }
     switch (head_dim) {
         case 64: LAUNCH_8D(64); break;
         case 80: LAUNCH_8D(80); break;

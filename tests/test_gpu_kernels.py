@@ -318,3 +318,67 @@ def test_gemm_operand_extent_capacity(L):
                             None, None, 0, 0, ctypes.c_void_p(c.data_ptr()), 64, 1, None, 1 << 24, 64,
                             64, 0, None)
     assert rc == -3       # BF_ERR_CAPACITY
+
+
+@pytest.mark.parametrize("B,H,S", [(128, 16, 257), (19, 16, 257), (3, 5, 200), (7, 9, 288), (40, 16, 230)])
+def test_attention_persistent_ring_equals_attn2(L, B, H, S):
+    """variant 9 (k_attn_p: persistent workgroups, LDS-DMA ring three key steps deep, Q of the next
+    (batch, head) prefetched) runs k_attn2's arithmetic in the same order: bit-identical output,
+    for pair counts above / below / not a multiple of the CU count and 4 or 5 key steps"""
+    from boxfusion_amd._lib import lib
+    g = torch.Generator(device="cuda").manual_seed(S + B)
+    D = 80
+    W = H * D
+    qkv = (torch.randn(B * S, 3 * W + 64, device="cuda", generator=g) * 2).bfloat16()
+    q, k, v = qkv[:, :W], qkv[:, W:2 * W], qkv[:, 2 * W:3 * W]
+    outs = []
+    try:
+        for var in (6, 9):
+            lib().bf_attention_set_variant(var)
+            o = torch.full((B * S, W), float("nan"), device="cuda", dtype=torch.bfloat16)
+            L.attention(q, k, v, o, B, H, S, S, D, D ** -0.5)
+            torch.cuda.synchronize()
+            outs.append(o)
+    finally:
+        lib().bf_attention_set_variant(6)
+    assert torch.isfinite(outs[1].float()).all()
+    assert torch.equal(outs[0], outs[1])
+    qq, kk, vv = (x.float().reshape(B, S, H, D).transpose(1, 2)[:2] for x in (q, k, v))
+    ref = F.scaled_dot_product_attention(qq, kk, vv).transpose(1, 2).reshape(2 * S, W)
+    assert (outs[1][:2 * S].float() - ref).abs().max().item() < 3e-2
+
+
+@pytest.mark.parametrize("var", [10])
+@pytest.mark.parametrize("B,H,S,D", [(128, 16, 257, 80), (5, 3, 257, 64), (9, 16, 225, 80)])
+def test_attention_extra_query_variant(L, B, H, S, D, var):
+    """variant 10 (k_attn2 XQ: 8 MFMA waves for queries 0..S-2, the last query in f32 VALU beside
+    them, merged through LDS): rows 0..S-2 bit-identical to the 9-wave kernel; the last row within
+    bf16 rounding of the f32 SDPA (it is computed in f32, P unrounded); fp8 output the same way"""
+    from boxfusion_amd._lib import lib
+    g = torch.Generator(device="cuda").manual_seed(S + D + B)
+    W = H * D
+    qkv = (torch.randn(B * S, 3 * W, device="cuda", generator=g) * 2).bfloat16()
+    q, k, v = qkv[:, :W], qkv[:, W:2 * W], qkv[:, 2 * W:]
+    outs, outs8 = [], []
+    try:
+        for v_ in (6, var):
+            lib().bf_attention_set_variant(v_)
+            o = torch.full((B * S, W), float("nan"), device="cuda", dtype=torch.bfloat16)
+            L.attention(q, k, v, o, B, H, S, S, D, D ** -0.5)
+            o8 = torch.zeros((B * S, W), device="cuda", dtype=L.FP8)
+            L.attention_fp8out(q, k, v, o8, B, H, S, S, D, D ** -0.5, 4.0)
+            torch.cuda.synchronize()
+            outs.append(o)
+            outs8.append(o8)
+    finally:
+        lib().bf_attention_set_variant(6)
+    a, b_ = outs[0].view(B, S, W), outs[1].view(B, S, W)
+    assert torch.isfinite(b_.float()).all()
+    assert torch.equal(a[:, :S - 1], b_[:, :S - 1])
+    qq, kk, vv = (x.float().reshape(B, S, H, D).transpose(1, 2) for x in (q, k, v))
+    ref = F.scaled_dot_product_attention(qq, kk, vv).transpose(1, 2).reshape(B, S, W)
+    assert (b_[:, S - 1].float() - ref[:, S - 1]).abs().max().item() < 2e-2
+    assert (b_[:, S - 1].float() - ref[:, S - 1]).abs().max() <= (a[:, S - 1].float() - ref[:, S - 1]).abs().max() + 1e-2
+    a8, b8 = outs8[0].view(B, S, W), outs8[1].view(B, S, W)
+    assert torch.equal(a8[:, :S - 1], b8[:, :S - 1])
+    assert ((b8[:, S - 1].float() - 4.0 * ref[:, S - 1]).abs() <= 4.0 * ref[:, S - 1].abs() * 0.07 + 0.05).all()
