@@ -99,6 +99,11 @@ def parse(argv=None):
     p.add_argument("--scene-objects", type=int, default=30,
                    help="objects in the seeded synthetic scene (150: global box sets past the "
                         "one-wave NMS scan's 96, so the 256-thread scan runs)")
+    p.add_argument("--gap", type=int, default=1,
+                   help="keyframe gap (demo.py:134 `count % gap == 0`): every step covers batch*gap "
+                        "frames per GPU; the non-keyframes get demo.py's per-frame preprocessing "
+                        "(depth standardisation), the keyframes detect + CLIP + fusion.  Default "
+                        "steps at gap > 1: the 1000-frame stream")
     p.add_argument("--cpu-rehearsal", action="store_true",
                    help="CPU/gloo rehearsal of the N-rank control flow (no kernels; test harness)")
     return p.parse_args(argv)
@@ -452,6 +457,8 @@ def rehearse_cpu(args, dist, world, rank):
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
+    if args.gap > 1 and "--steps" not in " ".join(argv):
+        args.steps = max(1, -(-1000 // (args.batch * args.gap * args.gpus)))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(argv, args.gpus)
     if args.breakdown:
@@ -519,12 +526,25 @@ def main(argv=None):
     total_steps = args.warmup + args.steps
     coeff = CFG["box_fusion"]["clip_sim_coeff"]
 
+    G = max(1, args.gap)
+    CFG["data"]["gap"] = G
+
     def my_frames(step):
-        return [step * per_step + rank * B + j for j in range(B)]
+        """this rank's keyframes of a step (frame ids; gap G: every G-th frame of the stream)"""
+        return [(step * per_step + rank * B + j) * G for j in range(B)]
 
     # ---- inputs resident in HBM before timing -----------------------------------------------
     all_mine = [f for s in range(total_steps) for f in my_frames(s)]
     rgb_all, depth_all = gen_frames(all_mine, dev)
+    nk_depth = None
+    if G > 1:
+        # the rank's non-keyframes of every step: depth maps only (demo.py:129-131 standardises
+        # every frame's depth; nothing else runs on a non-keyframe)
+        gnk = torch.Generator(device=dev)
+        gnk.manual_seed(4321 + rank)
+        nk_depth = torch.empty((total_steps, (G - 1) * B, 480, 640), dtype=torch.float32, device=dev)
+        nk_depth.uniform_(0.5, 4.5, generator=gnk)
+        nk_depth.masked_fill_(torch.rand(nk_depth.shape, device=dev, generator=gnk) < 0.05, 0.0)
     poses_all = np.stack([scene.pose(f) for f in all_mine]).astype(np.float32)
     dets_mine = [scene.detections(f) for f in all_mine]
     rec_all = torch.from_numpy(pack_records(dets_mine, poses_all)).to(dev)
@@ -559,6 +579,8 @@ def main(argv=None):
             st_ctx = torch.cuda.stream(det_streams[k])
             st_ctx.__enter__()      # this step's detect, gather and fusion hand-off on its stream
             det = detects[k]
+            if nk_depth is not None:          # the step's non-keyframes: preprocessing only
+                _lib.depth_standardize(nk_depth[s])
             det(rgb_all[sl], depth_all[sl], poses_all[sl], return_instances=False,
                 crop_boxes=crops_all[s * B * args.crops:(s + 1) * B * args.crops])
             if args.breakdown:
@@ -573,7 +595,7 @@ def main(argv=None):
                 g_clip = g_clip.repeat(args.sim_ranks, 1)
             if rank == 0:
                 base = s * (per_step if sim is None else B * args.sim_ranks)
-                counts = [base + j - s0 * (g_rec.shape[0]) for j in range(g_rec.shape[0])]
+                counts = [(base + j - s0 * (g_rec.shape[0])) * G for j in range(g_rec.shape[0])]
                 if args.sync_fusion:
                     g_pose, g_cnt = record_meta(g_rec)
                     fusion.keyframes(counts, g_pose, unpack_records(g_rec, g_cnt, dev, g_clip,
@@ -643,6 +665,11 @@ def main(argv=None):
             if rank == 0:
                 print(f"fusion worker busy {1e3 * worker.busy_s / args.steps:.1f} ms/step "
                       f"({fusion.stats['keyframes']} keyframes)", file=sys.stderr, flush=True)
+        if rank == 0 and G > 1:
+            # demo.py:200: the stream's last frame is not a keyframe -> the stale re-fusion of the
+            # previous keyframe's instances with the last pose
+            last = per_step * args.steps * G - 1
+            fusion.finish(last, scene.pose(total_steps * per_step * G - 1), False)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -665,7 +692,7 @@ def main(argv=None):
         torch.cuda.synchronize()
         detect.use_graph = not args.eager
         source = f"eager re-run of {args.roofline_steps} timed steps"
-    frames = per_step * args.steps
+    frames = per_step * args.steps * G
 
     if rank == 0:
         big = lambda t: t["kind"] == "gemm" and t["large"]
@@ -692,7 +719,12 @@ def main(argv=None):
         for v in comps.values():
             v["measured"] = source
         r_all["measured"] = source
-        line = base_line(args, N, frames, dt, per_step, n_inflight)
+        line = base_line(args, N, frames, dt, per_step * G, n_inflight)
+        if G > 1:
+            line["config"]["workload"] = line["config"]["workload"].replace(
+                "gap=1", f"gap={G} (demo.py keyframe rule: {B} keyframes + {(G - 1) * B} non-keyframe "
+                         f"depth standardisations per step per GPU)")
+            line["config"]["keyframes"] = per_step * args.steps
         line["config"].update(scene_objects=args.scene_objects, fused_boxes=fusion.stats["fused"],
                               global_boxes=len(fusion.all_pred_box) if fusion.all_pred_box is not None else 0)
         if args.clip_fp8:
