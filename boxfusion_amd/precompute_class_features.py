@@ -25,12 +25,14 @@ from boxfusion_amd.tokenizer import SimpleTokenizer
 TEXT_KEYS = ("token_embedding.", "positional_embedding", "transformer.", "ln_final.", "text_projection")
 
 
-def load_text_tower(path, device="cuda"):
+def load_text_tower(path, device="cuda", text=None):
+    """the text-tower entries of an open_clip checkpoint (optionally under "state_dict" / with a
+    "module." prefix; the visual.* entries are ignored) loaded into `text` (default ViT-H-14)"""
     sd = torch.load(path, map_location="cpu", weights_only=True)
     if "state_dict" in sd:
         sd = sd["state_dict"]
     sd = {k[len("module."):] if k.startswith("module.") else k: v for k, v in sd.items()}
-    text = text_h14()
+    text = text_h14() if text is None else text
     missing, _ = text.load_state_dict({k: v for k, v in sd.items() if k.startswith(TEXT_KEYS)},
                                       strict=False)
     if missing:

@@ -97,3 +97,23 @@ def test_text_engine_vith_class_features(L):
     assert tab.shape == (20, 1024)
     assert torch.allclose(tab.norm(dim=1), torch.ones(20, device="cuda"), atol=1e-5)
     assert F.cosine_similarity(tab, ref, dim=1).min().item() > 0.999
+
+
+def test_vocabulary_builder_end_to_end(L):
+    """precompute_class_features.build_class_features: class names -> BPE tokens -> HIP text tower
+    -> L2-normalised table, against the fp32 TextTransformer on the same token ids"""
+    from boxfusion_amd.clip import TextTransformer
+    from boxfusion_amd.precompute_class_features import build_class_features
+    from boxfusion_amd.tokenizer import SimpleTokenizer
+    from tests.test_tokenizer import MERGES
+    tok = SimpleTokenizer(MERGES)
+    torch.manual_seed(3)
+    text = TextTransformer(77, tok.vocab_size, 256, 4, 3, 1024).cuda().eval()
+    names = ["chair", "table", "sofa", "kitchen cabinet", "tv stand", "a chair, and a table!"]
+    tab = build_class_features(names, text, tok, max_prompts=4)
+    ids = torch.from_numpy(tok(names)).cuda()
+    with torch.no_grad():
+        ref = F.normalize(text(ids), dim=-1)
+    assert tab.shape == (len(names), 1024)
+    assert F.cosine_similarity(tab, ref, dim=1).min().item() > 0.999
+    assert torch.allclose(tab.norm(dim=1), torch.ones(len(names), device="cuda"), atol=1e-5)

@@ -56,3 +56,24 @@ def test_merges_file(tmp_path):
     a, b = SimpleTokenizer(str(p)), SimpleTokenizer(MERGES)
     assert a.encoder == b.encoder
     assert (a(["sofa chair"]) == b(["sofa chair"])).all()
+
+
+def test_load_text_tower_from_open_clip_style_checkpoint(tmp_path):
+    """precompute_class_features.load_text_tower: text entries of a checkpoint with a "module."
+    prefix, a "state_dict" wrapper and unrelated visual.* entries load into the TextTransformer
+    (open_clip parameter names); a checkpoint without them is rejected"""
+    import torch
+    from boxfusion_amd.clip import TextTransformer
+    from boxfusion_amd.precompute_class_features import load_text_tower
+    torch.manual_seed(0)
+    src = TextTransformer(77, 300, 64, 2, 2, 32)
+    sd = {"module." + k: v for k, v in src.state_dict().items()}
+    sd["module.visual.proj"] = torch.zeros(3)
+    torch.save({"state_dict": sd}, tmp_path / "ckpt.pt")
+    dst = load_text_tower(str(tmp_path / "ckpt.pt"), device="cpu", text=TextTransformer(77, 300, 64, 2, 2, 32))
+    for k, v in src.state_dict().items():
+        assert torch.equal(dst.state_dict()[k], v), k
+    torch.save({"visual.proj": torch.zeros(3)}, tmp_path / "bad.pt")
+    import pytest
+    with pytest.raises(KeyError):
+        load_text_tower(str(tmp_path / "bad.pt"), device="cpu", text=TextTransformer(77, 300, 64, 2, 2, 32))
