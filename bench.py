@@ -55,6 +55,9 @@ CFG = dict(
                     random_opt=dict(center_init_size=0.1, center_scaling_coefficient=0.1,
                                     shape_init_size=0.5, shape_scaling_coefficient=0.5)),
 )
+# the stream's frame geometry (set by --dataset): image H x W, depth at 1/r, intrinsics K
+CA1M_K = np.array([[360.0, 0.0, 191.5], [0.0, 360.0, 255.5], [0.0, 0.0, 1.0]], np.float32)
+FRAME = dict(H=480, W=640, r=1, K=None)
 REC_ROWS, REC_W = 64, 22     # per-frame detection record: rows x (score, xyxy, xyzlhw, R, proj_xy)
 REC_HEAD = 17                # record head: detection count, camera pose (4x4)
 CLIP_W = 1026                # per-crop CLIP row: feature[1024], best similarity, class index
@@ -104,6 +107,9 @@ def parse(argv=None):
                         "frames per GPU; the non-keyframes get demo.py's per-frame preprocessing "
                         "(depth standardisation), the keyframes detect + CLIP + fusion.  Default "
                         "steps at gap > 1: the 1000-frame stream")
+    p.add_argument("--dataset", choices=("scannet", "ca1m"), default="scannet",
+                   help="ca1m: BASELINE configs[1]'s stream shape -- 384x512 portrait frames, depth at 1/2 "
+                        "resolution (RGB:depth ratio 2), ca1m.yaml thresholds and gap 20")
     p.add_argument("--cpu-rehearsal", action="store_true",
                    help="CPU/gloo rehearsal of the N-rank control flow (no kernels; test harness)")
     return p.parse_args(argv)
@@ -131,14 +137,15 @@ def launch_ranks(argv, n):
 def gen_frames(frame_ids, dev):
     """seeded synthetic RGB-D frames generated on the device (seed 1234 + frame)."""
     n = len(frame_ids)
-    rgb = torch.empty((n, 480, 640, 3), dtype=torch.uint8, device=dev)
-    depth = torch.empty((n, 480, 640), dtype=torch.float32, device=dev)
+    H, W, r = FRAME["H"], FRAME["W"], FRAME["r"]
+    rgb = torch.empty((n, H, W, 3), dtype=torch.uint8, device=dev)
+    depth = torch.empty((n, H // r, W // r), dtype=torch.float32, device=dev)
     g = torch.Generator(device=dev)
     for j, f in enumerate(frame_ids):
         g.manual_seed(1234 + int(f))
         rgb[j].random_(0, 256, generator=g)
         depth[j].uniform_(0.5, 4.5, generator=g)
-        depth[j].masked_fill_(torch.rand((480, 640), device=dev, generator=g) < 0.05, 0.0)
+        depth[j].masked_fill_(torch.rand(depth.shape[1:], device=dev, generator=g) < 0.05, 0.0)
     return rgb, depth
 
 
@@ -197,7 +204,7 @@ def unpack_record(rec, dev, n=None):
     if n is None:
         n = int(rec[0].item())
     rows = rec[REC_HEAD:REC_HEAD + n * REC_W].view(n, REC_W)
-    p = Instances3D((480, 640))
+    p = Instances3D((FRAME["H"], FRAME["W"]))
     p.scores = rows[:, 0].contiguous()
     p.pred_boxes = rows[:, 1:5].contiguous()
     p.pred_boxes_3d = GeneralInstance3DBoxes(rows[:, 5:11], rows[:, 11:20].reshape(n, 3, 3))
@@ -229,7 +236,7 @@ def unpack_records(recs, cnts, dev, clip=None, crops=16, clip_coeff=1.0):
     idx, cidx = record_rows(cnts, crops)
     rows = recs[:, REC_HEAD:REC_HEAD + REC_ROWS * REC_W].reshape(-1, REC_W).index_select(
         0, _lib.h2d(idx, dev))
-    p = Instances3D((480, 640))
+    p = Instances3D((FRAME["H"], FRAME["W"]))
     p.scores = rows[:, 0].contiguous()
     p.pred_boxes = rows[:, 1:5].contiguous()
     p.pred_boxes_3d = GeneralInstance3DBoxes._views(rows[:, 5:11].contiguous(),
@@ -457,6 +464,16 @@ def rehearse_cpu(args, dist, world, rank):
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
+    if args.dataset == "ca1m":
+        # ca1m.yaml (config/ca1m.yaml): cam 384 x 512 (portrait after BoxFusion's H/W swap), gap 20,
+        # score 0.4, small_threshold 0.2; the synthetic CA-1M frame geometry of the CuTR goldens
+        FRAME.update(H=512, W=384, r=2, K=CA1M_K)
+        CFG.update(dataset="CA1M", cam=dict(H=384, W=512, png_depth_scale=1000.0))
+        CFG["detection"].update(score_thresh=0.4)
+        CFG["association"].update(small_threshold=0.2)
+        CFG["box_fusion"].update(small_size=0.5)
+        if "--gap" not in " ".join(argv):
+            args.gap = 20
     if args.gap > 1 and "--steps" not in " ".join(argv):
         args.steps = max(1, -(-1000 // (args.batch * args.gap * args.gpus)))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -514,10 +531,13 @@ def main(argv=None):
         # the reference; the first `vocab` rows of its 473-class table stand in (same match kernel
         # path, vocabulary-sized)
         text, names = text[:args.vocab].clone(), names[:args.vocab]
-    detects = [DetectStage(cutr, clip_vis, CFG, B, 480, 640, SCANNET_K, text_features=text.clone(),
+    Kf = SCANNET_K if FRAME["K"] is None else FRAME["K"]
+    FH, FW = FRAME["H"], FRAME["W"]
+    detects = [DetectStage(cutr, clip_vis, CFG, B, FH, FW, Kf, text_features=text.clone(),
                            class_names=names, crops_per_frame=args.crops,
                            crop_source="given", backproject=True, clip_capacity=B * args.crops,
-                           device=dev, graph=not args.eager, clip_fp8=args.clip_fp8)
+                           device=dev, graph=not args.eager, clip_fp8=args.clip_fp8,
+                           depth_ratio=FRAME["r"])
                for _ in range(n_inflight)]
     detect = detects[0]
     scene = Scene(seed=0, n_objects=args.scene_objects)
@@ -542,18 +562,19 @@ def main(argv=None):
         # every frame's depth; nothing else runs on a non-keyframe)
         gnk = torch.Generator(device=dev)
         gnk.manual_seed(4321 + rank)
-        nk_depth = torch.empty((total_steps, (G - 1) * B, 480, 640), dtype=torch.float32, device=dev)
+        nk_depth = torch.empty((total_steps, (G - 1) * B, FH // FRAME["r"], FW // FRAME["r"]),
+                               dtype=torch.float32, device=dev)
         nk_depth.uniform_(0.5, 4.5, generator=gnk)
         nk_depth.masked_fill_(torch.rand(nk_depth.shape, device=dev, generator=gnk) < 0.05, 0.0)
     poses_all = np.stack([scene.pose(f) for f in all_mine]).astype(np.float32)
-    dets_mine = [scene.detections(f) for f in all_mine]
+    dets_mine = [scene.detections(f, Kf, (FW, FH)) for f in all_mine]
     rec_all = torch.from_numpy(pack_records(dets_mine, poses_all)).to(dev)
     crops_all = torch.from_numpy(crop_boxes(dets_mine, args.crops)).to(dev)
     if args.clip_fp8:
         # static fp8 activation scales: calibrated once (bf16 forward of this rank's first batch
         # of crops, untimed) and shared by every in-flight detect stage
         from boxfusion_amd.pipeline import scale_boxes
-        bi = scale_boxes(crops_all[:B * args.crops], 480, 640, detect.scale_box).to(torch.int32)
+        bi = scale_boxes(crops_all[:B * args.crops], FH, FW, detect.scale_box).to(torch.int32)
         scales = detect.clip.calibrate(rgb_all[:B], bi.contiguous(), detect.top_b32)
         for d in detects[1:]:
             d.clip.act_scales = scales
@@ -564,7 +585,7 @@ def main(argv=None):
         sim = {"rec": []}
         for s_ in range(total_steps):
             fr = [s_ * B * R + j for j in range(B * R)]
-            rh = pack_records([scene.detections(f) for f in fr], [scene.pose(f) for f in fr])
+            rh = pack_records([scene.detections(f, Kf, (FW, FH)) for f in fr], [scene.pose(f) for f in fr])
             sim["rec"].append(torch.from_numpy(rh).to(dev))
     torch.cuda.synchronize()
 
@@ -643,7 +664,7 @@ def main(argv=None):
     torch.cuda.synchronize()
 
     def make_fusion():
-        st = FusionStage(CFG, SCANNET_K, device=dev)
+        st = FusionStage(CFG, Kf, H=FH, W=FW, device=dev)
         return st if args.sync_fusion else AsyncFusion(st, stream=fus_stream)
 
     wf = make_fusion()
@@ -720,6 +741,13 @@ def main(argv=None):
             v["measured"] = source
         r_all["measured"] = source
         line = base_line(args, N, frames, dt, per_step * G, n_inflight)
+        if args.dataset == "ca1m":
+            line["metric"] = "RGB-D frames/sec (whole node) on 384x512 portrait stream, depth at 1/2 resolution"
+            line["data"] = ("synthetic CA-1M-shaped RGB-D stream (seeded; CA-1M data absent offline), random-init "
+                            "weights, seeded scene detections")
+            line["config"]["workload"] = line["config"]["workload"].replace(
+                "configs[2]: synthetic 640x480 RGB-D", "configs[1]: CA-1M-shaped 384x512 portrait RGB-D, "
+                "depth 192x256 (RGB:depth 2), ca1m.yaml thresholds")
         if G > 1:
             line["config"]["workload"] = line["config"]["workload"].replace(
                 "gap=1", f"gap={G} (demo.py keyframe rule: {B} keyframes + {(G - 1) * B} non-keyframe "
@@ -739,7 +767,7 @@ def main(argv=None):
         line["roofline_components"] = comps
         if args.breakdown:
             line["breakdown_ms_per_step"] = {k: 1e3 * v / args.steps for k, v in brk.items()}
-        if not args.no_cpu_baseline and N == 1:      # rank 0 at N=1 only (a reported baseline)
+        if not args.no_cpu_baseline and N == 1 and args.dataset == "scannet":   # rank 0 at N=1 only
             line["cpu_baseline"] = cpu_baseline(cutr, clip_vis, args, scene)
         emit(line)
     if dist is not None:

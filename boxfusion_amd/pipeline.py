@@ -79,18 +79,23 @@ class DetectStage:
 
     def __init__(self, cutr_model, clip_visual, cfg, batch, H=480, W=640, K3=None, text_features=None,
                  class_names=None, crops_per_frame=16, crop_source="filtered", backproject=True,
-                 clip_capacity=256, device="cuda", graph=False, clip_fp8=False):
+                 clip_capacity=256, device="cuda", graph=False, clip_fp8=False, depth_ratio=1):
         self.cfg = cfg
         self.dev = torch.device(device)
         self.B, self.H, self.W = batch, H, W
+        self.r = int(depth_ratio)        # RGB:depth resolution ratio (CA-1M: 2 or 4)
         self.pad = square_pad_size(H, W)
-        self.cutr = CuTREngine(cutr_model, batch, H, W, pad=self.pad, device=device)
+        self.cutr = CuTREngine(cutr_model, batch, H, W, pad=self.pad, device=device, depth_ratio=self.r)
         self.clip = (CLIPEngine(clip_visual, clip_capacity, device=device, fp8=clip_fp8)
                      if clip_visual is not None else None)
         self.K3 = np.asarray(K3, np.float32)
         self.K_host = np.stack([self.K3] * batch)
         self.K_dev = torch.from_numpy(self.K_host).to(self.dev)
         self.Kinv_dev = torch.linalg.inv(self.K_dev)
+        # the depth map's intrinsics (image K at 1/r, the synthetic CA-1M K_depth) for unproject
+        Kd = self.K3.copy()
+        Kd[:2] /= self.r
+        self.Kd_dev = torch.from_numpy(np.stack([Kd] * batch)).to(self.dev)
         self.text = (text_features if text_features is not None else load_class_features()).to(self.dev).contiguous()
         names = class_names if class_names is not None else load_class_names()
         self.prompt = np.concatenate([np.asarray(names), np.full(1, "")])
@@ -103,7 +108,7 @@ class DetectStage:
         self.coeff = float(dict(FUSION_DEFAULTS, **cfg["box_fusion"])["clip_sim_coeff"])
         # fixed input buffers (the graph reads these)
         self.in_rgb = torch.zeros((batch, H, W, 3), dtype=torch.uint8, device=self.dev)
-        self.in_depth = torch.zeros((batch, H, W), dtype=torch.float32, device=self.dev)
+        self.in_depth = torch.zeros((batch, H // self.r, W // self.r), dtype=torch.float32, device=self.dev)
         self.in_Tg = torch.zeros((batch, 3, 3), dtype=torch.float32, device=self.dev)
         self.in_pose = torch.zeros((batch, 4, 4), dtype=torch.float32, device=self.dev)
         k = crops_per_frame
@@ -134,7 +139,7 @@ class DetectStage:
         B, H, W = self.B, self.H, self.W
         dstd, params = _lib.depth_standardize(self.in_depth)
         if self.backproject:
-            self.out["xyz"] = [_lib.backproject(self.in_depth[b], self.K_dev[b], self.in_pose[b])
+            self.out["xyz"] = [_lib.backproject(self.in_depth[b], self.Kd_dev[b], self.in_pose[b])
                                for b in range(B)]
         res = self.cutr(self.in_rgb, dstd, params, self.K_dev, self.in_Tg, [(H, W)] * B,
                         K_host=self.K_host, K_inv=self.Kinv_dev)
@@ -176,7 +181,7 @@ class DetectStage:
         self.last (device tensors) and the call never waits for the device.
         crop_boxes: f32 device [B*crops_per_frame, 4] (crop_source "given")."""
         B, H, W = self.B, self.H, self.W
-        assert rgb_u8.shape == (B, H, W, 3) and depth.shape == (B, H, W)
+        assert rgb_u8.shape == (B, H, W, 3) and depth.shape == (B, H // self.r, W // self.r)
         self.in_rgb.copy_(rgb_u8, non_blocking=True)
         self.in_depth.copy_(depth, non_blocking=True)
         if self.crop_source == "given":

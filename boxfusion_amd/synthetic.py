@@ -86,8 +86,10 @@ class Scene:
     def pose(self, frame):
         return trajectory_pose(frame, self.period)
 
-    def detections(self, frame, K=SCANNET_K):
-        """Detections of keyframe `frame` in CuTR's output layout (camera frame)."""
+    def detections(self, frame, K=SCANNET_K, size=(W, H)):
+        """Detections of keyframe `frame` in CuTR's output layout (camera frame); size = (W, H) of
+        the image the 2-D boxes live in."""
+        W, H = size
         rng = np.random.default_rng(10_000 + self.seed * 7919 + frame)
         P = self.pose(frame).astype(np.float64)
         Rc, tc = P[:3, :3], P[:3, 3]

@@ -375,3 +375,39 @@ def test_pipeline_run_vs_reference_demo_gap25(dev, monkeypatch):
     np.testing.assert_array_equal(cls, d["fw_class"])
     np.testing.assert_array_equal(pf.pred_boxes_3d.corners.cpu().numpy(), d["fw_corners"])
     np.testing.assert_allclose(pf.features.cpu().numpy(), d["fw_features"], rtol=1e-6, atol=1e-7)
+
+
+def test_detect_stage_ca1m_depth_ratio(dev):
+    """CA-1M-shaped detect stage (BASELINE configs[1]): 384x512 portrait frames with the depth map
+    at half resolution (RGB:depth 2) -- the CuTR depth tokens on their own grid, back-projection
+    with the depth intrinsics -- equals CuTREngine called directly on the same standardised depth"""
+    from boxfusion_amd import _lib
+    from boxfusion_amd.clip import VisionTransformer
+    from boxfusion_amd.cubify_transformer import make_cubify_transformer
+    from boxfusion_amd.pipeline import DetectStage
+    from boxfusion_amd.sensor import camera_to_gravity
+    from boxfusion_amd.synthetic import Scene
+    K = np.array([[360.0, 0.0, 191.5], [0.0, 360.0, 255.5], [0.0, 0.0, 1.0]], np.float32)
+    torch.manual_seed(0)
+    with torch.device(dev):
+        cutr = make_cubify_transformer(192, True).eval()
+        vis = VisionTransformer(224, 14, 1280, 2, 16, 1024).eval()
+    B, H, W = 2, 512, 384
+    det = DetectStage(cutr, vis, TU.SCANNET_CFG, B, H, W, K, crop_source="top", crops_per_frame=4,
+                      clip_capacity=8, device=dev, depth_ratio=2)
+    g = torch.Generator(device=dev).manual_seed(5)
+    rgb = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=dev, generator=g)
+    depth = torch.rand((B, H // 2, W // 2), device=dev, generator=g) * 4 + 0.5
+    poses = np.stack([Scene().pose(f) for f in range(B)])
+    det(rgb, depth, poses, return_instances=False)
+    torch.cuda.synchronize()
+    xyz, valid = det.last["xyz"][0]
+    assert xyz.shape == (H // 2, W // 2, 3) and valid.all()
+    dstd, params = _lib.depth_standardize(depth)
+    Kd = torch.from_numpy(np.stack([K] * B)).to(dev)
+    Tg = torch.from_numpy(np.stack([camera_to_gravity(p) for p in poses])).to(dev)
+    ref = det.cutr(rgb, dstd, params, Kd, Tg, [(H, W)] * B, K_host=np.stack([K] * B))
+    for a, b in zip(det.last["res"], ref):
+        assert torch.equal(a.scores, b.scores)
+        assert torch.equal(a.pred_boxes_3d.tensor, b.pred_boxes_3d.tensor)
+    assert torch.isfinite(det.last["clip"][3]).all()
