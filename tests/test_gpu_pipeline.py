@@ -403,11 +403,13 @@ def test_detect_stage_ca1m_depth_ratio(dev):
     torch.cuda.synchronize()
     xyz, valid = det.last["xyz"][0]
     assert xyz.shape == (H // 2, W // 2, 3) and valid.all()
+    got = [(r.scores.clone(), r.pred_boxes_3d.tensor.clone()) for r in det.last["res"]]
     dstd, params = _lib.depth_standardize(depth)
     Kd = torch.from_numpy(np.stack([K] * B)).to(dev)
     Tg = torch.from_numpy(np.stack([camera_to_gravity(p) for p in poses])).to(dev)
     ref = det.cutr(rgb, dstd, params, Kd, Tg, [(H, W)] * B, K_host=np.stack([K] * B))
-    for a, b in zip(det.last["res"], ref):
-        assert torch.equal(a.scores, b.scores)
-        assert torch.equal(a.pred_boxes_3d.tensor, b.pred_boxes_3d.tensor)
+    for (sa, ba), b in zip(got, ref):
+        assert torch.isfinite(sa).all() and torch.isfinite(ba).all()
+        assert torch.equal(sa, b.scores)
+        assert torch.equal(ba, b.pred_boxes_3d.tensor)
     assert torch.isfinite(det.last["clip"][3]).all()
