@@ -107,6 +107,13 @@ def parse(argv=None):
                         "frames per GPU; the non-keyframes get demo.py's per-frame preprocessing "
                         "(depth standardisation), the keyframes detect + CLIP + fusion.  Default "
                         "steps at gap > 1: the 1000-frame stream")
+    p.add_argument("--rank0-batch", type=int, default=-1,
+                   help="frames rank 0 detects per step when it also fuses other ranks' frames (N > 1 or "
+                        "--sim-ranks): the fusion owner's share of detection is lowered so its serial "
+                        "fusion keeps pace; the other ranks detect --batch; -1: auto")
+    p.add_argument("--switch-interval", type=float, default=-1.0,
+                   help="Python thread switch interval in ms for the host threads (detect launcher vs "
+                        "the fusion worker); <0: the interpreter default")
     p.add_argument("--dataset", choices=("scannet", "ca1m"), default="scannet",
                    help="ca1m: BASELINE configs[1]'s stream shape -- 384x512 portrait frames, depth at 1/2 "
                         "resolution (RGB:depth ratio 2), ca1m.yaml thresholds and gap 20")
@@ -376,6 +383,17 @@ def roofline_obj(ks, kernel, bound, pmc_key=None, peak_tflops=PEAK_BF16_TFLOPS):
             "algorithmic_bytes_per_launch": ks.get("bytes_per_launch", 0.0)}
 
 
+def auto_rank0_batch(B, ranks):
+    """rank 0's detection share when it also fuses `ranks` ranks' frames: its fusion worker must
+    keep pace with ranks * B keyframes per step (measured on one MI355X with --sim-ranks: the
+    worker is busy 15.6 / 32.7 / 58.4 ms per 54.6-ms step at 2 / 4 / 8 ranks of 8 frames)"""
+    if ranks >= 8:
+        return max(1, B - 2)
+    if ranks >= 4:
+        return max(1, B - 1)
+    return B
+
+
 def emit(line):
     print(json.dumps(line), flush=True)
 
@@ -480,6 +498,8 @@ def main(argv=None):
         return launch_ranks(argv, args.gpus)
     if args.breakdown:
         args.sync_fusion = True
+    if args.switch_interval > 0:
+        sys.setswitchinterval(args.switch_interval * 1e-3)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -523,6 +543,10 @@ def main(argv=None):
         cutr = make_cubify_transformer(args.dim, True).eval()
         clip_vis = VisionTransformer(224, 14, 1280, args.clip_layers, 16, 1024).eval()
     B = args.batch
+    R_fuse = world if world > 1 else max(1, args.sim_ranks)      # ranks whose frames rank 0 fuses
+    B0 = args.rank0_batch if args.rank0_batch > 0 else auto_rank0_batch(B, R_fuse)
+    B0 = min(B, B0) if R_fuse > 1 else B
+    Bm = B0 if rank == 0 else B                                  # this rank's frames per step
     n_inflight = args.inflight if args.inflight > 0 else 2
     from boxfusion_amd.pipeline import load_class_features, load_class_names
     text, names = load_class_features(), load_class_names()
@@ -533,16 +557,16 @@ def main(argv=None):
         text, names = text[:args.vocab].clone(), names[:args.vocab]
     Kf = SCANNET_K if FRAME["K"] is None else FRAME["K"]
     FH, FW = FRAME["H"], FRAME["W"]
-    detects = [DetectStage(cutr, clip_vis, CFG, B, FH, FW, Kf, text_features=text.clone(),
+    detects = [DetectStage(cutr, clip_vis, CFG, Bm, FH, FW, Kf, text_features=text.clone(),
                            class_names=names, crops_per_frame=args.crops,
-                           crop_source="given", backproject=True, clip_capacity=B * args.crops,
+                           crop_source="given", backproject=True, clip_capacity=Bm * args.crops,
                            device=dev, graph=not args.eager, clip_fp8=args.clip_fp8,
                            depth_ratio=FRAME["r"])
                for _ in range(n_inflight)]
     detect = detects[0]
     scene = Scene(seed=0, n_objects=args.scene_objects)
     N = world
-    per_step = B * N
+    per_step = B * N - (B - B0)          # frames per step (all ranks; rank 0 detects B0)
     total_steps = args.warmup + args.steps
     coeff = CFG["box_fusion"]["clip_sim_coeff"]
 
@@ -550,8 +574,10 @@ def main(argv=None):
     CFG["data"]["gap"] = G
 
     def my_frames(step):
-        """this rank's keyframes of a step (frame ids; gap G: every G-th frame of the stream)"""
-        return [(step * per_step + rank * B + j) * G for j in range(B)]
+        """this rank's keyframes of a step (frame ids; gap G: every G-th frame of the stream):
+        rank 0 the first B0 of the step, rank r >= 1 the B after B0 + (r - 1) B"""
+        first = step * per_step + (0 if rank == 0 else B0 + (rank - 1) * B)
+        return [(first + j) * G for j in range(Bm)]
 
     # ---- inputs resident in HBM before timing -----------------------------------------------
     all_mine = [f for s in range(total_steps) for f in my_frames(s)]
@@ -562,7 +588,7 @@ def main(argv=None):
         # every frame's depth; nothing else runs on a non-keyframe)
         gnk = torch.Generator(device=dev)
         gnk.manual_seed(4321 + rank)
-        nk_depth = torch.empty((total_steps, (G - 1) * B, FH // FRAME["r"], FW // FRAME["r"]),
+        nk_depth = torch.empty((total_steps, (G - 1) * Bm, FH // FRAME["r"], FW // FRAME["r"]),
                                dtype=torch.float32, device=dev)
         nk_depth.uniform_(0.5, 4.5, generator=gnk)
         nk_depth.masked_fill_(torch.rand(nk_depth.shape, device=dev, generator=gnk) < 0.05, 0.0)
@@ -574,17 +600,17 @@ def main(argv=None):
         # static fp8 activation scales: calibrated once (bf16 forward of this rank's first batch
         # of crops, untimed) and shared by every in-flight detect stage
         from boxfusion_amd.pipeline import scale_boxes
-        bi = scale_boxes(crops_all[:B * args.crops], FH, FW, detect.scale_box).to(torch.int32)
-        scales = detect.clip.calibrate(rgb_all[:B], bi.contiguous(), detect.top_b32)
+        bi = scale_boxes(crops_all[:Bm * args.crops], FH, FW, detect.scale_box).to(torch.int32)
+        scales = detect.clip.calibrate(rgb_all[:Bm], bi.contiguous(), detect.top_b32)
         for d in detects[1:]:
             d.clip.act_scales = scales
     sim = None
     if args.sim_ranks > 1 and world == 1:
         # what rank 0 of an R-GPU run fuses: R*B frames per step (stress test, not the metric)
         R = args.sim_ranks
-        sim = {"rec": []}
+        sim = {"rec": [], "per_step": B * R - (B - B0)}
         for s_ in range(total_steps):
-            fr = [s_ * B * R + j for j in range(B * R)]
+            fr = [s_ * sim["per_step"] + j for j in range(sim["per_step"])]
             rh = pack_records([scene.detections(f, Kf, (FW, FH)) for f in fr], [scene.pose(f) for f in fr])
             sim["rec"].append(torch.from_numpy(rh).to(dev))
     torch.cuda.synchronize()
@@ -593,8 +619,8 @@ def main(argv=None):
 
     def run_steps(s0, s1, fusion, timer=None):
         for s in range(s0, s1):
-            o = s * B
-            sl = slice(o, o + B)
+            o = s * Bm
+            sl = slice(o, o + Bm)
             tb = time.perf_counter()
             k = s % n_inflight
             st_ctx = torch.cuda.stream(det_streams[k])
@@ -603,19 +629,27 @@ def main(argv=None):
             if nk_depth is not None:          # the step's non-keyframes: preprocessing only
                 _lib.depth_standardize(nk_depth[s])
             det(rgb_all[sl], depth_all[sl], poses_all[sl], return_instances=False,
-                crop_boxes=crops_all[s * B * args.crops:(s + 1) * B * args.crops])
+                crop_boxes=crops_all[s * Bm * args.crops:(s + 1) * Bm * args.crops])
             if args.breakdown:
                 torch.cuda.synchronize()
                 brk["detect"] += time.perf_counter() - tb
                 tb = time.perf_counter()
             bidx, iidx, cat_idx, feats, sims = det.last["clip"]
             clip = clip_rows(feats, sims, cat_idx)
-            g_rec, g_clip = gather_step(rec_all[sl], clip, dist, N)
+            recs = rec_all[sl]
+            if N > 1 and Bm < B:      # equal all-gather chunks: rank 0 pads to B frames
+                recs = torch.cat([recs, recs.new_zeros((B - Bm,) + tuple(recs.shape[1:]))])
+                clip = torch.cat([clip, clip.new_zeros(((B - Bm) * args.crops, clip.shape[1]))])
+            g_rec, g_clip = gather_step(recs, clip, dist, N)
+            if N > 1 and B0 < B and rank == 0:   # drop rank 0's padding: frames in global order
+                g_rec = torch.cat([g_rec[:B0], g_rec[B:]])
+                g_clip = torch.cat([g_clip[:B0 * args.crops], g_clip[B * args.crops:]])
             if sim is not None:       # --sim-ranks: rank 0 fuses the frames of R virtual ranks
                 g_rec = sim["rec"][s]
-                g_clip = g_clip.repeat(args.sim_ranks, 1)
+                reps = -(-sim["per_step"] // Bm)
+                g_clip = g_clip.repeat(reps, 1)[:sim["per_step"] * args.crops]
             if rank == 0:
-                base = s * (per_step if sim is None else B * args.sim_ranks)
+                base = s * (per_step if sim is None else sim["per_step"])
                 counts = [(base + j - s0 * (g_rec.shape[0])) * G for j in range(g_rec.shape[0])]
                 if args.sync_fusion:
                     g_pose, g_cnt = record_meta(g_rec)
@@ -659,8 +693,8 @@ def main(argv=None):
     # another thread's synchronising calls
     for k, d in enumerate(detects):
         with torch.cuda.stream(det_streams[k]):
-            d(rgb_all[:B], depth_all[:B], poses_all[:B], return_instances=False,
-              crop_boxes=crops_all[:B * args.crops])
+            d(rgb_all[:Bm], depth_all[:Bm], poses_all[:Bm], return_instances=False,
+              crop_boxes=crops_all[:Bm * args.crops])
     torch.cuda.synchronize()
 
     def make_fusion():
@@ -707,9 +741,9 @@ def main(argv=None):
         timer = _lib.KernelTimer()
         with timer:
             for s in range(args.warmup, min(total_steps, args.warmup + args.roofline_steps)):
-                sl = slice(s * B, s * B + B)
+                sl = slice(s * Bm, s * Bm + Bm)
                 detect(rgb_all[sl], depth_all[sl], poses_all[sl], return_instances=False,
-                       crop_boxes=crops_all[s * B * args.crops:(s + 1) * B * args.crops])
+                       crop_boxes=crops_all[s * Bm * args.crops:(s + 1) * Bm * args.crops])
         torch.cuda.synchronize()
         detect.use_graph = not args.eager
         source = f"eager re-run of {args.roofline_steps} timed steps"
@@ -741,6 +775,8 @@ def main(argv=None):
             v["measured"] = source
         r_all["measured"] = source
         line = base_line(args, N, frames, dt, per_step * G, n_inflight)
+        if B0 < B:
+            line["config"]["rank0_batch"] = B0
         if args.dataset == "ca1m":
             line["metric"] = "RGB-D frames/sec (whole node) on 384x512 portrait stream, depth at 1/2 resolution"
             line["data"] = ("synthetic CA-1M-shaped RGB-D stream (seeded; CA-1M data absent offline), random-init "
