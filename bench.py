@@ -276,6 +276,28 @@ def gather_step(recs, clip, dist, world):
     return g_rec, g_clip
 
 
+def rank_frames(step, rank, B, B0, per_step, G=1):
+    """frame ids a rank detects in a step: rank 0 the step's first B0 frames, rank r >= 1 the B
+    frames after B0 + (r - 1) B (per_step = B0 + (N - 1) B); gap G: every G-th frame"""
+    first = step * per_step + (0 if rank == 0 else B0 + (rank - 1) * B)
+    return [(first + j) * G for j in range(B0 if rank == 0 else B)]
+
+
+def exchange_step(recs, clip, dist, N, B, B0, crops, rank):
+    """gather_step with rank 0's smaller share: its chunk is padded to B frames (all_gather needs
+    equal chunks) and the padding is dropped from the gathered tensors on rank 0, so the fusion
+    owner sees the step's frames in global order"""
+    if N > 1 and recs.shape[0] < B:
+        pad = B - recs.shape[0]
+        recs = torch.cat([recs, recs.new_zeros((pad,) + tuple(recs.shape[1:]))])
+        clip = torch.cat([clip, clip.new_zeros((pad * crops,) + tuple(clip.shape[1:]))])
+    g_rec, g_clip = gather_step(recs, clip, dist, N)
+    if N > 1 and B0 < B and rank == 0:
+        g_rec = torch.cat([g_rec[:B0], g_rec[B:]])
+        g_clip = torch.cat([g_clip[:B0 * crops], g_clip[B * crops:]])
+    return g_rec, g_clip
+
+
 # ------------------------------------------------------------------------------------------------
 def cpu_baseline(cutr, clip_vis, args, scene):
     """The parity-checked CPU restatement timed on this host, both SURVEY §8(d) configs:
@@ -434,11 +456,13 @@ def rehearse_cpu(args, dist, world, rank):
     from boxfusion_amd.synthetic import Scene
     scene = Scene(seed=0, n_objects=args.scene_objects)
     B, N = args.batch, world
-    per_step = B * N
+    B0 = min(B, args.rank0_batch if args.rank0_batch > 0 else auto_rank0_batch(B, N)) if N > 1 else B
+    Bm = B0 if rank == 0 else B
+    per_step = B * N - (B - B0)
     total = args.warmup + args.steps
 
     def my_frames(step):
-        return [step * per_step + rank * B + j for j in range(B)]
+        return rank_frames(step, rank, B, B0, per_step)
 
     mine = [f for s_ in range(total) for f in my_frames(s_)]
     dets = [scene.detections(f) for f in mine]
@@ -451,10 +475,10 @@ def rehearse_cpu(args, dist, world, rank):
             if dist is not None:
                 dist.barrier()
             t0 = time.perf_counter()
-        sl = slice(s_ * B, s_ * B + B)
+        sl = slice(s_ * Bm, s_ * Bm + Bm)
         fr = torch.tensor(mine[sl], dtype=torch.float32)
         clip = fr.repeat_interleave(args.crops)[:, None].expand(-1, CLIP_W).contiguous()
-        g_rec, g_clip = gather_step(rec_all[sl], clip, dist, N)
+        g_rec, g_clip = exchange_step(rec_all[sl], clip, dist, N, B, B0, args.crops, rank)
         if rank == 0:
             want = [s_ * per_step + j for j in range(per_step)]
             g_pose, g_cnt = record_meta(g_rec)
@@ -473,6 +497,8 @@ def rehearse_cpu(args, dist, world, rank):
         dt = float(t.item())
     if rank == 0:
         line = base_line(args, N, per_step * args.steps, dt, per_step, 1)
+        if B0 < B:
+            line["config"]["rank0_batch"] = B0
         line.update(data="cpu rehearsal of the N-rank control flow (no kernels; not a measurement)",
                     rehearsal={"frame_order_ok": bool(ok), "frames_received": fused_frames})
         emit(line)
@@ -574,10 +600,8 @@ def main(argv=None):
     CFG["data"]["gap"] = G
 
     def my_frames(step):
-        """this rank's keyframes of a step (frame ids; gap G: every G-th frame of the stream):
-        rank 0 the first B0 of the step, rank r >= 1 the B after B0 + (r - 1) B"""
-        first = step * per_step + (0 if rank == 0 else B0 + (rank - 1) * B)
-        return [(first + j) * G for j in range(Bm)]
+        """this rank's keyframes of a step (frame ids; gap G: every G-th frame of the stream)"""
+        return rank_frames(step, rank, B, B0, per_step, G)
 
     # ---- inputs resident in HBM before timing -----------------------------------------------
     all_mine = [f for s in range(total_steps) for f in my_frames(s)]
@@ -636,14 +660,7 @@ def main(argv=None):
                 tb = time.perf_counter()
             bidx, iidx, cat_idx, feats, sims = det.last["clip"]
             clip = clip_rows(feats, sims, cat_idx)
-            recs = rec_all[sl]
-            if N > 1 and Bm < B:      # equal all-gather chunks: rank 0 pads to B frames
-                recs = torch.cat([recs, recs.new_zeros((B - Bm,) + tuple(recs.shape[1:]))])
-                clip = torch.cat([clip, clip.new_zeros(((B - Bm) * args.crops, clip.shape[1]))])
-            g_rec, g_clip = gather_step(recs, clip, dist, N)
-            if N > 1 and B0 < B and rank == 0:   # drop rank 0's padding: frames in global order
-                g_rec = torch.cat([g_rec[:B0], g_rec[B:]])
-                g_clip = torch.cat([g_clip[:B0 * args.crops], g_clip[B * args.crops:]])
+            g_rec, g_clip = exchange_step(rec_all[sl], clip, dist, N, B, B0, args.crops, rank)
             if sim is not None:       # --sim-ranks: rank 0 fuses the frames of R virtual ranks
                 g_rec = sim["rec"][s]
                 reps = -(-sim["per_step"] // Bm)

@@ -54,3 +54,29 @@ def test_bench_fp8_workload_line():
     assert line["config"]["workload"].startswith("configs[4]")
     assert "200-class" in line["config"]["workload"]
     assert "fp8" in line["dtype"]
+
+
+def test_bench_rank0_share_rehearsal():
+    """rank 0 (the fusion owner) detecting fewer frames: its all-gather chunk is padded and the
+    padding dropped, so rank 0 still receives every frame of the step in global order"""
+    r, lines = _bench("--gpus", "3", "--cpu-rehearsal", "--no-cpu-baseline", "--steps", "3",
+                      "--warmup", "1", "--batch", "4", "--rank0-batch", "2")
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(lines[0])
+    assert line["config"]["rank0_batch"] == 2
+    assert line["config"]["global_batch"] == 2 + 2 * 4
+    assert line["config"]["frames"] == 3 * 10
+    assert line["rehearsal"]["frame_order_ok"] is True
+    assert line["rehearsal"]["frames_received"] == 4 * 10
+
+
+def test_rank_frames_partition():
+    import bench
+    B, B0, N = 8, 6, 8
+    per = B0 + (N - 1) * B
+    for step in range(3):
+        got = sorted(f for r in range(N) for f in bench.rank_frames(step, r, B, B0, per))
+        assert got == list(range(step * per, (step + 1) * per))
+    assert bench.rank_frames(1, 0, B, B0, per, G=25) == [(per + j) * 25 for j in range(B0)]
+    assert bench.auto_rank0_batch(8, 1) == 8 and bench.auto_rank0_batch(8, 2) == 8
+    assert bench.auto_rank0_batch(8, 4) == 7 and bench.auto_rank0_batch(8, 8) == 6
