@@ -51,3 +51,4 @@ torch.cuda.synchronize()
 print(f"{1e3 * (time.perf_counter() - t0) / (steps * PER):.3f} ms/keyframe (plain)")
 ps = pstats.Stats(pr)
 ps.sort_stats("tottime").print_stats(25)
+ps.sort_stats("cumulative").print_stats(40)
