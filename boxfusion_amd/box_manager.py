@@ -9,6 +9,7 @@ bf_corr_assoc); `pack`/`unpack` move the lists to and from the kernels' fixed-ca
 from __future__ import annotations
 
 import copy
+import itertools
 
 import numpy as np
 import torch
@@ -24,6 +25,7 @@ class BoxManager:
         self.last_fusion_frame = []
         self._fusion_flag = []
         self._already_fusion = []
+        self._already_set, self._already_n = set(), 0   # tuple mirror of already_fusion (membership)
         self._pending = None      # resolves a deferred BoxFusion result (box_fusion.py)
         self.num_record = {}
         self.cfg = cfg
@@ -52,6 +54,7 @@ class BoxManager:
     @already_fusion.setter
     def already_fusion(self, v):
         self._already_fusion = v
+        self._already_n = -1                 # rebuild the membership mirror on the next check
 
     def flush(self):
         if self._pending is not None:
@@ -66,10 +69,20 @@ class BoxManager:
             self._fusion_flag.append(0)     # order-independent of a pending fusion result
 
     def add_fusion_ind(self, idx_list):
-        self._already_fusion.append(copy.deepcopy(idx_list))
+        row = copy.deepcopy(idx_list)
+        self._already_fusion.append(row)
+        if self._already_n == len(self._already_fusion) - 1:
+            self._already_set.add(tuple(row))
+            self._already_n += 1
 
     def check_if_fusion(self, idx_list):
-        return idx_list in self.already_fusion
+        """`idx_list in already_fusion` (list equality) as a set lookup on a tuple mirror: the list
+        grows with every fused box and is searched for every candidate of every keyframe"""
+        af = self.already_fusion
+        if self._already_n != len(af):      # appended to from outside: rebuild
+            self._already_set = {tuple(r) for r in af}
+            self._already_n = len(af)
+        return tuple(idx_list) in self._already_set
 
     def update(self, keep_idx):
         self.fusion_list = [self.fusion_list[i] for i in keep_idx]
@@ -133,20 +146,24 @@ class BoxManager:
 
     def pack_host(self):
         """fusion lists as host arrays (items [n, cap] padded with -1, lengths [n])"""
-        n = len(self.fusion_list)
+        fl = self.fusion_list
+        n = len(fl)
         cap = self.list_capacity
         items = np.full((max(n, 1), cap), -1, np.int32)
         lens = np.zeros(max(n, 1), np.int32)
-        for i, row in enumerate(self.fusion_list):
-            if len(row) > cap:
-                raise _lib.HipError(f"fusion list of {len(row)} > capacity {cap}; raise "
+        if n:
+            ln = np.fromiter(map(len, fl), np.int64, n)
+            if int(ln.max()) > cap:
+                raise _lib.HipError(f"fusion list of {int(ln.max())} > capacity {cap}; raise "
                                     "box_fusion.list_capacity")
-            items[i, :len(row)] = row
-            lens[i] = len(row)
+            lens[:n] = ln
+            rows = np.repeat(np.arange(n), ln)
+            cols = np.arange(int(ln.sum())) - np.repeat(np.cumsum(ln) - ln, ln)
+            items[rows, cols] = np.fromiter(itertools.chain.from_iterable(fl), np.int64, int(ln.sum()))
         return items, lens
 
     def unpack_host(self, items, lens):
-        self.fusion_list = [[int(v) for v in items[i, :lens[i]]] for i in range(len(self.fusion_list))]
+        self.fusion_list = [items[i, :lens[i]].tolist() for i in range(len(self.fusion_list))]
 
     def unpack(self, items, lens):
         it = items.cpu().numpy()
