@@ -524,7 +524,12 @@ __device__ __forceinline__ void attn2_softmax(f32x16 (&s)[2], bool sub1, bool ma
 // last query runs beside them in f32 VALU while each K/V tile is in LDS: wave w scores keys
 // 8w..8w+7 of the tile (lane group of 8 = one key, D/8 dims per lane), keeps its own online
 // softmax (m, l, o[D]); the eight partial states merge through LDS after the loop.
-template <int D, int NW, bool F8O = false, bool CAUSAL = false, bool XQ = false>
+// LW (light last wave, short heads with sq = 32 (NW - 1) + 1..16, CLIP's 257 tokens): waves 0..NW-2
+// take queries 0..32 (NW - 1) - 1 on 32x32x16 MFMAs; the last wave takes only the next 16 queries on
+// v_mfma_f32_16x16x32_bf16 (S^T = K Q^T in four 16-key blocks, O^T += V^T P^T in 16-row blocks with
+// the same transposed V reads and the ones row), i.e. half the MFMA cycles of a full 32-query wave
+// on the SIMD that holds three waves.  Its accumulators alias the registers of o / qf / s.
+template <int D, int NW, bool F8O = false, bool CAUSAL = false, bool XQ = false, bool LW = false>
 __global__ void __launch_bounds__(NW * 64) k_attn2(const u16* __restrict__ Q, const u16* __restrict__ K,
                                                       const u16* __restrict__ V, u16* __restrict__ O,
                                                       int sq, int sk, int q_rs, int k_rs, int v_rs,
@@ -549,15 +554,29 @@ __global__ void __launch_bounds__(NW * 64) k_attn2(const u16* __restrict__ Q, co
     const AttnBlk blk = attn_block(1);
     const int h = blk.h, b = blk.b;
     const int fr = lane & 31, fh = lane >> 5;
-    const int q = blk.qb * (NW * 32) + wave * 32 + fr;
+    static_assert(!LW || (ONES && !CAUSAL && !XQ && D % 16 == 0), "LW: short non-causal heads, D % 32 != 0");
+    constexpr int QPB = LW ? (NW - 1) * 32 + 16 : NW * 32;      // queries per workgroup
+    const bool light = LW && wave == NW - 1;                    // wave-uniform
+    const int c16 = lane & 15, g4 = lane >> 4;
+    const int q = blk.qb * QPB + (light ? (NW - 1) * 32 + c16 : wave * 32 + fr);
     const u16* Qb = Q + b * q_bs + h * D;
     const u16* Kb = K + b * k_bs + h * D;
     const u16* Vb = V + b * v_bs + h * D;
 
+    // the light wave's 16x16x32 operands: Q^T columns = its 16 queries, k = dims 32 ks + 8 g4 .. + 8
+    constexpr int KS16 = (D + 31) / 32;
     bf16x8 qf[KS];
+    if (light) {
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-        qf[ks] = *reinterpret_cast<const bf16x8*>(Qb + (size_t)min(q, sq - 1) * q_rs + 16 * ks + 8 * fh);
+        for (int ks = 0; ks < KS16; ++ks) {
+            const int d0 = 32 * ks + 8 * g4;
+            qf[ks] = d0 < D ? *reinterpret_cast<const bf16x8*>(Qb + (size_t)min(q, sq - 1) * q_rs + d0) : bf16x8{};
+        }
+    } else {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+            qf[ks] = *reinterpret_cast<const bf16x8*>(Qb + (size_t)min(q, sq - 1) * q_rs + 16 * ks + 8 * fh);
+    }
     // V padding columns: a ones column at d = D (the row sum), zeros after it
     if (VROW > D)
         for (int i = t; i < NBUF * AT_KT * (VROW - D); i += NT) {
@@ -707,7 +726,83 @@ __global__ void __launch_bounds__(NW * 64) k_attn2(const u16* __restrict__ Q, co
         }
         if constexpr (XQ) extra_query(kt, vt, k0);
     };
+    // LW: the light wave's tile.  S^T blocks: lane (c16, g4) holds query c16, keys 16 kb + 4 g4 + r;
+    // O^T block i (rows d = 16 i .. + 16) lives in o[i / 4][4 (i % 4) + r], r < 4
+    constexpr int NB16 = (D + 16) / 16;                          // D / 16 value blocks + the ones row
+    static_assert(!LW || NB16 * 4 <= DB * 16, "LW: O^T blocks alias o");
+    auto light_tile = [&](int tile, auto mask_tag) {
+        constexpr bool MASK = decltype(mask_tag)::value;
+        typedef float f32x4 __attribute__((ext_vector_type(4)));
+        const int k0 = tile * AT_KT;
+        const u16* kt = sK + (tile % NBUF) * KTILE;
+        const u16* vt = sV + (tile % NBUF) * VTILE;
+        f32x4 sl[4];
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+            sl[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < KS16; ++ks) {
+                const int d0 = 32 * ks + 8 * g4;
+                bf16x8 kf = *reinterpret_cast<const bf16x8*>(kt + (kb * 16 + c16) * KROW + (d0 < D ? d0 : 0));
+                if (d0 >= D) kf = bf16x8{};
+                sl[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], sl[kb], 0, 0, 0);
+            }
+        }
+        if (MASK) {
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (k0 + kb * 16 + 4 * g4 + r >= sk) sl[kb][r] = -INFINITY;
+        }
+        float mt = sl[0][0];
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mt = fmaxf(mt, sl[kb][r]);
+        mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+        mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * scale_log2;
+        if (__any(mt > m_run + AT2_THR)) {
+            const float m_new = fmaxf(m_run, mt);
+            const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+            m_run = m_new;
+#pragma unroll
+            for (int i = 0; i < NB16; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[i >> 2][4 * (i & 3) + r] *= alpha;
+        }
+        // P^T as the B operand: k-slots 8 g4 + j = keys 32 ks + 4 g4 + j (j < 4), 32 ks + 16 + 4 g4 + j - 4
+        bf16x8 pl[2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                pl[ks][j] = (__bf16)__builtin_amdgcn_exp2f(fmaf(sl[2 * ks + (j >> 2)][j & 3], scale_log2, -m_run));
+#pragma unroll
+        for (int i = 0; i < NB16; ++i) {
+            f32x4 acc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[r] = o[i >> 2][4 * (i & 3) + r];
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                // per 16-lane group: rows 32 ks + 4 g4 + q4 (+ 16), columns 16 i + 4 p4 -> lane c16 gets
+                // V^T row d = 16 i + c16 at those four keys
+                typedef __attribute__((address_space(3))) s16x4* lds_s4;
+                const u16* vb = vt + (32 * ks + 4 * g4 + q4) * VROW + 16 * i + 4 * p4;
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4)vb);
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4)(vb + 16 * VROW));
+                typedef short s16x8 __attribute__((ext_vector_type(8)));
+                const s16x8 lohi = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, lohi), pl[ks], acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[i >> 2][4 * (i & 3) + r] = acc[r];
+        }
+    };
     auto tile_body = [&](int tile, auto mask_tag) {
+        if constexpr (LW) {
+            if (light) { light_tile(tile, mask_tag); return; }
+        }
         f32x16 s[2];
         qk(tile, s, decltype(mask_tag)::value);
         sm_pv(tile, s, mask_tag);
@@ -782,6 +877,37 @@ __global__ void __launch_bounds__(NW * 64) k_attn2(const u16* __restrict__ Q, co
         }
     }
 
+    if constexpr (LW) {
+        if (light) {
+            // row sum: O^T row D = block D / 16, row D % 16 -> lane group (D % 16) / 4, register D % 4
+            constexpr int il = D / 16, rl = D % 16;
+            const float ll = __shfl(o[il >> 2][4 * (il & 3) + (rl & 3)], (rl >> 2) * 16 + c16, 64);
+            const long long lo_off = attn_out_offset(o_map, b, q, sq, o_bs, o_rs);
+            if (q < sq && lo_off >= 0) {
+                const float inv = 1.0f / ll;
+#pragma unroll
+                for (int i = 0; i < D / 16; ++i) {
+                    const int d0 = 16 * i + 4 * g4;
+                    float a[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) a[r] = o[i >> 2][4 * (i & 3) + r] * inv;
+                    if constexpr (F8O) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) a[r] = fminf(fmaxf(a[r] * oqs, -448.f), 448.f);
+                        int pk = __builtin_amdgcn_cvt_pk_fp8_f32(a[0], a[1], 0, false);
+                        pk = __builtin_amdgcn_cvt_pk_fp8_f32(a[2], a[3], pk, true);
+                        *reinterpret_cast<int*>(reinterpret_cast<unsigned char*>(O) + lo_off + h * D + d0) = pk;
+                    } else {
+                        V64 w;
+                        w.x = (uint32_t)at_f2bf(a[0]) | ((uint32_t)at_f2bf(a[1]) << 16);
+                        w.y = (uint32_t)at_f2bf(a[2]) | ((uint32_t)at_f2bf(a[3]) << 16);
+                        *reinterpret_cast<V64*>(O + lo_off + h * D + d0) = w;
+                    }
+                }
+            }
+            return;
+        }
+    }
     // row sum: the ones row D of O^T (lane half 0, register 8 of block D / 32) or the f32 sum
     float l;
     if (ONES) {
@@ -1316,7 +1442,8 @@ static int launch_attn_p(hipStream_t st, const void* q, const void* k, const voi
 // 1/2: k_attn_s (with / without the XCD block order), 3: k_attn_r for short sequences, 4/5:
 // k_attn_s with 5/3 waves per workgroup for short sequences, 0: k_attn.  Env BF_ATTN_VARIANT.
 // 9: k_attn_p (persistent, LDS-DMA ring 3 steps deep, next head's Q prefetched), 10: k_attn2 XQ
-// (8 MFMA waves + the 257th query in VALU).
+// (8 MFMA waves + the 257th query in VALU), 11: k_attn2 LW (8 MFMA waves + a ninth wave of 16
+// queries on 16x16x32 MFMAs).
 // Measured (scripts/attn_bench.py, one MI355X): CLIP 128x16x257x80 k_attn_s 153.7 us -> k_attn2
 // 128.6 us; CuTR windows 72x12x512x64 122.0 -> 109.9; CuTR global 8x12x1600x64 124.8 -> 105.0.
 // CLIP, this round: v6 130.9-132.5 us, v9 131.0 (equal: same FETCH, +9 M SALU / +7 M VALU for
@@ -1324,7 +1451,9 @@ static int launch_attn_p(hipStream_t st, const void* q, const void* k, const voi
 // waitcnt / barrier, 32 % issue-stalled; a 3-slot ring issuing tile t+1's S^T MFMAs beside tile
 // t's softmax on top of it: 149.7, dropped).  scripts/attn_rounds.py: 17 us per round of 256
 // (batch, head) workgroups from 1 to 16 rounds, also with every operand MALL-resident -- the
-// per-workgroup chain, not HBM, sets the time.
+// per-workgroup chain, not HBM, sets the time.  v11 130.9 us vs v6 130.8 in the same process
+// (the ninth wave's halved MFMA work is not on the critical path either); 16-byte epilogue
+// stores (halves of a query swapping 4-value chunks): 132.6, not kept.
 static int g_attn_variant = [] {
     const char* e = getenv("BF_ATTN_VARIANT");
     return e ? atoi(e) : 6;
@@ -1373,7 +1502,14 @@ BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, v
                                q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs, o_bs, sl2, o_map, 1.f);
         return bf_check_launch();
     }
-    if (g_attn_variant >= 6 && g_attn_variant <= 10) {
+    // variant 11: CLIP-like short heads (D = 80, 257..272 queries): 8 full waves + the light ninth
+    if (g_attn_variant == 11 && head_dim == 80 && nw_one == 9 && sq <= 8 * 32 + 16) {
+        hipLaunchKernelGGL((k_attn2<80, 9, false, false, false, true>), dim3(1, heads, batch), dim3(9 * 64), 0,
+                           bf_stream(stream), (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, sq, sk,
+                           q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs, o_bs, sl2, o_map, 1.f);
+        return bf_check_launch();
+    }
+    if (g_attn_variant >= 6 && g_attn_variant <= 11) {
 #define LAUNCH_2(DD, NWV)                                                                         \
     hipLaunchKernelGGL((k_attn2<DD, NWV>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch),    \
                        dim3(NWV * 64), 0, bf_stream(stream), (const u16*)q, (const u16*)k,          \
@@ -1477,6 +1613,11 @@ BF_API int bf_attention_fp8out(const void* q, const void* k, const void* v, void
 #define LAUNCH_8D(DD)                                                                             \
     if (g_attn_variant == 10 && nw_one == 9 && sq % 32 == 1) {                                    \
         hipLaunchKernelGGL((k_attn2<DD, 8, true, false, true>), dim3(1, heads, batch), dim3(512), 0,  \
+                           bf_stream(stream), (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, sq, \
+                           sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs, o_bs, sl2,                 \
+                           (const int32_t*)nullptr, out_qscale);                                    \
+    } else if (DD == 80 && g_attn_variant == 11 && nw_one == 9 && sq <= 8 * 32 + 16) {            \
+        hipLaunchKernelGGL((k_attn2<80, 9, true, false, false, true>), dim3(1, heads, batch), dim3(576), 0, \
                            bf_stream(stream), (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, sq, \
                            sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs, o_bs, sl2,                 \
                            (const int32_t*)nullptr, out_qscale);                                    \
