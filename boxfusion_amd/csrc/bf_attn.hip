@@ -1453,7 +1453,9 @@ static int launch_attn_p(hipStream_t st, const void* q, const void* k, const voi
 // (batch, head) workgroups from 1 to 16 rounds, also with every operand MALL-resident -- the
 // per-workgroup chain, not HBM, sets the time.  v11 130.9 us vs v6 130.8 in the same process
 // (the ninth wave's halved MFMA work is not on the critical path either); 16-byte epilogue
-// stores (halves of a query swapping 4-value chunks): 132.6, not kept.
+// stores (halves of a query swapping 4-value chunks): 132.6, not kept.  Softmax + P.V per 32-key
+// sub-tile (sub-tile 0's P.V MFMAs issued before sub-tile 1's exp work): 134.1-141.8 vs v6
+// 132.5-133.3 in three interleaved runs, not kept.
 static int g_attn_variant = [] {
     const char* e = getenv("BF_ATTN_VARIANT");
     return e ? atoi(e) : 6;
