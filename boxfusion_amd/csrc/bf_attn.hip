@@ -1455,7 +1455,8 @@ static int launch_attn_p(hipStream_t st, const void* q, const void* k, const voi
 // (the ninth wave's halved MFMA work is not on the critical path either); 16-byte epilogue
 // stores (halves of a query swapping 4-value chunks): 132.6, not kept.  Softmax + P.V per 32-key
 // sub-tile (sub-tile 0's P.V MFMAs issued before sub-tile 1's exp work): 134.1-141.8 vs v6
-// 132.5-133.3 in three interleaved runs, not kept.
+// 132.5-133.3 in three interleaved runs, not kept.  s_setprio 1 over the MFMA blocks: 129.2-133.1
+// vs 131.7-133.1 (the first variant in a run reads ~2 % slow: order bias), not kept.
 static int g_attn_variant = [] {
     const char* e = getenv("BF_ATTN_VARIANT");
     return e ? atoi(e) : 6;
