@@ -11,13 +11,17 @@
 // In torch that is a [B*nq*w, 512] hidden activation per axis, a broadcast [B,nq,h,w,heads] bias,
 // an index_put add, a clip and a softmax over [B,heads,Nq,h*w] — about 1.6 GB of HBM traffic per
 // decoder layer.  Here:
-//   k_cpb_mlp      8 lanes per (b, q, position), each over 1/8 of the hidden layer (weights in
-//                  LDS, broadcast reads), xor-shuffle reduction; writes rx / ry [B,nq,n,heads] only
+//   k_cpb_mlp_r    the reference width (hidden 512, 8 heads): one wave per 4 positions, every weight
+//                  in registers, a butterfly reduce-scatter of the 32 head sums; 28 us vs 57 us for
+//                  the LDS form at 8 x 300 x 40 (scripts/cpb_bench.py); writes rx / ry [B,nq,n,heads]
+//   k_cpb_mlp      other widths: 8 lanes per (b, q, position), each over 1/8 of the hidden layer
+//                  (weights in LDS, broadcast reads), xor-shuffle reduction
 //   k_rpe_softmax  one wave per attention row: the row's two 1-D bias tables into LDS, the row
 //                  read once, bias + clip + softmax, written once (in place)
 // Numerics: f32 throughout; the sums run in a fixed order (not the BLAS blocking of the torch
 // path), so results match the torch decoder to f32 rounding (tests compare with a tolerance).
 #include "bf_common.h"
+#include <cstdlib>
 
 #define CPB_MAX_HIDDEN 512
 #define CPB_MAX_HEADS 16
@@ -99,6 +103,85 @@ __global__ void __launch_bounds__(256) k_cpb_mlp(const float* __restrict__ ref, 
     }
 }
 
+// The reference shape (hidden 512, 8 heads): one wave per group of 4 positions, every weight in
+// registers (lane l owns hidden units l + 64 u, u < 8: w1, b1 and its 8 W2 entries = 88 VGPRs), no
+// LDS traffic in the loop.  Each lane accumulates the 4 x 8 partial head sums of its 8 units; a
+// butterfly reduce-scatter over the 64 lanes (xor 32 .. 2, then xor 1) leaves lane l with the total
+// of value (l >> 1) = (position (l >> 4), head (l >> 1) & 7), and the even lanes store the group's
+// 32 contiguous outputs.
+// one reduce-scatter step: lanes with (lane & SEL) keep values HALF..2 HALF-1, the others 0..HALF-1,
+// each adding its xor-SEL partner's copy of the values it keeps
+template <int HALF, int SEL>
+__device__ __forceinline__ void cpb_halve(float* acc, int lane) {
+    const bool up = (lane & SEL) != 0;
+#pragma unroll
+    for (int i = 0; i < HALF; ++i) {
+        const float keep = up ? acc[i + HALF] : acc[i];
+        const float give = up ? acc[i] : acc[i + HALF];
+        acc[i] = keep + __shfl_xor(give, SEL, 64);
+    }
+}
+#define CPB_R_UNITS 8
+#define CPB_R_HEADS 8
+#define CPB_R_POS 4
+__global__ void __launch_bounds__(256) k_cpb_mlp_r(const float* __restrict__ ref, long long total, int n,
+                                                   const float* __restrict__ pos, int axis,
+                                                   const float* __restrict__ w1,
+                                                   const float* __restrict__ b1,
+                                                   const float* __restrict__ w2, float* __restrict__ out) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float wa[CPB_R_UNITS], wb[CPB_R_UNITS], bb[CPB_R_UNITS], wt[CPB_R_UNITS][CPB_R_HEADS];
+#pragma unroll
+    for (int u = 0; u < CPB_R_UNITS; ++u) {
+        const int j = lane + 64 * u;
+        wa[u] = w1[2 * j];
+        wb[u] = w1[2 * j + 1];
+        bb[u] = b1[j];
+#pragma unroll
+        for (int hd = 0; hd < CPB_R_HEADS; ++hd) wt[u][hd] = w2[hd * 64 * CPB_R_UNITS + j];
+    }
+    const long long ngroups = (total + CPB_R_POS - 1) / CPB_R_POS;
+    const int last_bq = (int)((total - 1) / n), last_p = (int)((total - 1) % n);
+    for (long long g = (long long)blockIdx.x * 4 + wave; g < ngroups; g += (long long)gridDim.x * 4) {
+        float in0[CPB_R_POS], in1[CPB_R_POS];
+        // (box, position) of the group's first element by one division, then stepped (total < 2^31)
+        const int e0 = (int)g * CPB_R_POS;
+        int bq = e0 / n, p = e0 - bq * n;
+#pragma unroll
+        for (int pp = 0; pp < CPB_R_POS; ++pp) {
+            const bool live = e0 + pp < total;           // the tail group repeats the last element
+            const int pq = live ? p : last_p;
+            const float* r = ref + (size_t)(live ? bq : last_bq) * 4;
+            const float c = r[axis], half = r[2 + axis] / 2;
+            in0[pp] = (c - half) - pos[pq];
+            in1[pp] = (c + half) - pos[pq];
+            if (++p == n) { p = 0; ++bq; }
+        }
+        float acc[CPB_R_POS * CPB_R_HEADS];
+#pragma unroll
+        for (int i = 0; i < CPB_R_POS * CPB_R_HEADS; ++i) acc[i] = 0.f;
+#pragma unroll
+        for (int u = 0; u < CPB_R_UNITS; ++u)
+#pragma unroll
+            for (int pp = 0; pp < CPB_R_POS; ++pp) {
+                float hv = in0[pp] * wa[u] + in1[pp] * wb[u] + bb[u];
+                hv = hv > 0.f ? hv : 0.f;
+#pragma unroll
+                for (int hd = 0; hd < CPB_R_HEADS; ++hd) acc[pp * CPB_R_HEADS + hd] += wt[u][hd] * hv;
+            }
+        // reduce-scatter: at width w, lanes with bit (lane & sel) keep the upper half of the values
+        static_assert(CPB_R_POS * CPB_R_HEADS == 32, "five halving steps");
+        cpb_halve<16, 32>(acc, lane);
+        cpb_halve<8, 16>(acc, lane);
+        cpb_halve<4, 8>(acc, lane);
+        cpb_halve<2, 4>(acc, lane);
+        cpb_halve<1, 2>(acc, lane);
+        const float tot = acc[0] + __shfl_xor(acc[0], 1, 64);
+        const long long e = g * CPB_R_POS + (lane >> 4);
+        if ((lane & 1) == 0 && e < total) out[e * CPB_R_HEADS + ((lane >> 1) & 7)] = tot;
+    }
+}
+
 BF_API int bf_cpb_mlp(const float* ref, int B, int nq, const float* pos, int n, int axis,
                       const float* w1, const float* b1, const float* w2, int hidden, int heads,
                       float* out, void* stream) {
@@ -109,6 +192,14 @@ BF_API int bf_cpb_mlp(const float* ref, int B, int nq, const float* pos, int n, 
         return BF_ERR_CAPACITY;
     const long long total = (long long)B * nq * n;
     if (total == 0) return BF_OK;
+    static const int use_r = [] { const char* e = getenv("BF_CPB_VARIANT"); return e ? atoi(e) : 1; }();
+    if (use_r && hidden == 64 * CPB_R_UNITS && heads == CPB_R_HEADS && total < (1LL << 31) - CPB_R_POS) {
+        const long long groups = (total + CPB_R_POS - 1) / CPB_R_POS;
+        const long long blocks = (groups + 3) / 4;
+        hipLaunchKernelGGL(k_cpb_mlp_r, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0,
+                           bf_stream(stream), ref, total, n, pos, axis, w1, b1, w2, out);
+        return bf_check_launch();
+    }
     const long long blocks = (total * CPB_LANES + 255) / 256;
     hipLaunchKernelGGL(k_cpb_mlp, dim3((unsigned)(blocks < CPB_BLOCKS ? blocks : CPB_BLOCKS)), dim3(256), 0,
                        bf_stream(stream), ref, B, nq, pos, n, axis, w1, b1, w2, hidden, heads, out);

@@ -318,3 +318,24 @@ def test_unproject_vs_reference(dev):
                            torch.from_numpy(u["RT"]).to(dev), max_depth=10.0)
     np.testing.assert_array_equal(valid.cpu().numpy(), u["valid"])
     np.testing.assert_allclose(xyz.cpu().numpy(), u["xyz"], rtol=1e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("B,nq,n,hidden,heads", [(3, 301, 39, 512, 8), (1, 7, 5, 512, 8), (2, 50, 30, 256, 8)])
+def test_cpb_mlp_shapes_vs_torch(dev, B, nq, n, hidden, heads):
+    """bf_cpb_mlp against Linear(2, hidden) + ReLU + Linear(hidden, heads) in f32: the register form
+    (hidden 512, 8 heads) with a ragged last group of positions (B*nq*n % 4 != 0), and the LDS form
+    for other widths"""
+    from boxfusion_amd import _lib
+    g = torch.Generator(device=dev).manual_seed(B * nq + n)
+    ref = torch.rand(B, nq, 4, device=dev, generator=g) * 400
+    pos = torch.linspace(0.5, n - 0.5, n, device=dev) * 16
+    w1 = torch.randn(hidden, 2, device=dev, generator=g) * 0.05
+    b1 = torch.randn(hidden, device=dev, generator=g)
+    w2 = torch.randn(heads, hidden, device=dev, generator=g) * 0.05
+    for axis in (0, 1):
+        got = _lib.cpb_mlp(ref, pos, axis, w1, b1, w2)
+        c, half = ref[..., axis], ref[..., 2 + axis] / 2
+        x = torch.stack([(c - half)[..., None] - pos, (c + half)[..., None] - pos], -1)
+        want = torch.relu(x @ w1.t() + b1) @ w2.t()
+        assert got.shape == (B, nq, n, heads)
+        torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4)
