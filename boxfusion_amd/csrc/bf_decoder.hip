@@ -344,7 +344,7 @@ typedef float xa_f32x16 __attribute__((ext_vector_type(16)));
 // CubifyTransformer.decode: the q0 metric queries see only the q0 metric keys, the box queries
 // only the box keys): no bias tables, keys = queries (N = Nq), key j valid for query i iff
 // (j < q0) == (i < q0).
-template <bool SELF, bool PK = false>
+template <bool SELF>
 __global__ void __launch_bounds__(XA_WAVES * 64) k_xattn(
     const float* __restrict__ q, int ldq, const float* __restrict__ k, int ldk,
     const float* __restrict__ v, int ldv, const float* __restrict__ rx, const float* __restrict__ ry,
@@ -391,23 +391,21 @@ __global__ void __launch_bounds__(XA_WAVES * 64) k_xattn(
     for (int r = 0; r < 16; ++r) o[r] = 0.f;
     float m_run = -INFINITY, l_run = 0.f;
     const float FMAX = 3.40282347e38f;
-    // PK: the next block's K fragment is loaded while this block computes
-    auto load_k = [&](int kb_, float (&dst)[16]) {
-        const int key = min(kb_ * 32 + jq, N - 1);
-        const float* kp = kbase + (size_t)key * ldk + 16 * hf;
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-            const float4 x = *reinterpret_cast<const float4*>(kp + 4 * s4);
-            dst[4 * s4 + 0] = x.x; dst[4 * s4 + 1] = x.y; dst[4 * s4 + 2] = x.z; dst[4 * s4 + 3] = x.w;
-        }
-    };
-    float kf[16];
-    if (PK && kb0 < kb1) load_k(kb0, kf);
     for (int kb = kb0; kb < kb1; ++kb) {
         // K fragment: key kb*32 + jq, dims 16*hf + [0,16).  (Loading the next block's K / V a
-        // block ahead cost occupancy and measured slower: 96.7 -> 108.9 us per decoder layer.)
-        float kn[16];
-        if (!PK) load_k(kb, kf);
+        // block ahead cost occupancy and measured slower: 96.7 -> 108.9 us per decoder layer; the
+        // next K alone, 123 VGPRs: 97.9-98.0 vs 98.0-99.2 us, bit-identical, not kept --
+        // scripts/xattn_bench.py.)
+        float kf[16];
+        {
+            const int key = min(kb * 32 + jq, N - 1);
+            const float* kp = kbase + (size_t)key * ldk + 16 * hf;
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const float4 x = *reinterpret_cast<const float4*>(kp + 4 * s4);
+                kf[4 * s4 + 0] = x.x; kf[4 * s4 + 1] = x.y; kf[4 * s4 + 2] = x.z; kf[4 * s4 + 3] = x.w;
+            }
+        }
         // V^T fragment per k-step s: V[key of S^T register s in half hf][dim jq]
         float vf[16];
 #pragma unroll
@@ -418,7 +416,6 @@ __global__ void __launch_bounds__(XA_WAVES * 64) k_xattn(
         xa_f32x16 sc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) sc[r] = 0.f;
-        if (PK) load_k(min(kb + 1, kb1 - 1), kn);
 #pragma unroll
         for (int s = 0; s < 16; ++s) sc = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[s], qf[s], sc, 0, 0, 0);
         // bias, clip, mask; register r holds key kb*32 + (r&3) + 8*(r>>2) + 4*hf
@@ -468,10 +465,6 @@ __global__ void __launch_bounds__(XA_WAVES * 64) k_xattn(
         }
 #pragma unroll
         for (int s = 0; s < 16; ++s) o = __builtin_amdgcn_mfma_f32_32x32x2f32(vf[s], sc[s], o, 0, 0, 0);
-        if (PK) {
-#pragma unroll
-            for (int s = 0; s < 16; ++s) kf[s] = kn[s];
-        }
     }
     // combine the 4 waves: O^T lane (jq, hf) register r = dim (r&3) + 8*(r>>2) + 4*hf of query jq
     l_run += __shfl_xor(l_run, 32, 64);
@@ -518,13 +511,8 @@ BF_API int bf_xattn_f32(const float* q, int ldq, const float* k, int ldk, const 
     if (hh > XA_MAX_SIDE || ww > XA_MAX_SIDE || ww < 4) return BF_ERR_CAPACITY;
     if (B == 0 || Nq == 0) return BF_OK;
     const int N = hh * ww;
-    static const int var = [] { const char* e = getenv("BF_XATTN_VARIANT"); return e ? atoi(e) : 0; }();
-    if (var == 1)
-        hipLaunchKernelGGL((k_xattn<false, true>), dim3((Nq + 31) / 32, H, B), dim3(XA_WAVES * 64), 0,
-                           bf_stream(stream), q, ldq, k, ldk, v, ldv, rx, ry, out, ldo, H, Nq, N, q0, hh, ww, scale);
-    else
-        hipLaunchKernelGGL(k_xattn<false>, dim3((Nq + 31) / 32, H, B), dim3(XA_WAVES * 64), 0, bf_stream(stream), q,
-                           ldq, k, ldk, v, ldv, rx, ry, out, ldo, H, Nq, N, q0, hh, ww, scale);
+    hipLaunchKernelGGL(k_xattn<false>, dim3((Nq + 31) / 32, H, B), dim3(XA_WAVES * 64), 0, bf_stream(stream), q,
+                       ldq, k, ldk, v, ldv, rx, ry, out, ldo, H, Nq, N, q0, hh, ww, scale);
     return bf_check_launch();
 }
 

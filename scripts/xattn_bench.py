@@ -1,6 +1,5 @@
 """Microbenchmark of the decoder's fused RPE cross-attention (bf_xattn_f32) at the decoder shape
-(8 frames x 302 queries x 8 heads x 32 dims over a 40x40 memory); the BF_XATTN_VARIANT env var
-selects the kernel form in the library."""
+(8 frames x 302 queries x 8 heads x 32 dims over a 40x40 memory)."""
 import os
 import sys
 import torch
@@ -25,5 +24,5 @@ for _ in range(20):
     _lib.xattn(q, k, v, rx, ry, hh, ww, q0, H, 32 ** -0.5, out=out)
 e1.record()
 torch.cuda.synchronize()
-print(f"xattn variant {os.environ.get('BF_XATTN_VARIANT', 'default')}: {e0.elapsed_time(e1) / 20 * 1e3:.1f} us"
+print(f"xattn: {e0.elapsed_time(e1) / 20 * 1e3:.1f} us"
       f"  checksum {out.double().sum().item():.6f}", flush=True)
