@@ -476,8 +476,12 @@ class CubifyTransformer(nn.Module):
         engines = self.__dict__.setdefault("_engines", {})
         if key not in engines:
             engines[key] = CuTREngine(self, B, H, W, pad=x["pad"], device=raw.device, depth_ratio=x["ratio"])
-        return engines[key](raw.contiguous(), x["depth_std"], x["depth_params"], x["K"], x["T_gravity"],
-                            x["image_sizes"], chw=True, pixel_mean=x["pixel_mean"], pixel_std=x["pixel_std"])
+        res = engines[key](raw.contiguous(), x["depth_std"], x["depth_params"], x["K"], x["T_gravity"],
+                           x["image_sizes"], chw=True, pixel_mean=x["pixel_mean"], pixel_std=x["pixel_std"])
+        # the engine's instances are views of its persistent output buffers (the next call reuses
+        # them); the reference's model(packaged) hands out fresh tensors, so the boundary copies
+        # (100 rows per frame, one small device copy per field)
+        return [r.clone() for r in res]
 
     def _memory_kv(self, src, pos):
         """Every decoder layer's cross-attention k(src + pos) and v(src) in one GEMM each (the

@@ -31,15 +31,26 @@ def value_for(name, shape, seed=0, std=0.02):
     return (std * rng.standard_normal(shape)).astype(np.float32)
 
 
-def seeded_state_dict(model: torch.nn.Module, seed=0, std=0.02):
+UNIFORM_QUERY_KEY = "prompting.prompters.1.query_embed.weight"
+
+
+def seeded_state_dict(model: torch.nn.Module, seed=0, std=0.02, uniform_queries=False):
+    """uniform_queries: every row of the encoder-proposal content embedding (EncoderProposals.
+    query_embed, cubify_transformer.py:759,830) set to row 0.  The decoder is then equivariant to
+    the order of its 300 proposal queries (self-attention without a mask, per-query cross-
+    attention and heads), so near-tied encoder logits that bf16 rounding reorders no longer swap
+    which content row a proposal gets: the end-to-end instances become comparable one by one."""
     sd = model.state_dict()
     out = {}
     for k, v in sd.items():
         val = value_for(k, tuple(v.shape), seed, std)
         out[k] = v.clone() if val is None else torch.from_numpy(val).to(v.dtype)
+    if uniform_queries:
+        q = out[UNIFORM_QUERY_KEY]
+        out[UNIFORM_QUERY_KEY] = q[:1].expand_as(q).clone()
     return out
 
 
-def init_seeded(model: torch.nn.Module, seed=0, std=0.02):
-    model.load_state_dict(seeded_state_dict(model, seed, std))
+def init_seeded(model: torch.nn.Module, seed=0, std=0.02, uniform_queries=False):
+    model.load_state_dict(seeded_state_dict(model, seed, std, uniform_queries))
     return model

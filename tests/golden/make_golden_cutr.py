@@ -150,6 +150,17 @@ def run_case(name, dim, frame, seed, H, W, ratio, K, thr, keep_features=False):
         boxes3d=pred.pred_boxes_3d.tensor.numpy(), R=pred.pred_boxes_3d.R.numpy(),
         object_desc=pred.object_desc.numpy().astype(np.float16),
         pred_proj_xy=pred.pred_proj_xy.numpy())
+    # the same frame with the proposal content embedding made uniform (weights.py
+    # uniform_queries): the end-to-end GPU test compares these instances one by one
+    model_u = make_cubify_transformer(dimension=dim, depth_model=True).eval()
+    model_u.load_state_dict(seeded_state_dict(model_u, seed, uniform_queries=True))
+    with torch.no_grad():
+        pu = model_u(packaged)[0]
+    out.update(uq_scores=pu.scores.numpy(), uq_pred_classes=pu.pred_classes.numpy(),
+               uq_pred_boxes=pu.pred_boxes.numpy(), uq_pred_logits=pu.pred_logits.numpy(),
+               uq_boxes3d=pu.pred_boxes_3d.tensor.numpy(), uq_R=pu.pred_boxes_3d.R.numpy(),
+               uq_object_desc=pu.object_desc.numpy().astype(np.float16),
+               uq_pred_proj_xy=pu.pred_proj_xy.numpy())
     if keep_features:
         out["features"] = feats.numpy()          # f32: the GPU test feeds them to the decoder
     out["depth_sum"] = np.float64(sensor["depth"].data.tensor.double().sum())

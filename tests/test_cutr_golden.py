@@ -49,12 +49,48 @@ def cpu_frame_batch(g):
                       image_sizes=[(int(g["H"]), int(g["W"]))]), params
 
 
-def model_for(g):
+def model_for(g, uniform_queries=False):
     from boxfusion_amd.cubify_transformer import make_cubify_transformer
     from boxfusion_amd.weights import init_seeded
     torch.manual_seed(0)
     m = make_cubify_transformer(int(g["dim"]), depth_model=True).eval()
-    return init_seeded(m, int(g["seed"]))
+    return init_seeded(m, int(g["seed"]), uniform_queries=uniform_queries)
+
+
+INSTANCE_FIELDS = ("scores", "pred_classes", "pred_boxes", "pred_logits", "boxes3d", "R", "object_desc",
+                   "pred_proj_xy")
+
+
+def uniform_view(g):
+    """the golden's uniform-query run (make_golden_cutr.py, weights.uniform_queries) under the
+    plain instance field names"""
+    out = dict(g)
+    out.update({k: g["uq_" + k] for k in INSTANCE_FIELDS})
+    return out
+
+
+def instance_arrays(r):
+    return dict(scores=r.scores.cpu().numpy(), pred_classes=r.pred_classes.cpu().numpy(),
+                pred_boxes=r.pred_boxes.cpu().numpy(), pred_logits=r.pred_logits.cpu().numpy(),
+                boxes3d=r.pred_boxes_3d.tensor.cpu().numpy(), R=r.pred_boxes_3d.R.cpu().numpy(),
+                object_desc=r.object_desc.cpu().float().numpy(), pred_proj_xy=r.pred_proj_xy.cpu().numpy())
+
+
+def match_instances(got, g, box_px=0.5):
+    """pair each golden instance with the got instance of the same class whose 2-D box is nearest
+    (boxes of different proposals sit >= 8 px apart; the same proposal appears at most once per
+    class).  Returns (golden index, got index) pairs and the unpaired golden indices."""
+    pairs, unpaired, used = [], [], set()
+    for i in range(len(g["scores"])):
+        d = np.abs(got["pred_boxes"] - g["pred_boxes"][i]).max(1)
+        d[got["pred_classes"] != g["pred_classes"][i]] = np.inf
+        j = int(np.argmin(d))
+        if d[j] <= box_px and j not in used:
+            pairs.append((i, j))
+            used.add(j)
+        else:
+            unpaired.append(i)
+    return pairs, unpaired
 
 
 @pytest.fixture(scope="module")
@@ -104,6 +140,29 @@ def test_forward_matches_reference(case):
             assert ((feat - ref).norm() / ref.norm()).item() < 2e-3
         r = m(batch)[0]
     assert_instances(r, g)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_forward_uniform_queries_matches_reference(case):
+    """the uniform-query fixture (the one the GPU end-to-end test pairs instance by instance):
+    the fp32 restatement reproduces the reference rank by rank, and with every backbone feature
+    perturbed at the bf16 backbone's size (3e-3 relative) >= 97 of 100 instances still pair up
+    one by one (the decoder is equivariant to the order of its proposal queries)"""
+    torch.set_num_threads(8)
+    g = TU.load(case)
+    gu = uniform_view(g)
+    m = model_for(g, uniform_queries=True)
+    batch, _ = cpu_frame_batch(g)
+    with torch.no_grad():
+        feat = m.backbone.backbone.forward_tensors(batch.image, batch.depth)
+        r = m.decode(feat, batch)[0]
+        assert_instances(r, gu, min_ok=30)
+        # equivariance: the same decode with every proposal feature perturbed at 3e-3 relative
+        # (the bf16 backbone's size) still pairs >= 97 of 100 instances with the reference
+        gen = torch.Generator().manual_seed(1)
+        r2 = m.decode(feat + 3e-3 * feat.std() * torch.randn(feat.shape, generator=gen), batch)[0]
+    pairs, unpaired = match_instances(instance_arrays(r2), gu)
+    assert len(pairs) >= 97, unpaired
 
 
 def test_filters_match_reference():
