@@ -808,6 +808,10 @@ def main(argv=None):
             line["config"]["keyframes"] = per_step * args.steps
         line["config"].update(scene_objects=args.scene_objects, fused_boxes=fusion.stats["fused"],
                               global_boxes=len(fusion.all_pred_box) if fusion.all_pred_box is not None else 0)
+        # box-fusion calls with a particle whose 2-D intersection hull exceeds the reference
+        # kernel's convex_inter[8] (box_fusion.py:381: undefined behaviour there; exact hull here)
+        line["hull_overflow"] = {"calls": fusion.fuser.hull_overflow_calls,
+                                 "fusion_calls": fusion.fuser.fit_calls}
         if args.clip_fp8:
             f8 = roofline_obj(timer.summary(lambda t: t["kind"] == "gemm_fp8"),
                               "k_gemm256p<*, *, fp8> (CLIP qkv, fc1 + GELU -> fp8, fc2 + f32 residual; "

@@ -24,6 +24,7 @@ BF_DEV_FUSION_LIST_OVERFLOW = 1
 BF_DEV_HULL_OVERFLOW = 2
 BF_DEV_VIEW_OVERFLOW = 4
 BF_DEV_INDEX_RANGE = 8
+BF_DEV_HULL_TRUNC = 16
 
 
 class NmsCfg(ctypes.Structure):
@@ -179,12 +180,16 @@ _STATUS = {}
 
 
 def status_word(device):
-    """persistent int32 device word per device that rows_gather launches without a caller status
-    OR their BF_DEV_* flags into (an out-of-range index skips its row); check_status() reads and
-    clears it -- FusionStage does so at the read-back it already makes per keyframe"""
-    key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+    """persistent int32 device word per (device, host thread) that rows_gather launches without a
+    caller status OR their BF_DEV_* flags into (an out-of-range index skips its row);
+    check_status() reads and clears it -- FusionStage does so at the read-back it already makes
+    per keyframe.  One word per thread: the fusion worker's flags never mix with (or get cleared
+    by) another thread's reads."""
+    import threading
+    d = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+    key = (d, threading.get_ident())
     if key not in _STATUS:
-        _STATUS[key] = torch.zeros(1, dtype=torch.int32, device=torch.device("cuda", key))
+        _STATUS[key] = torch.zeros(1, dtype=torch.int32, device=torch.device("cuda", d))
     return _STATUS[key]
 
 

@@ -29,6 +29,20 @@ def load_pst(path=None):
     return np.load(os.path.join(DATA, "pst_1024_0.npy")).astype(np.float32)
 
 
+_HULL_WARNED = [False]
+
+
+def _warn_hull_once():
+    if _HULL_WARNED[0]:
+        return
+    _HULL_WARNED[0] = True
+    warnings.warn("BoxFusion.boxfusion: a particle's 2-D intersection hull has more than the 8 points "
+                  "the reference kernel's convex_inter[8] holds (box_fusion.py:381; undefined "
+                  "behaviour there); the exact hull was used.  BoxFusion.hull_overflow_calls counts "
+                  "the calls; cfg box_fusion.strict_hull=True raises instead.", RuntimeWarning,
+                  stacklevel=4)
+
+
 class BoxFusion:
     def __init__(self, cfg, device="cuda", legacy_promotion=True):
         self.cfg = cfg
@@ -48,6 +62,12 @@ class BoxFusion:
             if os.path.exists(kd):
                 Kd = np.loadtxt(kd).reshape(3, 3)
                 self.K[:3, :3] = [[Kd[0, 0], 0.0, Kd[0, 2]], [0.0, Kd[1, 1], Kd[1, 2]], [0, 0, 1]]
+            elif "fx" not in cam:
+                # the reference's np.loadtxt raises here; demo.py:117 would replace K before the
+                # first fusion anyway, so warn (a run without update_intrinsics fuses with K = I)
+                warnings.warn(f"BoxFusion: {kd} not found and cfg.cam has no fx: K stays identity "
+                              "until update_intrinsics() (the reference raises here)", RuntimeWarning,
+                              stacklevel=2)
             self.H, self.W = cam.get("W", 480), cam.get("H", 640)
         self.update_K_flag = False
         bf = cfg["box_fusion"]
@@ -67,8 +87,8 @@ class BoxFusion:
         # BF_DEV_HULL_OVERFLOW policy: False = count + warn once (the exact hull is used),
         # True = raise (cfg box_fusion.strict_hull)
         self.strict_hull = bool(bf.get("strict_hull", False))
-        self.hull_overflow_calls = 0
-        self._warned_hull = False
+        self.hull_overflow_calls = 0    # boxfusion calls with >= 1 such evaluation
+        self.fit_calls = 0              # boxfusion calls that refined >= 1 box
 
     def update_intrinsics(self, size, K):
         self.H = size[1]
@@ -110,6 +130,7 @@ class BoxFusion:
         self.last_stats = dict(jobs=len(jobs), updated=0, views=sum(len(f) for _, f in jobs))
         if not jobs:
             return
+        self.fit_calls += 1
         dev = self.device
         nj = len(jobs)
         nv = np.array([len(fl) for _, fl in jobs], np.int32)
@@ -149,21 +170,21 @@ class BoxFusion:
                 raise _lib.HipError("bf_fusion_fit: a fusion list has more views than the kernel holds")
             if st & _lib.BF_DEV_INDEX_RANGE:
                 raise _lib.HipError("boxfusion: a fusion list names a per-frame box that does not exist")
+            if st & _lib.BF_DEV_HULL_TRUNC:
+                raise _lib.HipError("bf_fusion_fit: more 2-D intersection candidates than the kernel "
+                                    "holds (BF_DEV_HULL_TRUNC): the IoU would not be exact")
             if st & _lib.BF_DEV_HULL_OVERFLOW:
                 # an intersection polygon with more points than the reference kernel's fixed
                 # buffers hold (convex_inter[8] / corners_i[36], box_fusion.py:378-384; two
                 # overlapping projected hexagons can intersect in up to 12 points): the reference
-                # writes past its array there, the kernel here keeps 64 slots and returns the
-                # intended IoU.  Counted (and warned once) by default; strict_hull raises.
+                # writes past its stack arrays there (undefined behaviour), the kernel here keeps
+                # 64 slots and returns the exact IoU.  Counted per call (hull_overflow_calls) and
+                # warned once per process by default; strict_hull raises.
                 self.hull_overflow_calls += 1
                 if self.strict_hull:
                     raise _lib.HipError("bf_fusion_fit: hull capacity exceeded (BF_DEV_HULL_OVERFLOW): "
                                         "the reference kernel overruns its fixed buffers on this input")
-                if not self._warned_hull:
-                    self._warned_hull = True
-                    warnings.warn("bf_fusion_fit: an intersection hull exceeded the reference kernel's "
-                                  "8-point buffer (BF_DEV_HULL_OVERFLOW); the exact hull was used",
-                                  RuntimeWarning, stacklevel=2)
+                _warn_hull_once()
             n_upd = 0
             for j, (i, fl) in enumerate(jobs):
                 if upd[j]:

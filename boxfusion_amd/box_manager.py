@@ -19,13 +19,40 @@ from boxfusion_amd import _lib
 DEFAULT_LIST_CAPACITY = 64
 
 
+class _TrackedList(list):
+    """already_fusion: a list whose in-place changes bump `version`, so the membership mirror of
+    BoxManager.check_if_fusion is rebuilt after any outside edit (append, item assignment, pop,
+    slice writes, ...), not only after length changes.  Rows themselves are treated as values
+    (the reference deep-copies them on insertion, box_manager.py:31)."""
+    __slots__ = ("version",)
+
+    def __init__(self, *a):
+        super().__init__(*a)
+        self.version = 0
+
+
+def _bumping(name):
+    base = getattr(list, name)
+
+    def f(self, *a, **k):
+        self.version += 1
+        return base(self, *a, **k)
+    f.__name__ = name
+    return f
+
+
+for _m in ("append", "extend", "insert", "pop", "remove", "clear", "sort", "reverse", "__setitem__",
+           "__delitem__", "__iadd__", "__imul__"):
+    setattr(_TrackedList, _m, _bumping(_m))
+
+
 class BoxManager:
     def __init__(self, cfg):
         self.fusion_list = []
         self.last_fusion_frame = []
         self._fusion_flag = []
-        self._already_fusion = []
-        self._already_set, self._already_n = set(), 0   # tuple mirror of already_fusion (membership)
+        self._already_fusion = _TrackedList()
+        self._already_set, self._already_ver = set(), 0   # tuple mirror of already_fusion (membership)
         self._pending = None      # resolves a deferred BoxFusion result (box_fusion.py)
         self.num_record = {}
         self.cfg = cfg
@@ -53,8 +80,8 @@ class BoxManager:
 
     @already_fusion.setter
     def already_fusion(self, v):
-        self._already_fusion = v
-        self._already_n = -1                 # rebuild the membership mirror on the next check
+        self._already_fusion = _TrackedList(v)
+        self._already_ver = -1               # rebuild the membership mirror on the next check
 
     def flush(self):
         if self._pending is not None:
@@ -70,18 +97,20 @@ class BoxManager:
 
     def add_fusion_ind(self, idx_list):
         row = copy.deepcopy(idx_list)
-        self._already_fusion.append(row)
-        if self._already_n == len(self._already_fusion) - 1:
+        af = self._already_fusion
+        in_sync = self._already_ver == af.version
+        af.append(row)
+        if in_sync:                          # keep the mirror incrementally
             self._already_set.add(tuple(row))
-            self._already_n += 1
+            self._already_ver = af.version
 
     def check_if_fusion(self, idx_list):
         """`idx_list in already_fusion` (list equality) as a set lookup on a tuple mirror: the list
         grows with every fused box and is searched for every candidate of every keyframe"""
         af = self.already_fusion
-        if self._already_n != len(af):      # appended to from outside: rebuild
+        if self._already_ver != af.version:  # changed from outside: rebuild
             self._already_set = {tuple(r) for r in af}
-            self._already_n = len(af)
+            self._already_ver = af.version
         return tuple(idx_list) in self._already_set
 
     def update(self, keep_idx):

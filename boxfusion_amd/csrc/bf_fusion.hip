@@ -18,7 +18,9 @@
 // Arithmetic follows the reference kernel's float32 (+ f64 line intersection) expression by
 // expression; compiled with -ffp-contract=off.  Hull buffers have fixed capacity; inputs that
 // would overflow the reference's own fixed buffers (corners_i[36], convex_inter[8]) set
-// BF_DEV_HULL_OVERFLOW (the result is still the mathematically intended one).
+// BF_DEV_HULL_OVERFLOW (the result is still the mathematically intended one); more candidates
+// than this kernel's own 64 slots set BF_DEV_HULL_TRUNC (never seen: two convex 8-gons give at
+// most 16 vertices + 32 crossings; the host raises on it).
 #include "bf_common.h"
 
 #define FUSE_MAX_VIEWS 32
@@ -118,12 +120,12 @@ __device__ float iou_hull_pre(P2* c0, const P2* ht, int nt, float at, int* flags
     for (int i = 0; i < n0; ++i)
         if (point_in_polygon(h0[i], ht, nt)) {
             if (nc < CAND_CAP) cand[nc++] = h0[i];
-            else *flags |= BF_DEV_HULL_OVERFLOW;
+            else *flags |= BF_DEV_HULL_TRUNC;
         }
     for (int i = 0; i < nt; ++i)
         if (point_in_polygon(ht[i], h0, n0)) {
             if (nc < CAND_CAP) cand[nc++] = ht[i];
-            else *flags |= BF_DEV_HULL_OVERFLOW;
+            else *flags |= BF_DEV_HULL_TRUNC;
         }
     for (int i = 0; i < n0; ++i)
         for (int j = 0; j < nt; ++j) {
@@ -132,7 +134,7 @@ __device__ float iou_hull_pre(P2* c0, const P2* ht, int nt, float at, int* flags
             P2 pt;
             if (line_intersection(a1, a2, b1, b2, &pt)) {
                 if (nc < CAND_CAP) cand[nc++] = pt;
-                else *flags |= BF_DEV_HULL_OVERFLOW;
+                else *flags |= BF_DEV_HULL_TRUNC;
             }
         }
     if (nc > 36) *flags |= BF_DEV_HULL_OVERFLOW;

@@ -50,8 +50,10 @@ def _clean(text):
 
 
 class SimpleTokenizer:
-    PAT = re.compile(r"""<\|startoftext\|>|<\|endoftext\|>|'s|'t|'re|'ve|'m|'ll|'d|[\p{L}]+|[\p{N}]|[^\s\p{L}\p{N}]+""",
-                     re.IGNORECASE)
+    # open_clip builds the pattern from its own special tokens (SOT / EOT above), so a special
+    # inside the text is one token
+    PAT = re.compile("|".join(re.escape(t) for t in (SOT, EOT)) +
+                     r"""|'s|'t|'re|'ve|'m|'ll|'d|[\p{L}]+|[\p{N}]|[^\s\p{L}\p{N}]+""", re.IGNORECASE)
 
     def __init__(self, merges, n_merges=49152 - 256 - 2):
         """merges: path of a BPE merges file (.txt or .txt.gz; first line is a header), or a list

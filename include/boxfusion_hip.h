@@ -38,6 +38,8 @@ typedef enum {
 #define BF_DEV_HULL_OVERFLOW 2          /* a 2-D hull / clip buffer exceeded its capacity */
 #define BF_DEV_VIEW_OVERFLOW 4          /* a fusion job has 0 or more than 32 views (skipped) */
 #define BF_DEV_INDEX_RANGE 8            /* a gather index outside its source rows (row skipped) */
+#define BF_DEV_HULL_TRUNC 16            /* more 2-D intersection candidates than the fitness kernel
+                                           holds (64): candidates dropped, the IoU is not exact */
 
 #define BF_MAX_BOXES 4096               /* NMS / association scan limit per call */
 

@@ -33,6 +33,15 @@ def lib():
     return _LIB
 
 
+def hull_overflow(reset=True):
+    """(calls with > 36 intersection candidates, calls with an intersection hull > 8 points) since
+    the last reset: the reference kernel's corners_i[36] / convex_inter[8] overflow there
+    (box_fusion.py:378-384)"""
+    out = (ctypes.c_long * 2)()
+    lib().or_hull_overflow(out, ctypes.c_int(1 if reset else 0))
+    return int(out[0]), int(out[1])
+
+
 def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 

@@ -96,6 +96,7 @@ def _install_stubs():
                     OR._p(cbuf))
                 value.a += vbuf
                 count.a += cbuf
+                STATE["launches"] = STATE.get("launches", 0) + 1
 
             return kernel
 
@@ -273,6 +274,11 @@ def gen_trace(n_keyframes=14, frame_step=25, seed=3, period=400, **scene_kw):
                            "post_valid_num"]}
     fl = {k: [] for k in ["pre_fl", "nms_fl", "corr_fl", "post_fl", "fused"]}
     dets = []
+    # per keyframe: fitness evaluations whose candidate list / intersection hull exceed the
+    # reference kernel's corners_i[36] / convex_inter[8] (box_fusion.py:378-384, undefined
+    # behaviour in the reference; the trace holds the exact-hull result there)
+    hull_over = []
+    OR.hull_overflow()
     for k in range(n_keyframes):
         frame = k * frame_step
         det = scene.detections(frame)
@@ -358,8 +364,10 @@ def gen_trace(n_keyframes=14, frame_step=25, seed=3, period=400, **scene_kw):
         rec["post_valid_num"].append(all_pred_box.valid_num.numpy().copy())
         fl["post_fl"].append([list(map(int, r)) for r in box_manager.fusion_list])
         fl["fused"].append([list(map(int, r)) for r in box_manager.already_fusion])
+        hull_over.append(OR.hull_overflow())
 
     out = {}
+    out["hull_over"] = np.asarray([(0, 0)] + hull_over, np.int64)   # keyframe 0 runs no fusion
     # per-frame (cumulative) arrays as the reference left them
     out["pf_tensor"] = per_frame_ins.pred_boxes_3d.tensor.numpy()
     out["pf_R"] = per_frame_ins.pred_boxes_3d.R.numpy()
@@ -393,8 +401,82 @@ def gen_trace(n_keyframes=14, frame_step=25, seed=3, period=400, **scene_kw):
     return out
 
 
+def gen_faceon(n_obj=8, seed=11):
+    """Box fusion pinned to the reference with NO buffer overrun.
+
+    On a realistic scene the reference kernel's convex_inter[8] overflows constantly: a box seen
+    obliquely projects to a hexagon, and two nearly coincident hexagons intersect in up to 12
+    points (gen_trace records hundreds of thousands of such evaluations).  Here every view looks
+    straight at a large face of its box from inside the box's slabs (lateral offset < 0.1 m
+    against half extents >= 0.5 m), so every projected hull -- observed and particle -- is the
+    front-face quadrilateral: candidates <= 24 < 36 and intersection hulls <= 8 points, checked
+    below.  The reference's own BoxFusion.boxfusion (init_opt_params, cal_transform, update_PST,
+    momentum, write-back) runs over these jobs with the kernel restatement, which is exact
+    wherever the reference's buffers hold."""
+    from boxfusion_amd.synthetic import look_at_pose, rot_z, _A
+    cfg = SCANNET_CFG
+    rng = np.random.default_rng(seed)
+    K = SCANNET_K.astype(np.float32)
+    STUB_STATE["cfg"] = OR.fuse_cfg(cfg, np.eye(4), 480, 640, legacy=False)
+    with quiet():
+        box_manager = BoxManager(cfg)
+        fuser = BoxFusion(cfg)
+    fuser.update_intrinsics((640, 480), K)
+    tens, Rs, scores, poses, lists = [], [], [], [], []
+    for k in range(n_obj):
+        yaw = rng.uniform(-np.pi, np.pi)
+        l, h, w = rng.uniform(1.2, 1.7), rng.uniform(1.0, 1.3), rng.uniform(0.3, 0.9)
+        c = np.array([rng.uniform(-3, 3), rng.uniform(-3, 3), rng.uniform(1.0, 1.4)])
+        R = rot_z(yaw) @ _A
+        lat, nrm = R[:, 0], R[:, 2]          # box-local l axis and face normal (horizontal)
+        nv = int(rng.integers(3, 7))
+        lst = []
+        for v in range(nv):
+            d = rng.uniform(2.4, 4.0) + w / 2
+            eye = c - d * nrm + rng.uniform(-0.08, 0.08) * lat + np.array([0, 0, rng.uniform(-0.06, 0.06)])
+            P = look_at_pose(eye, eye + nrm)
+            b = np.r_[c + rng.normal(0, 0.02, 3), np.array([l, h, w]) * (1 + rng.normal(0, 0.03, 3))]
+            Rv = rot_z(yaw + rng.normal(0, np.deg2rad(0.7))) @ _A
+            lst.append(len(tens))
+            tens.append(b.astype(np.float32))
+            Rs.append(Rv.astype(np.float32))
+            scores.append(np.float32(rng.uniform(0.5, 0.95)))
+            poses.append(P.astype(np.float32))
+        lists.append(lst)
+    n = len(tens)
+    pf = Instances3D((480, 640))
+    pf.scores = torch.from_numpy(np.asarray(scores, np.float32))
+    pf.pred_boxes_3d = GeneralInstance3DBoxes(torch.from_numpy(np.stack(tens)), torch.from_numpy(np.stack(Rs)))
+    pf.cam_pose = torch.from_numpy(np.stack(poses))
+    pf.pred_boxes = torch.zeros(n, 4)
+    pf.project_3d_boxes(torch.from_numpy(K), H=480, W=640)
+    glob_rows = [ls[0] for ls in lists]
+    allb = pf[torch.tensor(glob_rows)]
+    box_manager.init_new_predictions(n_obj, 0)
+    box_manager.fusion_list = [list(ls) for ls in lists]
+    before = allb.pred_boxes_3d.tensor.numpy().copy()
+    OR.hull_overflow()
+    STUB_STATE["launches"] = 0
+    with quiet():
+        fuser.boxfusion(allb, pf, box_manager)
+    over = OR.hull_overflow()
+    assert over == (0, 0), over
+    after = allb.pred_boxes_3d.tensor.numpy().copy()
+    flat, off = ragged(lists)
+    fflat, foff = ragged([list(map(int, r)) for r in box_manager.already_fusion])
+    print("faceon: jobs", n_obj, "views", n, "kernel launches", STUB_STATE["launches"],
+          "updated", int((np.abs(after - before).max(1) > 0).sum()))
+    return dict(pf_tensor=np.stack(tens), pf_R=np.stack(Rs), pf_scores=np.asarray(scores, np.float32),
+                pf_pose=np.stack(poses), pf_proj=pf.projected_boxes.numpy(), glob_rows=np.asarray(glob_rows, np.int32),
+                lists_flat=flat, lists_off=off, before=before, after=after, fused_flat=fflat,
+                fused_off=foff, launches=np.int64(STUB_STATE["launches"]), hull_over=np.asarray(over, np.int64))
+
+
 def main():
     torch.set_num_threads(8)
+    if sys.argv[1:] == ["faceon"]:
+        np.savez_compressed(os.path.join(HERE, "fusion_faceon.npz"), **gen_faceon())
+        return
     np.savez_compressed(os.path.join(HERE, "obb_pairs.npz"), **gen_obb_pairs())
     print("obb_pairs done")
     np.savez_compressed(os.path.join(HERE, "geometry.npz"), **gen_geometry())
@@ -407,6 +489,8 @@ def main():
                         **gen_trace(n_keyframes=16, frame_step=10, seed=5, period=300, noise=3.0,
                                     dim_lo=0.08, dim_hi=0.6, n_objects=40))
     print("small-object trace done")
+    np.savez_compressed(os.path.join(HERE, "fusion_faceon.npz"), **gen_faceon())
+    print("face-on fusion done")
 
 
 if __name__ == "__main__":

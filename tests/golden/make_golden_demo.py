@@ -172,12 +172,16 @@ def main():
 
     Instances3D.project_3d_boxes = project_rec
     MG.STUB_STATE["cfg"] = MG.OR.fuse_cfg(MG.SCANNET_CFG, np.eye(4), 480, 640, legacy=False)
+    MG.OR.hull_overflow()
     with tempfile.TemporaryDirectory() as out_dir, MG.quiet():
         cfg = cfg_demo(out_dir)
         demo.run(cfg, SceneModel(scene, keyframes), Stream(scene), StubCLIP(text), None, names, text.clone(),
                  Augmentor(("wide/image", "wide/depth")), Preprocessor(),
                  score_thresh=cfg["detection"]["score_thresh"], viz_on_gt_points=False, gap=GAP,
                  re_vis=False)
+    # fitness evaluations past the reference kernel's corners_i[36] / convex_inter[8]
+    # (box_fusion.py:378-384): the run is the reference's with the exact hull there
+    hull_over = np.asarray(MG.OR.hull_overflow(), np.int64)
     glob_list = saved["synthetic_boxes.pkl"][0]
     fw = saved["framewise_boxes.pkl"][0]
     bm = managers[0]
@@ -195,7 +199,7 @@ def main():
                num_record=np.array([bm.num_record[k] for k in sorted(bm.num_record)], np.int64),
                geom_tensor=np.stack([geom[i][0] for i in range(len(geom))]),
                geom_R=np.stack([geom[i][1] for i in range(len(geom))]),
-               geom_proj=np.stack([geom[i][2] for i in range(len(geom))]))
+               geom_proj=np.stack([geom[i][2] for i in range(len(geom))]), hull_over=hull_over)
     assert sorted(geom) == list(range(len(geom)))
     np.savez_compressed(os.path.join(HERE, "demo_gap25.npz"), **out)
     print("demo golden:", {k: getattr(v, "shape", v) for k, v in out.items()})

@@ -116,3 +116,21 @@ def test_text_prompt_matches_reference():
     np.testing.assert_allclose(mx.numpy(), u["max_values"], rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(text[:4].numpy(), u["text_after"], rtol=1e-6, atol=1e-7)
     assert (cats == "").sum() > 0 and (cats != "").sum() > 0
+
+
+def test_already_fusion_membership_tracks_in_place_edits():
+    """BoxManager.check_if_fusion (a set mirror of `idx_list in already_fusion`) stays exact when
+    the list is edited in place without a length change (item assignment, pop + append)"""
+    from boxfusion_amd.box_manager import BoxManager
+    cfg = dict(association=dict(rotation_gap=30, translation_gap=0.8), box_fusion=dict(small_size=0.35))
+    bm = BoxManager(cfg)
+    bm.add_fusion_ind([1, 2, 3])
+    assert bm.check_if_fusion([1, 2, 3])
+    bm.already_fusion[0] = [4, 5, 6]
+    assert not bm.check_if_fusion([1, 2, 3]) and bm.check_if_fusion([4, 5, 6])
+    bm.already_fusion.pop()
+    bm.already_fusion.append([7, 8, 9])
+    assert not bm.check_if_fusion([4, 5, 6]) and bm.check_if_fusion([7, 8, 9])
+    bm.already_fusion = [[9, 10, 11]]
+    bm.add_fusion_ind([1, 2, 3])
+    assert bm.check_if_fusion([9, 10, 11]) and bm.check_if_fusion([1, 2, 3]) and not bm.check_if_fusion([7, 8, 9])

@@ -113,14 +113,58 @@ class HipBackend:
                                                 _t(cat[0]), _t(cat[1]), _t(cat[2]), _t(cat[3]),
                                                 _t(cat[4]), self.pst, self.fcfg)
         b, u = box.cpu().numpy(), upd.cpu().numpy()
+        self._over = getattr(self, "_over", False) | bool(int(st.item()) & self.L.BF_DEV_HULL_OVERFLOW)
+        assert not int(st.item()) & self.L.BF_DEV_HULL_TRUNC
         return [(b[i], int(u[i])) for i in range(len(views))]
+
+    def hull_overflow(self):
+        o, self._over = getattr(self, "_over", False), False
+        return o
 
 
 @pytest.mark.parametrize("name", ["fusion_trace.npz", "fusion_trace_small.npz"])
 def test_trace_replay_hip(L, name):
     """NMS keep/success, fusion lists, association and fused boxes bit-exact vs the reference."""
     stats = TU.replay(TU.load(name), HipBackend(L, legacy=False))
-    assert stats["fused"] > 10
+    print(name, stats)
+    assert stats["fused"] > 10 and stats["reference_pinned"] >= 1
+
+
+def test_faceon_fusion_reference_pinned(L):
+    """BoxFusion.boxfusion (bf_fusion_fit + bf_fusion_writeback) against the reference's own
+    boxfusion on the face-on jobs where no fitness evaluation overruns the reference kernel's
+    buffers (tests/golden/make_golden.gen_faceon): fused boxes and already_fusion bit for bit,
+    with strict_hull on (any BF_DEV_HULL_OVERFLOW would raise)"""
+    import copy
+    from boxfusion_amd.box_fusion import BoxFusion
+    from boxfusion_amd.box_manager import BoxManager
+    from boxfusion_amd.boxes import GeneralInstance3DBoxes
+    from boxfusion_amd.instances import Instances3D
+    from tests.test_oracle_golden import faceon_jobs
+    g = TU.load("fusion_faceon.npz")
+    lists, _ = faceon_jobs(g)
+    cfg = copy.deepcopy(TU.SCANNET_CFG)
+    cfg["box_fusion"]["strict_hull"] = True
+    pf = Instances3D((480, 640))
+    pf.pred_boxes_3d = GeneralInstance3DBoxes(_t(g["pf_tensor"]), _t(g["pf_R"]))
+    pf.scores = _t(g["pf_scores"])
+    pf.cam_pose = _t(g["pf_pose"])
+    pf.projected_boxes = _t(g["pf_proj"])
+    rows = g["glob_rows"]
+    allb = Instances3D((480, 640))
+    allb.pred_boxes_3d = GeneralInstance3DBoxes(_t(g["pf_tensor"][rows]), _t(g["pf_R"][rows]))
+    bm = BoxManager(cfg)
+    bm.init_new_predictions(len(rows), 0)
+    bm.fusion_list = [[int(i) for i in ls] for ls in lists]
+    bf = BoxFusion(cfg, device=DEV, legacy_promotion=False)
+    bf.update_intrinsics((640, 480), np.array(fuse_cfg(L, False).K).reshape(4, 4)[:3, :3])
+    bf.boxfusion(allb, pf, bm)
+    np.testing.assert_array_equal(g["before"], g["pf_tensor"][rows])
+    np.testing.assert_array_equal(allb.pred_boxes_3d.tensor.cpu().numpy(), g["after"])
+    want = [[int(v) for v in g["fused_flat"][g["fused_off"][k]:g["fused_off"][k + 1]]]
+            for k in range(len(g["fused_off"]) - 1)]
+    assert bm.already_fusion == want
+    assert bf.hull_overflow_calls == 0 and bf.last_stats["updated"] == len(lists)
 
 
 def test_obb_iou_pairs_hip(L):
@@ -296,11 +340,16 @@ def test_boxfusion_hull_overflow_policy(L):
             with pytest.raises(L.HipError, match="HULL_OVERFLOW"):
                 bf.boxfusion(allb, pf, bm)
         else:
+            from boxfusion_amd import box_fusion as BFM
+            BFM._HULL_WARNED[0] = False
             with warnings.catch_warnings(record=True) as w:
                 warnings.simplefilter("always")
                 bf.boxfusion(allb, pf, bm)
-            assert bf.hull_overflow_calls == 1
-            assert any("HULL_OVERFLOW" in str(x.message) for x in w)
+                bm.fusion_list = [[0, 1, 2]]
+                bm.already_fusion = []
+                bf.boxfusion(allb, pf, bm)        # counted again, not warned again
+            assert bf.hull_overflow_calls == 2
+            assert sum("convex_inter[8]" in str(x.message) for x in w) == 1
 
 
 @pytest.mark.parametrize("n_glo,n_new", [(150, 25), (97, 0), (300, 40)])

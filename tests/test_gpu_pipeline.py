@@ -38,7 +38,11 @@ def _inject_geometry(monkeypatch, dev, src):
 @pytest.mark.parametrize("name", ["fusion_trace.npz", "fusion_trace_small.npz"])
 def test_fusion_stage_vs_trace(dev, name, monkeypatch):
     """demo.py keyframe state machine on the GPU == the reference's recorded chain, bit for bit,
-    given the reference's own world-space boxes and projections (pf_* of the trace)."""
+    given the reference's own world-space boxes and projections (pf_* of the trace).  The trace
+    is the reference's control flow with the exact hull wherever its kernel overruns
+    convex_inter[8] (recorded per keyframe, hull_over): the keyframes before the first such
+    fusion are reference-pinned outright, and BoxFusion's BF_DEV_HULL_OVERFLOW count matches the
+    record keyframe by keyframe."""
     from boxfusion_amd.fusion_stage import FusionStage
     from boxfusion_amd.pipeline import scene_instances
     from boxfusion_amd.synthetic import SCANNET_K
@@ -49,10 +53,13 @@ def test_fusion_stage_vs_trace(dev, name, monkeypatch):
     for k, frame in enumerate(t["frame"]):
         a, b = int(nd[:k].sum()), int(nd[:k + 1].sum())
         det = {key: t["det_" + key][a:b] for key in ["scores", "pred_boxes", "xyzlhw", "R", "proj_xy"]}
+        calls = st.fuser.hull_overflow_calls
         st.keyframe(int(frame), t["pose"][k], scene_instances(det, dev))
         got, _ = st.boxes()
         assert st.box_manager.fusion_list == TU._lists(t, "post_fl", k), f"kf {k}"
         assert st.box_manager.already_fusion == TU._lists(t, "fused", k), f"kf {k}"
+        # (the read of already_fusion above resolved the deferred fusion result)
+        assert (st.fuser.hull_overflow_calls > calls) == bool(t["hull_over"][k].any()), f"kf {k}"
         np.testing.assert_array_equal(got, TU._rows(t, "post_tensor", k), err_msg=f"kf {k}")
         np.testing.assert_array_equal(st.all_pred_box.valid_num.cpu().numpy(),
                                       TU._rows(t, "post_valid_num", k), err_msg=f"kf {k}")
@@ -333,7 +340,10 @@ def test_pipeline_run_vs_reference_demo_gap25(dev, monkeypatch):
     (tests/golden/make_golden_demo.py): final fusion lists, fused sets and num_record equal; the
     global boxes (demo.py:371-379) and the framewise boxes / class indices / CLIP features
     (demo.py:382-386) equal.  World-space geometry as the reference computed it is injected by
-    init_id (the particle search amplifies the 1-ulp difference of the GPU transform)."""
+    init_id (the particle search amplifies the 1-ulp difference of the GPU transform).  The
+    reference's fusion kernel overruns convex_inter[8] in this run (d["hull_over"]): the match
+    is with its control flow and the exact hull there (test_gpu_fusion.py's face-on fixture is
+    the overrun-free pin)."""
     import copy
     from boxfusion_amd.fusion_stage import FusionStage
     from boxfusion_amd.pipeline import Pipeline, load_class_features, load_class_names
@@ -375,6 +385,9 @@ def test_pipeline_run_vs_reference_demo_gap25(dev, monkeypatch):
     np.testing.assert_array_equal(cls, d["fw_class"])
     np.testing.assert_array_equal(pf.pred_boxes_3d.corners.cpu().numpy(), d["fw_corners"])
     np.testing.assert_allclose(pf.features.cpu().numpy(), d["fw_features"], rtol=1e-6, atol=1e-7)
+    # the run holds fitness evaluations past the reference kernel's convex_inter[8] (recorded by
+    # the generator): there the reference is undefined and both sides use the exact hull
+    assert (fusion.fuser.hull_overflow_calls > 0) == bool(d["hull_over"].any())
 
 
 def test_detect_stage_ca1m_depth_ratio(dev):

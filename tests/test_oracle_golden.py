@@ -77,11 +77,46 @@ class OracleBackend:
             out.append((r["box"], r["updated"]))
         return out
 
+    def hull_overflow(self):
+        return any(OR.hull_overflow(reset=True))
+
 
 @pytest.mark.parametrize("name", ["fusion_trace.npz", "fusion_trace_small.npz"])
 def test_trace_replay(name):
     stats = TU.replay(TU.load(name), OracleBackend())
+    print(name, stats)
+    assert stats["reference_pinned"] >= 1 and stats["hull_overflow_keyframes"] > 0
     assert stats["suppressions"] > 100
     assert stats["fused"] > 10
     if "small" in name:
         assert stats["corr_changes"] > 5
+
+
+def faceon_jobs(g):
+    """the face-on fusion fixture's jobs: (views of job k, global row before, after)"""
+    lists = [g["lists_flat"][g["lists_off"][k]:g["lists_off"][k + 1]] for k in range(len(g["lists_off"]) - 1)]
+    views = [(g["pf_tensor"][i], g["pf_R"][i], g["pf_scores"][i], g["pf_pose"][i], g["pf_proj"][i])
+             for i in lists]
+    return lists, views
+
+
+def test_faceon_fusion_reference_pinned():
+    """box fusion against the reference with NO buffer overrun anywhere: the
+    reference's BoxFusion.boxfusion on face-on views (make_golden.gen_faceon) -- every fitness
+    evaluation of every iteration stays inside corners_i[36] / convex_inter[8] -- and the oracle
+    reproduces its fused boxes bit for bit, again with zero overflow"""
+    g = TU.load("fusion_faceon.npz")
+    assert tuple(g["hull_over"]) == (0, 0) and int(g["launches"]) > 50
+    be = OracleBackend()
+    lists, views = faceon_jobs(g)
+    OR.hull_overflow()
+    n_upd = 0
+    for k, v in enumerate(views):
+        r = OR.fusion_fit(*v, be.pst, be.fcfg)
+        want = g["after"][k]
+        assert bool(r["updated"]) == bool((want != g["before"][k]).any())
+        if r["updated"]:
+            np.testing.assert_array_equal(r["box"], want)
+            n_upd += 1
+    assert OR.hull_overflow() == (0, 0)
+    assert n_upd == len(views)

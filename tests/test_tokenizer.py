@@ -77,3 +77,13 @@ def test_load_text_tower_from_open_clip_style_checkpoint(tmp_path):
     import pytest
     with pytest.raises(KeyError):
         load_text_tower(str(tmp_path / "bad.pt"), device="cpu", text=TextTransformer(77, 300, 64, 2, 2, 32))
+
+
+def test_special_tokens_in_text_are_single_tokens():
+    """the split pattern is built from the vocabulary's own SOT / EOT strings (as open_clip builds
+    it from its special tokens), so a special inside the text encodes to its one id"""
+    from boxfusion_amd.tokenizer import EOT, SOT, SimpleTokenizer
+    t = SimpleTokenizer([("a", "b")])
+    ids = t.encode(f"x {SOT} y {EOT}")
+    assert t.encoder[SOT] in ids and t.encoder[EOT] in ids
+    assert t.encode("<|startoftext|>") != [t.encoder[SOT]]

@@ -110,10 +110,20 @@ def replay(t, backend, fuse_legacy=False):
         corr(corners, dims, scores, boxes2d, init_id, cam_poses, pose, K, n_glo, keep, success,
              fusion_list, valid_num) -> dict
         fuse(list of (view_box, view_R, view_score, view_pose, view_tc)) -> list of (box, updated)
+    A backend with hull_overflow() (True when a fitness evaluation since the last call had an
+    intersection hull the reference kernel's fixed buffers cannot hold) is checked against the
+    trace's per-keyframe record.  Keyframes before the first such evaluation are pinned to the
+    reference outright (stats["reference_pinned"]); from there on the trace is the reference's
+    control flow with the exact hull where its kernel overruns convex_inter[8] / corners_i[36]
+    (box_fusion.py:378-384, undefined behaviour in the reference).
     Returns counters of the exercised paths."""
     K = np.array([[574.540771, 0.0, 322.522827], [0.0, 577.583740, 238.558853], [0, 0, 1]],
                  np.float32)
-    stats = dict(keyframes=0, suppressions=0, corr_changes=0, fused=0)
+    stats = dict(keyframes=0, suppressions=0, corr_changes=0, fused=0, reference_pinned=0,
+                 hull_overflow_keyframes=0)
+    over_seen = False
+    if hasattr(backend, "hull_overflow"):
+        backend.hull_overflow()
     for kf in keyframes(t):
         msg = f"keyframe {kf.k}"
         corners = backend.corners(kf.tensor, kf.R)
@@ -154,6 +164,14 @@ def replay(t, backend, fuse_legacy=False):
                     done.append(fl)
                     stats["fused"] += 1
         np.testing.assert_array_equal(post, kf.post_tensor, err_msg=msg)
+        if not over_seen:
+            stats["reference_pinned"] += 1
+        if "hull_over" in t:
+            want = bool(np.asarray(t["hull_over"][kf.k]).any())
+            if hasattr(backend, "hull_overflow"):
+                assert backend.hull_overflow() == want, msg + ": hull-overflow record"
+            over_seen |= want
+            stats["hull_overflow_keyframes"] += int(want)
         stats["keyframes"] += 1
         stats["suppressions"] += len(kf.nms_success)
     return stats
