@@ -77,6 +77,8 @@ def parse(argv=None):
                    help="synchronous fusion, sync between stages, report ms/step of each")
     p.add_argument("--eager", action="store_true", help="no HIP graph for the detect stage")
     p.add_argument("--roofline-steps", type=int, default=2)
+    p.add_argument("--roofline-keyframes", type=int, default=24,
+                   help="keyframes of the post-timing fusion re-run (pairs/s, particle-views/s)")
     p.add_argument("--fusion-cus", type=int, default=-1,
                    help="CUs reserved for the fusion stream (-1: 32 on rank 0 when N > 1, else 0)")
     p.add_argument("--sim-ranks", type=int, default=1,
@@ -616,6 +618,12 @@ def main(argv=None):
                                dtype=torch.float32, device=dev)
         nk_depth.uniform_(0.5, 4.5, generator=gnk)
         nk_depth.masked_fill_(torch.rand(nk_depth.shape, device=dev, generator=gnk) < 0.05, 0.0)
+        # their camera poses and the depth intrinsics: demo.py:121-127 back-projects every
+        # frame's depth too (viz_on_gt_points defaults to True)
+        nk_ids = [[kf + o for kf in my_frames(s_) for o in range(1, G)] for s_ in range(total_steps)]
+        nk_RT = torch.from_numpy(np.stack([np.stack([scene.pose(f) for f in ids]) for ids in nk_ids])
+                                 .astype(np.float32)).to(dev)
+        nk_K = detect.Kd_dev[:1].expand((G - 1) * Bm, 3, 3).contiguous()
     poses_all = np.stack([scene.pose(f) for f in all_mine]).astype(np.float32)
     dets_mine = [scene.detections(f, Kf, (FW, FH)) for f in all_mine]
     rec_all = torch.from_numpy(pack_records(dets_mine, poses_all)).to(dev)
@@ -650,8 +658,8 @@ def main(argv=None):
             st_ctx = torch.cuda.stream(det_streams[k])
             st_ctx.__enter__()      # this step's detect, gather and fusion hand-off on its stream
             det = detects[k]
-            if nk_depth is not None:          # the step's non-keyframes: preprocessing only
-                _lib.depth_standardize(nk_depth[s])
+            if nk_depth is not None:          # the step's non-keyframes: per-frame work only
+                _lib.depth_preprocess(nk_depth[s], nk_K, nk_RT[s], 10.0)
             det(rgb_all[sl], depth_all[sl], poses_all[sl], return_instances=False,
                 crop_boxes=crops_all[s * Bm * args.crops:(s + 1) * Bm * args.crops])
             if args.breakdown:
@@ -751,7 +759,7 @@ def main(argv=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     source = "timed region"
-    if not timer.records:
+    if not any(r[0]["kind"] in ("gemm", "gemm_fp8") for r in timer.records):
         # graph mode: time the same kernels launched eagerly on the same inputs, right after the
         # timed region (HIP events on the launch stream, every GEMM / attention launch of the steps)
         detect.use_graph = False
@@ -765,6 +773,20 @@ def main(argv=None):
         detect.use_graph = not args.eager
         source = f"eager re-run of {args.roofline_steps} timed steps"
     frames = per_step * args.steps * G
+    fus_timer = None
+    if rank == 0:
+        # the fusion kernels (pairs/s of the 3-D IoU matrix, particle-views/s of the
+        # box-fusion fitness) on their own after the timed region: a fresh fusion state machine
+        # over the stream's first keyframes, synchronous, HIP events around every launch
+        from boxfusion_amd.pipeline import scene_instances
+        fst = FusionStage(CFG, Kf, H=FH, W=FW, device=dev)
+        fus_timer = _lib.KernelTimer()
+        with fus_timer:
+            for k in range(args.roofline_keyframes):
+                f = k * G
+                fst.keyframe(f, scene.pose(f), scene_instances(scene.detections(f, Kf, (FW, FH)), dev, FH, FW))
+            fst.boxes()
+        torch.cuda.synchronize()
 
     if rank == 0:
         big = lambda t: t["kind"] == "gemm" and t["large"]
@@ -790,6 +812,27 @@ def main(argv=None):
         }
         for v in comps.values():
             v["measured"] = source
+        dsel = (lambda t: t["kind"] == "depth" and t["b"] > Bm) if G > 1 else (lambda t: t["kind"] == "depth")
+        dks = timer.summary(dsel)
+        if dks["launches"]:
+            comps["depth_preprocess"] = roofline_obj(
+                dks, "bf_depth_preprocess (a1 + a13: trimmed depth standardisation + back-projection, "
+                     "3-level radix select over the whole chip)", "hbm", pmc_key="k_ds")
+            comps["depth_preprocess"]["measured"] = (source if G == 1 else
+                                                     "timed region (non-keyframe batches)")
+            comps["depth_preprocess"]["frames_per_launch"] = (G - 1) * Bm if G > 1 else Bm
+        if fus_timer is not None:
+            for kind, unit, name in (("obb_iou", "pairs/s", "bf_obb_iou_matrix (k_obb_gate + k_obb_grid): "
+                                      "box pairs of the 3-D IoU matrix"),
+                                     ("nms_scan", "boxes/s", "bf_nms_scan (greedy scan + record)"),
+                                     ("fusion_fit", "particle-views/s", "bf_fusion_fit (k_fuse_terms + "
+                                      "k_fuse_step): particle x view fitness evaluations, all iterations")):
+                ks = fus_timer.summary(lambda t, k_=kind: t["kind"] == k_)
+                if ks["launches"]:
+                    comps[kind] = {"bound": "latency / VALU", "kernel": name, "unit": unit,
+                                   "achieved": ks["flops"] / (ks["ms"] * 1e-3), "launches": ks["launches"],
+                                   "avg_us": ks["avg_us"], "work_per_launch": ks["flops_per_launch"],
+                                   "measured": f"fusion re-run over {args.roofline_keyframes} keyframes"}
         r_all["measured"] = source
         line = base_line(args, N, frames, dt, per_step * G, n_inflight)
         if B0 < B:

@@ -76,6 +76,8 @@ def lib():
         _LIB.bf_version.restype = ctypes.c_char_p
         _LIB.bf_obb_iou_workspace_size.restype = c_size_t
         _LIB.bf_obb_iou_workspace_size.argtypes = [c_int]
+        _LIB.bf_depth_standardize_workspace_size.restype = c_size_t
+        _LIB.bf_depth_standardize_workspace_size.argtypes = [c_int, c_int, c_int]
     return _LIB
 
 
@@ -395,14 +397,53 @@ def detection_filter(scores, proj_xy, box3d, cfg: FilterCfg, with_bits=False):
 # ------------------------------------------------------------------------------------------
 # per-frame depth
 # ------------------------------------------------------------------------------------------
-def depth_standardize(depth):
+_DS_WS = {}
+
+
+def depth_workspace(b, h, w, device):
+    """zero-filled workspace of bf_depth_standardize / bf_depth_preprocess, one per (device,
+    stream, shape): the kernels leave it zeroed, so it is reused as is.  Graph captures keep
+    their own (the captured kernels own its address)."""
+    dev = torch.device(device)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    key = (dev.index, stream, b, h, w)
+    ws = _DS_WS.get(key)
+    if ws is None:
+        size = int(lib().bf_depth_standardize_workspace_size(c_int(b), c_int(h), c_int(w)))
+        ws = torch.zeros(max(size, 1), dtype=torch.uint8, device=dev)
+        _DS_WS[key] = ws
+    return ws
+
+
+def depth_standardize(depth, out=None, params=None):
     """depth f32[b,h,w] -> (standardised f32[b,h,w], params f32[b,2])"""
+    return depth_preprocess(depth, out=out, params=params)
+
+
+def depth_preprocess(depth, K=None, RT=None, max_depth=10.0, out=None, params=None, xyz=None, valid=None):
+    """demo.py:121-131 per-frame depth work for a batch: depth f32[b,h,w] -> (standardised,
+    params f32[b,2]) and, with K f32[b,3,3] / RT f32[b,4,4], the back-projection (xyz f32[b,h,w,3],
+    valid bool[b,h,w]) from the same pass"""
     depth = _need(depth.contiguous(), torch.float32, "depth")
     b, h, w = depth.shape
-    out = torch.empty_like(depth)
-    params = torch.empty((b, 2), dtype=torch.float32, device=depth.device)
-    _check(lib().bf_depth_standardize(_ptr(depth), c_int(b), c_int(h), c_int(w), _ptr(out),
-                                      _ptr(params), None, _stream()), "bf_depth_standardize")
+    out = torch.empty_like(depth) if out is None else out
+    params = torch.empty((b, 2), dtype=torch.float32, device=depth.device) if params is None else params
+    bp = K is not None
+    if bp:
+        K = _need(K.contiguous(), torch.float32, "K")
+        RT = _need(RT.contiguous(), torch.float32, "RT")
+        if K.shape != (b, 3, 3) or RT.shape != (b, 4, 4):
+            raise HipError(f"bf_depth_preprocess: K {tuple(K.shape)} / RT {tuple(RT.shape)} for {b} frames")
+        xyz = torch.empty((b, h, w, 3), dtype=torch.float32, device=depth.device) if xyz is None else xyz
+        valid = torch.empty((b, h, w), dtype=torch.uint8, device=depth.device) if valid is None else valid
+    ws = depth_workspace(b, h, w, depth.device)
+    _check(lib().bf_depth_preprocess(_ptr(depth), c_int(b), c_int(h), c_int(w), _ptr(out), _ptr(params),
+                                     _ptr(K) if bp else None, _ptr(RT) if bp else None,
+                                     c_float(max_depth if max_depth is not None else 0.0),
+                                     _ptr(xyz) if bp else None, _ptr(valid) if bp else None, _ptr(ws),
+                                     _stream()), "bf_depth_preprocess")
+    if bp:
+        return out, params, xyz, valid.view(torch.bool)
     return out, params
 
 
@@ -739,6 +780,8 @@ class KernelTimer:
 
     def __enter__(self):
         global _TIMER
+        import threading
+        self.thread = threading.get_ident()     # records launches made from this thread only
         _TIMER = self
         self.active = True
         return self
@@ -762,7 +805,9 @@ class KernelTimer:
         if not sel:
             return dict(launches=0, flops=0.0, bytes=0.0, ms=0.0)
         ms = sum(s.elapsed_time(e) for _, _, _, s, e in sel)
-        fl = sum(f for _, f, _, _, _ in sel)
+        # work may be a callable resolved now (e.g. particle-views from the iteration counts a
+        # fusion launch wrote)
+        fl = sum(f() if callable(f) else f for _, f, _, _, _ in sel)
         nb = sum(b for _, _, b, _, _ in sel)
         return dict(launches=len(sel), flops=fl, bytes=nb, ms=ms, avg_us=1e3 * ms / len(sel),
                     tflops=fl / (ms * 1e-3) / 1e12, gbs=nb / (ms * 1e-3) / 1e9,
@@ -770,6 +815,18 @@ class KernelTimer:
 
 
 _TIMER = None
+
+
+def _timer():
+    """the active KernelTimer if it was entered on this thread (a fusion worker thread's
+    launches are not recorded by the detect thread's timer)"""
+    t = _TIMER
+    if t is None:
+        return None
+    import threading
+    return t if t.thread == threading.get_ident() else None
+
+
 _gemm_untimed = gemm
 _gemm_fp8_untimed = gemm_fp8
 _attention_untimed = attention
@@ -778,7 +835,7 @@ _attention_fp8out_untimed = attention_fp8out
 
 def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype=torch.bfloat16,
          row_map=None, m=None):
-    t = _TIMER
+    t = _timer()
     if t is None:
         return _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m)
     M = a.shape[0] if m is None else m
@@ -795,7 +852,7 @@ def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype
 
 def gemm_fp8(a, w, scale, bias=None, act=None, resid=None, out=None, out_dtype=torch.bfloat16,
              out_qscale=1.0):
-    t = _TIMER
+    t = _timer()
     if t is None:
         return _gemm_fp8_untimed(a, w, scale, bias, act, resid, out, out_dtype, out_qscale)
     M, K = a.shape
@@ -809,7 +866,7 @@ def gemm_fp8(a, w, scale, bias=None, act=None, resid=None, out=None, out_dtype=t
 
 def attention(q, k, v, o, batch, heads, sq, sk, head_dim, scale, q_bs=None, k_bs=None, v_bs=None,
               o_bs=None, o_map=None):
-    t = _TIMER
+    t = _timer()
     if t is None:
         return _attention_untimed(q, k, v, o, batch, heads, sq, sk, head_dim, scale, q_bs, k_bs, v_bs,
                                   o_bs, o_map)
@@ -822,7 +879,7 @@ def attention(q, k, v, o, batch, heads, sq, sk, head_dim, scale, q_bs=None, k_bs
 
 def attention_fp8out(q, k, v, o, batch, heads, sq, sk, head_dim, scale, out_qscale, q_bs=None,
                      k_bs=None, v_bs=None, o_bs=None):
-    t = _TIMER
+    t = _timer()
     fn = lambda: _attention_fp8out_untimed(q, k, v, o, batch, heads, sq, sk, head_dim, scale, out_qscale,
                                            q_bs, k_bs, v_bs, o_bs)
     if t is None:
@@ -830,6 +887,69 @@ def attention_fp8out(q, k, v, o, batch, heads, sq, sk, head_dim, scale, out_qsca
     tags = dict(kind="attn", D=head_dim, sq=sq, sk=sk, batch=batch, heads=heads, fp8out=True)
     bh = float(batch * heads)
     return t.record(tags, 4.0 * bh * sq * sk * head_dim, bh * head_dim * (2 * sq + 4 * sk + sq), fn)
+
+
+_depth_preprocess_untimed = depth_preprocess
+_obb_iou_matrix_untimed = obb_iou_matrix
+_nms_scan_untimed = nms_scan
+_fusion_fit_untimed = fusion_fit
+
+
+def obb_iou_matrix(corners):
+    t = _timer()
+    if t is None:
+        return _obb_iou_matrix_untimed(corners)
+    n = int(corners.shape[0])
+    # work = box pairs (i < j) of the IoU matrix (gate + 25^3 grid count launches)
+    return t.record(dict(kind="obb_iou", n=n), n * (n - 1) / 2.0, 96.0 * n + 8.0 * n * n,
+                    lambda: _obb_iou_matrix_untimed(corners))
+
+
+def nms_scan(iou, corners, scores, init_id, cam_poses, fl_items, fl_len, valid_num, cfg, out=None):
+    t = _timer()
+    fn = lambda: _nms_scan_untimed(iou, corners, scores, init_id, cam_poses, fl_items, fl_len, valid_num,
+                                   cfg, out)
+    if t is None:
+        return fn()
+    n = int(scores.shape[0])
+    return t.record(dict(kind="nms_scan", n=n), float(n), 8.0 * n * n, fn)
+
+
+def fusion_fit(view_off, n_views, view_box, view_R, view_score, view_pose, view_tc, pst, cfg,
+               trace=False, max_views=None, packed_out=False, packed=None):
+    t = _timer()
+    fn = lambda: _fusion_fit_untimed(view_off, n_views, view_box, view_R, view_score, view_pose, view_tc,
+                                     pst, cfg, trace, max_views, packed_out, packed)
+    if t is None:
+        return fn()
+    res = []
+    nj = int(view_off.shape[0])
+    P = int(cfg.pst_size)
+    # work = particle-view fitness evaluations: sum over jobs of views * particles * iterations
+    # (the iteration counts are read when the summary is taken)
+    work = lambda: float((res[0][1][nj:2 * nj].long() * n_views.long()).sum().item() * P if packed_out
+                         else (res[0][2].long() * n_views.long()).sum().item() * P)
+    t.record(dict(kind="fusion_fit", jobs=nj), work, 0.0, lambda: res.append(fn()))
+    return res[0]
+
+
+def depth_preprocess(depth, K=None, RT=None, max_depth=10.0, out=None, params=None, xyz=None, valid=None):
+    t = _timer()
+    fn = lambda: _depth_preprocess_untimed(depth, K, RT, max_depth, out, params, xyz, valid)
+    if t is None:
+        return fn()
+    b, h, w = depth.shape
+    n = float(b * h * w)
+    # algorithmic bytes: read the depth once, write the standardised map (+ xyz and
+    # the valid mask when back-projecting)
+    nbytes = 8.0 * n + (13.0 * n if K is not None else 0.0)
+    tags = dict(kind="depth", backproject=K is not None, b=b, h=h, w=w)
+    return t.record(tags, 0.0, nbytes, fn)
+
+
+def depth_standardize(depth, out=None, params=None):
+    """depth f32[b,h,w] -> (standardised f32[b,h,w], params f32[b,2])"""
+    return depth_preprocess(depth, out=out, params=params)
 
 
 # ------------------------------------------------------------------------------------------

@@ -21,6 +21,7 @@ EXACT = ["-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt"]
 SOURCES = {
     "bf_misc.hip": [],
     "bf_geom.hip": EXACT,
+    "bf_depth.hip": EXACT,
     "bf_iou3d.hip": EXACT,
     "bf_assoc.hip": EXACT,
     "bf_fusion.hip": EXACT,

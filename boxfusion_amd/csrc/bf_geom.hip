@@ -160,198 +160,6 @@ BF_API int bf_backproject(const float* depth, const float* K, const float* RT, i
 }
 
 // ------------------------------------------------------------------------------------------
-// depth standardisation: trimmed mean/std by radix select (3 x 11-bit digit passes over the
-// positive-float bit patterns), one 1024-thread workgroup per frame.
-//   valid = d > 0 (NaN and <= 0 are invalid), m = #valid,
-//   slice = sorted[int(0.1 m) : int(0.9 m)]  (preprocessor.py:117)
-// ------------------------------------------------------------------------------------------
-#define DS_THREADS 1024
-#define DS_BINS 2048
-
-__device__ __forceinline__ bool ds_valid(float x) { return x > 0.0f; }
-
-// block-wide exclusive scan over DS_BINS counters in LDS: find the bin holding rank `r`
-// (0-based) and return it; *below receives the count of elements in lower bins.
-__device__ int ds_find_bin(unsigned* hist, long long r, long long* below, int* red) {
-    // each of the 1024 threads owns 2 bins
-    int t = threadIdx.x;
-    unsigned a = hist[2 * t], b = hist[2 * t + 1];
-    unsigned s = a + b;
-    // inclusive scan of s across the block (wave scan + wave offsets)
-    unsigned incl = s;
-    for (int o = 1; o < 64; o <<= 1) {
-        unsigned y = __shfl_up(incl, o, 64);
-        if (bf_lane() >= o) incl += y;
-    }
-    __shared__ unsigned wsum[DS_THREADS / 64];
-    if (bf_lane() == 63) wsum[t >> 6] = incl;
-    __syncthreads();
-    unsigned off = 0;
-    for (int wv = 0; wv < (t >> 6); ++wv) off += wsum[wv];
-    unsigned excl = off + incl - s;  // count before bin 2t
-    if ((long long)excl <= r && r < (long long)(excl + a)) {
-        red[0] = 2 * t;
-        red[1] = (int)excl;
-    } else if ((long long)(excl + a) <= r && r < (long long)(excl + s)) {
-        red[0] = 2 * t + 1;
-        red[1] = (int)(excl + a);
-    }
-    __syncthreads();
-    int bin = red[0];
-    *below = red[1];
-    __syncthreads();
-    return bin;
-}
-
-__global__ void __launch_bounds__(DS_THREADS) k_depth_std(const float* __restrict__ depth, int n,
-                                                          float* __restrict__ out,
-                                                          float* __restrict__ params) {
-    const float* d = depth + (size_t)blockIdx.x * n;
-    float* o = out + (size_t)blockIdx.x * n;
-    __shared__ unsigned hist[2][DS_BINS];
-    __shared__ int red[2];
-    __shared__ long long s_m;
-    __shared__ double s_acc[2][DS_THREADS / 64];
-    __shared__ long long s_cnt[4][DS_THREADS / 64];
-    const int t = threadIdx.x;
-
-    // pass 0: count valid
-    long long m = 0;
-    for (int i = t; i < n; i += DS_THREADS) m += ds_valid(d[i]) ? 1 : 0;
-    m = bf_wave_sum_i64(m);
-    if (bf_lane() == 0) s_cnt[0][t >> 6] = m;
-    __syncthreads();
-    if (t == 0) {
-        long long s = 0;
-        for (int w = 0; w < DS_THREADS / 64; ++w) s += s_cnt[0][w];
-        s_m = s;
-    }
-    __syncthreads();
-    m = s_m;
-    long long klo = (long long)(0.1 * (double)m);
-    long long khi = (long long)((1.0 - 0.1) * (double)m);
-    long long L = khi - klo;
-    float mean_f, std_f;
-    if (L <= 1) {
-        mean_f = 0.0f;
-        std_f = 1.0f;
-    } else {
-        // radix select the values of rank klo and khi-1
-        long long r[2] = {klo, khi - 1};
-        unsigned prefix[2] = {0u, 0u};
-        const int shifts[3] = {21, 10, 0};
-        const unsigned widths[3] = {11, 11, 10};
-        for (int pass = 0; pass < 3; ++pass) {
-            for (int b = t; b < DS_BINS; b += DS_THREADS) { hist[0][b] = 0; hist[1][b] = 0; }
-            __syncthreads();
-            const int sh = shifts[pass];
-            const unsigned hi_shift = sh + widths[pass];
-            for (int i = t; i < n; i += DS_THREADS) {
-                float x = d[i];
-                if (!ds_valid(x)) continue;
-                unsigned u = __float_as_uint(x);
-                unsigned digit = (u >> sh) & ((1u << widths[pass]) - 1u);
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    bool match = (pass == 0) ? true : ((u >> hi_shift) == (prefix[q] >> hi_shift));
-                    if (match) atomicAdd(&hist[q][digit], 1u);
-                }
-            }
-            __syncthreads();
-            for (int q = 0; q < 2; ++q) {
-                long long below;
-                int bin = ds_find_bin(hist[q], r[q], &below, red);
-                prefix[q] |= ((unsigned)bin) << sh;
-                r[q] -= below;
-            }
-        }
-        float vlo = __uint_as_float(prefix[0]);
-        float vhi = __uint_as_float(prefix[1]);
-        // pass 4: sums of the middle, counts around the two order statistics
-        double sum = 0.0, sq = 0.0;
-        long long c_lt_lo = 0, c_eq_lo = 0, c_lt_hi = 0;
-        for (int i = t; i < n; i += DS_THREADS) {
-            float x = d[i];
-            if (!ds_valid(x)) continue;
-            c_lt_lo += x < vlo;
-            c_eq_lo += x == vlo;
-            c_lt_hi += x < vhi;
-            if (x > vlo && x < vhi) {
-                sum += (double)x;
-                sq += (double)x * (double)x;
-            }
-        }
-        for (int off = 32; off > 0; off >>= 1) {
-            sum += __shfl_xor(sum, off, 64);
-            sq += __shfl_xor(sq, off, 64);
-        }
-        c_lt_lo = bf_wave_sum_i64(c_lt_lo);
-        c_eq_lo = bf_wave_sum_i64(c_eq_lo);
-        c_lt_hi = bf_wave_sum_i64(c_lt_hi);
-        if (bf_lane() == 0) {
-            s_acc[0][t >> 6] = sum;
-            s_acc[1][t >> 6] = sq;
-            s_cnt[1][t >> 6] = c_lt_lo;
-            s_cnt[2][t >> 6] = c_eq_lo;
-            s_cnt[3][t >> 6] = c_lt_hi;
-        }
-        __syncthreads();
-        __shared__ float s_mean, s_std;
-        if (t == 0) {
-            double S = 0, Q = 0;
-            long long a = 0, e = 0, hl = 0;
-            for (int w = 0; w < DS_THREADS / 64; ++w) {
-                S += s_acc[0][w]; Q += s_acc[1][w];
-                a += s_cnt[1][w]; e += s_cnt[2][w]; hl += s_cnt[3][w];
-            }
-            double dl = (double)vlo, dh = (double)vhi;
-            if (vlo == vhi) {
-                S = (double)L * dl;
-                Q = (double)L * dl * dl;
-            } else {
-                long long n_lo = (a + e) - klo;
-                long long n_hi = khi - hl;
-                S += (double)n_lo * dl + (double)n_hi * dh;
-                Q += (double)n_lo * dl * dl + (double)n_hi * dh * dh;
-            }
-            double mu = S / (double)L;
-            double var = (Q - S * mu) / (double)(L - 1);
-            if (var < 0) var = 0;
-            float mf = (float)mu;
-            float vf = (float)var;
-            s_mean = mf;
-            s_std = sqrtf(vf + 1e-2f);
-        }
-        __syncthreads();
-        mean_f = s_mean;
-        std_f = s_std;
-    }
-    for (int i = t; i < n; i += DS_THREADS) {
-        float x = d[i];
-        float y = ds_valid(x) ? x : mean_f;
-        o[i] = (y - mean_f) / std_f;
-    }
-    if (t == 0) {
-        params[2 * blockIdx.x] = mean_f;
-        params[2 * blockIdx.x + 1] = std_f;
-    }
-}
-
-BF_API size_t bf_depth_standardize_workspace_size(int b, int h, int w) {
-    (void)b; (void)h; (void)w;
-    return 0;
-}
-
-BF_API int bf_depth_standardize(const float* depth, int b, int h, int w, float* out, float* params,
-                                void* workspace, void* stream) {
-    (void)workspace;
-    if (b <= 0 || h <= 0 || w <= 0 || !depth || !out || !params) return BF_ERR_ARG;
-    hipLaunchKernelGGL(k_depth_std, dim3(b), dim3(DS_THREADS), 0, bf_stream(stream), depth, h * w,
-                       out, params);
-    return bf_check_launch();
-}
-
-// ------------------------------------------------------------------------------------------
 // detection filters of demo.py:138-148 (box_manager.py:217-245) over a batch of frames' top-k
 // instances, one thread per instance: keep = score >= thr & uv inside [gap, size - gap] & !floor
 // & !large.  Every comparison in f32 like the reference's torch ops on f32 tensors (a python

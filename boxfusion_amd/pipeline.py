@@ -137,10 +137,12 @@ class DetectStage:
     def _device_forward(self):
         """host-sync-free device work on the input buffers -> self.out"""
         B, H, W = self.B, self.H, self.W
-        dstd, params = _lib.depth_standardize(self.in_depth)
         if self.backproject:
-            self.out["xyz"] = [_lib.backproject(self.in_depth[b], self.Kd_dev[b], self.in_pose[b])
-                               for b in range(B)]
+            # depth standardisation + unproject of the same depth maps in one pass (demo.py:121-131)
+            dstd, params, xyz, valid = _lib.depth_preprocess(self.in_depth, self.Kd_dev, self.in_pose, 10.0)
+            self.out["xyz"] = [(xyz[b], valid[b]) for b in range(B)]
+        else:
+            dstd, params = _lib.depth_standardize(self.in_depth)
         res = self.cutr(self.in_rgb, dstd, params, self.K_dev, self.in_Tg, [(H, W)] * B,
                         K_host=self.K_host, K_inv=self.Kinv_dev)
         scores = torch.stack([r.scores for r in res])
@@ -172,6 +174,20 @@ class DetectStage:
             with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
                 self._device_forward()
         self.graph.replay()
+
+    @torch.no_grad()
+    def preprocess_frames(self, depth, poses):
+        """demo.py:121-131 on frames that are not keyframes: depth standardisation (Preprocessor)
+        and, with backproject, the unproject of the same depth (viz_on_gt_points, on by default)
+        -- one bf_depth_preprocess pass over any number of frames.  Nothing reads the results
+        back (in the reference they feed rerun only); they stay in self.last_frames."""
+        n = depth.shape[0]
+        if self.backproject:
+            RT = torch.from_numpy(np.ascontiguousarray(poses, np.float32)).to(self.dev, non_blocking=True)
+            self.last_frames = _lib.depth_preprocess(depth, self.Kd_dev[:1].expand(n, 3, 3), RT, 10.0)
+        else:
+            self.last_frames = _lib.depth_standardize(depth)
+        return self.last_frames
 
     @torch.no_grad()
     def __call__(self, rgb_u8, depth, poses, return_instances=True, crop_boxes=None):
@@ -247,12 +263,21 @@ class Pipeline:
     def __init__(self, detect: DetectStage, fusion: FusionStage, gap):
         self.detect, self.fusion, self.gap = detect, fusion, gap
 
-    def run(self, frames, n_frames):
-        """frames(i0, i1) -> (rgb [b,H,W,3] u8 dev, depth [b,H,W] f32 dev, poses [b,4,4] host)"""
+    def run(self, frames, n_frames, per_frame=True, frames_per_call=64):
+        """frames(ids) -> (rgb [b,H,W,3] u8 dev, depth [b,H,W] f32 dev, poses [b,4,4] host).
+        per_frame: the frames between keyframes get demo.py:121-131's per-frame work too
+        (DetectStage.preprocess_frames, up to `frames_per_call` frames per call)."""
         B = self.detect.B
         kf = [i for i in range(n_frames) if i % self.gap == 0]
+        self.frames_preprocessed = 0
         for s in range(0, len(kf), B):
             ids = kf[s:s + B]
+            if per_frame:
+                nk = [i for i in range(ids[0], min(ids[-1] + self.gap, n_frames)) if i % self.gap != 0]
+                for c in range(0, len(nk), frames_per_call):
+                    _, depth, poses = frames(nk[c:c + frames_per_call])
+                    self.detect.preprocess_frames(depth.contiguous(), poses)
+                    self.frames_preprocessed += len(nk[c:c + frames_per_call])
             rgb, depth, poses = frames(ids)
             if len(ids) < B:   # ragged tail: pad the batch with the last frame, drop its results
                 pad = B - len(ids)

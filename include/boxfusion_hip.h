@@ -251,10 +251,22 @@ int bf_fusion_fitness(const float* box, const float* R, int n_views, const float
  * ------------------------------------------------------------------------------------------ */
 /* Preprocessor.standardize_depth_map (preprocessor.py:97-129) for a batch of b frames:
  *   depth f32[b,h,w] -> out f32[b,h,w] standardised (invalid -> mean), params f32[b,2] =
- *   (trunc_mean, trunc_std).  Trimmed order statistics by radix select, no sort. */
+ *   (trunc_mean, trunc_std).  Trimmed order statistics by a 3-level radix select spread over
+ *   the whole chip (8192-element slices), no sort.
+ *   workspace: bf_depth_standardize_workspace_size(b, h, w) bytes, ZERO-FILLED by the caller
+ *   before its first use; every call leaves it zero-filled again (histograms are cleared by the
+ *   kernels that consume them).  One workspace per stream (calls sharing one must not overlap). */
 size_t bf_depth_standardize_workspace_size(int b, int h, int w);
 int bf_depth_standardize(const float* depth, int b, int h, int w, float* out, float* params,
                          void* workspace, void* stream);
+
+/* demo.py:121-131's per-frame depth work in one call: bf_depth_standardize plus, when xyz is not
+ * NULL, the back-projection of the same frames (tools/utils.py:232-287, bf_backproject's
+ * arithmetic) fused into the normalise pass: K f32[b,3,3] (the depth map's intrinsics),
+ * RT f32[b,4,4] (camera -> world), xyz f32[b,h,w,3], valid u8[b,h,w]. */
+int bf_depth_preprocess(const float* depth, int b, int h, int w, float* out, float* params,
+                        const float* K, const float* RT, float max_depth, float* xyz,
+                        uint8_t* valid, void* workspace, void* stream);
 
 /* tools/utils.py unproject + get_camera_coords (:232-287):
  *   depth f32[h,w], K f32[3,3], RT f32[4,4] -> xyz f32[h,w,3], valid u8[h,w]

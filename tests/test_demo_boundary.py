@@ -134,3 +134,55 @@ def test_already_fusion_membership_tracks_in_place_edits():
     bm.already_fusion = [[9, 10, 11]]
     bm.add_fusion_ind([1, 2, 3])
     assert bm.check_if_fusion([9, 10, 11]) and bm.check_if_fusion([1, 2, 3]) and not bm.check_if_fusion([7, 8, 9])
+
+
+def test_pipeline_run_call_order_per_frame_work():
+    """Pipeline.run follows demo.py:88-332's per-frame order: every frame that is not a keyframe
+    gets the per-frame preprocessing (demo.py:121-131: depth standardisation + unproject, through
+    DetectStage.preprocess_frames), keyframes (count % gap == 0) go through detect in batches and
+    then the fusion state machine in frame order, and a non-keyframe last frame triggers the
+    stale re-fusion (demo.py:200).  Stand-in stages on CPU record the calls."""
+    import numpy as np
+    import torch
+    from boxfusion_amd.pipeline import Pipeline
+
+    class Det:
+        B = 3
+
+        def __init__(self):
+            self.pre, self.det = [], []
+
+        def preprocess_frames(self, depth, poses):
+            self.pre += [int(p[0, 3]) for p in poses]
+
+        def __call__(self, rgb, depth, poses):
+            self.det.append([int(p[0, 3]) for p in poses])
+            return [f"inst{int(p[0, 3])}" for p in poses]
+
+    class Fus:
+        def __init__(self):
+            self.kf, self.fin = [], []
+
+        def keyframe(self, i, pose, inst):
+            self.kf.append((i, inst))
+
+        def finish(self, i, pose, is_kf):
+            self.fin.append(i)
+
+    def frames(ids):
+        poses = np.stack([np.eye(4, dtype=np.float32) for _ in ids])
+        poses[:, 0, 3] = ids
+        return (torch.zeros(len(ids), 2, 2, 3, dtype=torch.uint8), torch.ones(len(ids), 2, 2), poses)
+
+    for n, gap in [(23, 5), (21, 5), (7, 1), (9, 25)]:
+        det, fus = Det(), Fus()
+        pipe = Pipeline(det, fus, gap)
+        pipe.run(frames, n)
+        kf = [i for i in range(n) if i % gap == 0]
+        assert sorted(det.pre) == [i for i in range(n) if i % gap != 0]
+        assert pipe.frames_preprocessed == n - len(kf)
+        # the batch padding repeats the last keyframe; its results are dropped
+        flat = [i for b in det.det for i in b]
+        assert flat[:len(kf)] == kf and set(flat[len(kf):]) <= {kf[-1]}
+        assert [i for i, _ in fus.kf] == kf and all(x == f"inst{i}" for i, x in fus.kf)
+        assert fus.fin == ([n - 1] if (n - 1) % gap else [])

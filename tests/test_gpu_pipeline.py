@@ -312,6 +312,16 @@ class _DemoDetect:
         f[near] = t[pick[near]] * 30.0 + f[near] * 0.4
         return torch.from_numpy(f), None
 
+    def preprocess_frames(self, depth, poses):
+        """demo.py:121-131 on non-keyframes: bf_depth_preprocess (standardise + unproject)"""
+        from boxfusion_amd import _lib
+        from boxfusion_amd.synthetic import SCANNET_K
+        n = depth.shape[0]
+        K = torch.from_numpy(np.stack([SCANNET_K] * n)).to(self.dev)
+        RT = torch.from_numpy(np.asarray(poses, np.float32)).to(self.dev)
+        self.frames_done = getattr(self, "frames_done", 0) + n
+        return _lib.depth_preprocess(depth, K, RT, 10.0)
+
     def __call__(self, rgb, depth, poses):
         from boxfusion_amd import _lib
         from boxfusion_amd.pipeline import scene_instances
@@ -370,7 +380,9 @@ def test_pipeline_run_vs_reference_demo_gap25(dev, monkeypatch):
         return (torch.from_numpy(rgb).to(dev), torch.from_numpy(depth).to(dev),
                 np.stack([scene.pose(i) for i in ids]))
 
-    Pipeline(det, fusion, gap).run(frames, n)
+    pipe = Pipeline(det, fusion, gap)
+    pipe.run(frames, n)
+    assert pipe.frames_preprocessed == det.frames_done == n - len(range(0, n, gap))
     bm = fusion.box_manager
     ragged = lambda flat, off: [flat[off[i]:off[i + 1]].tolist() for i in range(len(off) - 1)]
     assert bm.fusion_list == ragged(d["fusion_list_flat"], d["fusion_list_off"])

@@ -120,3 +120,14 @@ def test_faceon_fusion_reference_pinned():
             n_upd += 1
     assert OR.hull_overflow() == (0, 0)
     assert n_upd == len(views)
+
+
+def test_backproject_vs_reference_unproject():
+    """oracle.backproject (the a13 checker of test_gpu_fusion.py) against the reference's own
+    tools/utils.unproject output on the same depth / K / RT (utils.npz, make_golden_utils.py):
+    valid mask bit for bit, points to f32 rounding of the 4x4 inverse"""
+    u = TU.load("utils.npz")
+    xyz, valid = OR.backproject(u["depth"], u["K"], u["RT"], 10.0)
+    np.testing.assert_array_equal(valid, u["valid"])
+    assert valid.sum() > 1000 and (~valid).sum() > 100
+    np.testing.assert_allclose(xyz, u["xyz"], rtol=1e-5, atol=2e-5)
