@@ -425,6 +425,8 @@ def depth_preprocess(depth, K=None, RT=None, max_depth=10.0, out=None, params=No
     params f32[b,2]) and, with K f32[b,3,3] / RT f32[b,4,4], the back-projection (xyz f32[b,h,w,3],
     valid bool[b,h,w]) from the same pass"""
     depth = _need(depth.contiguous(), torch.float32, "depth")
+    if not depth.is_cuda:
+        raise HipError("bf_depth_preprocess: depth must be a device tensor (no CPU path)")
     b, h, w = depth.shape
     out = torch.empty_like(depth) if out is None else out
     params = torch.empty((b, 2), dtype=torch.float32, device=depth.device) if params is None else params
