@@ -420,10 +420,12 @@ def depth_standardize(depth, out=None, params=None):
     return depth_preprocess(depth, out=out, params=params)
 
 
-def depth_preprocess(depth, K=None, RT=None, max_depth=10.0, out=None, params=None, xyz=None, valid=None):
+def depth_preprocess(depth, K=None, RT=None, max_depth=10.0, out=None, params=None, xyz=None, valid=None,
+                     ws=None):
     """demo.py:121-131 per-frame depth work for a batch: depth f32[b,h,w] -> (standardised,
     params f32[b,2]) and, with K f32[b,3,3] / RT f32[b,4,4], the back-projection (xyz f32[b,h,w,3],
-    valid bool[b,h,w]) from the same pass"""
+    valid bool[b,h,w]) from the same pass.  ws: a zero-filled workspace of
+    bf_depth_standardize_workspace_size bytes owned by the caller (default: one per stream)"""
     depth = _need(depth.contiguous(), torch.float32, "depth")
     if not depth.is_cuda:
         raise HipError("bf_depth_preprocess: depth must be a device tensor (no CPU path)")
@@ -438,7 +440,8 @@ def depth_preprocess(depth, K=None, RT=None, max_depth=10.0, out=None, params=No
             raise HipError(f"bf_depth_preprocess: K {tuple(K.shape)} / RT {tuple(RT.shape)} for {b} frames")
         xyz = torch.empty((b, h, w, 3), dtype=torch.float32, device=depth.device) if xyz is None else xyz
         valid = torch.empty((b, h, w), dtype=torch.uint8, device=depth.device) if valid is None else valid
-    ws = depth_workspace(b, h, w, depth.device)
+    if ws is None:
+        ws = depth_workspace(b, h, w, depth.device)
     _check(lib().bf_depth_preprocess(_ptr(depth), c_int(b), c_int(h), c_int(w), _ptr(out), _ptr(params),
                                      _ptr(K) if bp else None, _ptr(RT) if bp else None,
                                      c_float(max_depth if max_depth is not None else 0.0),
@@ -935,9 +938,10 @@ def fusion_fit(view_off, n_views, view_box, view_R, view_score, view_pose, view_
     return res[0]
 
 
-def depth_preprocess(depth, K=None, RT=None, max_depth=10.0, out=None, params=None, xyz=None, valid=None):
+def depth_preprocess(depth, K=None, RT=None, max_depth=10.0, out=None, params=None, xyz=None, valid=None,
+                     ws=None):
     t = _timer()
-    fn = lambda: _depth_preprocess_untimed(depth, K, RT, max_depth, out, params, xyz, valid)
+    fn = lambda: _depth_preprocess_untimed(depth, K, RT, max_depth, out, params, xyz, valid, ws)
     if t is None:
         return fn()
     b, h, w = depth.shape
@@ -949,9 +953,15 @@ def depth_preprocess(depth, K=None, RT=None, max_depth=10.0, out=None, params=No
     return t.record(tags, 0.0, nbytes, fn)
 
 
-def depth_standardize(depth, out=None, params=None):
+def depth_standardize(depth, out=None, params=None, ws=None):
     """depth f32[b,h,w] -> (standardised f32[b,h,w], params f32[b,2])"""
-    return depth_preprocess(depth, out=out, params=params)
+    return depth_preprocess(depth, out=out, params=params, ws=ws)
+
+
+def new_depth_workspace(b, h, w, device):
+    """a caller-owned zero-filled workspace for bf_depth_preprocess (one per concurrent user)"""
+    size = int(lib().bf_depth_standardize_workspace_size(c_int(b), c_int(h), c_int(w)))
+    return torch.zeros(max(size, 1), dtype=torch.uint8, device=device)
 
 
 # ------------------------------------------------------------------------------------------

@@ -111,6 +111,9 @@ class DetectStage:
         self.in_depth = torch.zeros((batch, H // self.r, W // self.r), dtype=torch.float32, device=self.dev)
         self.in_Tg = torch.zeros((batch, 3, 3), dtype=torch.float32, device=self.dev)
         self.in_pose = torch.zeros((batch, 4, 4), dtype=torch.float32, device=self.dev)
+        # the depth kernels' workspace (zero-filled, left zeroed by every call; eager and graph
+        # replays of this stage use it one at a time)
+        self.ds_ws = _lib.new_depth_workspace(batch, H // self.r, W // self.r, self.dev)
         k = crops_per_frame
         self.top_b = torch.arange(batch, device=self.dev).repeat_interleave(k)
         self.top_b32 = self.top_b.to(torch.int32)
@@ -139,10 +142,11 @@ class DetectStage:
         B, H, W = self.B, self.H, self.W
         if self.backproject:
             # depth standardisation + unproject of the same depth maps in one pass (demo.py:121-131)
-            dstd, params, xyz, valid = _lib.depth_preprocess(self.in_depth, self.Kd_dev, self.in_pose, 10.0)
+            dstd, params, xyz, valid = _lib.depth_preprocess(self.in_depth, self.Kd_dev, self.in_pose, 10.0,
+                                                             ws=self.ds_ws)
             self.out["xyz"] = [(xyz[b], valid[b]) for b in range(B)]
         else:
-            dstd, params = _lib.depth_standardize(self.in_depth)
+            dstd, params = _lib.depth_standardize(self.in_depth, ws=self.ds_ws)
         res = self.cutr(self.in_rgb, dstd, params, self.K_dev, self.in_Tg, [(H, W)] * B,
                         K_host=self.K_host, K_inv=self.Kinv_dev)
         scores = torch.stack([r.scores for r in res])
