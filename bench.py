@@ -783,7 +783,7 @@ def main(argv=None):
         # box-fusion fitness) on their own after the timed region: a fresh fusion state machine
         # over the stream's first keyframes, synchronous, HIP events around every launch
         from boxfusion_amd.pipeline import scene_instances
-        fst = FusionStage(CFG, Kf, H=FH, W=FW, device=dev)
+        fst = FusionStage(CFG, Kf, H=FH, W=FW, device=dev, native=False)   # Python-driven: per-kernel timers
         fus_timer = _lib.KernelTimer()
         with fus_timer:
             for k in range(args.roofline_keyframes):

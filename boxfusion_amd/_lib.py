@@ -363,6 +363,90 @@ def fusion_fitness(box, R, view_pose, view_tc, pst, search_size, cfg: FuseCfg):
     return out
 
 
+# ------------------------------------------------------------------------------------------
+# keyframe sequencer (bf_fseq_*)
+# ------------------------------------------------------------------------------------------
+class FseqCfg(ctypes.Structure):
+    _fields_ = [("nms", NmsCfg), ("corr", CorrCfg), ("fuse", FuseCfg), ("use_fusion", ctypes.c_int32),
+                ("strict_hull", ctypes.c_int32)]
+
+
+FSEQ_STATE_N = 16
+
+
+class FusionSequencer:
+    """Owner of one bf_fseq: the demo.py:200-305 keyframe sequence over batches of keyframes,
+    all_pred_box on the device and BoxManager's lists in the library (include/boxfusion_hip.h).
+    Calls launch on the calling thread's current stream."""
+
+    def __init__(self):
+        L = lib()
+        L.bf_fseq_error.restype = ctypes.c_char_p
+        L.bf_fseq_error.argtypes = [c_void_p]
+        L.bf_fseq_destroy.restype = None
+        L.bf_fseq_destroy.argtypes = [c_void_p]
+        self._L = L
+        self.h = c_void_p()
+        _check(L.bf_fseq_create(ctypes.byref(self.h)), "bf_fseq_create")
+        self._state = np.zeros(FSEQ_STATE_N, np.int64)
+
+    def _rc(self, rc, name):
+        if rc != 0:
+            raise HipError(f"{name}: {self._L.bf_fseq_error(self.h).decode()} (bf_status {rc})")
+        if _SYNC_DEBUG:
+            torch.cuda.synchronize()
+
+    def keyframes(self, cfg: FseqCfg, sizes, p_base, fields, K, pst):
+        """sizes: int32 [n_kf]; fields: (box, R, score, box2d, pose, proj) of the per-frame table,
+        contiguous f32 device tensors with p_rows rows"""
+        sizes = np.ascontiguousarray(sizes, np.int32)
+        p_rows = int(fields[0].shape[0])
+        self._rc(self._L.bf_fseq_keyframes(
+            self.h, ctypes.byref(cfg), c_int(len(sizes)), sizes.ctypes.data_as(c_void_p),
+            ctypes.c_int64(int(p_base)), ctypes.c_int64(p_rows), *[_ptr(t) for t in fields], _ptr(K),
+            _ptr(pst), _stream()), "bf_fseq_keyframes")
+
+    def sync(self):
+        self._rc(self._L.bf_fseq_sync(self.h), "bf_fseq_sync")
+
+    def state(self):
+        """bf_fseq_state (waits for the stream and applies a pending fusion result)"""
+        self._rc(self._L.bf_fseq_state(self.h, self._state.ctypes.data_as(c_void_p)), "bf_fseq_state")
+        return self._state.copy()
+
+    def lists(self, which, rows, items):
+        lens = np.zeros(max(rows, 1), np.int32)
+        flat = np.zeros(max(items, 1), np.int32)
+        self._rc(self._L.bf_fseq_lists(self.h, c_int(which), lens.ctypes.data_as(c_void_p),
+                                       flat.ctypes.data_as(c_void_p)), "bf_fseq_lists")
+        off = np.concatenate([[0], np.cumsum(lens[:rows])])
+        fl = flat.tolist()
+        return [fl[off[i]:off[i + 1]] for i in range(rows)]
+
+    def flags(self, n):
+        out = np.zeros(max(n, 1), np.int32)
+        self._rc(self._L.bf_fseq_flags(self.h, out.ctypes.data_as(c_void_p)), "bf_fseq_flags")
+        return out[:n].tolist()
+
+    def global_rows(self, n, device):
+        """all_pred_box's init_id (host int32), xyzlhw [n,6] and valid_num [n] (device copies)"""
+        ids = np.zeros(max(n, 1), np.int32)
+        xyz = torch.empty((n, 6), dtype=torch.float32, device=device)
+        vn = torch.empty(n, dtype=torch.float32, device=device)
+        self._rc(self._L.bf_fseq_global(self.h, ids.ctypes.data_as(c_void_p), _ptr(xyz) if n else None,
+                                        _ptr(vn) if n else None, _stream()), "bf_fseq_global")
+        return ids[:n], xyz, vn
+
+    def __del__(self):
+        h, L = getattr(self, "h", None), getattr(self, "_L", None)
+        try:
+            if h is not None and h.value and L is not None:
+                L.bf_fseq_destroy(h)
+                self.h = None
+        except Exception:  # noqa: BLE001 - interpreter teardown: the process frees everything
+            pass
+
+
 def filter_cfg(det_cfg, W, H):
     """FilterCfg from a config's `detection` section (demo.py:138-148 keys)"""
     c = FilterCfg()

@@ -53,6 +53,21 @@ __device__ __forceinline__ void box_center(const float* corners, int i, float* c
     }
 }
 
+// global -> LDS copy with 8 independent loads in flight per lane (a plain strided loop waits for
+// every load before the next: one memory latency per 64 elements)
+template <typename T>
+__device__ __forceinline__ void stage_lds(T* dst, const T* __restrict__ src, int count, int t, int nt) {
+    int q = t;
+    for (; q + 7 * nt < count; q += 8 * nt) {
+        T v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = src[q + k * nt];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) dst[q + k * nt] = v[k];
+    }
+    for (; q < count; q += nt) dst[q] = src[q];
+}
+
 // rank sort of distinct int values in LDS (ascending), in place via a scratch buffer
 __device__ void block_sort_distinct(int* a, int* tmp, int n) {
     for (int q = threadIdx.x; q < n; q += SCAN_THREADS) tmp[q] = a[q];
@@ -94,8 +109,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_nms_scan(
     const int cap = cfg.list_capacity;
 
     for (int i = t; i < n; i += SCAN_THREADS) box_center(corners, i, cen + 3 * i);
-    if (iou_lds)
-        for (int q = t; q < n * n; q += SCAN_THREADS) iou_s[q] = iou[q];
+    if (iou_lds) stage_lds(iou_s, iou, n * n, t, SCAN_THREADS);
     const double* I = iou_lds ? iou_s : iou;
     // order = scores.argsort()[::-1]: descending, ties -> higher index first
     for (int i = t; i < n; i += SCAN_THREADS) {
@@ -278,8 +292,8 @@ __global__ void __launch_bounds__(64) k_nms_scan_w(
     int* supp = bufB + n + 1;
     int* keep = supp + n + 1;
     int* succ = keep + n + 2;
-    for (int q = t; q < n * n; q += 64) I[q] = iou[q];
-    for (int q = t; q < n * cap; q += 64) fls[q] = fl[q];
+    stage_lds(I, iou, n * n, t, 64);
+    stage_lds(fls, fl, n * cap, t, 64);
     for (int q = t; q < n; q += 64) {
         fll[q] = fl_len[q];
         iid[q] = init_id[q];

@@ -29,43 +29,169 @@ import numpy as np
 import torch
 
 from boxfusion_amd import _lib
-from boxfusion_amd.box_fusion import BoxFusion
+from boxfusion_amd.box_fusion import BoxFusion, _warn_hull_once
 from boxfusion_amd.box_manager import BoxManager
 from boxfusion_amd.instances import Instances3D
 
 
 class FusionStage:
+    """`native` (default: env BF_NATIVE_FUSION, on): the keyframe sequence after the per-box
+    geometry runs in the library's sequencer (bf_fseq, one call per batch of keyframes), with
+    all_pred_box's rows and BoxManager's lists owned there; `box_manager`, `all_pred_box`,
+    `all_poses`, `fuser` and `stats` are then read-only mirrors refreshed on access.  native=False
+    (or the non-joint association, or box_fusion.check_valid) drives the same kernels from Python
+    with the reference's containers.  Both give bit-identical results."""
+
     def __init__(self, cfg, K3, H=480, W=640, device="cuda", legacy_promotion=True,
-                 stale_last_frame=True):
+                 stale_last_frame=True, native=None):
         self.cfg = cfg
         self.dev = torch.device(device)
         self.K3 = np.asarray(K3, np.float32)
         self.H, self.W = H, W
         self.gap = int(cfg["data"].get("gap", 1)) if "data" in cfg else 1
-        self.box_manager = BoxManager(cfg)
-        self.fuser = BoxFusion(cfg, device=device, legacy_promotion=legacy_promotion)
-        self.fuser.update_intrinsics((W, H), self.K3)
-        self.fuser.update_K_flag = True
+        self._bm = BoxManager(cfg)
+        self._fuser = BoxFusion(cfg, device=device, legacy_promotion=legacy_promotion)
+        self._fuser.update_intrinsics((W, H), self.K3)
+        self._fuser.update_K_flag = True
         self.stale_last_frame = stale_last_frame
-        self.all_pred_box = None
-        self.all_poses = None
+        self._apb = None
+        self._all_poses = None
         self.per_frame_ins = None
         self.all_kf_pose = {}
         self.box_count = 0
-        self.last_pred = None
+        self._last_pred = None
         self._stats = dict(keyframes=0, suppressed=0)
         self.K_dev = torch.from_numpy(self.K3).to(self.dev)     # uploaded once
         self._pf_table = None    # append-only device table behind per_frame_ins
         # nms + correspondence association chained on the device (one host round trip);
         # False: the reference's two separate calls (same results)
         self.joint = os.environ.get("BF_JOINT_ASSOC", "1") != "0"
+        self.native = (os.environ.get("BF_NATIVE_FUSION", "1") != "0") if native is None else bool(native)
+        self._mode = None        # "native" | "python", fixed by the first keyframe
+        self._seq = None         # _lib.FusionSequencer in native mode
+        self._ver = 0            # sequencer calls so far (mirror cache key)
+        self._mirror_ver = -1
+        self._apb_ver = -1
+        self._seq_cfg = None
+
+    # -- mode and mirrors ------------------------------------------------------------------------
+    def _select_mode(self):
+        if self._mode is None:
+            bf = self.cfg["box_fusion"]
+            ok = self.native and self.joint and not bf.get("check_valid", False)
+            self._mode = "native" if ok else "python"
+        return self._mode
+
+    def _refresh(self):
+        """pull the sequencer's BoxManager / BoxFusion state into the mirrors (one wait)"""
+        if self._mode != "native" or self._seq is None or self._mirror_ver == self._ver:
+            return
+        st = self._seq.state()
+        bm, f = self._bm, self._fuser
+        bm.fusion_list = self._seq.lists(0, int(st[1]), int(st[2]))
+        bm._fusion_flag = self._seq.flags(int(st[3]))
+        bm.already_fusion = self._seq.lists(1, int(st[4]), int(st[5]))
+        if int(st[9]) > f.hull_overflow_calls:
+            _warn_hull_once()
+        f.hull_overflow_calls, f.fit_calls, f.updated_total = int(st[9]), int(st[8]), int(st[7])
+        f.last_stats = dict(jobs=int(st[10]), updated=int(st[11]), views=int(st[13]), iters=int(st[12]))
+        self._stats["suppressed"] = int(st[6])
+        self._mirror_ver = self._ver
+
+    @property
+    def box_manager(self):
+        self._refresh()
+        return self._bm
+
+    @property
+    def fuser(self):
+        self._refresh()
+        return self._fuser
+
+    @property
+    def all_pred_box(self):
+        if self._mode != "native" or self._seq is None:
+            return self._apb
+        if self._apb_ver != self._ver:
+            st = self._seq.state()
+            n = int(st[0])
+            if n < 0:
+                self._apb = None
+            else:
+                ids, xyz, vn = self._seq.global_rows(n, self.dev)
+                apb = self.per_frame_ins[ids.astype(np.int64)]
+                b = apb.pred_boxes_3d
+                apb.pred_boxes_3d = type(b)._views(xyz, b.R)      # fused rows refined
+                apb.valid_num = vn
+                self._apb = apb
+            self._apb_ver = self._ver
+        return self._apb
+
+    @all_pred_box.setter
+    def all_pred_box(self, v):
+        if self._mode == "native":
+            raise _lib.HipError("all_pred_box is owned by the native sequencer (native=False to edit it)")
+        self._apb = v
+
+    @property
+    def all_poses(self):
+        if self._mode != "native" or self._seq is None:
+            return self._all_poses
+        apb = self.all_pred_box
+        return None if apb is None else apb.cam_pose.cpu().numpy()
+
+    @all_poses.setter
+    def all_poses(self, v):
+        if self._mode == "native":
+            raise _lib.HipError("all_poses is owned by the native sequencer")
+        self._all_poses = v
+
+    @property
+    def last_pred(self):
+        lp = self._last_pred
+        if isinstance(lp, tuple):        # native batches: (batch, first row, rows), sliced lazily
+            preds, off, n = lp
+            lp = self._last_pred = preds[off:off + n]
+        return lp
+
+    @last_pred.setter
+    def last_pred(self, v):
+        self._last_pred = v
 
     @property
     def stats(self):
         """keyframes, suppressed boxes, fused boxes (resolves a deferred fusion result)"""
-        self.box_manager.flush()
-        return dict(self._stats, fused=self.fuser.updated_total)
+        bm = self.box_manager
+        bm.flush()
+        return dict(self._stats, fused=self._fuser.updated_total)
 
+    def _to_python(self):
+        """hand the state from the sequencer to the Python-driven path (same values)"""
+        if self._mode != "native":
+            return
+        if self._seq is not None:
+            self._refresh()
+            apb = self.all_pred_box
+            self._all_poses = self.all_poses
+            self._apb = apb
+            self._seq = None
+        self._mode = "python"
+
+    def _fseq_cfg(self):
+        f = self._fuser
+        key = (f.H, f.W, f.K.tobytes(), f.legacy_promotion, f.strict_hull, f.fusion_iters, f.pst_size)
+        if self._seq_cfg is None or self._seq_cfg[0] != key:
+            c = _lib.FseqCfg()
+            bf = self.cfg["box_fusion"]
+            c.nms = self._bm.nms_cfg(bf["nms_threshold"])
+            c.corr = self._bm.corr_cfg(self.cfg["association"]["small_threshold"], self.W, self.H)
+            c.fuse = f.fuse_cfg()
+            c.use_fusion = 1 if bf.get("use", True) else 0
+            c.strict_hull = 1 if f.strict_hull else 0
+            self._seq_cfg = (key, c)
+        return self._seq_cfg[1]
+
+    # -- keyframes -------------------------------------------------------------------------------
     def keyframes(self, counts, poses, preds, sizes):
         """Several keyframes in frame order whose detections arrive as ONE Instances3D `preds`
         (camera frame, keyframe j's boxes are rows [off_j, off_j + sizes[j])): the per-box
@@ -86,6 +212,9 @@ class FusionStage:
             preds.valid_num = torch.zeros(n_tot, device=self.dev)
             preds.pred_boxes_3d.transform2world(preds.cam_pose)
             preds.project_3d_boxes(self.K_dev, H=self.H, W=self.W)
+        if self._select_mode() == "native":
+            self._native_batch(counts, poses, preds if n_tot else None, sizes)
+            return
         off = 0
         for j, c in enumerate(counts):
             n = int(sizes[j])
@@ -93,12 +222,46 @@ class FusionStage:
             off += n
         _lib.check_status(self.dev)     # row gathers of the batch (one read per batch)
 
+    def _native_batch(self, counts, poses, preds, sizes):
+        if self._seq is None:
+            self._seq = _lib.FusionSequencer()
+        n_tot = int(sizes.sum())
+        p_base = len(self.per_frame_ins) if self.per_frame_ins is not None else 0
+        if n_tot:
+            # per_frame_ins = cat(per_frame_ins, pred) for the whole batch (one gather)
+            cur = self.per_frame_ins if self.per_frame_ins is not None else preds[0:0]
+            self.per_frame_ins = self._per_frame_append(preds, cur)
+            pf = self.per_frame_ins
+            b3 = pf.pred_boxes_3d
+            fields = [t if t.dtype == torch.float32 and t.is_contiguous() else t.float().contiguous()
+                      for t in (b3.tensor, b3.R, pf.scores, pf.pred_boxes, pf.cam_pose, pf.projected_boxes)]
+            self._ver += 1
+            self._seq.keyframes(self._fseq_cfg(), sizes, p_base, fields, self.K_dev, self._fuser._pst_dev)
+        bm = self._bm
+        off = 0
+        for j, c in enumerate(counts):
+            n = int(sizes[j])
+            self.all_kf_pose[c] = np.asarray(poses[j], np.float32)
+            if n:
+                self._stats["keyframes"] += 1
+                self.box_count += n
+                bm.last_fusion_frame.extend([0] for _ in range(n))
+                self._last_pred = (preds, off, n)
+            else:
+                self._last_pred = None
+            bm.num_record[c] = self.box_count
+            off += n
+
     def keyframe(self, count, pose, pred, prepared=False):
         """pred: Instances3D of this keyframe in CAMERA coordinates (after the detection filters
         and the CLIP step), tensors on the device; it is modified in place like the reference's.
         prepared=True: world transform, projection and the id fields were already applied
         (keyframes())."""
-        cfg, bm = self.cfg, self.box_manager
+        if not prepared and self._select_mode() == "native":
+            n = len(pred) if pred is not None and len(pred._fields) else 0
+            self.keyframes([count], np.asarray(pose, np.float32)[None], pred if n else None, [n])
+            return
+        cfg, bm = self.cfg, self._bm
         self.last_pred = pred
         pose = np.asarray(pose, np.float32)
         self.all_kf_pose[count] = pose
@@ -117,18 +280,18 @@ class FusionStage:
             pred.project_3d_boxes(self.K_dev, H=self.H, W=self.W)
         self.box_count += n
         bm.num_record[count] = self.box_count
-        if self.all_pred_box is None and (count < self.gap or self.per_frame_ins is None):
-            self.all_pred_box = pred
-            self.all_poses = pose_np
+        if self._apb is None and (count < self.gap or self.per_frame_ins is None):
+            self._apb = pred
+            self._all_poses = pose_np
             self.per_frame_ins = pred
             bm.init_new_predictions(n, 0)
             return
         bm.init_new_predictions(n, len(self.per_frame_ins))
-        n_before = len(self.all_pred_box)
-        cur_global = self.all_pred_box
-        all_pred_box = Instances3D.cat([self.all_pred_box, pred])
+        n_before = len(self._apb)
+        cur_global = self._apb
+        all_pred_box = Instances3D.cat([self._apb, pred])
         self.per_frame_ins = self._per_frame_append(pred)
-        all_poses = np.concatenate((self.all_poses, pose_np), axis=0)
+        all_poses = np.concatenate((self._all_poses, pose_np), axis=0)
         corners = all_pred_box.pred_boxes_3d.corners       # shared by both association steps
         if self.joint and len(all_pred_box) > 1:
             # nms + correspondence back to back on the device, one read-back
@@ -144,7 +307,7 @@ class FusionStage:
             if not any_cur:
                 self._stats["suppressed"] += len(success)
                 bm.update(keep_idx)
-                self.all_pred_box, self.all_poses = all_pred_box, all_poses
+                self._apb, self._all_poses = all_pred_box, all_poses
                 return
         else:
             mask, success = Instances3D.spatial_association(all_pred_box, cfg["box_fusion"]["nms_threshold"],
@@ -165,19 +328,20 @@ class FusionStage:
             if cfg["box_fusion"].get("check_valid", False):
                 all_pred_box = bm.check_valid_num(all_pred_box, count, self.gap)
             if cfg["box_fusion"].get("use", True):
-                self.fuser.boxfusion(all_pred_box, self.per_frame_ins, bm, defer=True)
+                self._fuser.boxfusion(all_pred_box, self.per_frame_ins, bm, defer=True)
         else:
             all_pred_box = all_pred_box[_lib.h2d(np.asarray(keep_idx, np.int64), self.dev)]
             all_poses = all_poses[keep_idx]
             bm.update(keep_idx)
-        self.all_pred_box, self.all_poses = all_pred_box, all_poses
+        self._apb, self._all_poses = all_pred_box, all_poses
 
-    def _per_frame_append(self, pred):
+    def _per_frame_append(self, pred, cur=None):
         """per_frame_ins = cat(per_frame_ins, pred) on an append-only table: every field lives in a
         preallocated device buffer (capacity doubling), the new rows are written into its tail by
         one bf_rows_gather launch and per_frame_ins becomes views of the first n rows.  Rows never
-        change once written, so earlier views stay valid."""
-        cur = self.per_frame_ins
+        change once written, so earlier views stay valid.  `cur`: the rows to append to (default
+        per_frame_ins)."""
+        cur = self.per_frame_ins if cur is None else cur
         n, m = len(cur), len(pred)
         specs = []   # (key, box_type or None, [tensors of cur], [tensors of pred])
         for k, v in cur._fields.items():
@@ -225,14 +389,23 @@ class FusionStage:
         """demo.py:200 `count == len(dataset) - 1` re-entry on a non-keyframe last frame."""
         if last_was_keyframe or not self.stale_last_frame or self.last_pred is None:
             return
+        if self._mode == "native" and self._stats["keyframes"] == 1:
+            # one keyframe so far: the reference's all_pred_box and per_frame_ins ARE that
+            # keyframe's pred object (demo.py:226-241), and the re-entry transforms it in place
+            # through those aliases; the Python path reproduces the aliasing
+            last = self.last_pred
+            self._to_python()
+            self._apb = self.per_frame_ins = last
+            self._pf_table = None
         self.keyframe(count, pose, self.last_pred)
 
     # -- results ---------------------------------------------------------------------------------
     def boxes(self):
         """global boxes (xyzlhw [N,6], R [N,3,3]) on the host"""
-        if self.all_pred_box is None:
+        apb = self.all_pred_box
+        if apb is None:
             return np.zeros((0, 6), np.float32), np.zeros((0, 3, 3), np.float32)
-        b = self.all_pred_box.pred_boxes_3d
+        b = apb.pred_boxes_3d
         return b.tensor.cpu().numpy(), b.R.cpu().numpy()
 
 

@@ -247,6 +247,58 @@ int bf_fusion_fitness(const float* box, const float* R, int n_views, const float
                       void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Keyframe sequencer: the state machine of demo.py:200-305 over a batch of keyframes in one call
+ *   (FusionStage.keyframe's per-keyframe sequence: Instances3D.cat (demo.py:245),
+ *   init_new_predictions, spatial_association + correspondence_association (:247-262, the
+ *   bf_nms_scan / bf_corr_assoc_chained pair), all_pred_box[keep_idx] + BoxManager.update
+ *   (:263-268 / :300-304), BoxFusion.boxfusion (:270-299, bf_fusion_fit + write-back)).
+ * The exception to "stateless, caller-owned memory": a bf_fseq owns all_pred_box's device rows
+ * (stream-ordered allocations that grow by doubling), BoxManager's fusion_list / fusion_flag /
+ * already_fusion on the host, and pinned staging buffers.  One host wait per keyframe (the
+ * association read-back); a BoxFusion result is applied at the next keyframe's wait or at
+ * bf_fseq_sync, where BoxManager.flush applies it in the Python path.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct bf_fseq bf_fseq;
+typedef struct {
+    bf_nms_cfg nms;          /* nms_threshold, association gaps, list capacity */
+    bf_corr_cfg corr;        /* small_threshold, image size, same list capacity */
+    bf_fuse_cfg fuse;        /* BoxFusion's particle search */
+    int32_t use_fusion;      /* cfg box_fusion.use */
+    int32_t strict_hull;     /* 1: BF_DEV_HULL_OVERFLOW is an error (box_fusion.strict_hull) */
+} bf_fseq_cfg;
+
+int bf_fseq_create(bf_fseq** out);
+void bf_fseq_destroy(bf_fseq* s);
+/* message of the last failing call */
+const char* bf_fseq_error(const bf_fseq* s);
+
+/* n_kf keyframes in frame order; keyframe j's detections are the per-frame rows
+ * [p_base + sizes[0] + .. + sizes[j-1], + sizes[j]) (sizes[j] = 0: a keyframe without boxes).
+ * The per-frame table (per_frame_ins, p_rows rows, the new keyframes' rows already world-space,
+ * projected and appended): p_box f32[p_rows,6], p_R f32[p_rows,3,3], p_score f32[p_rows],
+ * p_box2d f32[p_rows,4], p_pose f32[p_rows,4,4] (cam_pose), p_proj f32[p_rows,8,2]
+ * (projected_boxes).  A row's init_id is its row index.  K f32[3,3], pst f32[pst_size,6]. */
+int bf_fseq_keyframes(bf_fseq* s, const bf_fseq_cfg* cfg, int n_kf, const int32_t* sizes,
+                      int64_t p_base, int64_t p_rows, const float* p_box, const float* p_R,
+                      const float* p_score, const float* p_box2d, const float* p_pose,
+                      const float* p_proj, const float* K, const float* pst, void* stream);
+/* wait for the sequencer's stream and apply a pending BoxFusion result */
+int bf_fseq_sync(bf_fseq* s);
+/* (after a sync) [0] all_pred_box rows (-1: None), [1] fusion_list rows, [2] their items,
+ * [3] fusion_flag length, [4] already_fusion rows, [5] their items, [6] boxes suppressed,
+ * [7] boxes fused (updated), [8] boxfusion calls with jobs, [9] of them with
+ * BF_DEV_HULL_OVERFLOW, [10..13] the last call's jobs / updated / iterations / views,
+ * [14] association steps, [15] 0 */
+#define BF_FSEQ_STATE_N 16
+int bf_fseq_state(bf_fseq* s, int64_t* out);
+/* which 0: fusion_list, 1: already_fusion -> host lens[rows], items[total] (concatenated) */
+int bf_fseq_lists(bf_fseq* s, int which, int32_t* lens, int32_t* items);
+int bf_fseq_flags(bf_fseq* s, int32_t* flags);
+/* all_pred_box: host init_id[rows] (= per-frame row), device xyzlhw f32[rows,6] (fused rows
+ * refined) and valid_num f32[rows], copied on `stream` */
+int bf_fseq_global(bf_fseq* s, int32_t* init_id, float* xyzlhw, float* valid_num, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Per-frame depth work
  * ------------------------------------------------------------------------------------------ */
 /* Preprocessor.standardize_depth_map (preprocessor.py:97-129) for a batch of b frames:

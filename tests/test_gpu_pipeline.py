@@ -35,20 +35,22 @@ def _inject_geometry(monkeypatch, dev, src):
     monkeypatch.setattr(Instances3D, "project_3d_boxes", project)
 
 
+@pytest.mark.parametrize("native", [True, False])
 @pytest.mark.parametrize("name", ["fusion_trace.npz", "fusion_trace_small.npz"])
-def test_fusion_stage_vs_trace(dev, name, monkeypatch):
+def test_fusion_stage_vs_trace(dev, name, native, monkeypatch):
     """demo.py keyframe state machine on the GPU == the reference's recorded chain, bit for bit,
     given the reference's own world-space boxes and projections (pf_* of the trace).  The trace
     is the reference's control flow with the exact hull wherever its kernel overruns
     convex_inter[8] (recorded per keyframe, hull_over): the keyframes before the first such
     fusion are reference-pinned outright, and BoxFusion's BF_DEV_HULL_OVERFLOW count matches the
-    record keyframe by keyframe."""
+    record keyframe by keyframe.  native: the library's keyframe sequencer (bf_fseq) runs the
+    state machine; else Python drives the same kernels."""
     from boxfusion_amd.fusion_stage import FusionStage
     from boxfusion_amd.pipeline import scene_instances
     from boxfusion_amd.synthetic import SCANNET_K
     t = TU.load(name)
     _inject_geometry(monkeypatch, dev, dict(tensor=t["pf_tensor"], R=t["pf_R"], proj=t["pf_proj"]))
-    st = FusionStage(TU.SCANNET_CFG, SCANNET_K, device=dev, legacy_promotion=False)
+    st = FusionStage(TU.SCANNET_CFG, SCANNET_K, device=dev, legacy_promotion=False, native=native)
     nd = t["n_det"]
     for k, frame in enumerate(t["frame"]):
         a, b = int(nd[:k].sum()), int(nd[:k + 1].sum())
@@ -86,7 +88,8 @@ def test_fusion_stage_own_geometry(dev):
         np.testing.assert_allclose(got[fused], want[fused], rtol=0, atol=5e-2, err_msg=f"kf {k}")
 
 
-def test_fusion_stage_vs_oracle_chain_gap1(dev, monkeypatch):
+@pytest.mark.parametrize("native", [True, False])
+def test_fusion_stage_vs_oracle_chain_gap1(dev, native, monkeypatch):
     """40 consecutive keyframes (gap=1, the benchmark's regime, numpy<2 promotion) against
     oracle/chain.py, bit for bit given the chain's geometry."""
     from boxfusion_amd.box_fusion import load_pst
@@ -96,7 +99,7 @@ def test_fusion_stage_vs_oracle_chain_gap1(dev, monkeypatch):
     from oracle.chain import OracleChain
     cfg = dict(TU.SCANNET_CFG, data=dict(gap=1))
     scene = Scene(seed=0)
-    st = FusionStage(cfg, SCANNET_K, device=dev)
+    st = FusionStage(cfg, SCANNET_K, device=dev, native=native)
     ch = OracleChain(cfg, SCANNET_K, pst=load_pst(), legacy=True)
     src = {}
     _inject_geometry(monkeypatch, dev, src)
@@ -141,14 +144,15 @@ def test_detect_stage_filtered(dev):
 
 
 def test_async_fusion_equals_sync(dev):
-    """AsyncFusion (worker thread + side stream) produces exactly the synchronous state."""
+    """AsyncFusion (worker thread + side stream, native sequencer) produces exactly the
+    synchronous Python-driven state."""
     from boxfusion_amd.fusion_stage import AsyncFusion, FusionStage
     from boxfusion_amd.pipeline import scene_instances
     from boxfusion_amd.synthetic import SCANNET_K, Scene
     cfg = dict(TU.SCANNET_CFG, data=dict(gap=1))
     scene = Scene(seed=0)
-    sync = FusionStage(cfg, SCANNET_K, device=dev)
-    asyn = AsyncFusion(FusionStage(cfg, SCANNET_K, device=dev))
+    sync = FusionStage(cfg, SCANNET_K, device=dev, native=False)
+    asyn = AsyncFusion(FusionStage(cfg, SCANNET_K, device=dev, native=True))
     for f in range(30):
         d = scene.detections(f)
         sync.keyframe(f, scene.pose(f), scene_instances(d, dev))
@@ -194,15 +198,16 @@ def test_detect_stage_graph_equals_eager(dev):
 
 def test_fusion_stage_batched_keyframes(dev):
     """FusionStage.keyframes (world transform / projection / ids batched over 8 keyframes, then
-    the serial association) == keyframe() one at a time, bit for bit, over 48 keyframes."""
+    the serial association in the native sequencer) == the Python-driven keyframe() one at a
+    time, bit for bit, over 48 keyframes."""
     from boxfusion_amd.fusion_stage import FusionStage
     from boxfusion_amd.instances import Instances3D
     from boxfusion_amd.pipeline import scene_instances
     from boxfusion_amd.synthetic import SCANNET_K, Scene
     cfg = dict(TU.SCANNET_CFG, data=dict(gap=1))
     scene = Scene(seed=0)
-    one = FusionStage(cfg, SCANNET_K, device=dev)
-    bat = FusionStage(cfg, SCANNET_K, device=dev)
+    one = FusionStage(cfg, SCANNET_K, device=dev, native=False)
+    bat = FusionStage(cfg, SCANNET_K, device=dev, native=True)
     for s0 in range(0, 48, 8):
         fr = list(range(s0, s0 + 8))
         dets = [scene.detections(f) for f in fr]
@@ -216,6 +221,77 @@ def test_fusion_stage_batched_keyframes(dev):
         for a, b in zip(bat.boxes(), one.boxes()):
             np.testing.assert_array_equal(a, b, err_msg=f"step at {s0}")
     assert bat.stats == one.stats and bat.stats["fused"] > 5
+
+
+@pytest.mark.parametrize("n_objects,batch", [(30, 8), (150, 16)])
+def test_native_sequencer_equals_python_path(dev, n_objects, batch):
+    """The library's keyframe sequencer (bf_fseq: one call per batch of keyframes) == the
+    Python-driven state machine, bit for bit after every batch: fusion lists, fusion flags,
+    fused sets, global boxes, valid_num, init_ids, per-row poses and the statistics, at the
+    benchmark's 30-object scene and a 150-object one (lists, NMS and fusion jobs several times
+    larger); then the stale last-frame re-entry (demo.py:200) on both."""
+    from boxfusion_amd.fusion_stage import FusionStage
+    from boxfusion_amd.instances import Instances3D
+    from boxfusion_amd.pipeline import scene_instances
+    from boxfusion_amd.synthetic import SCANNET_K, Scene
+    cfg = dict(TU.SCANNET_CFG, data=dict(gap=1))
+    scene = Scene(seed=2, n_objects=n_objects)
+    py = FusionStage(cfg, SCANNET_K, device=dev, native=False)
+    nat = FusionStage(cfg, SCANNET_K, device=dev, native=True)
+    for s0 in range(0, 6 * batch, batch):
+        fr = list(range(s0, s0 + batch))
+        dets = [scene.detections(f) for f in fr]
+        if s0 == batch:            # a keyframe without boxes inside a batch
+            dets[3] = {k: v[:0] for k, v in dets[3].items()}
+        for f, d in zip(fr, dets):
+            py.keyframe(f, scene.pose(f), scene_instances(d, dev))
+        preds = Instances3D.cat([scene_instances(d, dev) for d in dets])
+        nat.keyframes(fr, np.stack([scene.pose(f) for f in fr]), preds, [len(d["scores"]) for d in dets])
+        msg = f"batch at {s0}"
+        assert nat._mode == "native" and py._mode == "python"
+        assert nat.box_manager.fusion_list == py.box_manager.fusion_list, msg
+        assert nat.box_manager.fusion_flag == py.box_manager.fusion_flag, msg
+        assert nat.box_manager.already_fusion == py.box_manager.already_fusion, msg
+        assert nat.box_manager.num_record == py.box_manager.num_record, msg
+        assert len(nat.box_manager.last_fusion_frame) == len(py.box_manager.last_fusion_frame), msg
+        for a, b in zip(nat.boxes(), py.boxes()):
+            np.testing.assert_array_equal(a, b, err_msg=msg)
+        na, pa = nat.all_pred_box, py.all_pred_box
+        for k in ("valid_num", "init_id", "scores", "pred_boxes", "frame_id"):
+            np.testing.assert_array_equal(na.get(k).cpu().numpy(), pa.get(k).cpu().numpy(), err_msg=f"{k} {msg}")
+        np.testing.assert_array_equal(nat.all_poses, py.all_poses, err_msg=msg)
+        assert nat.stats == py.stats, msg
+        assert nat.fuser.fit_calls == py.fuser.fit_calls and nat.box_count == py.box_count
+    assert py.stats["fused"] >= 3 and py.stats["suppressed"] > 50
+    last = 6 * batch + 3
+    nat.finish(last, scene.pose(last), False)
+    py.finish(last, scene.pose(last), False)
+    assert nat.box_manager.fusion_list == py.box_manager.fusion_list
+    assert nat.box_manager.already_fusion == py.box_manager.already_fusion
+    for a, b in zip(nat.boxes(), py.boxes()):
+        np.testing.assert_array_equal(a, b)
+    assert nat.stats == py.stats
+
+
+def test_native_sequencer_single_keyframe_stale_reentry(dev):
+    """demo.py:200's re-entry after ONE keyframe: the reference's all_pred_box / per_frame_ins
+    alias that keyframe's pred and are transformed again through it; the native stage hands
+    over to the Python path there and matches it"""
+    from boxfusion_amd.fusion_stage import FusionStage
+    from boxfusion_amd.pipeline import scene_instances
+    from boxfusion_amd.synthetic import SCANNET_K, Scene
+    cfg = dict(TU.SCANNET_CFG, data=dict(gap=25))
+    scene = Scene(seed=4)
+    st = {}
+    for native in (True, False):
+        s = FusionStage(cfg, SCANNET_K, device=dev, native=native)
+        s.keyframe(0, scene.pose(0), scene_instances(scene.detections(0), dev))
+        s.finish(9, scene.pose(9), False)
+        st[native] = s
+    assert st[True].box_manager.fusion_list == st[False].box_manager.fusion_list
+    for a, b in zip(st[True].boxes(), st[False].boxes()):
+        np.testing.assert_array_equal(a, b)
+    assert st[True].stats == st[False].stats
 
 
 @pytest.mark.gpu
@@ -344,7 +420,8 @@ class _DemoDetect:
         return [p]
 
 
-def test_pipeline_run_vs_reference_demo_gap25(dev, monkeypatch):
+@pytest.mark.parametrize("native", [True, False])
+def test_pipeline_run_vs_reference_demo_gap25(dev, native, monkeypatch):
     """Pipeline.run + FusionStage (keyframes every 25 frames, stale re-fusion of the non-keyframe
     last frame, demo.py:200) against the REFERENCE's own demo.py run() on the same stream
     (tests/golden/make_golden_demo.py): final fusion lists, fused sets and num_record equal; the
@@ -372,7 +449,7 @@ def test_pipeline_run_vs_reference_demo_gap25(dev, monkeypatch):
     det = _DemoDetect(scene, [f for f in range(n) if f % gap == 0], names, text.to(dev), cfg, dev,
                       int(d["clip_seed"]))
     det.text_rows = text.numpy()
-    fusion = FusionStage(cfg, SCANNET_K, device=dev, legacy_promotion=False)
+    fusion = FusionStage(cfg, SCANNET_K, device=dev, legacy_promotion=False, native=native)
 
     def frames(ids):
         rgb = np.stack([frame_rgbd(i)[0] for i in ids])
