@@ -409,11 +409,11 @@ def roofline_obj(ks, kernel, bound, pmc_key=None, peak_tflops=PEAK_BF16_TFLOPS):
 
 def auto_rank0_batch(B, ranks):
     """rank 0's detection share when it also fuses `ranks` ranks' frames: its fusion worker must
-    keep pace with ranks * B keyframes per step (measured on one MI355X with --sim-ranks: the
-    worker is busy 15.6 / 32.7 / 58.4 ms per 54.6-ms step at 2 / 4 / 8 ranks of 8 frames)"""
+    keep pace with ranks * B keyframes per step.  Measured on one MI355X with --sim-ranks 8 and the
+    native keyframe sequencer (worker busy 0.85 ms per keyframe under the detect load): rank 0 on
+    6 / 7 / 8 frames -> 49.2 / 55.0 / 59.9 ms per step against the 54.7-ms N=1 step, i.e. 62/64,
+    63/64 x 54.7/55.0 and 54.7/59.9 = 0.97 / 0.98 / 0.91 of the ideal"""
     if ranks >= 8:
-        return max(1, B - 2)
-    if ranks >= 4:
         return max(1, B - 1)
     return B
 

@@ -79,4 +79,4 @@ def test_rank_frames_partition():
         assert got == list(range(step * per, (step + 1) * per))
     assert bench.rank_frames(1, 0, B, B0, per, G=25) == [(per + j) * 25 for j in range(B0)]
     assert bench.auto_rank0_batch(8, 1) == 8 and bench.auto_rank0_batch(8, 2) == 8
-    assert bench.auto_rank0_batch(8, 4) == 7 and bench.auto_rank0_batch(8, 8) == 6
+    assert bench.auto_rank0_batch(8, 4) == 8 and bench.auto_rank0_batch(8, 8) == 7
