@@ -794,15 +794,15 @@ def main(argv=None):
 
     if rank == 0:
         big = lambda t: t["kind"] == "gemm" and t["large"]
-        r_all = roofline_obj(timer.summary(big), "k_gemm256p (persistent bf16 GEMM, every launch: "
-                             "qkv, proj/fc2 + f32 residual, fc1 + GELU of CLIP ViT-H and CuTR)",
+        r_all = roofline_obj(timer.summary(big), "k_gemm256q / k_gemm256p (persistent bf16 GEMM, every "
+                             "launch: qkv, proj/fc2 + f32 residual, fc1 + GELU of CLIP ViT-H and CuTR)",
                              "mfma", pmc_key="k_gemm256p")
         comps = {
             "resid_gemm": roofline_obj(timer.summary(lambda t: big(t) and t["resid"]),
                                        "k_gemm256p<false, 0> (proj / fc2 + f32 residual)", "mfma",
                                        pmc_key="k_gemm256p<false, 0>"),
             "gelu_gemm": roofline_obj(timer.summary(lambda t: big(t) and t["act"] == 1),
-                                      "k_gemm256p<true, 1> (fc1 + GELU)", "mfma",
+                                      "k_gemm256q<true, 1> (fc1 + GELU)", "mfma",
                                       pmc_key="k_gemm256p<true, 1>"),
             "attention": roofline_obj(timer.summary(lambda t: t["kind"] == "attn"),
                                       "k_attn_* (every ViT attention launch: CuTR window + global, "

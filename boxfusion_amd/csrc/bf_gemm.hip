@@ -1026,8 +1026,290 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
 #undef ACC_INIT
 }
 
-static int g_gemm_variant = 1;   // 0: k_gemm256, 1: k_gemm256p (staggered 4-phase schedule), 2: k_gemm256p unstaggered
+// ------------------------------------------------------------------------------------------
+// k_gemm256q: k_gemm256p's K loop with the epilogue spread over the phases around the tile
+// boundary instead of run as one block after the last K-tile.
+//
+// The accumulators are transposed (C^T = W A^T on the MFMA): lane (lr, lq) of block (i, j) holds
+// row 16i + lr, columns 16j + 4lq + [0,4) -- four consecutive columns, so a lane adds its bias /
+// residual and stores straight from registers (f32: one 16-B store per block; bf16: two blocks'
+// packed halves exchanged between lane rows by v_permlane16_swap, one 16-B store per block pair).
+// No LDS round trip, so nothing in the epilogue touches LDS but the bias row (staged once per
+// walk by LDS-DMA into the 32 KiB beside the stages).
+//
+// A wave's 128x64 sub-tile is four 64x32 quadrants Q(mi, ni); phase P1..P4 of every K-tile runs the
+// MFMAs of Q00, Q01, Q11, Q10.  On the last K-tile of a tile, quadrant Q is final after its phase;
+// its epilogue (+ bias, activation, store) and its re-initialisation for the next tile (zero, or
+// the next tile's residual for an in-place residual GEMM) run in the memory section of the next
+// phase -- Q00 in P2, Q01 in P3, Q11 in P4, Q10 in P1 of the next tile's first K-tile -- where the
+// staggered partner wave on the same SIMD is in its MFMA section.  So the store burst is spread
+// over four phases and the epilogue VALU work runs beside MFMAs instead of on an idle chip.
+//
+// Counted waits (per wave, S stores and R residual loads per quadrant epilogue, VMEM ops are
+// counted in issue order): the last K-tile's P4 retires K-tile g+1 with its own 8 LDS-DMA and the
+// three epilogues' 3(S+R) younger ops in flight; the first K-tile's P4 with 8 + S + R (the Q10
+// epilogue of P1).  Stores go through a buffer descriptor with out-of-range offsets for rows >= M
+// / columns >= N, so every store instruction is issued by every wave and the counts hold.
+// Needs nk >= 3 K-tiles, N <= 8192 (bias row in LDS), no row map / broadcast residual; the host
+// falls back to k_gemm256p otherwise.
+// ------------------------------------------------------------------------------------------
+#define G2Q_BIAS_MAX 8192
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2v));
+}
+
+template <bool OUT_BF16, int ACT, bool RES>
+__global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restrict__ A, int lda,
+                                                            const u16* __restrict__ W, int ldw,
+                                                            const float* __restrict__ bias,
+                                                            const float* __restrict__ resid, int ldr,
+                                                            void* __restrict__ Cv, int ldc, int M,
+                                                            int N, int K, int tiles_n, int tiles_m,
+                                                            int stagger, int gm) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char g_smem[];
+    constexpr int S = OUT_BF16 ? 4 : 8;             // stores per quadrant epilogue (per lane)
+    constexpr int R = RES ? 8 : 0;                  // residual loads per quadrant re-init
+    const int t = threadIdx.x;
+    const int lane = t & 63, wave = t >> 6;
+    const int wr = wave >> 2, wc = wave & 3;
+    const int lr = lane & 15, lq = lane >> 4;
+    const int ntiles = tiles_m * tiles_n;
+    const int G = gridDim.x;
+    const int slot = (G % 8 == 0) ? ((int)blockIdx.x % 8) * (G / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
+    const int my_tiles = ntiles > slot ? (ntiles - slot + G - 1) / G : 0;
+    const int nk = K / GB_K;
+    const int total = my_tiles * nk;
+    if (total == 0) return;
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+
+    // bias row -> LDS (retired with K-tile 0 by the prologue's counted wait)
+    const float* bias_lds = reinterpret_cast<const float*>(g_smem + G2_STAGES_BYTES);
+    if (bias) {
+        for (int c = wave_u; c * 256 < N; c += 8)
+            glds_buf16(bias, N * 4, g_smem + G2_STAGES_BYTES + c * 1024, lane * 16, c * 1024);
+    } else {
+        for (int n = t; n < N; n += G2_THREADS) reinterpret_cast<float*>(g_smem + G2_STAGES_BYTES)[n] = 0.f;
+    }
+
+    int a_row[2][2], b_row[2][2], scol[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int L = (wave * 2 + i) * 8 + (lane >> 3);
+        scol[i] = ((lane & 7) ^ swz_key(L)) * 16;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            a_row[h][i] = (L >> 6) * 128 + h * 64 + (L & 63);
+            b_row[h][i] = (L >> 5) * 64 + h * 32 + (L & 31);
+        }
+    }
+    const int bytesA = (int)(((size_t)(M - 1) * lda + K) * 2);
+    const int bytesW = (int)(((size_t)(N - 1) * ldw + K) * 2);
+    struct KT { int idx, m0, n0, k0, buf; };
+    auto kt_at_tile = [&](int tile_k, int idx) {
+        const int tile = slot + tile_k * G;
+        KT r;
+        r.idx = idx; tile_coords(tile, tiles_m, tiles_n, gm, r.m0, r.n0); r.k0 = 0; r.buf = idx & 1;
+        return r;
+    };
+    int tile_ord = 0;
+    auto kt_next = [&](KT c) {
+        if (c.idx >= total - 1) return c;
+        if (c.k0 + GB_K < K) { c.k0 += GB_K; c.idx += 1; c.buf ^= 1; return c; }
+        ++tile_ord;
+        return kt_at_tile(tile_ord, c.idx + 1);
+    };
+    struct VO { int a[2][2], b[2][2]; };
+    auto vo_of = [&](const KT& c) {
+        VO v;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                v.a[h][i] = min(c.m0 + a_row[h][i], M - 1) * lda * 2 + scol[i];
+                v.b[h][i] = min(c.n0 + b_row[h][i], N - 1) * ldw * 2 + scol[i];
+            }
+        return v;
+    };
+#define STAGE_HALF(c, v, which)                                                                    \
+    {                                                                                              \
+        unsigned char* dst_ = g_smem + (c).buf * 65536 + (which) * 16384 + wave_u * 2048;          \
+        _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                         \
+            if ((which) < 2)                                                                       \
+                glds_buf16(A, bytesA, dst_ + i_ * 1024, (v).a[(which) & 1][i_], (c).k0 * 2);       \
+            else                                                                                   \
+                glds_buf16(W, bytesW, dst_ + i_ * 1024, (v).b[(which) & 1][i_], (c).k0 * 2);       \
+        }                                                                                          \
+    }
+
+    f32x4 acc[8][4];
+    // quadrant (MI, NI) <- zero or the residual of the tile at (m0_, n0_) (clamped rows / columns:
+    // every load is issued, out-of-range values are never stored)
+#define QINIT(MI, NI, m0_, n0_)                                                                    \
+    {                                                                                              \
+        if constexpr (RES) {                                                                       \
+            _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                       \
+                const float* rp_ = resid + (size_t)min((m0_) + wr * 128 + (MI) * 64 + i * 16 + lr, M - 1) * ldr; \
+                _Pragma("unroll") for (int j = 0; j < 2; ++j)                                      \
+                    acc[(MI) * 4 + i][(NI) * 2 + j] = *reinterpret_cast<const f32x4*>(            \
+                        rp_ + min((n0_) + wc * 64 + (NI) * 32 + j * 16 + 4 * lq, N - 4));          \
+            }                                                                                      \
+        } else {                                                                                   \
+            _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) \
+                acc[(MI) * 4 + i][(NI) * 2 + j] = (f32x4){0.f, 0.f, 0.f, 0.f};                     \
+        }                                                                                          \
+    }
+    // output buffer descriptor: byte offsets of rows < M only (the rest are dropped)
+    const int esz = OUT_BF16 ? 2 : 4;
+    const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+        Cv, 0, (int)(((size_t)(M - 1) * ldc + N) * esz), 0x00020000);
+    // epilogue of quadrant (MI, NI) of the tile at (em0_, en0_)
+#define QEPI(MI, NI, em0_, en0_)                                                                   \
+    {                                                                                              \
+        const int cb_ = (en0_) + wc * 64 + (NI) * 32 + 4 * lq;                                     \
+        const f32x4 b0_ = *reinterpret_cast<const f32x4*>(bias_lds + min(cb_, N - 4));            \
+        const f32x4 b1_ = *reinterpret_cast<const f32x4*>(bias_lds + min(cb_ + 16, N - 4));       \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                           \
+            const int r_ = (em0_) + wr * 128 + (MI) * 64 + i * 16 + lr;                            \
+            f32x4 x0 = acc[(MI) * 4 + i][(NI) * 2] + b0_;                                         \
+            f32x4 x1 = acc[(MI) * 4 + i][(NI) * 2 + 1] + b1_;                                     \
+            if constexpr (ACT == 1) {                                                              \
+                f32x2 p0 = {x0.x, x0.y}, p1 = {x0.z, x0.w}, p2 = {x1.x, x1.y}, p3 = {x1.z, x1.w}; \
+                gelu_erf2x2(p0, p1); gelu_erf2x2(p2, p3);                                          \
+                x0 = (f32x4){p0.x, p0.y, p1.x, p1.y}; x1 = (f32x4){p2.x, p2.y, p3.x, p3.y};         \
+            } else if constexpr (ACT == 2) {                                                       \
+                x0 = __builtin_elementwise_max(x0, (f32x4){0.f, 0.f, 0.f, 0.f});                   \
+                x1 = __builtin_elementwise_max(x1, (f32x4){0.f, 0.f, 0.f, 0.f});                   \
+            }                                                                                      \
+            if constexpr (OUT_BF16) {                                                              \
+                uint32_t X0 = pk_bf16(x0.x, x0.y), X1 = pk_bf16(x0.z, x0.w);                       \
+                uint32_t Y0 = pk_bf16(x1.x, x1.y), Y1 = pk_bf16(x1.z, x1.w);                       \
+                const auto s0_ = __builtin_amdgcn_permlane16_swap(X0, Y0, false, false);           \
+                const auto s1_ = __builtin_amdgcn_permlane16_swap(X1, Y1, false, false);           \
+                const int c_ = (en0_) + wc * 64 + (NI) * 32 + 16 * (lq & 1) + 8 * (lq >> 1);        \
+                const int off_ = (r_ < M && c_ < N) ? (r_ * ldc + c_) * 2 : (int)0x80000000;       \
+                __builtin_amdgcn_raw_buffer_store_b128((u32x4v){s0_[0], s1_[0], s0_[1], s1_[1]},   \
+                                                       crs, off_, 0, 2);                           \
+            } else {                                                                               \
+                const int o0_ = (r_ < M && cb_ < N) ? (r_ * ldc + cb_) * 4 : (int)0x80000000;      \
+                const int o1_ = (r_ < M && cb_ + 16 < N) ? (r_ * ldc + cb_ + 16) * 4 : (int)0x80000000; \
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, x0), crs, o0_, 0, 2); \
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, x1), crs, o1_, 0, 2); \
+            }                                                                                      \
+        }                                                                                          \
+    }
+
+    bf16x8 fa[8], fb0[4], fb1[4];
+#define LDS16(off) (*reinterpret_cast<const bf16x8*>(g_smem + (off)))
+#define RD_A(stage, mi)                                                                            \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) \
+        fa[i * 2 + ks] = LDS16((stage) * 65536 + (mi) * 16384 + swz(wr * 64 + i * 16 + lr, ks * 4 + lq));
+#define RD_B(FB, stage, ni)                                                                        \
+    _Pragma("unroll") for (int j = 0; j < 2; ++j) _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) \
+        FB[j * 2 + ks] = LDS16((stage) * 65536 + 32768 + (ni) * 16384 + swz(wc * 32 + j * 16 + lr, ks * 4 + lq));
+#define MFMA_Q(mi, ni, FB)                                                                         \
+    {                                                                                              \
+        __builtin_amdgcn_s_setprio(1);                                                             \
+        _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i) \
+            _Pragma("unroll") for (int j = 0; j < 2; ++j) acc[(mi) * 4 + i][(ni) * 2 + j] =        \
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j * 2 + ks], fa[i * 2 + ks],            \
+                                                        acc[(mi) * 4 + i][(ni) * 2 + j], 0, 0, 0); \
+        __builtin_amdgcn_s_setprio(0);                                                             \
+    }
+
+    KT kc = kt_at_tile(0, 0);
+    KT k1 = kt_next(kc);
+    KT k2 = kt_next(k1);
+    VO v2 = vo_of(k2);
+    QINIT(0, 0, kc.m0, kc.n0); QINIT(0, 1, kc.m0, kc.n0); QINIT(1, 1, kc.m0, kc.n0); QINIT(1, 0, kc.m0, kc.n0);
+    {
+        const VO v0 = vo_of(kc);
+        STAGE_HALF(kc, v0, 2); STAGE_HALF(kc, v0, 0); STAGE_HALF(kc, v0, 3); STAGE_HALF(kc, v0, 1);
+    }
+    {
+        const VO v1 = vo_of(k1);
+        STAGE_HALF(k1, v1, 2); STAGE_HALF(k1, v1, 0); STAGE_HALF(k1, v1, 3); STAGE_HALF(k1, v1, 1);
+    }
+    asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+    PHASE_BARRIER();
+    if (stagger && wr == 1) PHASE_BARRIER();
+
+    int em0 = 0, en0 = 0;     // the tile whose quadrant Q10 is still pending
+    for (int g = 0; g < total; ++g) {
+        const int st = g & 1;
+        const bool isL = kc.k0 == K - GB_K;
+        const bool isF = kc.k0 == 0 && g > 0;
+        // ---- P1: Q00; reads B0 then A0; [first K-tile: the previous tile's Q10]
+        RD_B(fb0, st, 0);
+        SB0();
+        RD_A(st, 0);
+        if (isF) { QEPI(1, 0, em0, en0); QINIT(1, 0, kc.m0, kc.n0); }
+        CBAR();
+        asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+        PHASE_BARRIER();
+        MFMA_Q(0, 0, fb0);
+        PHASE_BARRIER();
+        // ---- P2: Q01; reads B1; stage B0 of g+2; [last K-tile: Q00]
+        RD_B(fb1, st, 1);
+        STAGE_HALF(k2, v2, 2);
+        if (isL) { QEPI(0, 0, kc.m0, kc.n0); QINIT(0, 0, k1.m0, k1.n0); }
+        CBAR();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        PHASE_BARRIER();
+        MFMA_Q(0, 1, fb1);
+        PHASE_BARRIER();
+        // ---- P3: Q11; reads A1; stage A0 of g+2; [last K-tile: Q01]
+        RD_A(st, 1);
+        STAGE_HALF(k2, v2, 0);
+        if (isL) { QEPI(0, 1, kc.m0, kc.n0); QINIT(0, 1, k1.m0, k1.n0); }
+        CBAR();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        PHASE_BARRIER();
+        MFMA_Q(1, 1, fb1);
+        PHASE_BARRIER();
+        // ---- P4: Q10 from registers; stage B1 and A1 of g+2; [last K-tile: Q11]; retire g+1
+        STAGE_HALF(k2, v2, 3);
+        STAGE_HALF(k2, v2, 1);
+        if (isL) {
+            QEPI(1, 1, kc.m0, kc.n0); QINIT(1, 1, k1.m0, k1.n0);
+            CBAR();
+            asm volatile("s_waitcnt vmcnt(%0)" :: "n"(8 + 3 * (S + R)) : "memory");
+            em0 = kc.m0; en0 = kc.n0;
+        } else if (isF) {
+            asm volatile("s_waitcnt vmcnt(%0)" :: "n"(8 + S + R) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        }
+        PHASE_BARRIER();
+        MFMA_Q(1, 0, fb0);
+        PHASE_BARRIER();
+        kc = k1; k1 = k2;
+        {
+            const KT kn = kt_next(k2);
+            if (kn.k0 == 0 && kn.idx != k2.idx) v2 = vo_of(kn);
+            k2 = kn;
+        }
+    }
+    QEPI(1, 0, em0, en0);          // the last tile's Q10
+    if (stagger && wr == 0) PHASE_BARRIER();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#undef RD_A
+#undef RD_B
+#undef LDS16
+#undef MFMA_Q
+#undef STAGE_HALF
+#undef QINIT
+#undef QEPI
+}
+
+// 0: k_gemm256, 1: k_gemm256p (staggered 4-phase schedule), 2: k_gemm256p unstaggered,
+// 5 (default): k_gemm256q for bf16 outputs, k_gemm256p otherwise, 6: k_gemm256q wherever it applies
+static int g_gemm_variant = [] {
+    const char* e = getenv("BF_GEMM_VARIANT");
+    return e ? atoi(e) : 5;
+}();
 BF_API void bf_gemm_set_variant(int v) { g_gemm_variant = v; }
+BF_API int bf_gemm_get_variant(void) { return g_gemm_variant; }
 // row panels per tile group (tile_coords); 1 = row-major.  Default 8, env BF_GEMM_GROUP_M.
 static int g_group_m = [] {
     const char* e = getenv("BF_GEMM_GROUP_M");
@@ -1052,7 +1334,8 @@ static void launch_gemm256(int grid, hipStream_t st, const void* A, int lda, con
     if (g_gemm_variant >= 1)
         hipLaunchKernelGGL((k_gemm256p<OB, AC>), dim3(grid), dim3(G2_THREADS), G2_LDS, st, (const u16*)A,
                            lda, (const u16*)W, ldw, bias, resid, ldr, resid_mod, C, ldc, row_map, M, N,
-                           K, tiles_n, tiles_m, g_gemm_variant == 2 ? 0 : 1, g_group_m, g_gemm_variant >= 3 ? g_gemm_variant - 2 : 0);
+                           K, tiles_n, tiles_m, g_gemm_variant == 2 ? 0 : 1, g_group_m,
+                           (g_gemm_variant == 3 || g_gemm_variant == 4) ? g_gemm_variant - 2 : 0);
     else
         hipLaunchKernelGGL((k_gemm256<OB, AC>), dim3(grid), dim3(G2_THREADS), G2_LDS, st, (const u16*)A,
                            lda, (const u16*)W, ldw, bias, resid, ldr, resid_mod, C, ldc, row_map, M, N,
@@ -1148,6 +1431,33 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
             const long long rounds = (t2 + n_cu - 1) / n_cu;
             const int g = (int)(((t2 + rounds - 1) / rounds + 7) & ~7LL);
             grid2 = g < n_cu ? g : n_cu;
+        }
+        // the overlapped-epilogue kernel: plain / in-place residual outputs, >= 3 K-tiles, the bias
+        // row fits its LDS slot, 32-bit byte offsets into C and the residual
+        // (variant 5, the default: bf16 outputs only -- the f32 residual GEMMs measured 1-4 % slower
+        // on it than on k_gemm256p; variant 6: every eligible shape)
+        const bool q_ok = (g_gemm_variant == 6 || (g_gemm_variant == 5 && c_bf16)) && row_map == nullptr &&
+                          resid_mod <= 0 && K / 64 >= 3 && N <= G2Q_BIAS_MAX && act <= 1 && !(resid && act) && !(resid && c_bf16) && !(act && !c_bf16) &&
+                          (long long)(M - 1) * ldc * (c_bf16 ? 2 : 4) + (long long)N * 4 < (1LL << 31) &&
+                          (!resid || (long long)(M - 1) * ldr * 4 + (long long)N * 4 < (1LL << 31));
+        if (q_ok) {
+            static bool qattr = false;
+            if (!qattr) {
+                hipFuncSetAttribute((const void*)k_gemm256q<true, 0, false>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
+                hipFuncSetAttribute((const void*)k_gemm256q<true, 1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
+                hipFuncSetAttribute((const void*)k_gemm256q<false, 0, false>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
+                hipFuncSetAttribute((const void*)k_gemm256q<false, 0, true>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
+                qattr = true;
+            }
+#define GEMMQ(OB, AC, RS) hipLaunchKernelGGL((k_gemm256q<OB, AC, RS>), dim3(grid2), dim3(G2_THREADS), G2_LDS,   \
+                                             bf_stream(stream), (const u16*)A, lda, (const u16*)W, ldw, bias, resid, \
+                                             ldr, C, ldc, M, N, K, t2n, t2m, 1, g_group_m)
+            if (resid) GEMMQ(false, 0, true);
+            else if (!c_bf16) GEMMQ(false, 0, false);
+            else if (act == 0) GEMMQ(true, 0, false);
+            else GEMMQ(true, 1, false);
+#undef GEMMQ
+            return bf_check_launch();
         }
 #define GEMM2(OB, AC) launch_gemm256<OB, AC>(grid2, bf_stream(stream), A, lda, W, ldw, bias, \
                                             resid, ldr, resid_mod, C, ldc, row_map, M, N, K, t2n, t2m)

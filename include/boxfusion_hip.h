@@ -347,8 +347,12 @@ int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bi
  * heuristic. */
 void bf_gemm_force_small_tiles(int on);
 /* Persistent 256x256 kernel variant: 0 = k_gemm256 (one barrier per K-tile), 1 = k_gemm256p
- * (staggered 4-phase schedule, default).  Test/benchmark hook; results are identical in value. */
+ * (staggered 4-phase schedule), 5 = k_gemm256q (k_gemm256p's K loop, epilogue of each 64x32
+ * quadrant overlapped with the next phases' MFMAs) for bf16 outputs and k_gemm256p for the rest
+ * (default; env BF_GEMM_VARIANT), 6 = k_gemm256q for every eligible shape (no row map / broadcast
+ * residual, K >= 192, N <= 8192).  Test/benchmark hook; results agree to f32 rounding. */
 void bf_gemm_set_variant(int v);
+int bf_gemm_get_variant(void);
 /* Row panels per tile group of the persistent kernels' tile order (default 8; 1 = row-major).
  * Test/benchmark hook; results are identical in value. */
 void bf_gemm_set_group_m(int g);

@@ -65,8 +65,12 @@ for name, ctrs in per.items():
     kernels[name] = k
 # the bench line's roofline kernels: launch-weighted averages over the matching kernel names
 # (regular expressions over the demangled names; k_gemm256p<OUT_BF16, ACT, F8>)
-groups = {"k_gemm256p": [r"k_gemm256p<\w+, \d, 0>"], "k_gemm256p<false, 0>": [r"k_gemm256p<false, 0, 0>"],
-          "k_gemm256p<true, 1>": [r"k_gemm256p<true, 1, 0>"], "k_gemm256p_fp8": [r"k_gemm256p<\w+, \d, [13]>"],
+# (k_gemm256q, the overlapped-epilogue form, runs the bf16-output GEMMs from round 3 on: it joins
+# the bf16 GEMM groups under the same keys)
+groups = {"k_gemm256p": [r"k_gemm256p<\w+, \d, 0>", r"k_gemm256q<"],
+          "k_gemm256p<false, 0>": [r"k_gemm256p<false, 0, 0>", r"k_gemm256q<false, 0, true>"],
+          "k_gemm256p<true, 1>": [r"k_gemm256p<true, 1, 0>", r"k_gemm256q<true, 1,"],
+          "k_gemm256p_fp8": [r"k_gemm256p<\w+, \d, [13]>"],
           "k_attn": ["k_attn"],
           "k_attn_clip": ["k_attn_clip", "k_attn_s<80", "k_attn_r<80", "k_attn2<80"],
           "k_attn_cutr": ["k_attn_s<64", "k_attn_w", "k_attn_g", "k_attn2<64"]}

@@ -111,6 +111,7 @@ def test_gemm_resid_persistent(L, variant, shape, inplace, out_bf16):
     b = torch.randn(N, device="cuda", generator=g)
     resid = torch.randn(M, N, device="cuda", generator=g)
     ref = resid + a.float() @ w.float().T + b
+    prev = lib().bf_gemm_get_variant()
     lib().bf_gemm_set_variant(variant)
     try:
         if inplace:
@@ -124,7 +125,62 @@ def test_gemm_resid_persistent(L, variant, shape, inplace, out_bf16):
             out2 = L.gemm(a, w, b, resid=resid, out_dtype=out.dtype)
             assert torch.equal(out2, out)
     finally:
-        lib().bf_gemm_set_variant(1)
+        lib().bf_gemm_set_variant(prev)
+
+
+@pytest.mark.parametrize("shape", [(3000, 2816, 320), (8292, 1280, 640), (600, 384, 192),
+                                   (4112, 5120, 1280), (32896, 1280, 1280), (12800, 768, 3072)])
+@pytest.mark.parametrize("kind", ["bf16", "gelu", "f32", "resid_inplace", "resid", "nobias"])
+def test_gemm_overlapped_epilogue(L, shape, kind):
+    """k_gemm256q (variant 6, every eligible shape; 5, the default, for bf16 outputs: the epilogue of every 64x32 quadrant spread over the phases around
+    the tile boundary, transposed accumulators, permlane-widened bf16 stores) vs fp32 torch and vs
+    the k_gemm256p default on the same operands: partial M / N tiles, 3..48 K-tiles, bias / no
+    bias, GELU, f32 / bf16 out, residual in place and out of place"""
+    from boxfusion_amd._lib import lib
+    g = torch.Generator(device="cuda").manual_seed(sum(shape))
+    M, N, K = shape
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).bfloat16()
+    b = None if kind == "nobias" else torch.randn(N, device="cuda", generator=g)
+    resid = torch.randn(M, N, device="cuda", generator=g) if kind.startswith("resid") else None
+    y = a.float() @ w.float().T + (b if b is not None else 0.0)
+    act = "gelu" if kind == "gelu" else None
+    if act:
+        y = F.gelu(y)
+    if resid is not None:
+        y = y + resid
+    od = torch.bfloat16 if kind in ("bf16", "gelu", "nobias") else torch.float32
+
+    prev = lib().bf_gemm_get_variant()
+
+    def run(variant):
+        lib().bf_gemm_set_variant(variant)
+        try:
+            if kind == "resid_inplace":
+                out = resid.clone()
+                L.gemm(a, w, b, resid=out, out=out)
+            else:
+                out = torch.full((M, N), float("nan"), device="cuda", dtype=od)
+                L.gemm(a, w, b, act=act, resid=resid, out=out)
+            torch.cuda.synchronize()
+            return out
+        finally:
+            lib().bf_gemm_set_variant(prev)
+    out_q, out_p = run(6), run(1)
+    assert torch.isfinite(out_q).all(), "rows / columns left unwritten"
+    tol = 5e-3 if od == torch.bfloat16 else 1e-5
+    assert rel_err(out_q, y) < tol
+    assert rel_err(out_q, out_p) < (2e-3 if od == torch.bfloat16 else 1e-6)
+    # out-of-range rows / columns untouched: a padded output view keeps its sentinels
+    if kind == "bf16":
+        big = torch.full((M + 3, N + 8), 7.0, device="cuda", dtype=od)
+        lib().bf_gemm_set_variant(6)
+        try:
+            L.gemm(a, w, b, out=big[:M, :N])
+        finally:
+            lib().bf_gemm_set_variant(prev)
+        assert torch.equal(big[:M, :N], out_q)
+        assert (big[M:] == 7.0).all() and (big[:, N:] == 7.0).all()
 
 
 def _attn_ref(q, k, v, B, H, S, D, scale):
