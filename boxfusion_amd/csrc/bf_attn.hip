@@ -529,8 +529,10 @@ __device__ __forceinline__ void attn2_softmax(f32x16 (&s)[2], bool sub1, bool ma
 // v_mfma_f32_16x16x32_bf16 (S^T = K Q^T in four 16-key blocks, O^T += V^T P^T in 16-row blocks with
 // the same transposed V reads and the ones row), i.e. half the MFMA cycles of a full 32-query wave
 // on the SIMD that holds three waves.  Its accumulators alias the registers of o / qf / s.
+// (3- and 5-wave workgroups of short heads -- several per CU -- are held to 3 waves per SIMD, as
+// the 9-wave workgroup is by its size: without it they compile to one wave per SIMD)
 template <int D, int NW, bool F8O = false, bool CAUSAL = false, bool XQ = false, bool LW = false>
-__global__ void __launch_bounds__(NW * 64) k_attn2(const u16* __restrict__ Q, const u16* __restrict__ K,
+__global__ void __launch_bounds__(NW * 64, (NW == 3 || NW == 5) ? 3 : 1) k_attn2(const u16* __restrict__ Q, const u16* __restrict__ K,
                                                       const u16* __restrict__ V, u16* __restrict__ O,
                                                       int sq, int sk, int q_rs, int k_rs, int v_rs,
                                                       int o_rs, long long q_bs, long long k_bs,

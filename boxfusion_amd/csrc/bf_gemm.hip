@@ -1052,6 +1052,16 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
 // / columns >= N, so every store instruction is issued by every wave and the counts hold.
 // Needs nk >= 3 K-tiles, N <= 8192 (bias row in LDS), no row map / broadcast residual; the host
 // falls back to k_gemm256p otherwise.
+//
+// Measured (scripts/gemm_bench.py, interleaved in one process): bf16 outputs gain 6-16 % (CLIP
+// fc1+GELU 444.6 -> 397.2 us, qkv 278.2 -> 253.2, CuTR fc1 145.7 -> 123.0); the f32 residual
+// GEMMs do not (CLIP fc2 400.1 vs 406.5, proj 139.5 vs 141.9), so those keep k_gemm256p by
+// default.  Their cost is the residual read at the tile boundaries (proj: 139.5 us with it, 106.2
+// without).  Tried for it and not kept: touching the next tile's residual rows in the middle of
+// the current tile (LDS-DMA into a dummy slot, plain or streaming: 3-9 % slower -- the lines evict
+// the operand panels), and skewing the tile boundaries per XCD (the first tile split into a
+// leading and a trailing segment, the trailing one re-initialised from C: proj 151.9 -> 189.9 us
+// -- the XCDs' lock-step walk over the same A / W panels is what keeps them in the Infinity Cache).
 // ------------------------------------------------------------------------------------------
 #define G2Q_BIAS_MAX 8192
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
@@ -1159,6 +1169,24 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
                 acc[(MI) * 4 + i][(NI) * 2 + j] = (f32x4){0.f, 0.f, 0.f, 0.f};                     \
         }                                                                                          \
     }
+    // the same inside the K loop: the residual arrives by loads hidden from the compiler's waitcnt
+    // pass (which would otherwise wait for nearly every outstanding operation before the next
+    // MFMA on the quadrant), retired by the counted waits of the following phases
+#define QINIT_ASYNC(MI, NI, T_)                                                                    \
+    {                                                                                              \
+        if constexpr (RES) {                                                                       \
+            _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                       \
+                const float* rp_ = resid + (size_t)min((T_).m0 + wr * 128 + (MI) * 64 + i * 16 + lr, M - 1) * ldr; \
+                _Pragma("unroll") for (int j = 0; j < 2; ++j)                                      \
+                    asm volatile("global_load_dwordx4 %0, %1, off"                                 \
+                                 : "=v"(acc[(MI) * 4 + i][(NI) * 2 + j])                           \
+                                 : "v"(rp_ + min((T_).n0 + wc * 64 + (NI) * 32 + j * 16 + 4 * lq, N - 4)) \
+                                 : "memory");                                                      \
+            }                                                                                      \
+        } else {                                                                                   \
+            QINIT(MI, NI, (T_).m0, (T_).n0);                                                       \
+        }                                                                                          \
+    }
     // output buffer descriptor: byte offsets of rows < M only (the rest are dropped)
     const int esz = OUT_BF16 ? 2 : 4;
     const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
@@ -1243,7 +1271,11 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         RD_B(fb0, st, 0);
         SB0();
         RD_A(st, 0);
-        if (isF) { QEPI(1, 0, em0, en0); QINIT(1, 0, kc.m0, kc.n0); }
+        if (isF) {
+            QEPI(1, 0, em0, en0); QINIT_ASYNC(1, 0, kc);
+            CBAR();
+            if constexpr (RES) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + 3 * (S + R)) : "memory");  // Q00's residual (L.P2)
+        }
         CBAR();
         asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
         PHASE_BARRIER();
@@ -1252,7 +1284,10 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         // ---- P2: Q01; reads B1; stage B0 of g+2; [last K-tile: Q00]
         RD_B(fb1, st, 1);
         STAGE_HALF(k2, v2, 2);
-        if (isL) { QEPI(0, 0, kc.m0, kc.n0); QINIT(0, 0, k1.m0, k1.n0); }
+        if (isL) { QEPI(0, 0, kc.m0, kc.n0); QINIT_ASYNC(0, 0, k1); }
+        if (isF) {
+            if constexpr (RES) { CBAR(); asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + 2 * (S + R)) : "memory"); }  // Q01 (L.P3)
+        }
         CBAR();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         PHASE_BARRIER();
@@ -1261,7 +1296,10 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         // ---- P3: Q11; reads A1; stage A0 of g+2; [last K-tile: Q01]
         RD_A(st, 1);
         STAGE_HALF(k2, v2, 0);
-        if (isL) { QEPI(0, 1, kc.m0, kc.n0); QINIT(0, 1, k1.m0, k1.n0); }
+        if (isL) { QEPI(0, 1, kc.m0, kc.n0); QINIT_ASYNC(0, 1, k1); }
+        if (isF) {
+            if constexpr (RES) { CBAR(); asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 + S + R) : "memory"); }      // Q11 (L.P4)
+        }
         CBAR();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         PHASE_BARRIER();
@@ -1271,12 +1309,13 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         STAGE_HALF(k2, v2, 3);
         STAGE_HALF(k2, v2, 1);
         if (isL) {
-            QEPI(1, 1, kc.m0, kc.n0); QINIT(1, 1, k1.m0, k1.n0);
+            QEPI(1, 1, kc.m0, kc.n0); QINIT_ASYNC(1, 1, k1);
             CBAR();
             asm volatile("s_waitcnt vmcnt(%0)" :: "n"(8 + 3 * (S + R)) : "memory");
             em0 = kc.m0; en0 = kc.n0;
         } else if (isF) {
-            asm volatile("s_waitcnt vmcnt(%0)" :: "n"(8 + S + R) : "memory");
+            // K-tile g+1, and (RES) Q10's residual from P1: 8 younger LDS-DMA
+            asm volatile("s_waitcnt vmcnt(%0)" :: "n"(RES ? 8 : 8 + S) : "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         }
@@ -1299,6 +1338,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
 #undef MFMA_Q
 #undef STAGE_HALF
 #undef QINIT
+#undef QINIT_ASYNC
 #undef QEPI
 }
 
@@ -1310,6 +1350,7 @@ static int g_gemm_variant = [] {
 }();
 BF_API void bf_gemm_set_variant(int v) { g_gemm_variant = v; }
 BF_API int bf_gemm_get_variant(void) { return g_gemm_variant; }
+
 // row panels per tile group (tile_coords); 1 = row-major.  Default 8, env BF_GEMM_GROUP_M.
 static int g_group_m = [] {
     const char* e = getenv("BF_GEMM_GROUP_M");
