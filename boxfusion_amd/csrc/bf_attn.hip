@@ -531,7 +531,15 @@ __device__ __forceinline__ void attn2_softmax(f32x16 (&s)[2], bool sub1, bool ma
 // on the SIMD that holds three waves.  Its accumulators alias the registers of o / qf / s.
 // (3- and 5-wave workgroups of short heads -- several per CU -- are held to 3 waves per SIMD, as
 // the 9-wave workgroup is by its size: without it they compile to one wave per SIMD)
-template <int D, int NW, bool F8O = false, bool CAUSAL = false, bool XQ = false, bool LW = false>
+// PP (variant 12, measured slower: CLIP 153.1 vs 124.2 us; 168 VGPRs with 20 spilled, and five
+// staging waves instead of nine).  Ping-pong for short non-causal heads: waves 4-7 run every tile's chain rotated by half a tile
+// -- softmax and P.V of tile n-1, then S^T of tile n, whose scores they carry across the barrier --
+// while the other waves run S^T, softmax, P.V of tile n.  Waves w and w + 4 share a SIMD, so one
+// of them issues MFMAs while the other runs its softmax instead of both doing the same kind of
+// work between two barriers.  K / V ring of three tiles (P.V of tile n-1 reads V n-1 while tile
+// n + 1 is staged).  Arithmetic per query is unchanged (bit-identical to the default).
+template <int D, int NW, bool F8O = false, bool CAUSAL = false, bool XQ = false, bool LW = false,
+          bool PP = false>
 __global__ void __launch_bounds__(NW * 64, (NW == 3 || NW == 5) ? 3 : 1) k_attn2(const u16* __restrict__ Q, const u16* __restrict__ K,
                                                       const u16* __restrict__ V, u16* __restrict__ O,
                                                       int sq, int sk, int q_rs, int k_rs, int v_rs,
@@ -548,7 +556,8 @@ __global__ void __launch_bounds__(NW * 64, (NW == 3 || NW == 5) ? 3 : 1) k_attn2
     constexpr int CPR = D / 8;
     constexpr int CH = AT_KT * CPR;
     constexpr int NT = NW * 64;
-    constexpr int NBUF = 2;
+    constexpr int NBUF = PP ? 3 : 2;
+    static_assert(!PP || (!CAUSAL && !XQ && !LW && NW > 4), "PP: short non-causal heads");
     __shared__ __attribute__((aligned(16))) u16 sK[NBUF * KTILE];
     __shared__ __attribute__((aligned(16))) u16 sV[NBUF * VTILE];
 
@@ -587,17 +596,21 @@ __global__ void __launch_bounds__(NW * 64, (NW == 3 || NW == 5) ? 3 : 1) k_attn2
         }
 
     static_assert(CH % 64 == 0 && NT % 64 == 0, "wave-uniform staging guard");
-    constexpr int NSO = (CH + NT - 1) / NT;
+    // PP: only waves 0-3 and 8 stage K / V (the late waves carry their scores instead)
+    constexpr int NTS = PP ? 5 * 64 : NT;
+    const int ts = !PP ? t : (wave < 4 ? t : (wave == 8 ? 4 * 64 + lane : -1));
+    constexpr int NSO = (CH + NTS - 1) / NTS;
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
     u32x4 stk[NSO], stv[NSO];
     int srow[NSO], scol[NSO];
 #pragma unroll
     for (int i = 0; i < NSO; ++i) {
-        const int c = min(t + i * NT, CH - 1);
+        const int c = min(max(ts, 0) + i * NTS, CH - 1);
         srow[i] = c / CPR;
         scol[i] = (c % CPR) * 8;
     }
     auto stage_load = [&](int k0_) {
+        if (PP && ts < 0) return;
 #pragma unroll
         for (int i = 0; i < NSO; ++i) {
             const int key = min(k0_ + srow[i], sk - 1);
@@ -606,9 +619,10 @@ __global__ void __launch_bounds__(NW * 64, (NW == 3 || NW == 5) ? 3 : 1) k_attn2
         }
     };
     auto stage_store = [&](int buf_) {
+        if (PP && ts < 0) return;
 #pragma unroll
         for (int i = 0; i < NSO; ++i) {
-            if (t + i * NT < CH) {
+            if (ts + i * NTS < CH) {
                 *reinterpret_cast<u32x4*>(sK + buf_ * KTILE + srow[i] * KROW + scol[i]) = stk[i];
                 *reinterpret_cast<u32x4*>(sV + buf_ * VTILE + srow[i] * VROW + scol[i]) = stv[i];
             }
@@ -823,12 +837,40 @@ __global__ void __launch_bounds__(NW * 64, (NW == 3 || NW == 5) ? 3 : 1) k_attn2
             if (more) stage_store((tile + 1) & 1);
             __syncthreads();
         }
+    } else if constexpr (PP) {
+        const bool late = wave >= 4 && wave < 8;                   // wave-uniform
+        f32x16 sl[2];                                              // the late waves' pending scores
+        for (int tile = 0; tile < nfull; ++tile) {
+            const bool more = tile + 1 < ntiles;
+            if (more) stage_load((tile + 1) * AT_KT);
+            if (!late) {                 // (the same score registers as the late waves' carried ones)
+                qk(tile, sl, false);
+                sm_pv(tile, sl, std::false_type{});
+            } else {
+                if (tile > 0) sm_pv(tile - 1, sl, std::false_type{});
+                qk(tile, sl, false);
+            }
+            if (more) stage_store((tile + 1) % NBUF);
+            __syncthreads();
+        }
+        if (nfull < ntiles) {
+            if (!late) {
+                qk(nfull, sl, true);
+                sm_pv(nfull, sl, std::true_type{});
+            } else {
+                if (nfull > 0) sm_pv(nfull - 1, sl, std::false_type{});
+                qk(nfull, sl, true);
+                sm_pv(nfull, sl, std::true_type{});
+            }
+        } else if (late && nfull > 0) {
+            sm_pv(nfull - 1, sl, std::false_type{});
+        }
     } else {
         for (int tile = 0; tile < nfull; ++tile) {
             const bool more = tile + 1 < ntiles;
             if (more) stage_load((tile + 1) * AT_KT);          // in flight during this tile
             tile_body(tile, std::false_type{});
-            if (more) stage_store((tile + 1) & 1);
+            if (more) stage_store((tile + 1) % NBUF);
             __syncthreads();
         }
         if (nfull < ntiles) tile_body(nfull, std::true_type{});
@@ -1505,6 +1547,19 @@ BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, v
             hipLaunchKernelGGL((k_attn2<64, 8, false, false, true>), dim3(1, heads, batch), dim3(512), 0,
                                bf_stream(stream), (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, sq, sk,
                                q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs, o_bs, sl2, o_map, 1.f);
+        return bf_check_launch();
+    }
+    // variant 12: short heads (5..9 query blocks, one 9-wave workgroup per (batch, head)), the
+    // ping-pong tile order (k_attn2 PP)
+    if (g_attn_variant == 12 && nw_one > 4 && nw_one <= 9 && (head_dim == 80 || head_dim == 64)) {
+        if (head_dim == 80)
+            hipLaunchKernelGGL((k_attn2<80, 9, false, false, false, false, true>), dim3(1, heads, batch),
+                               dim3(9 * 64), 0, bf_stream(stream), (const u16*)q, (const u16*)k, (const u16*)v,
+                               (u16*)o, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs, o_bs, sl2, o_map, 1.f);
+        else
+            hipLaunchKernelGGL((k_attn2<64, 9, false, false, false, false, true>), dim3(1, heads, batch),
+                               dim3(9 * 64), 0, bf_stream(stream), (const u16*)q, (const u16*)k, (const u16*)v,
+                               (u16*)o, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs, o_bs, sl2, o_map, 1.f);
         return bf_check_launch();
     }
     // variant 11: CLIP-like short heads (D = 80, 257..272 queries): 8 full waves + the light ninth

@@ -211,6 +211,27 @@ def test_attention(L, B, H, S, D, variant):
     assert rel_err(o, ref) < 1e-2
 
 
+@pytest.mark.parametrize("B,H,S,D", [(3, 16, 257, 80), (2, 4, 288, 80), (3, 12, 272, 64),
+                                     (2, 16, 256, 80), (2, 4, 200, 64), (2, 3, 160, 80)])
+def test_attention_pingpong_equals_default(L, B, H, S, D):
+    """variant 12 (k_attn2 PP: waves 4-7 run each tile rotated by half a tile, three-tile K/V ring,
+    staging by waves 0-3 and 8) computes every query exactly as the default schedule"""
+    g = torch.Generator(device="cuda").manual_seed(B * S + D + 12)
+    qkv = torch.randn(B * S, 3 * H * D, device="cuda", generator=g).bfloat16()
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    outs = {}
+    for var in (6, 12):
+        o = torch.full((B * S, H * D), float("nan"), device="cuda", dtype=torch.bfloat16)
+        L.lib().bf_attention_set_variant(var)
+        try:
+            L.attention(q, k, v, o, B, H, S, S, D, D ** -0.5)
+        finally:
+            L.lib().bf_attention_set_variant(6)
+        outs[var] = o
+    assert torch.equal(outs[12], outs[6])
+    assert rel_err(outs[12], _attn_ref(q, k, v, B, H, S, D, D ** -0.5)) < 1e-2
+
+
 @pytest.mark.parametrize("sq,D", [(1, 80), (1, 64), (40, 80), (64, 32)])
 def test_attention_few_queries(L, sq, D):
     """<= 64 queries against 257 keys (CLIP's last block: the class token of every crop), the
