@@ -1025,10 +1025,17 @@ def fusion_fit(view_off, n_views, view_box, view_R, view_score, view_pose, view_
 def depth_preprocess(depth, K=None, RT=None, max_depth=10.0, out=None, params=None, xyz=None, valid=None,
                      ws=None):
     t = _timer()
-    fn = lambda: _depth_preprocess_untimed(depth, K, RT, max_depth, out, params, xyz, valid, ws)
     if t is None:
-        return fn()
+        return _depth_preprocess_untimed(depth, K, RT, max_depth, out, params, xyz, valid, ws)
     b, h, w = depth.shape
+    # outputs and workspace allocated before the start event: the events bracket the launches only
+    out = torch.empty_like(depth) if out is None else out
+    params = torch.empty((b, 2), dtype=torch.float32, device=depth.device) if params is None else params
+    if K is not None:
+        xyz = torch.empty((b, h, w, 3), dtype=torch.float32, device=depth.device) if xyz is None else xyz
+        valid = torch.empty((b, h, w), dtype=torch.uint8, device=depth.device) if valid is None else valid
+    ws = depth_workspace(b, h, w, depth.device) if ws is None else ws
+    fn = lambda: _depth_preprocess_untimed(depth, K, RT, max_depth, out, params, xyz, valid, ws)
     n = float(b * h * w)
     # algorithmic bytes: read the depth once, write the standardised map (+ xyz and
     # the valid mask when back-projecting)
