@@ -267,10 +267,13 @@ class Pipeline:
     def __init__(self, detect: DetectStage, fusion: FusionStage, gap):
         self.detect, self.fusion, self.gap = detect, fusion, gap
 
-    def run(self, frames, n_frames, per_frame=True, frames_per_call=64):
+    def run(self, frames, n_frames, per_frame=True, frames_per_call=64, viz=None):
         """frames(ids) -> (rgb [b,H,W,3] u8 dev, depth [b,H,W] f32 dev, poses [b,4,4] host).
         per_frame: the frames between keyframes get demo.py:121-131's per-frame work too
-        (DetectStage.preprocess_frames, up to `frames_per_call` frames per call)."""
+        (DetectStage.preprocess_frames, up to `frames_per_call` frames per call).
+        viz: a visualize.FrameLogger -- demo.py's per-frame rerun calls (pose, pinhole, trajectory)
+        for every frame and the global boxes after each keyframe's fusion (host side, after the
+        frame's GPU work; not used by the bench)."""
         B = self.detect.B
         kf = [i for i in range(n_frames) if i % self.gap == 0]
         self.frames_preprocessed = 0
@@ -282,6 +285,9 @@ class Pipeline:
                     _, depth, poses = frames(nk[c:c + frames_per_call])
                     self.detect.preprocess_frames(depth.contiguous(), poses)
                     self.frames_preprocessed += len(nk[c:c + frames_per_call])
+                    if viz is not None:
+                        for j, i in enumerate(nk[c:c + frames_per_call]):
+                            viz.frame(i, poses[j])
             rgb, depth, poses = frames(ids)
             if len(ids) < B:   # ragged tail: pad the batch with the last frame, drop its results
                 pad = B - len(ids)
@@ -291,8 +297,13 @@ class Pipeline:
             preds = self.detect(rgb.contiguous(), depth.contiguous(), poses)
             for j, i in enumerate(ids):
                 self.fusion.keyframe(i, poses[j], preds[j])
+                if viz is not None:
+                    viz.frame(i, poses[j])
+                    viz.boxes(self.fusion.all_pred_box, i)
         last = n_frames - 1
         if last % self.gap != 0:
             _, _, p = frames([last])
             self.fusion.finish(last, p[0], False)
+            if viz is not None:        # demo.py:330: the boxes after the last frame's block too
+                viz.boxes(self.fusion.all_pred_box, last)
         return self.fusion

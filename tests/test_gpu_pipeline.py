@@ -457,9 +457,21 @@ def test_pipeline_run_vs_reference_demo_gap25(dev, native, monkeypatch):
         return (torch.from_numpy(rgb).to(dev), torch.from_numpy(depth).to(dev),
                 np.stack([scene.pose(i) for i in ids]))
 
+    from boxfusion_amd.visualize import FrameLogger, Recording
+    rec = Recording(forward=False)
+    viz = FrameLogger(rec, SCANNET_K, (640, 480), show_class=True)
     pipe = Pipeline(det, fusion, gap)
-    pipe.run(frames, n)
+    pipe.run(frames, n, viz=viz)
     assert pipe.frames_preprocessed == det.frames_done == n - len(range(0, n, gap))
+    # f4: every frame's pose logged once, the global boxes after each keyframe and the last frame
+    # (demo.py:330), the last of them the final global boxes
+    poses = [a for p_, _, k, a in rec.records if p_ == "/world/image" and k == "Transform3D"]
+    assert len(poses) == n
+    boxes_logged = [a for p_, _, k, a in rec.records if p_ == "/device/wide/pred_instances"]
+    assert len(boxes_logged) == len(range(0, n, gap)) + 1
+    fin = fusion.all_pred_box
+    np.testing.assert_array_equal(boxes_logged[-1]["centers"], fin.pred_boxes_3d.tensor[:, :3].cpu().numpy())
+    assert boxes_logged[-1]["labels"] == [str(c) for c in fin.categories]
     bm = fusion.box_manager
     ragged = lambda flat, off: [flat[off[i]:off[i + 1]].tolist() for i in range(len(off) - 1)]
     assert bm.fusion_list == ragged(d["fusion_list_flat"], d["fusion_list_off"])
