@@ -1069,15 +1069,23 @@ __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2v));
 }
 
-template <bool OUT_BF16, int ACT, bool RES>
+// F8 (as in k_gemm256p): bit 0 fp8 e4m3 operands (128-element K-tiles, block-scaled MFMA with unit
+// scales, epilogue acc * csc + bias), bit 1 fp8 output (v * oqs saturated to +-448; 8 bytes per lane
+// after the permlane exchange).  Not combined with RES.
+template <bool OUT_BF16, int ACT, bool RES, int F8 = 0>
 __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restrict__ A, int lda,
                                                             const u16* __restrict__ W, int ldw,
                                                             const float* __restrict__ bias,
                                                             const float* __restrict__ resid, int ldr,
                                                             void* __restrict__ Cv, int ldc, int M,
                                                             int N, int K, int tiles_n, int tiles_m,
-                                                            int stagger, int gm) {
+                                                            int stagger, int gm, float csc = 1.f,
+                                                            float oqs = 1.f) {
     extern __shared__ __attribute__((aligned(16))) unsigned char g_smem[];
+    static_assert(!(RES && F8), "fp8 residual GEMMs keep k_gemm256p");
+    static_assert(!(F8 & 2) || OUT_BF16, "fp8 output takes the narrow store path");
+    constexpr int ESZ = (F8 & 1) ? 1 : 2;           // operand bytes
+    constexpr int KTE = GB_K * 2 / ESZ;             // K elements per 128-B K-tile row
     constexpr int S = OUT_BF16 ? 4 : 8;             // stores per quadrant epilogue (per lane)
     constexpr int R = RES ? 8 : 0;                  // residual loads per quadrant re-init
     const int t = threadIdx.x;
@@ -1088,7 +1096,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
     const int G = gridDim.x;
     const int slot = (G % 8 == 0) ? ((int)blockIdx.x % 8) * (G / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
     const int my_tiles = ntiles > slot ? (ntiles - slot + G - 1) / G : 0;
-    const int nk = K / GB_K;
+    const int nk = K / KTE;
     const int total = my_tiles * nk;
     if (total == 0) return;
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
@@ -1113,8 +1121,8 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
             b_row[h][i] = (L >> 5) * 64 + h * 32 + (L & 31);
         }
     }
-    const int bytesA = (int)(((size_t)(M - 1) * lda + K) * 2);
-    const int bytesW = (int)(((size_t)(N - 1) * ldw + K) * 2);
+    const int bytesA = (int)(((size_t)(M - 1) * lda + K) * ESZ);
+    const int bytesW = (int)(((size_t)(N - 1) * ldw + K) * ESZ);
     struct KT { int idx, m0, n0, k0, buf; };
     auto kt_at_tile = [&](int tile_k, int idx) {
         const int tile = slot + tile_k * G;
@@ -1125,7 +1133,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
     int tile_ord = 0;
     auto kt_next = [&](KT c) {
         if (c.idx >= total - 1) return c;
-        if (c.k0 + GB_K < K) { c.k0 += GB_K; c.idx += 1; c.buf ^= 1; return c; }
+        if (c.k0 + KTE < K) { c.k0 += KTE; c.idx += 1; c.buf ^= 1; return c; }
         ++tile_ord;
         return kt_at_tile(tile_ord, c.idx + 1);
     };
@@ -1136,8 +1144,8 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         for (int h = 0; h < 2; ++h)
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                v.a[h][i] = min(c.m0 + a_row[h][i], M - 1) * lda * 2 + scol[i];
-                v.b[h][i] = min(c.n0 + b_row[h][i], N - 1) * ldw * 2 + scol[i];
+                v.a[h][i] = min(c.m0 + a_row[h][i], M - 1) * lda * ESZ + scol[i];
+                v.b[h][i] = min(c.n0 + b_row[h][i], N - 1) * ldw * ESZ + scol[i];
             }
         return v;
     };
@@ -1146,9 +1154,9 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         unsigned char* dst_ = g_smem + (c).buf * 65536 + (which) * 16384 + wave_u * 2048;          \
         _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                         \
             if ((which) < 2)                                                                       \
-                glds_buf16(A, bytesA, dst_ + i_ * 1024, (v).a[(which) & 1][i_], (c).k0 * 2);       \
+                glds_buf16(A, bytesA, dst_ + i_ * 1024, (v).a[(which) & 1][i_], (c).k0 * ESZ);     \
             else                                                                                   \
-                glds_buf16(W, bytesW, dst_ + i_ * 1024, (v).b[(which) & 1][i_], (c).k0 * 2);       \
+                glds_buf16(W, bytesW, dst_ + i_ * 1024, (v).b[(which) & 1][i_], (c).k0 * ESZ);     \
         }                                                                                          \
     }
 
@@ -1188,7 +1196,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         }                                                                                          \
     }
     // output buffer descriptor: byte offsets of rows < M only (the rest are dropped)
-    const int esz = OUT_BF16 ? 2 : 4;
+    const int esz = (F8 & 2) ? 1 : OUT_BF16 ? 2 : 4;
     const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
         Cv, 0, (int)(((size_t)(M - 1) * ldc + N) * esz), 0x00020000);
     // epilogue of quadrant (MI, NI) of the tile at (em0_, en0_)
@@ -1199,8 +1207,36 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         const f32x4 b1_ = *reinterpret_cast<const f32x4*>(bias_lds + min(cb_ + 16, N - 4));       \
         _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                           \
             const int r_ = (em0_) + wr * 128 + (MI) * 64 + i * 16 + lr;                            \
-            f32x4 x0 = acc[(MI) * 4 + i][(NI) * 2] + b0_;                                         \
-            f32x4 x1 = acc[(MI) * 4 + i][(NI) * 2 + 1] + b1_;                                     \
+            if constexpr ((F8 & 2) != 0) {                                                         \
+                /* fp8 row segments, one block at a time (fewer live registers): 4 bytes per      \
+                   block, exchanged between lane rows -> 8 consecutive bytes */                     \
+                int XY_[2];                                                                        \
+                _Pragma("unroll") for (int jj = 0; jj < 2; ++jj) {                                 \
+                    f32x4 x_ = acc[(MI) * 4 + i][(NI) * 2 + jj] * csc + (jj ? b1_ : b0_);          \
+                    if constexpr (ACT == 1) {                                                      \
+                        f32x2 p0 = {x_.x, x_.y}, p1 = {x_.z, x_.w};                                \
+                        gelu_erf2x2(p0, p1);                                                       \
+                        x_ = (f32x4){p0.x, p0.y, p1.x, p1.y};                                      \
+                    }                                                                              \
+                    x_ = __builtin_elementwise_min(__builtin_elementwise_max(x_ * oqs,             \
+                             (f32x4){-448.f, -448.f, -448.f, -448.f}), (f32x4){448.f, 448.f, 448.f, 448.f}); \
+                    int q_ = __builtin_amdgcn_cvt_pk_fp8_f32(x_.x, x_.y, 0, false);                \
+                    XY_[jj] = __builtin_amdgcn_cvt_pk_fp8_f32(x_.z, x_.w, q_, true);               \
+                }                                                                                  \
+                const auto s_ = __builtin_amdgcn_permlane16_swap((uint32_t)XY_[0], (uint32_t)XY_[1], false, false); \
+                const int c_ = (en0_) + wc * 64 + (NI) * 32 + 16 * (lq & 1) + 8 * (lq >> 1);        \
+                const int off_ = (r_ < M && c_ < N) ? (r_ * ldc + c_) : (int)0x80000000;          \
+                __builtin_amdgcn_raw_buffer_store_b64((u32x2v){s_[0], s_[1]}, crs, off_, 0, 2);   \
+                continue;                                                                          \
+            }                                                                                      \
+            f32x4 x0, x1;                                                                          \
+            if constexpr ((F8 & 1) != 0) {                                                         \
+                x0 = acc[(MI) * 4 + i][(NI) * 2] * csc + b0_;                                      \
+                x1 = acc[(MI) * 4 + i][(NI) * 2 + 1] * csc + b1_;                                  \
+            } else {                                                                               \
+                x0 = acc[(MI) * 4 + i][(NI) * 2] + b0_;                                            \
+                x1 = acc[(MI) * 4 + i][(NI) * 2 + 1] + b1_;                                        \
+            }                                                                                      \
             if constexpr (ACT == 1) {                                                              \
                 f32x2 p0 = {x0.x, x0.y}, p1 = {x0.z, x0.w}, p2 = {x1.x, x1.y}, p3 = {x1.z, x1.w}; \
                 gelu_erf2x2(p0, p1); gelu_erf2x2(p2, p3);                                          \
@@ -1209,7 +1245,8 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
                 x0 = __builtin_elementwise_max(x0, (f32x4){0.f, 0.f, 0.f, 0.f});                   \
                 x1 = __builtin_elementwise_max(x1, (f32x4){0.f, 0.f, 0.f, 0.f});                   \
             }                                                                                      \
-            if constexpr (OUT_BF16) {                                                              \
+            if constexpr (false) {                                                                 \
+            } else if constexpr (OUT_BF16) {                                                       \
                 uint32_t X0 = pk_bf16(x0.x, x0.y), X1 = pk_bf16(x0.z, x0.w);                       \
                 uint32_t Y0 = pk_bf16(x1.x, x1.y), Y1 = pk_bf16(x1.z, x1.w);                       \
                 const auto s0_ = __builtin_amdgcn_permlane16_swap(X0, Y0, false, false);           \
@@ -1228,20 +1265,46 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
     }
 
     bf16x8 fa[8], fb0[4], fb1[4];
+    i32x8 ga[4], gb0[2], gb1[2];      // fp8: a lane's two 16-B chunks as one 32-B fragment
 #define LDS16(off) (*reinterpret_cast<const bf16x8*>(g_smem + (off)))
 #define RD_A(stage, mi)                                                                            \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) \
-        fa[i * 2 + ks] = LDS16((stage) * 65536 + (mi) * 16384 + swz(wr * 64 + i * 16 + lr, ks * 4 + lq));
-#define RD_B(FB, stage, ni)                                                                        \
-    _Pragma("unroll") for (int j = 0; j < 2; ++j) _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) \
-        FB[j * 2 + ks] = LDS16((stage) * 65536 + 32768 + (ni) * 16384 + swz(wc * 32 + j * 16 + lr, ks * 4 + lq));
-#define MFMA_Q(mi, ni, FB)                                                                         \
+    if constexpr ((F8 & 1) != 0) {                                                                 \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                            \
+            const int b_ = (stage) * 65536 + (mi) * 16384;                                         \
+            ga[i] = frag32(LDS16(b_ + swz(wr * 64 + i * 16 + lr, lq)),                             \
+                           LDS16(b_ + swz(wr * 64 + i * 16 + lr, 4 + lq)));                        \
+        }                                                                                          \
+    } else {                                                                                       \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) \
+            fa[i * 2 + ks] = LDS16((stage) * 65536 + (mi) * 16384 + swz(wr * 64 + i * 16 + lr, ks * 4 + lq)); \
+    }
+#define RD_B(FB, GB, stage, ni)                                                                    \
+    if constexpr ((F8 & 1) != 0) {                                                                 \
+        _Pragma("unroll") for (int j = 0; j < 2; ++j) {                                            \
+            const int b_ = (stage) * 65536 + 32768 + (ni) * 16384;                                 \
+            GB[j] = frag32(LDS16(b_ + swz(wc * 32 + j * 16 + lr, lq)),                             \
+                           LDS16(b_ + swz(wc * 32 + j * 16 + lr, 4 + lq)));                        \
+        }                                                                                          \
+    } else {                                                                                       \
+        _Pragma("unroll") for (int j = 0; j < 2; ++j) _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) \
+            FB[j * 2 + ks] = LDS16((stage) * 65536 + 32768 + (ni) * 16384 + swz(wc * 32 + j * 16 + lr, ks * 4 + lq)); \
+    }
+#define MFMA_Q(mi, ni, FB, GB)                                                                     \
     {                                                                                              \
         __builtin_amdgcn_s_setprio(1);                                                             \
-        _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i) \
-            _Pragma("unroll") for (int j = 0; j < 2; ++j) acc[(mi) * 4 + i][(ni) * 2 + j] =        \
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j * 2 + ks], fa[i * 2 + ks],            \
-                                                        acc[(mi) * 4 + i][(ni) * 2 + j], 0, 0, 0); \
+        if constexpr ((F8 & 1) != 0) {                                                             \
+            _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) \
+                acc[(mi) * 4 + i][(ni) * 2 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4( \
+                    GB[j], ga[i], acc[(mi) * 4 + i][(ni) * 2 + j], 0, 0, 0, 127, 0, 127);          \
+            /* not convergent: pin the results to this phase (see k_gemm256p) */                   \
+            _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) \
+                asm volatile("" : "+v"(acc[(mi) * 4 + i][(ni) * 2 + j]));                          \
+        } else {                                                                                   \
+            _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i) \
+                _Pragma("unroll") for (int j = 0; j < 2; ++j) acc[(mi) * 4 + i][(ni) * 2 + j] =    \
+                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j * 2 + ks], fa[i * 2 + ks],        \
+                                                            acc[(mi) * 4 + i][(ni) * 2 + j], 0, 0, 0); \
+        }                                                                                          \
         __builtin_amdgcn_s_setprio(0);                                                             \
     }
 
@@ -1265,10 +1328,10 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
     int em0 = 0, en0 = 0;     // the tile whose quadrant Q10 is still pending
     for (int g = 0; g < total; ++g) {
         const int st = g & 1;
-        const bool isL = kc.k0 == K - GB_K;
+        const bool isL = kc.k0 == K - KTE;
         const bool isF = kc.k0 == 0 && g > 0;
         // ---- P1: Q00; reads B0 then A0; [first K-tile: the previous tile's Q10]
-        RD_B(fb0, st, 0);
+        RD_B(fb0, gb0, st, 0);
         SB0();
         RD_A(st, 0);
         if (isF) {
@@ -1279,10 +1342,10 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         CBAR();
         asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
         PHASE_BARRIER();
-        MFMA_Q(0, 0, fb0);
+        MFMA_Q(0, 0, fb0, gb0);
         PHASE_BARRIER();
         // ---- P2: Q01; reads B1; stage B0 of g+2; [last K-tile: Q00]
-        RD_B(fb1, st, 1);
+        RD_B(fb1, gb1, st, 1);
         STAGE_HALF(k2, v2, 2);
         if (isL) { QEPI(0, 0, kc.m0, kc.n0); QINIT_ASYNC(0, 0, k1); }
         if (isF) {
@@ -1291,7 +1354,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         CBAR();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         PHASE_BARRIER();
-        MFMA_Q(0, 1, fb1);
+        MFMA_Q(0, 1, fb1, gb1);
         PHASE_BARRIER();
         // ---- P3: Q11; reads A1; stage A0 of g+2; [last K-tile: Q01]
         RD_A(st, 1);
@@ -1303,7 +1366,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         CBAR();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         PHASE_BARRIER();
-        MFMA_Q(1, 1, fb1);
+        MFMA_Q(1, 1, fb1, gb1);
         PHASE_BARRIER();
         // ---- P4: Q10 from registers; stage B1 and A1 of g+2; [last K-tile: Q11]; retire g+1
         STAGE_HALF(k2, v2, 3);
@@ -1320,7 +1383,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         }
         PHASE_BARRIER();
-        MFMA_Q(1, 0, fb0);
+        MFMA_Q(1, 0, fb0, gb0);
         PHASE_BARRIER();
         kc = k1; k1 = k2;
         {
@@ -1574,6 +1637,31 @@ BF_API int bf_gemm_fp8(const void* A, int lda, const void* W, int ldw, float sca
         const long long rounds = (t2 + n_cu - 1) / n_cu;
         const int g = (int)(((t2 + rounds - 1) / rounds + 7) & ~7LL);
         grid = g < n_cu ? g : n_cu;
+    }
+    // the overlapped-epilogue kernel for the fp8 GEMMs with bf16 / fp8 outputs (qkv, fc1 + GELU)
+    if ((g_gemm_variant == 5 || g_gemm_variant == 6) && !resid && out_kind != 0 && K / 128 >= 3 &&
+        N <= G2Q_BIAS_MAX && (long long)(M - 1) * ldc * (out_kind == 1 ? 2 : 1) + (long long)N * 2 < (1LL << 31)) {
+        static bool qattr8 = false;
+        if (!qattr8) {
+            hipFuncSetAttribute((const void*)k_gemm256q<true, 0, false, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
+            hipFuncSetAttribute((const void*)k_gemm256q<true, 1, false, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
+            hipFuncSetAttribute((const void*)k_gemm256q<true, 0, false, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
+            hipFuncSetAttribute((const void*)k_gemm256q<true, 1, false, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
+            qattr8 = true;
+        }
+#define GEMMQ8(AC, F8) hipLaunchKernelGGL((k_gemm256q<true, AC, false, F8>), dim3(grid), dim3(G2_THREADS), G2_LDS, \
+                                          bf_stream(stream), (const u16*)A, lda, (const u16*)W, ldw, bias,     \
+                                          (const float*)nullptr, 0, C, ldc, M, N, K, t2n, t2m, 1, g_group_m,   \
+                                          scale, out_qscale)
+        if (out_kind == 1) {
+            if (act == 0) GEMMQ8(0, 1);
+            else GEMMQ8(1, 1);
+        } else {
+            if (act == 0) GEMMQ8(0, 3);
+            else GEMMQ8(1, 3);
+        }
+#undef GEMMQ8
+        return bf_check_launch();
     }
 #define GEMM8(OB, AC, F8) launch_gemm256_f8<OB, AC, F8>(grid, bf_stream(stream), A, lda, W, ldw, scale, bias, \
                                                          resid, ldr, C, ldc, out_qscale, M, N, K, t2n, t2m)

@@ -1,6 +1,12 @@
-"""CLIP ViT-H GEMMs and the whole crop tower: bf16 vs fp8 (one MI355X).
-python scripts/fp8_bench.py"""
+"""CLIP ViT-H GEMMs and the whole crop tower: bf16 vs fp8 (one MI355X), each GEMM under the GEMM
+variants given (default: 1 = k_gemm256p, 5 = k_gemm256q for bf16 / fp8 outputs).
+python scripts/fp8_bench.py [variant ...]"""
+import os
+import sys
+
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from boxfusion_amd import _lib
 
@@ -17,6 +23,9 @@ def timeit(fn, n=10):
     return e0.elapsed_time(e1) / n * 1e3
 
 
+VARIANTS = [int(v) for v in sys.argv[1:]] or [1, 5]
+
+
 def main():
     dev = torch.device("cuda")
     M = 128 * 257
@@ -29,14 +38,19 @@ def main():
         fl = 2.0 * M * N * K
         a16, w16 = a.bfloat16(), w.bfloat16()
         o16 = torch.empty(M, N, device=dev, dtype=torch.float32 if res else torch.bfloat16)
-        t16 = timeit(lambda: _lib.gemm(a16, w16, b, act=act, resid=x if res else None, out=x if res else o16))
         a8, w8 = a.to(_lib.FP8), (w * 20).to(_lib.FP8)
         od = {"bf16": torch.bfloat16, "fp8": _lib.FP8, "f32": torch.float32}[ob]
         o8 = torch.empty(M, N, device=dev, dtype=od)
-        t8 = timeit(lambda: _lib.gemm_fp8(a8, w8, 0.05, bias=b, act=act, resid=x if res else None,
-                                          out=x if res else o8, out_qscale=0.1))
-        print(f"{name:4s} M={M} N={N} K={K}: bf16 {t16:7.1f} us {fl / t16 / 1e6:7.1f} TF/s | "
-              f"fp8 {t8:7.1f} us {fl / t8 / 1e6:7.1f} TF/s ({t16 / t8:.2f}x)", flush=True)
+        msg = f"{name:4s} M={M} N={N} K={K}:"
+        for var in VARIANTS:
+            _lib.lib().bf_gemm_set_variant(var)
+            t16 = timeit(lambda: _lib.gemm(a16, w16, b, act=act, resid=x if res else None, out=x if res else o16))
+            t8 = timeit(lambda: _lib.gemm_fp8(a8, w8, 0.05, bias=b, act=act, resid=x if res else None,
+                                              out=x if res else o8, out_qscale=0.1))
+            msg += (f" | v{var} bf16 {t16:7.1f} us {fl / t16 / 1e6:7.1f} TF/s, "
+                    f"fp8 {t8:7.1f} us {fl / t8 / 1e6:7.1f} TF/s ({t16 / t8:.2f}x)")
+        _lib.lib().bf_gemm_set_variant(5)
+        print(msg, flush=True)
     from boxfusion_amd.clip import VisionTransformer
     from boxfusion_amd.engine import CLIPEngine
     from boxfusion_amd.weights import init_seeded

@@ -80,6 +80,37 @@ def test_gemm_fp8_bf16_and_fp8_out(L, act):
     assert rel(dec, ref) < 4e-2
 
 
+@pytest.mark.parametrize("M,N,K", [(2056, 5120, 1280), (300, 1280, 1280), (4112, 3840, 1280),
+                                   (513, 768, 384)])
+@pytest.mark.parametrize("act", [None, "gelu"])
+def test_gemm_fp8_overlapped_epilogue_vs_serial(L, M, N, K, act):
+    """k_gemm256q's fp8 forms (the default for bf16 / fp8 outputs) against k_gemm256p (variant 1)
+    on the same operands: bf16 outputs to bf16 rounding, fp8 outputs within one e4m3 step"""
+    a, w, g = _fp8_pair(M, N, K, M + K)
+    bias = torch.randn(N, device="cuda", generator=g)
+    scale = 0.01
+    ref = scale * (a.float() @ w.float().T) + bias
+    if act == "gelu":
+        ref = F.gelu(ref)
+    oqs = 448.0 / float(ref.abs().max()) * 0.5
+    prev = L.lib().bf_gemm_get_variant()
+    outs = {}
+    try:
+        for var in (5, 1):
+            L.lib().bf_gemm_set_variant(var)
+            outs[var] = (L.gemm_fp8(a, w, scale, bias=bias, act=act, out_dtype=torch.bfloat16),
+                         L.gemm_fp8(a, w, scale, bias=bias, act=act, out_dtype=L.FP8, out_qscale=oqs))
+            torch.cuda.synchronize()
+    finally:
+        L.lib().bf_gemm_set_variant(prev)
+    (bq, fq), (bp, fp) = outs[5], outs[1]
+    assert rel(bq, ref) < 5e-3 and rel(bq, bp) < 2e-3
+    dq, dp = fq.float() / oqs, fp.float() / oqs
+    tol = ref.abs() * 2.0 ** -3 + 2.0 ** -9 / oqs
+    assert bool(((dq - ref).abs() <= tol).all())
+    assert bool(((dq - dp).abs() <= tol).all())
+
+
 def test_gemm_fp8_saturates(L):
     a, w, g = _fp8_pair(256, 256, 128, 3)
     o8 = L.gemm_fp8(a, w, 1.0, out_dtype=L.FP8, out_qscale=1000.0)
