@@ -1060,8 +1060,10 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
 // without).  Tried for it and not kept: touching the next tile's residual rows in the middle of
 // the current tile (LDS-DMA into a dummy slot, plain or streaming: 3-9 % slower -- the lines evict
 // the operand panels), and skewing the tile boundaries per XCD (the first tile split into a
-// leading and a trailing segment, the trailing one re-initialised from C: proj 151.9 -> 189.9 us
-// -- the XCDs' lock-step walk over the same A / W panels is what keeps them in the Infinity Cache).
+// leading and a trailing segment, the trailing one re-initialised from C: proj 151.9 -> 189.9 us;
+// with offsets of only 1, 2 or 4 K-tiles per XCD index still 148.7 -> 187.8-190.0 us, CuTR fc2
+// 173.8 -> 191.6-192.2 -- the XCDs' lock-step walk over the same A / W panels is what keeps them
+// in the Infinity Cache).
 // ------------------------------------------------------------------------------------------
 #define G2Q_BIAS_MAX 8192
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
@@ -1080,7 +1082,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
                                                             void* __restrict__ Cv, int ldc, int M,
                                                             int N, int K, int tiles_n, int tiles_m,
                                                             int stagger, int gm, float csc = 1.f,
-                                                            float oqs = 1.f, int skew_kt = 0) {
+                                                            float oqs = 1.f) {
     extern __shared__ __attribute__((aligned(16))) unsigned char g_smem[];
     static_assert(!(RES && F8), "fp8 residual GEMMs keep k_gemm256p");
     static_assert(!(F8 & 2) || OUT_BF16, "fp8 output takes the narrow store path");
@@ -1123,34 +1125,19 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
     }
     const int bytesA = (int)(((size_t)(M - 1) * lda + K) * ESZ);
     const int bytesW = (int)(((size_t)(N - 1) * ldw + K) * ESZ);
-    // RES with skew_kt > 0: the walk is a sequence of segments -- segment 0 covers the first tile's
-    // K-tiles sk..nk-1 (its epilogue writes resid + that partial sum into C), the last segment the
-    // same tile's K-tiles 0..sk-1 (re-initialised from C, so the sum completes in place, no bias).
-    // sk = skew_kt x (XCD index): the tile boundaries, and the residual read burst that comes
-    // with each, are staggered by a few K-tiles from XCD to XCD.
-    int sk = 0;
-    if (RES && skew_kt > 0 && my_tiles >= 2) {
-        sk = ((int)blockIdx.x & 7) * skew_kt;               // blocks are dealt to XCDs round-robin
-        if (sk > nk / 2) sk = nk / 2;
-        if (sk == 1) sk = 2;
-        if (nk < 6) sk = 0;
-    }
-    struct KT { int idx, m0, n0, k0, buf, kend, fin; };
-    auto kt_seg = [&](int sg, int idx) {
-        const int tl = sg < my_tiles ? sg : 0;
+    struct KT { int idx, m0, n0, k0, buf; };
+    auto kt_at_tile = [&](int tile_k, int idx) {
+        const int tile = slot + tile_k * G;
         KT r;
-        r.idx = idx; tile_coords(slot + tl * G, tiles_m, tiles_n, gm, r.m0, r.n0); r.buf = idx & 1;
-        r.k0 = sg == 0 ? sk * KTE : 0;
-        r.fin = sg == my_tiles;
-        r.kend = r.fin ? (sk - 1) * KTE : K - KTE;
+        r.idx = idx; tile_coords(tile, tiles_m, tiles_n, gm, r.m0, r.n0); r.k0 = 0; r.buf = idx & 1;
         return r;
     };
-    int tile_ord = 0;       // segment ordinal of the newest KT built
+    int tile_ord = 0;
     auto kt_next = [&](KT c) {
         if (c.idx >= total - 1) return c;
-        if (c.k0 != c.kend) { c.k0 += KTE; c.idx += 1; c.buf ^= 1; return c; }
+        if (c.k0 + KTE < K) { c.k0 += KTE; c.idx += 1; c.buf ^= 1; return c; }
         ++tile_ord;
-        return kt_seg(tile_ord, c.idx + 1);
+        return kt_at_tile(tile_ord, c.idx + 1);
     };
     struct VO { int a[2][2], b[2][2]; };
     auto vo_of = [&](const KT& c) {
@@ -1198,10 +1185,8 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
 #define QINIT_ASYNC(MI, NI, T_)                                                                    \
     {                                                                                              \
         if constexpr (RES) {                                                                       \
-            const float* src_ = (T_).fin ? reinterpret_cast<const float*>(Cv) : resid;             \
-            const int ld_ = (T_).fin ? ldc : ldr;                                                  \
             _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                       \
-                const float* rp_ = src_ + (size_t)min((T_).m0 + wr * 128 + (MI) * 64 + i * 16 + lr, M - 1) * ld_; \
+                const float* rp_ = resid + (size_t)min((T_).m0 + wr * 128 + (MI) * 64 + i * 16 + lr, M - 1) * ldr; \
                 _Pragma("unroll") for (int j = 0; j < 2; ++j)                                      \
                     asm volatile("global_load_dwordx4 %0, %1, off"                                 \
                                  : "=v"(acc[(MI) * 4 + i][(NI) * 2 + j])                           \
@@ -1217,12 +1202,11 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
     const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
         Cv, 0, (int)(((size_t)(M - 1) * ldc + N) * esz), 0x00020000);
     // epilogue of quadrant (MI, NI) of the tile at (em0_, en0_)
-#define QEPI(MI, NI, em0_, en0_, fin_)                                                             \
+#define QEPI(MI, NI, em0_, en0_)                                                                   \
     {                                                                                              \
         const int cb_ = (en0_) + wc * 64 + (NI) * 32 + 4 * lq;                                     \
-        f32x4 b0_ = *reinterpret_cast<const f32x4*>(bias_lds + min(cb_, N - 4));                  \
-        f32x4 b1_ = *reinterpret_cast<const f32x4*>(bias_lds + min(cb_ + 16, N - 4));             \
-        if (RES && (fin_)) { b0_ = (f32x4){0.f, 0.f, 0.f, 0.f}; b1_ = b0_; }   /* segment 0 added it */ \
+        const f32x4 b0_ = *reinterpret_cast<const f32x4*>(bias_lds + min(cb_, N - 4));            \
+        const f32x4 b1_ = *reinterpret_cast<const f32x4*>(bias_lds + min(cb_ + 16, N - 4));       \
         _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                           \
             const int r_ = (em0_) + wr * 128 + (MI) * 64 + i * 16 + lr;                            \
             if constexpr ((F8 & 2) != 0) {                                                         \
@@ -1326,7 +1310,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         __builtin_amdgcn_s_setprio(0);                                                             \
     }
 
-    KT kc = kt_seg(0, 0);
+    KT kc = kt_at_tile(0, 0);
     KT k1 = kt_next(kc);
     KT k2 = kt_next(k1);
     VO v2 = vo_of(k2);
@@ -1343,17 +1327,17 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
     PHASE_BARRIER();
     if (stagger && wr == 1) PHASE_BARRIER();
 
-    int em0 = 0, en0 = 0, efin = 0;     // the segment whose quadrant Q10 is still pending
+    int em0 = 0, en0 = 0;     // the tile whose quadrant Q10 is still pending
     for (int g = 0; g < total; ++g) {
         const int st = g & 1;
-        const bool isL = kc.k0 == kc.kend;
+        const bool isL = kc.k0 == K - KTE;
         const bool isF = kc.k0 == 0 && g > 0;
         // ---- P1: Q00; reads B0 then A0; [first K-tile: the previous tile's Q10]
         RD_B(fb0, gb0, st, 0);
         SB0();
         RD_A(st, 0);
         if (isF) {
-            QEPI(1, 0, em0, en0, efin); QINIT_ASYNC(1, 0, kc);
+            QEPI(1, 0, em0, en0); QINIT_ASYNC(1, 0, kc);
             CBAR();
             if constexpr (RES) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + 3 * (S + R)) : "memory");  // Q00's residual (L.P2)
         }
@@ -1365,7 +1349,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         // ---- P2: Q01; reads B1; stage B0 of g+2; [last K-tile: Q00]
         RD_B(fb1, gb1, st, 1);
         STAGE_HALF(k2, v2, 2);
-        if (isL) { QEPI(0, 0, kc.m0, kc.n0, kc.fin); QINIT_ASYNC(0, 0, k1); }
+        if (isL) { QEPI(0, 0, kc.m0, kc.n0); QINIT_ASYNC(0, 0, k1); }
         if (isF) {
             if constexpr (RES) { CBAR(); asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + 2 * (S + R)) : "memory"); }  // Q01 (L.P3)
         }
@@ -1377,7 +1361,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         // ---- P3: Q11; reads A1; stage A0 of g+2; [last K-tile: Q01]
         RD_A(st, 1);
         STAGE_HALF(k2, v2, 0);
-        if (isL) { QEPI(0, 1, kc.m0, kc.n0, kc.fin); QINIT_ASYNC(0, 1, k1); }
+        if (isL) { QEPI(0, 1, kc.m0, kc.n0); QINIT_ASYNC(0, 1, k1); }
         if (isF) {
             if constexpr (RES) { CBAR(); asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 + S + R) : "memory"); }      // Q11 (L.P4)
         }
@@ -1390,10 +1374,10 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         STAGE_HALF(k2, v2, 3);
         STAGE_HALF(k2, v2, 1);
         if (isL) {
-            QEPI(1, 1, kc.m0, kc.n0, kc.fin); QINIT_ASYNC(1, 1, k1);
+            QEPI(1, 1, kc.m0, kc.n0); QINIT_ASYNC(1, 1, k1);
             CBAR();
             asm volatile("s_waitcnt vmcnt(%0)" :: "n"(8 + 3 * (S + R)) : "memory");
-            em0 = kc.m0; en0 = kc.n0; efin = kc.fin;
+            em0 = kc.m0; en0 = kc.n0;
         } else if (isF) {
             // K-tile g+1, and (RES) Q10's residual from P1: 8 younger LDS-DMA
             asm volatile("s_waitcnt vmcnt(%0)" :: "n"(RES ? 8 : 8 + S) : "memory");
@@ -1410,7 +1394,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
             k2 = kn;
         }
     }
-    QEPI(1, 0, em0, en0, efin);          // the last segment's Q10
+    QEPI(1, 0, em0, en0);          // the last tile's Q10
     if (stagger && wr == 0) PHASE_BARRIER();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #undef RD_A
@@ -1431,12 +1415,6 @@ static int g_gemm_variant = [] {
 }();
 BF_API void bf_gemm_set_variant(int v) { g_gemm_variant = v; }
 BF_API int bf_gemm_get_variant(void) { return g_gemm_variant; }
-// k_gemm256q residual GEMMs: K-tiles of tile-boundary skew per XCD index (0 = aligned).  Env BF_GEMMQ_SKEW.
-static int g_gemmq_skew = [] {
-    const char* e = getenv("BF_GEMMQ_SKEW");
-    return e ? atoi(e) : 0;
-}();
-BF_API void bf_gemm_set_skew(int kt) { g_gemmq_skew = kt > 0 ? kt : 0; }
 
 // row panels per tile group (tile_coords); 1 = row-major.  Default 8, env BF_GEMM_GROUP_M.
 static int g_group_m = [] {
@@ -1579,7 +1557,7 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
             }
 #define GEMMQ(OB, AC, RS) hipLaunchKernelGGL((k_gemm256q<OB, AC, RS>), dim3(grid2), dim3(G2_THREADS), G2_LDS,   \
                                              bf_stream(stream), (const u16*)A, lda, (const u16*)W, ldw, bias, resid, \
-                                             ldr, C, ldc, M, N, K, t2n, t2m, 1, g_group_m, 1.f, 1.f, g_gemmq_skew)
+                                             ldr, C, ldc, M, N, K, t2n, t2m, 1, g_group_m)
             if (resid) GEMMQ(false, 0, true);
             else if (!c_bf16) GEMMQ(false, 0, false);
             else if (act == 0) GEMMQ(true, 0, false);
