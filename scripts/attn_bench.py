@@ -42,6 +42,7 @@ for name, B, H, S, D in SHAPES:
         for var in variants:
             L.bf_attention_set_variant(var)
             times[var].append(timeit(f))
+    first = None
     for var in variants:
         L.bf_attention_set_variant(var)
         o.zero_()
@@ -50,6 +51,12 @@ for name, B, H, S, D in SHAPES:
         err = (o[:4 * S].float() - ref).abs().max().item()
         ms = sorted(times[var])[1]
         msg += f" | v{var} {ms*1e3:7.1f} us {fl/ms/1e9:6.1f} TF/s err {err:.1e}"
+        if first is None:
+            first = o.clone()
+        else:
+            # rows that differ from the first variant (bit for bit), max |diff|
+            nd = (o != first).any(dim=1).sum().item()
+            msg += f" neq_rows {nd} maxd {(o.float() - first.float()).abs().max().item():.1e}"
     mt = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(qq, kk, vv))
     msg += f" | sdpa {mt*1e3:7.1f} us {fl/mt/1e9:6.1f} TF/s"
     print(msg, flush=True)

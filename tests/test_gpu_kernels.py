@@ -215,12 +215,13 @@ def test_attention(L, B, H, S, D, variant):
                                      (2, 16, 256, 80), (2, 4, 200, 64), (2, 3, 160, 80)])
 def test_attention_pingpong_equals_default(L, B, H, S, D):
     """variant 12 (k_attn2 PP: waves 4-7 run each tile rotated by half a tile, three-tile K/V ring,
-    staging by waves 0-3 and 8) computes every query exactly as the default schedule"""
+    staging by waves 0-3 and 8) and variant 17 (k_attn5: every K / V tile resident by LDS-DMA, no
+    barrier after tile 0) compute every query exactly as the default schedule"""
     g = torch.Generator(device="cuda").manual_seed(B * S + D + 12)
     qkv = torch.randn(B * S, 3 * H * D, device="cuda", generator=g).bfloat16()
     q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
     outs = {}
-    for var in (6, 12):
+    for var in (6, 12, 17, 18):
         o = torch.full((B * S, H * D), float("nan"), device="cuda", dtype=torch.bfloat16)
         L.lib().bf_attention_set_variant(var)
         try:
@@ -229,7 +230,43 @@ def test_attention_pingpong_equals_default(L, B, H, S, D):
             L.lib().bf_attention_set_variant(6)
         outs[var] = o
     assert torch.equal(outs[12], outs[6])
+    assert torch.equal(outs[17], outs[6])
+    if D == 80:
+        assert torch.equal(outs[18], outs[6])
     assert rel_err(outs[12], _attn_ref(q, k, v, B, H, S, D, D ** -0.5)) < 1e-2
+
+
+@pytest.mark.parametrize("B,H,S,spike", [(3, 16, 257, 0.0), (2, 4, 272, 0.0), (2, 16, 256, 0.0),
+                                          (2, 4, 200, 0.0), (2, 3, 264, 0.0), (1, 2, 257, 4.0),
+                                          (1, 2, 257, 1.6)])
+def test_attention_two_block_waves(L, B, H, S, spike):
+    """variant 16 (k_attn4: 4 waves of two 32-query blocks, one wave per SIMD, the chains of the
+    two blocks half a tile apart; queries 256+ split over the waves by key and merged): queries
+    0..255 bit-identical to the default kernel, the rest within the SDPA tolerance; a spike key
+    forces the deferred-max rescale inside the pipelined order"""
+    D = 80
+    g = torch.Generator(device="cuda").manual_seed(B * S + 16)
+    qkv = torch.randn(B * S, 3 * H * D, device="cuda", generator=g)
+    if spike:
+        qkv[S - 20, H * D:2 * H * D] = qkv[0, :H * D] * spike
+        qkv[130, H * D:2 * H * D] = qkv[1, :H * D] * spike * 0.8
+        qkv[S - 1, H * D:2 * H * D] = qkv[S - 1, :H * D] * spike
+    qkv = qkv.bfloat16()
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    outs = {}
+    for var in (6, 16):
+        o = torch.full((B * S, H * D), float("nan"), device="cuda", dtype=torch.bfloat16)
+        L.lib().bf_attention_set_variant(var)
+        try:
+            L.attention(q, k, v, o, B, H, S, S, D, D ** -0.5)
+        finally:
+            L.lib().bf_attention_set_variant(6)
+        outs[var] = o.view(B, S, H * D)
+    assert torch.equal(outs[16][:, :256], outs[6][:, :256])
+    ref = _attn_ref(q, k, v, B, H, S, D, D ** -0.5).view(B, S, H * D)
+    assert rel_err(outs[16], ref) < 1e-2
+    if S > 256:
+        assert rel_err(outs[16][:, 256:], ref[:, 256:]) < 1e-2
 
 
 @pytest.mark.parametrize("sq,D", [(1, 80), (1, 64), (40, 80), (64, 32)])
