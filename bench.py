@@ -88,7 +88,7 @@ def parse(argv=None):
                         "streams) when CUs are reserved for fusion; -1: on when fusing for N > 1")
     p.add_argument("--sync-fusion", action="store_true",
                    help="run the fusion state machine inline instead of on the worker stream")
-    p.add_argument("--cpu-detect-frames", type=int, default=1)
+    p.add_argument("--cpu-detect-frames", type=int, default=2)
     p.add_argument("--inflight", type=int, default=-1,
                    help="detect steps in flight per GPU: independent batches replayed on this many "
                         "streams (each its own DetectStage buffers / graph), so one batch's CLIP "
