@@ -88,7 +88,8 @@ def parse(argv=None):
                         "streams) when CUs are reserved for fusion; -1: on when fusing for N > 1")
     p.add_argument("--sync-fusion", action="store_true",
                    help="run the fusion state machine inline instead of on the worker stream")
-    p.add_argument("--cpu-detect-frames", type=int, default=2)
+    p.add_argument("--cpu-detect-frames", type=int, default=2,
+                   help="frames of the CPU detect sample (0: no cpu_baseline, for A/B runs)")
     p.add_argument("--inflight", type=int, default=-1,
                    help="detect steps in flight per GPU: independent batches replayed on this many "
                         "streams (each its own DetectStage buffers / graph), so one batch's CLIP "
@@ -900,7 +901,7 @@ def main(argv=None):
         if args.breakdown:
             line["breakdown_ms_per_step"] = {k: 1e3 * v / args.steps for k, v in brk.items()}
         if not args.no_cpu_baseline and N == 1 and args.dataset == "scannet":   # rank 0 at N=1 only
-            line["cpu_baseline"] = cpu_baseline(cutr, clip_vis, args, scene)
+            line["cpu_baseline"] = (cpu_baseline(cutr, clip_vis, args, scene) if args.cpu_detect_frames > 0 else None)
         emit(line)
     if dist is not None:
         dist.barrier()

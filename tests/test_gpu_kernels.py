@@ -214,14 +214,15 @@ def test_attention(L, B, H, S, D, variant):
 @pytest.mark.parametrize("B,H,S,D", [(3, 16, 257, 80), (2, 4, 288, 80), (3, 12, 272, 64),
                                      (2, 16, 256, 80), (2, 4, 200, 64), (2, 3, 160, 80)])
 def test_attention_pingpong_equals_default(L, B, H, S, D):
-    """variant 12 (k_attn2 PP: waves 4-7 run each tile rotated by half a tile, three-tile K/V ring,
-    staging by waves 0-3 and 8) and variant 17 (k_attn5: every K / V tile resident by LDS-DMA, no
-    barrier after tile 0) compute every query exactly as the default schedule"""
+    """the short-head schedules compute every query exactly alike: the default (6 = 26, k_attn6:
+    persistent, output rows through LDS), 27 (the per-(batch, head) k_attn2 launch), 12 (k_attn2
+    PP: waves 4-7 one half-tile out of phase), 17 / 18 (k_attn5: every K / V tile resident by
+    LDS-DMA, no barrier after tile 0)"""
     g = torch.Generator(device="cuda").manual_seed(B * S + D + 12)
     qkv = torch.randn(B * S, 3 * H * D, device="cuda", generator=g).bfloat16()
     q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
     outs = {}
-    for var in (6, 12, 17, 18):
+    for var in (6, 12, 17, 18, 26, 27):
         o = torch.full((B * S, H * D), float("nan"), device="cuda", dtype=torch.bfloat16)
         L.lib().bf_attention_set_variant(var)
         try:
@@ -231,6 +232,7 @@ def test_attention_pingpong_equals_default(L, B, H, S, D):
         outs[var] = o
     assert torch.equal(outs[12], outs[6])
     assert torch.equal(outs[17], outs[6])
+    assert torch.equal(outs[26], outs[6]) and torch.equal(outs[27], outs[6])
     if D == 80:
         assert torch.equal(outs[18], outs[6])
     assert rel_err(outs[12], _attn_ref(q, k, v, B, H, S, D, D ** -0.5)) < 1e-2
