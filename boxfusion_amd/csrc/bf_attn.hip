@@ -1352,13 +1352,13 @@ __global__ void __launch_bounds__(256, 1) k_attn4(const u16* __restrict__ Q, con
 // pair overlaps the next pair's first tile instead of idling the CU at every workgroup boundary.
 // Output rows b*o_bs + q*o_rs (no o_map).
 // ------------------------------------------------------------------------------------------
-template <int D, int NW>
+template <int D, int NW, bool F8O = false>
 __global__ void __launch_bounds__(NW * 64, 1) k_attn6(const u16* __restrict__ Q, const u16* __restrict__ K,
                                                      const u16* __restrict__ V, u16* __restrict__ O,
                                                      int sq, int sk, int q_rs, int k_rs, int v_rs,
                                                      int o_rs, long long q_bs, long long k_bs,
                                                      long long v_bs, long long o_bs, float scale_log2,
-                                                     int heads, int npairs) {
+                                                     int heads, int npairs, float oqs = 1.f) {
     constexpr int KS = D / 16;
     constexpr int DB = (D + 31) / 32;
     constexpr bool ONES = (D % 32) != 0;
@@ -1369,7 +1369,9 @@ __global__ void __launch_bounds__(NW * 64, 1) k_attn6(const u16* __restrict__ Q,
     constexpr int CPR = D / 8;
     constexpr int CH = AT_KT * CPR;
     constexpr int NT = NW * 64;
-    constexpr int OROW = ((2 * D + 16) / 32) * 32 + 16;   // bytes per staged output row
+    constexpr int EB = F8O ? 1 : 2;                        // output bytes per element
+    constexpr int OROW = ((EB * D + 16) / 32) * 32 + 16;  // bytes per staged output row (16-B aligned)
+    constexpr int OCH = EB * D / 16;                       // 16-B chunks per output row
     __shared__ __attribute__((aligned(16))) u16 sK[2 * KTILE];
     __shared__ __attribute__((aligned(16))) u16 sV[2 * VTILE];
     __shared__ __attribute__((aligned(16))) unsigned char sO[NW * 32 * OROW];
@@ -1532,12 +1534,22 @@ __global__ void __launch_bounds__(NW * 64, 1) k_attn6(const u16* __restrict__ Q,
             for (int g = 0; g < 4; ++g) {
                 const int d0 = db * 32 + 8 * g + 4 * fh;
                 if (d0 >= D) continue;
-                V64 w;
-                w.x = (uint32_t)at_f2bf(o[db][4 * g + 0] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 1] * inv) << 16);
-                w.y = (uint32_t)at_f2bf(o[db][4 * g + 2] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 3] * inv) << 16);
-                *reinterpret_cast<V64*>(wreg + fr * OROW + 2 * d0) = w;
+                if constexpr (F8O) {     // saturate_448(o * oqs) as OCP e4m3 (bf_attention_fp8out)
+                    const float sc = inv * oqs;
+                    float a[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) a[i] = fminf(fmaxf(o[db][4 * g + i] * sc, -448.f), 448.f);
+                    int pk = __builtin_amdgcn_cvt_pk_fp8_f32(a[0], a[1], 0, false);
+                    pk = __builtin_amdgcn_cvt_pk_fp8_f32(a[2], a[3], pk, true);
+                    *reinterpret_cast<int*>(wreg + fr * OROW + d0) = pk;
+                } else {
+                    V64 w;
+                    w.x = (uint32_t)at_f2bf(o[db][4 * g + 0] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 1] * inv) << 16);
+                    w.y = (uint32_t)at_f2bf(o[db][4 * g + 2] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 3] * inv) << 16);
+                    *reinterpret_cast<V64*>(wreg + fr * OROW + 2 * d0) = w;
+                }
             }
-        const __amdgpu_buffer_rsrc_t ro = rsrc(O + bc_off(b) + h * D, 0x7FFFFFFF);
+        const __amdgpu_buffer_rsrc_t ro = rsrc(reinterpret_cast<unsigned char*>(O) + EB * (bc_off(b) + h * D), 0x7FFFFFFF);
         // ... the next pair's Q and first tile go out (older than this pair's stores) ...
         const int pn = p + (int)gridDim.x;
         const bool next = pn < npairs;                          // uniform
@@ -1548,15 +1560,16 @@ __global__ void __launch_bounds__(NW * 64, 1) k_attn6(const u16* __restrict__ Q,
         }
         // ... and this pair's rows leave as whole 2D-byte head rows
 #pragma unroll
-        for (int j = 0; j < (32 * CPR + 63) / 64; ++j) {
+        for (int j = 0; j < (32 * OCH + 63) / 64; ++j) {
             const int c = lane + 64 * j;
-            if (c >= 32 * CPR) break;
-            const int r = c / CPR, col = c % CPR;
+            const int cc = min(c, 32 * OCH - 1);
+            const int r = cc / OCH, col = cc % OCH;
             const int qr = wave * 32 + r;
             const u32x4 val = *reinterpret_cast<const u32x4*>(wreg + r * OROW + 16 * col);
-            // rows past sq: an offset past num_records, the store is dropped (every lane issues every
-            // store, so the waitcnt pass counts them exactly and the next pair's wait leaves them in flight)
-            const int off = qr < sq ? 2 * (qr * o_rs + 8 * col) : (int)0x80000000;
+            // rows past sq (and the surplus lanes of a partial last pass): an offset past num_records,
+            // the store is dropped -- every lane issues every store, so the waitcnt pass counts them
+            // exactly and the next pair's first wait leaves them in flight
+            const int off = (qr < sq && c < 32 * OCH) ? EB * qr * o_rs + 16 * col : (int)0x80000000;
             __builtin_amdgcn_raw_buffer_store_b128(val, ro, off, 0, 0);
         }
         if (!next) break;
@@ -2442,6 +2455,10 @@ BF_API int bf_attention_fp8out(const void* q, const void* k, const void* v, void
     if ((q_rs | k_rs | v_rs) % 8 != 0 || o_rs % 4 != 0 || o_bs % 4 != 0) return BF_ERR_UNSUPPORTED;
     const float sl2 = scale * 1.4426950408889634f;
     const int nw_one = (sq + 31) / 32;
+    // k_attn6 (the bf16 default's persistent short-head kernel) with the fp8 row store
+    const bool k6_ok = (long long)batch * heads < (1LL << 30) &&
+                       (long long)sq * o_rs + 2LL * ((long long)sq * q_rs + (long long)sk * (k_rs > v_rs ? k_rs : v_rs)) < (1LL << 31);
+    const int k6_grid = attn_num_cus() < batch * heads ? attn_num_cus() : batch * heads;
 #define LAUNCH_8(DD, NWV)                                                                         \
     hipLaunchKernelGGL((k_attn2<DD, NWV, true>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch), \
                        dim3(NWV * 64), 0, bf_stream(stream), (const u16*)q, (const u16*)k,          \
@@ -2458,6 +2475,10 @@ BF_API int bf_attention_fp8out(const void* q, const void* k, const void* v, void
                            bf_stream(stream), (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, sq, \
                            sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs, o_bs, sl2,                 \
                            (const int32_t*)nullptr, out_qscale);                                    \
+    } else if (nw_one > 4 && nw_one <= 9 && (g_attn_variant == 6 || g_attn_variant == 26) && k6_ok) {     \
+        hipLaunchKernelGGL((k_attn6<DD, 9, true>), dim3(k6_grid), dim3(576), 0, bf_stream(stream),        \
+                           (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, sq, sk, q_rs, k_rs, v_rs, \
+                           o_rs, q_bs, k_bs, v_bs, o_bs, sl2, heads, batch * heads, out_qscale);           \
     } else if (nw_one > 4 && nw_one <= 9) { LAUNCH_8(DD, 9); } else { LAUNCH_8(DD, 4); }
     switch (head_dim) {
         case 64: LAUNCH_8D(64); break;
