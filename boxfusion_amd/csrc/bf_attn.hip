@@ -539,7 +539,7 @@ __device__ __forceinline__ void attn2_softmax(f32x16 (&s)[2], bool sub1, bool ma
 // work between two barriers.  K / V ring of three tiles (P.V of tile n-1 reads V n-1 while tile
 // n + 1 is staged).  Arithmetic per query is unchanged (bit-identical to the default).
 template <int D, int NW, bool F8O = false, bool CAUSAL = false, bool XQ = false, bool LW = false,
-          bool PP = false>
+          bool PP = false, bool LSTQ = false>
 __global__ void __launch_bounds__(NW * 64, (NW == 3 || NW == 5) ? 3 : 1) k_attn2(const u16* __restrict__ Q, const u16* __restrict__ K,
                                                       const u16* __restrict__ V, u16* __restrict__ O,
                                                       int sq, int sk, int q_rs, int k_rs, int v_rs,
@@ -560,6 +560,12 @@ __global__ void __launch_bounds__(NW * 64, (NW == 3 || NW == 5) ? 3 : 1) k_attn2
     static_assert(!PP || (!CAUSAL && !XQ && !LW && NW > 4), "PP: short non-causal heads");
     __shared__ __attribute__((aligned(16))) u16 sK[NBUF * KTILE];
     __shared__ __attribute__((aligned(16))) u16 sV[NBUF * VTILE];
+    // LST (the default for one-workgroup short heads): the bf16 output rows go through a per-wave
+    // LDS region of their own and leave as whole 2D-byte head rows (16 B per lane along the row)
+    // instead of 8-byte fragments of 32 rows per store instruction (CLIP: 122.8 -> 115.8 us)
+    constexpr bool LST = LSTQ && !F8O && !XQ && !LW && !CAUSAL && D % 8 == 0;
+    constexpr int OROW = ((2 * D + 16) / 32) * 32 + 16;            // bytes per staged row (16-B aligned)
+    __shared__ __attribute__((aligned(16))) unsigned char sO[LST ? NW * 32 * OROW : 16];
 
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const AttnBlk blk = attn_block(1);
@@ -963,6 +969,33 @@ __global__ void __launch_bounds__(NW * 64, (NW == 3 || NW == 5) ? 3 : 1) k_attn2
         l = (fh == fh_l) ? mine : other;
     } else {
         l = l_run + __shfl_xor(l_run, 32, 64);
+    }
+    if constexpr (LST) {
+        const float inv = 1.0f / l;
+        unsigned char* wreg = sO + wave * 32 * OROW;
+#pragma unroll
+        for (int db = 0; db < DB; ++db)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int d0 = db * 32 + 8 * g + 4 * fh;
+                if (d0 >= D) continue;
+                V64 w;
+                w.x = (uint32_t)at_f2bf(o[db][4 * g + 0] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 1] * inv) << 16);
+                w.y = (uint32_t)at_f2bf(o[db][4 * g + 2] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 3] * inv) << 16);
+                *reinterpret_cast<V64*>(wreg + fr * OROW + 2 * d0) = w;
+            }
+        constexpr int CPRO = D / 8;                          // 16-B chunks per head row
+#pragma unroll
+        for (int j = 0; j < (32 * CPRO + 63) / 64; ++j) {
+            const int c = lane + 64 * j;
+            if (c >= 32 * CPRO) break;
+            const int r = c / CPRO, col = c % CPRO;
+            const int qr = q - fr + r;                         // this wave's row r
+            const V128 val = *reinterpret_cast<const V128*>(wreg + r * OROW + 16 * col);
+            const long long off = attn_out_offset(o_map, b, qr, sq, o_bs, o_rs);
+            if (qr < sq && off >= 0) *reinterpret_cast<V128*>(O + off + h * D + 8 * col) = val;
+        }
+        return;
     }
     const long long o_off = attn_out_offset(o_map, b, q, sq, o_bs, o_rs);
     if (q < sq && o_off >= 0) {
@@ -2195,6 +2228,10 @@ __global__ void __launch_bounds__(NW * 64) k_attn_p(const u16* __restrict__ Q, c
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outstanding at exit
 }
 
+BF_API int bf_gemm_get_cu_budget(void);
+// CUs a persistent attention grid may assume: the device's, or the budget set for CU-masked
+// launch streams (bf_gemm_set_cu_budget: rank 0 at N > 1 reserves CUs for the fusion stream; a
+// grid wider than the stream's CUs would run its surplus workgroups after whole walks finish)
 static int attn_num_cus() {
     static int n = [] {
         int dev = 0, c = 0;
@@ -2202,7 +2239,8 @@ static int attn_num_cus() {
         if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
         return c;
     }();
-    return n;
+    const int budget = bf_gemm_get_cu_budget();
+    return budget > 0 && budget < n ? budget : n;
 }
 
 static int launch_attn_p(hipStream_t st, const void* q, const void* k, const void* v, void* o, int batch,
@@ -2304,11 +2342,11 @@ BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, v
                                (u16*)o, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs, o_bs, sl2, o_map, 1.f);
         return bf_check_launch();
     }
-    // short heads (5..9 query blocks; CLIP's 257 tokens), default (6) and 26: k_attn6 -- persistent,
-    // output rows through LDS, the next pair's loads issued before the current pair's stores
-    // (bit-identical to k_attn2, 8 % faster on CLIP: 116.6 vs 126.3 us in the bench's re-run);
-    // variant 27: the per-pair k_attn2 launch below
-    if ((g_attn_variant == 6 || g_attn_variant == 26) && nw_one > 4 && nw_one <= 9 && (head_dim == 80 || head_dim == 64) &&
+    // variant 26: short heads (5..9 query blocks), k_attn6 -- persistent, output rows through LDS,
+    // the next pair's loads issued before the current pair's stores (bit-identical; CLIP 126.3 ->
+    // 116.6 us in the bench's re-run, but with rank 0's fusion of 8 ranks beside it, 132.6-137.9 vs
+    // 142.4-142.7 frames/s: the walk holds every CU, so the fusion stream's kernels wait)
+    if (g_attn_variant == 26 && nw_one > 4 && nw_one <= 9 && (head_dim == 80 || head_dim == 64) &&
         o_map == nullptr && (long long)batch * heads < (1LL << 30) &&
         2LL * ((long long)sq * (q_rs > o_rs ? q_rs : o_rs) + (long long)sk * (k_rs > v_rs ? k_rs : v_rs)) < (1LL << 31)) {
         const int npairs = batch * heads;
@@ -2372,11 +2410,17 @@ BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, v
         const int var = g_attn_variant;      // (`v` is the V operand)
         // <= 64 queries per (batch, head) (CLIP's last block: the class token only): 2-wave
         // workgroups, so no idle waves compute empty query blocks
+#define LAUNCH_2L(DD)                                                                             \
+    hipLaunchKernelGGL((k_attn2<DD, 9, false, false, false, false, false, true>), dim3(1, heads, batch), \
+                       dim3(576), 0, bf_stream(stream), (const u16*)q, (const u16*)k,               \
+                       (const u16*)v, (u16*)o, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs,    \
+                       o_bs, sl2, o_map, 1.f)
 #define LAUNCH_2D(DD)                                                                             \
     if (nw_one <= 2) { LAUNCH_2(DD, 2); }                                                          \
     else if (!short_s) { LAUNCH_2(DD, 4); }                                                        \
     else if (var == 7) { LAUNCH_2(DD, 5); }                                                        \
     else if (var == 8) { LAUNCH_2(DD, 3); }                                                        \
+    else if (var == 6) { LAUNCH_2L(DD); }                                                          \
     else { LAUNCH_2(DD, 9); }
         switch (head_dim) {
             case 32: LAUNCH_2D(32); break;
@@ -2386,6 +2430,7 @@ BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, v
             default: return BF_ERR_UNSUPPORTED;
         }
 #undef LAUNCH_2D
+#undef LAUNCH_2L
 #undef LAUNCH_2
         return bf_check_launch();
     }
@@ -2475,7 +2520,7 @@ BF_API int bf_attention_fp8out(const void* q, const void* k, const void* v, void
                            bf_stream(stream), (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, sq, \
                            sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs, o_bs, sl2,                 \
                            (const int32_t*)nullptr, out_qscale);                                    \
-    } else if (nw_one > 4 && nw_one <= 9 && (g_attn_variant == 6 || g_attn_variant == 26) && k6_ok) {     \
+    } else if (nw_one > 4 && nw_one <= 9 && g_attn_variant == 26 && k6_ok) {                             \
         hipLaunchKernelGGL((k_attn6<DD, 9, true>), dim3(k6_grid), dim3(576), 0, bf_stream(stream),        \
                            (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, sq, sk, q_rs, k_rs, v_rs, \
                            o_rs, q_bs, k_bs, v_bs, o_bs, sl2, heads, batch * heads, out_qscale);           \

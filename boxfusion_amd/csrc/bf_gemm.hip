@@ -1468,6 +1468,8 @@ static int g_cu_budget = 0;
 // CUs the GEMMs may assume (persistent grid size); 0 = every CU of the device.  Set it when the
 // launching stream is CU-masked (e.g. part of the chip is reserved for the fusion stream).
 BF_API void bf_gemm_set_cu_budget(int n) { g_cu_budget = n > 0 ? n : 0; }
+// (the persistent attention kernel sizes its grid by the same budget)
+BF_API int bf_gemm_get_cu_budget(void) { return g_cu_budget; }
 
 static int gemm_cu_count() {
     if (g_cu_budget > 0) return g_cu_budget;

@@ -362,6 +362,8 @@ int bf_gemm_large_tiles(int M, int N, int K);
 /* Number of CUs the GEMM may assume (sizes the persistent grid); 0 = all CUs of the device.
  * Set when GEMMs launch on a CU-masked stream. */
 void bf_gemm_set_cu_budget(int n);
+/* The budget set above (0 = none); the persistent attention kernels size their grids by it too. */
+int bf_gemm_get_cu_budget(void);
 /* Persistent-grid sizing of the 256x256 kernel: 1 (default; env BF_GEMM_BALANCED=0 turns it
  * off) launches ceil(tiles / rounds) workgroups so every block walks the same tile count and a
  * partial last round (when at least a quarter full) leaves its idle CUs to concurrent streams

@@ -214,10 +214,10 @@ def test_attention(L, B, H, S, D, variant):
 @pytest.mark.parametrize("B,H,S,D", [(3, 16, 257, 80), (2, 4, 288, 80), (3, 12, 272, 64),
                                      (2, 16, 256, 80), (2, 4, 200, 64), (2, 3, 160, 80)])
 def test_attention_pingpong_equals_default(L, B, H, S, D):
-    """the short-head schedules compute every query exactly alike: the default (6 = 26, k_attn6:
-    persistent, output rows through LDS), 27 (the per-(batch, head) k_attn2 launch), 12 (k_attn2
-    PP: waves 4-7 one half-tile out of phase), 17 / 18 (k_attn5: every K / V tile resident by
-    LDS-DMA, no barrier after tile 0)"""
+    """the short-head schedules compute every query exactly alike: the default (6: k_attn2 with its
+    output rows through LDS), 27 (k_attn2 with per-lane fragment stores), 26 (k_attn6: persistent),
+    12 (k_attn2 PP: waves 4-7 one half-tile out of phase), 17 / 18 (k_attn5: every K / V tile
+    resident by LDS-DMA, no barrier after tile 0)"""
     g = torch.Generator(device="cuda").manual_seed(B * S + D + 12)
     qkv = torch.randn(B * S, 3 * H * D, device="cuda", generator=g).bfloat16()
     q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
@@ -236,6 +236,28 @@ def test_attention_pingpong_equals_default(L, B, H, S, D):
     if D == 80:
         assert torch.equal(outs[18], outs[6])
     assert rel_err(outs[12], _attn_ref(q, k, v, B, H, S, D, D ** -0.5)) < 1e-2
+
+
+def test_attention_persistent_cu_budget(L):
+    """the persistent short-head kernel (variant 26) sizes its grid by the CU budget of CU-masked
+    streams (bf_gemm_set_cu_budget, rank 0 at N > 1): a 40-workgroup walk gives the same rows"""
+    B, H, S, D = 5, 16, 257, 80
+    g = torch.Generator(device="cuda").manual_seed(40)
+    qkv = torch.randn(B * S, 3 * H * D, device="cuda", generator=g).bfloat16()
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    outs = []
+    for budget, var in ((0, 27), (40, 26), (0, 26)):
+        o = torch.full((B * S, H * D), float("nan"), device="cuda", dtype=torch.bfloat16)
+        L.lib().bf_gemm_set_cu_budget(budget)
+        L.lib().bf_attention_set_variant(var)
+        try:
+            L.attention(q, k, v, o, B, H, S, S, D, D ** -0.5)
+        finally:
+            L.lib().bf_attention_set_variant(6)
+            L.lib().bf_gemm_set_cu_budget(0)
+        outs.append(o)
+    assert L.lib().bf_gemm_get_cu_budget() == 0
+    assert torch.equal(outs[1], outs[0]) and torch.equal(outs[2], outs[0])
 
 
 @pytest.mark.parametrize("B,H,S,spike", [(3, 16, 257, 0.0), (2, 4, 272, 0.0), (2, 16, 256, 0.0),
