@@ -563,9 +563,14 @@ __global__ void __launch_bounds__(NW * 64, (NW == 3 || NW == 5) ? 3 : 1) k_attn2
     // LST (the default for one-workgroup short heads): the bf16 output rows go through a per-wave
     // LDS region of their own and leave as whole 2D-byte head rows (16 B per lane along the row)
     // instead of 8-byte fragments of 32 rows per store instruction (CLIP: 122.8 -> 115.8 us)
-    constexpr bool LST = LSTQ && !F8O && !XQ && !LW && !CAUSAL && D % 8 == 0;
-    constexpr int OROW = ((2 * D + 16) / 32) * 32 + 16;            // bytes per staged row (16-B aligned)
-    __shared__ __attribute__((aligned(16))) unsigned char sO[LST ? NW * 32 * OROW : 16];
+    // (9-wave workgroups: an LDS region of their own, free at one workgroup per CU; 4-wave ones
+    // reuse the K ring after a barrier, so their occupancy is unchanged)
+    constexpr bool LST = LSTQ && !XQ && !LW && !CAUSAL && D % 16 == 0;
+    constexpr int EB = F8O ? 1 : 2;                                 // output bytes per element
+    constexpr int OROW = ((EB * D + 16) / 32) * 32 + 16;           // bytes per staged row (16-B aligned)
+    constexpr bool OWN = NW == 9;
+    static_assert(!LST || OWN || NW * 32 * OROW <= NBUF * KTILE * 2, "staged rows fit the K ring");
+    __shared__ __attribute__((aligned(16))) unsigned char sO[LST && OWN ? NW * 32 * OROW : 16];
 
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const AttnBlk blk = attn_block(1);
@@ -972,19 +977,31 @@ __global__ void __launch_bounds__(NW * 64, (NW == 3 || NW == 5) ? 3 : 1) k_attn2
     }
     if constexpr (LST) {
         const float inv = 1.0f / l;
-        unsigned char* wreg = sO + wave * 32 * OROW;
+        if constexpr (!OWN) __syncthreads();                 // every wave is done with the K ring
+        unsigned char* wreg = (OWN ? sO : reinterpret_cast<unsigned char*>(sK)) + wave * 32 * OROW;
 #pragma unroll
         for (int db = 0; db < DB; ++db)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const int d0 = db * 32 + 8 * g + 4 * fh;
                 if (d0 >= D) continue;
-                V64 w;
-                w.x = (uint32_t)at_f2bf(o[db][4 * g + 0] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 1] * inv) << 16);
-                w.y = (uint32_t)at_f2bf(o[db][4 * g + 2] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 3] * inv) << 16);
-                *reinterpret_cast<V64*>(wreg + fr * OROW + 2 * d0) = w;
+                if constexpr (F8O) {
+                    const float sc = inv * oqs;
+                    float a[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) a[i] = fminf(fmaxf(o[db][4 * g + i] * sc, -448.f), 448.f);
+                    int pk = __builtin_amdgcn_cvt_pk_fp8_f32(a[0], a[1], 0, false);
+                    pk = __builtin_amdgcn_cvt_pk_fp8_f32(a[2], a[3], pk, true);
+                    *reinterpret_cast<int*>(wreg + fr * OROW + d0) = pk;
+                } else {
+                    V64 w;
+                    w.x = (uint32_t)at_f2bf(o[db][4 * g + 0] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 1] * inv) << 16);
+                    w.y = (uint32_t)at_f2bf(o[db][4 * g + 2] * inv) | ((uint32_t)at_f2bf(o[db][4 * g + 3] * inv) << 16);
+                    *reinterpret_cast<V64*>(wreg + fr * OROW + 2 * d0) = w;
+                }
             }
-        constexpr int CPRO = D / 8;                          // 16-B chunks per head row
+        constexpr int CPRO = EB * D / 16;                    // 16-B chunks per head row
+        unsigned char* Ob = reinterpret_cast<unsigned char*>(O);
 #pragma unroll
         for (int j = 0; j < (32 * CPRO + 63) / 64; ++j) {
             const int c = lane + 64 * j;
@@ -993,7 +1010,7 @@ __global__ void __launch_bounds__(NW * 64, (NW == 3 || NW == 5) ? 3 : 1) k_attn2
             const int qr = q - fr + r;                         // this wave's row r
             const V128 val = *reinterpret_cast<const V128*>(wreg + r * OROW + 16 * col);
             const long long off = attn_out_offset(o_map, b, qr, sq, o_bs, o_rs);
-            if (qr < sq && off >= 0) *reinterpret_cast<V128*>(O + off + h * D + 8 * col) = val;
+            if (qr < sq && off >= 0) *reinterpret_cast<V128*>(Ob + EB * (off + h * D) + 16 * col) = val;
         }
         return;
     }
@@ -2415,8 +2432,14 @@ BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, v
                        dim3(576), 0, bf_stream(stream), (const u16*)q, (const u16*)k,               \
                        (const u16*)v, (u16*)o, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs,    \
                        o_bs, sl2, o_map, 1.f)
+#define LAUNCH_2L4(DD)                                                                            \
+    hipLaunchKernelGGL((k_attn2<DD, 4, false, false, false, false, false, true>),                  \
+                       dim3((sq + 127) / 128, heads, batch), dim3(256), 0, bf_stream(stream),       \
+                       (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, sq, sk, q_rs, k_rs,    \
+                       v_rs, o_rs, q_bs, k_bs, v_bs, o_bs, sl2, o_map, 1.f)
 #define LAUNCH_2D(DD)                                                                             \
     if (nw_one <= 2) { LAUNCH_2(DD, 2); }                                                          \
+    else if (!short_s && var == 6) { LAUNCH_2L4(DD); }                                             \
     else if (!short_s) { LAUNCH_2(DD, 4); }                                                        \
     else if (var == 7) { LAUNCH_2(DD, 5); }                                                        \
     else if (var == 8) { LAUNCH_2(DD, 3); }                                                        \
@@ -2431,6 +2454,7 @@ BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, v
         }
 #undef LAUNCH_2D
 #undef LAUNCH_2L
+#undef LAUNCH_2L4
 #undef LAUNCH_2
         return bf_check_launch();
     }
@@ -2505,6 +2529,13 @@ BF_API int bf_attention_fp8out(const void* q, const void* k, const void* v, void
                        (long long)sq * o_rs + 2LL * ((long long)sq * q_rs + (long long)sk * (k_rs > v_rs ? k_rs : v_rs)) < (1LL << 31);
     const int k6_grid = attn_num_cus() < batch * heads ? attn_num_cus() : batch * heads;
 #define LAUNCH_8(DD, NWV)                                                                         \
+    if (g_attn_variant == 6)                                                                      \
+        hipLaunchKernelGGL((k_attn2<DD, NWV, true, false, false, false, false, true>),             \
+                           dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch), dim3(NWV * 64), 0, \
+                           bf_stream(stream), (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, \
+                           sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs, o_bs, sl2,           \
+                           (const int32_t*)nullptr, out_qscale);                                  \
+    else                                                                                          \
     hipLaunchKernelGGL((k_attn2<DD, NWV, true>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch), \
                        dim3(NWV * 64), 0, bf_stream(stream), (const u16*)q, (const u16*)k,          \
                        (const u16*)v, (u16*)o, sq, sk, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs,    \

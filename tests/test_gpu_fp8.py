@@ -207,3 +207,10 @@ def test_attention_fp8_output(L, B, H, S, D):
     finally:
         L.lib().bf_attention_set_variant(6)
     assert torch.equal(o8.view(torch.uint8), o8b.view(torch.uint8))
+    # and == the per-lane fragment stores (variant 27)
+    L.lib().bf_attention_set_variant(27)
+    try:
+        L.attention_fp8out(q, k, v, o8b, B, H, S, S, D, D ** -0.5, qs)
+    finally:
+        L.lib().bf_attention_set_variant(6)
+    assert torch.equal(o8.view(torch.uint8), o8b.view(torch.uint8))

@@ -238,6 +238,32 @@ def test_attention_pingpong_equals_default(L, B, H, S, D):
     assert rel_err(outs[12], _attn_ref(q, k, v, B, H, S, D, D ** -0.5)) < 1e-2
 
 
+@pytest.mark.parametrize("B,H,S,D,scatter", [(9, 12, 512, 64, True), (2, 12, 1600, 64, False),
+                                               (2, 8, 302, 32, False), (3, 12, 320, 64, True),
+                                               (2, 4, 600, 80, True)])
+def test_attention_row_stores_equal_fragment_stores(L, B, H, S, D, scatter):
+    """the default epilogue (rows staged in LDS, stored as whole head rows; 4-wave workgroups reuse
+    the K ring after a barrier) writes exactly the rows of the per-lane fragment stores
+    (variant 27), also through an o_map row scatter with dropped rows (the CuTR window layout)"""
+    g = torch.Generator(device="cuda").manual_seed(B * S + D + 27)
+    qkv = torch.randn(B * S, 3 * H * D, device="cuda", generator=g).bfloat16()
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    om = None
+    if scatter:
+        perm = torch.randperm(B * S, device="cuda", generator=g).to(torch.int32)
+        om = torch.where(torch.arange(B * S, device="cuda") % 7 == 3, torch.full_like(perm, -1), perm)
+    outs = []
+    for var in (27, 6):
+        o = torch.full((B * S, H * D), float("nan"), device="cuda", dtype=torch.bfloat16)
+        L.lib().bf_attention_set_variant(var)
+        try:
+            L.attention(q, k, v, o, B, H, S, S, D, D ** -0.5, o_map=om)
+        finally:
+            L.lib().bf_attention_set_variant(6)
+        outs.append(o)
+    assert torch.equal(outs[1].nan_to_num(7.0), outs[0].nan_to_num(7.0))
+
+
 def test_attention_persistent_cu_budget(L):
     """the persistent short-head kernel (variant 26) sizes its grid by the CU budget of CU-masked
     streams (bf_gemm_set_cu_budget, rank 0 at N > 1): a 40-workgroup walk gives the same rows"""
