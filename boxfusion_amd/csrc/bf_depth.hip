@@ -476,6 +476,7 @@ __global__ void __launch_bounds__(DS_T) k_ds_norm(const float* __restrict__ dept
     float* o = out + (size_t)f * n;
     const float mean = params[2 * f], stdv = params[2 * f + 1];
     __shared__ float s_Ki[16], s_RT[16];
+    __shared__ float4 s_xyz[(DS_T / 64) * 192];
     const bool bp = xyz != nullptr;
     if (bp) {
         if (threadIdx.x == 0) {
@@ -500,16 +501,18 @@ __global__ void __launch_bounds__(DS_T) k_ds_norm(const float* __restrict__ dept
     for (int it = 0; it < KV; ++it) {
         const long long i0 = base + (long long)it * 4 * DS_T + 4 * threadIdx.x;
         const float x[4] = {v[it].x, v[it].y, v[it].z, v[it].w};
-        if (vec && i0 >= n) continue;
         if (vec) {
+            // lanes past the frame (x = 0) run along so the wave's staged xyz copy stays whole
+            const bool act = i0 < n;
+            if (!__any(act)) continue;                         // wave-uniform
             float y[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) y[e] = ((ds_valid(x[e]) ? x[e] : mean) - mean) / stdv;
-            *reinterpret_cast<float4*>(o + i0) = make_float4(y[0], y[1], y[2], y[3]);
+            if (act) *reinterpret_cast<float4*>(o + i0) = make_float4(y[0], y[1], y[2], y[3]);
             if (bp) {
                 float p[12];
                 unsigned vb = 0;
-                const int u0 = (int)(i0 % w), v0 = (int)(i0 / w);
+                const int u0 = (int)i0 % w, v0 = (int)i0 / w;       // (a frame is < 2^31 pixels)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     int u = u0 + e, vv = v0;
@@ -519,11 +522,21 @@ __global__ void __launch_bounds__(DS_T) k_ds_norm(const float* __restrict__ dept
                     if (max_depth > 0.f) ok = ok && (x[e] < max_depth);
                     vb |= (ok ? 1u : 0u) << (8 * e);
                 }
-                float4* xp = reinterpret_cast<float4*>(xo + 3 * i0);
-                xp[0] = make_float4(p[0], p[1], p[2], p[3]);
-                xp[1] = make_float4(p[4], p[5], p[6], p[7]);
-                xp[2] = make_float4(p[8], p[9], p[10], p[11]);
-                *reinterpret_cast<unsigned*>(vo + i0) = vb;
+                // xyz through a per-wave LDS region: the wave's 64 x 48 B leave as 3 float4 per lane
+                // along consecutive addresses (a lane's own 48 B at a 48-B stride would touch 3x
+                // the lines per store instruction)
+                float4* sw = s_xyz + (threadIdx.x >> 6) * 192;
+                const int ln = threadIdx.x & 63;
+                sw[3 * ln + 0] = make_float4(p[0], p[1], p[2], p[3]);
+                sw[3 * ln + 1] = make_float4(p[4], p[5], p[6], p[7]);
+                sw[3 * ln + 2] = make_float4(p[8], p[9], p[10], p[11]);
+                // from the wave's first pixel: the float4s of the pixels inside the frame
+                float4* xw = reinterpret_cast<float4*>(xo + 3 * (i0 - 4 * ln));
+                const long long lim4 = 3 * (n - (i0 - 4 * ln)) / 4;
+#pragma unroll
+                for (int k2 = 0; k2 < 3; ++k2)
+                    if (ln + 64 * k2 < lim4) xw[ln + 64 * k2] = sw[ln + 64 * k2];
+                if (act) *reinterpret_cast<unsigned*>(vo + i0) = vb;
             }
         } else {
 #pragma unroll

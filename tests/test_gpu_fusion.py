@@ -270,6 +270,27 @@ def test_backproject_vs_oracle(L):
     np.testing.assert_allclose(xyz.cpu().numpy(), rx, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("b,h,w", [(3, 480, 640), (2, 36, 64), (2, 37, 53), (5, 192, 256)])
+def test_depth_preprocess_backprojection_equals_backproject(L, b, h, w):
+    """bf_depth_preprocess's fused back-projection (xyz staged per wave in LDS, partial waves when
+    h*w is not a multiple of 256, the scalar path when it is not a multiple of 4) == bf_backproject
+    frame by frame, bit for bit; its standardisation == bf_depth_standardize"""
+    from boxfusion_amd.synthetic import SCANNET_K, Scene
+    g = torch.Generator(device="cuda").manual_seed(h * w + b)
+    d = torch.rand(b, h, w, device="cuda", generator=g) * 6.0
+    d[:, ::7, ::5] = 0.0
+    d[:, 1, :] = 11.0                                   # past max_depth
+    K = torch.tensor(SCANNET_K, device="cuda").expand(b, 3, 3).contiguous()
+    RT = torch.stack([torch.tensor(Scene().pose(f), device="cuda") for f in range(b)]).float()
+    out, params, xyz, valid = L.depth_preprocess(d, K, RT, 10.0)
+    o2, p2 = L.depth_standardize(d)
+    assert torch.equal(out, o2) and torch.equal(params, p2)
+    for f in range(b):
+        x1, v1 = L.backproject(d[f], K[f], RT[f], 10.0)
+        assert torch.equal(xyz[f], x1)
+        assert torch.equal(valid[f].to(torch.uint8), v1.to(torch.uint8))
+
+
 def _hexagon_views(n_views=3, twist_deg=14.0):
     """a box seen obliquely (projected hull = hexagon) in n views, each view's observed corners =
     the box's own projection twisted about its centroid: the intersection of the two hexagons has
