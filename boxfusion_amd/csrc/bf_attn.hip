@@ -2279,7 +2279,10 @@ static int launch_attn_p(hipStream_t st, const void* q, const void* k, const voi
     return bf_check_launch();
 }
 
-// 6 (default): k_attn2; 7 / 8: k_attn2 with two 5-wave / three 3-wave workgroups per short head;
+// 6 (default): k_attn2 with the LDS-staged whole-row output stores (27: the same kernel with the
+// per-lane fragment stores; 26: k_attn6, persistent; 16: k_attn4, one wave per SIMD with two query
+// blocks; 17 / 18: k_attn5, all K / V tiles resident by LDS-DMA; 12: k_attn2 PP, ping-pong tiles);
+// 7 / 8: k_attn2 with two 5-wave / three 3-wave workgroups per short head;
 // 1/2: k_attn_s (with / without the XCD block order), 3: k_attn_r for short sequences, 4/5:
 // k_attn_s with 5/3 waves per workgroup for short sequences, 0: k_attn.  Env BF_ATTN_VARIANT.
 // 9: k_attn_p (persistent, LDS-DMA ring 3 steps deep, next head's Q prefetched), 10: k_attn2 XQ
