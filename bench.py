@@ -118,8 +118,12 @@ def parse(argv=None):
                    help="Python thread switch interval in ms for the host threads (detect launcher vs "
                         "the fusion worker); <0: the interpreter default")
     p.add_argument("--dataset", choices=("scannet", "ca1m"), default="scannet",
-                   help="ca1m: BASELINE configs[1]'s stream shape -- 384x512 portrait frames, depth at 1/2 "
-                        "resolution (RGB:depth ratio 2), ca1m.yaml thresholds and gap 20")
+                   help="ca1m: BASELINE configs[1]'s stream as CA1MDataset delivers it -- 384x512 portrait "
+                        "frames with the depth resized to the image (RGB:depth ratio 1, "
+                        "capture_stream.py:445-459), ca1m.yaml thresholds and gap 20")
+    p.add_argument("--depth-ratio", type=int, default=1, choices=(1, 2, 4),
+                   help="RGB:depth resolution ratio of the stream (--dataset ca1m: 2 / 4 = a lower-"
+                        "resolution depth sensor through the CuTR depth grid; not what CA1MDataset streams)")
     p.add_argument("--cpu-rehearsal", action="store_true",
                    help="CPU/gloo rehearsal of the N-rank control flow (no kernels; test harness)")
     return p.parse_args(argv)
@@ -303,16 +307,18 @@ def exchange_step(recs, clip, dist, N, B, B0, crops, rank):
 
 # ------------------------------------------------------------------------------------------------
 def cpu_baseline(cutr, clip_vis, args, scene):
-    """The parity-checked CPU restatement timed on this host, both SURVEY §8(d) configs:
+    """The parity-checked CPU restatement timed on this host on the bench's own frame geometry
+    (FRAME: 640x480 ScanNet, or the CA-1M 384x512 portrait stream at its RGB:depth ratio) and CFG:
       per frame  depth standardisation + back-projection (oracle C), RGB normalise + pad
       keyframe   fp32 torch-CPU CuTR + CLIP on `crops` scene-detection crops (cpu_detect_frames
                  frames timed) + the oracle fusion chain (oracle/chain.py)
-    gap=1: every frame a keyframe; gap=25: one keyframe per 25 frames (fusion chain timed on
-    keyframes 0, 25, 50, ...)."""
+    Rates: every frame a keyframe (gap 1) and the stream's keyframe rule (gap 25 for ScanNet,
+    ca1m.yaml's 20 for CA-1M; fusion chain timed on keyframes 0, g, 2g, ...); `value` is the rate
+    at the bench's own --gap."""
     from oracle.chain import OracleChain
     from boxfusion_amd.box_fusion import load_pst
     from boxfusion_amd.cubify_transformer import FrameBatch
-    from boxfusion_amd.preprocessor import PIXEL_MEAN, PIXEL_STD
+    from boxfusion_amd.preprocessor import PIXEL_MEAN, PIXEL_STD, square_pad_size
     from boxfusion_amd.sensor import camera_to_gravity
     from boxfusion_amd.synthetic import SCANNET_K, frame_rgbd
     from boxfusion_amd.clip import CLIP_MEAN, CLIP_STD
@@ -321,6 +327,11 @@ def cpu_baseline(cutr, clip_vis, args, scene):
     cores = len(os.sched_getaffinity(0))
     cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
     torch.set_num_threads(cores)
+    H, W, r = FRAME["H"], FRAME["W"], FRAME["r"]
+    K = SCANNET_K if FRAME["K"] is None else FRAME["K"]
+    Kd = K.copy()
+    Kd[:2] /= r
+    pad = square_pad_size(H, W)
     cm = copy.deepcopy(cutr).float().cpu().eval()
     vm = copy.deepcopy(clip_vis).float().cpu().eval()
     nf = args.cpu_detect_frames
@@ -328,26 +339,27 @@ def cpu_baseline(cutr, clip_vis, args, scene):
     t_pre = t_model = 0.0
     with torch.no_grad():
         for f in range(nf):
-            rgb, depth = frame_rgbd(f)
+            rgb, depth = frame_rgbd(f, H, W)
+            depth = np.ascontiguousarray(depth[::r, ::r])
             t0 = time.perf_counter()
             mean = torch.tensor(PIXEL_MEAN).view(3, 1, 1)
             std = torch.tensor(PIXEL_STD).view(3, 1, 1)
             img = (torch.from_numpy(np.moveaxis(rgb, -1, 0)).float() - mean) / std
-            img = F.pad(img, (0, 0, 0, 160))[None]
+            img = F.pad(img, (0, pad - W, 0, pad - H))[None]
             d, params = OR.depth_standardize(depth)
-            OR.backproject(depth, SCANNET_K, scene.pose(f))
-            d = F.pad(torch.from_numpy(d), (0, 0, 0, 160))[None]
+            OR.backproject(depth, Kd, scene.pose(f))
+            d = F.pad(torch.from_numpy(d), (0, pad // r - d.shape[1], 0, pad // r - d.shape[0]))[None]
             t1 = time.perf_counter()
             batch = FrameBatch(image=img, depth=d, depth_params=torch.from_numpy(params)[None],
-                               K=torch.from_numpy(SCANNET_K)[None],
+                               K=torch.from_numpy(K)[None],
                                T_gravity=torch.from_numpy(camera_to_gravity(scene.pose(f)))[None],
-                               image_sizes=[(480, 640)])
+                               image_sizes=[(H, W)])
             cm(batch)
             crops = []
-            for x1, y1, x2, y2 in crop_boxes([scene.detections(f)], args.crops):
+            for x1, y1, x2, y2 in crop_boxes([scene.detections(f, K, (W, H))], args.crops):
                 cx, cy, w, h = (x1 + x2) / 2, (y1 + y2) / 2, (x2 - x1) * sb, (y2 - y1) * sb
-                x1, x2 = int(np.clip(cx - w / 2, 0, 640)), int(np.clip(cx + w / 2, 0, 640))
-                y1, y2 = int(np.clip(cy - h / 2, 0, 480)), int(np.clip(cy + h / 2, 0, 480))
+                x1, x2 = int(np.clip(cx - w / 2, 0, W)), int(np.clip(cx + w / 2, 0, W))
+                y1, y2 = int(np.clip(cy - h / 2, 0, H)), int(np.clip(cy + h / 2, 0, H))
                 c = torch.from_numpy(rgb[y1:y2, x1:x2]).permute(2, 0, 1).float()[None]
                 c = F.interpolate(c, (224, 224), mode="bilinear", align_corners=False) if c.numel() \
                     else torch.zeros((1, 3, 224, 224))
@@ -358,23 +370,25 @@ def cpu_baseline(cutr, clip_vis, args, scene):
             t_pre += t1 - t0
             t_model += time.perf_counter() - t1
     t_pre, t_model = t_pre / nf, t_model / nf
+    g_ref = 20 if CFG["dataset"] == "CA1M" else 25
     fuse = {}
-    for gap in (1, 25):
-        ch = OracleChain(CFG, SCANNET_K, pst=load_pst(), legacy=True)
+    for gap in sorted({1, g_ref, max(1, args.gap)}):
+        ch = OracleChain(CFG, K, H=H, W=W, pst=load_pst(), legacy=True)
         t0 = time.perf_counter()
         for k in range(args.cpu_fusion_frames):
             f = k * gap
-            ch.keyframe(f, scene.pose(f), scene.detections(f))
+            ch.keyframe(f, scene.pose(f), scene.detections(f, K, (W, H)))
         fuse[gap] = (time.perf_counter() - t0) / args.cpu_fusion_frames
-    v1 = 1.0 / (t_pre + t_model + fuse[1])
-    v25 = 25.0 / (25.0 * t_pre + t_model + fuse[25])
-    return {"value": v1, "unit": "frames/s", "cores": cores, "kind": "port", "gap25_value": v25,
-            "sample": (f"{nf} frame(s) of fp32 torch-CPU CuTR ViT-B + {args.crops} CLIP ViT-H/14 "
-                       f"crops ({t_model:.2f} s/keyframe), per-frame depth standardisation + "
-                       f"back-projection + normalise ({1e3 * t_pre:.1f} ms/frame), oracle fusion "
-                       f"chain over {args.cpu_fusion_frames} keyframes ({1e3 * fuse[1]:.1f} ms/keyframe "
-                       f"at gap 1, {1e3 * fuse[25]:.1f} at gap 25); value = gap 1, gap25_value = "
-                       f"25 frames per keyframe")}
+    rate = lambda g: g / (g * t_pre + t_model + fuse[g])
+    out = {"value": rate(max(1, args.gap)), "unit": "frames/s", "cores": cores, "kind": "port",
+           "gap": max(1, args.gap), "gap1_value": rate(1), f"gap{g_ref}_value": rate(g_ref),
+           "sample": (f"{nf} frame(s) of fp32 torch-CPU CuTR ViT-{ {768: 'B', 384: 'S', 192: 'T'}.get(args.dim, args.dim)} "
+                      f"on {W}x{H} RGB (depth 1/{r}) + {args.crops} CLIP ViT-H/14 crops ({t_model:.2f} "
+                      f"s/keyframe), per-frame depth standardisation + back-projection + normalise "
+                      f"({1e3 * t_pre:.1f} ms/frame), oracle fusion chain over {args.cpu_fusion_frames} "
+                      f"keyframes ({', '.join(f'{1e3 * v:.1f} ms/keyframe at gap {g}' for g, v in fuse.items())}); "
+                      f"value = the bench's gap {max(1, args.gap)} (keyframe every gap-th frame)")}
+    return out
 
 
 def load_pmc_traffic(kernel):
@@ -513,8 +527,9 @@ def main(argv=None):
     args = parse(argv)
     if args.dataset == "ca1m":
         # ca1m.yaml (config/ca1m.yaml): cam 384 x 512 (portrait after BoxFusion's H/W swap), gap 20,
-        # score 0.4, small_threshold 0.2; the synthetic CA-1M frame geometry of the CuTR goldens
-        FRAME.update(H=512, W=384, r=2, K=CA1M_K)
+        # score 0.4, small_threshold 0.2, small_size 0.5; CA1MDataset resizes the depth to the image
+        # (ratio 1); the synthetic CA-1M frame geometry of the CuTR goldens
+        FRAME.update(H=512, W=384, r=args.depth_ratio, K=CA1M_K)
         CFG.update(dataset="CA1M", cam=dict(H=384, W=512, png_depth_scale=1000.0))
         CFG["detection"].update(score_thresh=0.4)
         CFG["association"].update(small_threshold=0.2)
@@ -835,11 +850,12 @@ def main(argv=None):
                 poses_all[args.warmup * Bm:(args.warmup + 1) * Bm]).to(dev)
             gst = torch.cuda.Stream(dev)
             gst.wait_stream(torch.cuda.current_stream(dev))
+            g_ws = _lib.new_depth_workspace(*dsrc.shape, dev)       # the graph's own workspace
             with torch.cuda.stream(gst):
-                _lib.depth_preprocess(dsrc, dK, dRT, 10.0)          # workspace / outputs for this stream
+                _lib.depth_preprocess(dsrc, dK, dRT, 10.0, ws=g_ws)
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph, stream=gst):
-                    _lib.depth_preprocess(dsrc, dK, dRT, 10.0)
+                    _lib.depth_preprocess(dsrc, dK, dRT, 10.0, ws=g_ws)
                 for _ in range(3):
                     graph.replay()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -871,12 +887,17 @@ def main(argv=None):
         if B0 < B:
             line["config"]["rank0_batch"] = B0
         if args.dataset == "ca1m":
-            line["metric"] = "RGB-D frames/sec (whole node) on 384x512 portrait stream, depth at 1/2 resolution"
+            r_ = FRAME["r"]
+            line["metric"] = ("RGB-D frames/sec (whole node) on 384x512 portrait stream, depth at the image size"
+                              if r_ == 1 else
+                              f"RGB-D frames/sec (whole node) on 384x512 portrait stream, depth at 1/{r_} resolution")
             line["data"] = ("synthetic CA-1M-shaped RGB-D stream (seeded; CA-1M data absent offline), random-init "
                             "weights, seeded scene detections")
             line["config"]["workload"] = line["config"]["workload"].replace(
                 "configs[2]: synthetic 640x480 RGB-D", "configs[1]: CA-1M-shaped 384x512 portrait RGB-D, "
-                "depth 192x256 (RGB:depth 2), ca1m.yaml thresholds")
+                f"depth {384 // r_}x{512 // r_} (RGB:depth {r_}{', as CA1MDataset streams it' if r_ == 1 else ''}), "
+                "ca1m.yaml thresholds")
+            line["config"]["depth_ratio"] = r_
         if G > 1:
             line["config"]["workload"] = line["config"]["workload"].replace(
                 "gap=1", f"gap={G} (demo.py keyframe rule: {B} keyframes + {(G - 1) * B} non-keyframe "
@@ -900,7 +921,7 @@ def main(argv=None):
         line["roofline_components"] = comps
         if args.breakdown:
             line["breakdown_ms_per_step"] = {k: 1e3 * v / args.steps for k, v in brk.items()}
-        if not args.no_cpu_baseline and N == 1 and args.dataset == "scannet":   # rank 0 at N=1 only
+        if not args.no_cpu_baseline and N == 1:   # rank 0 at N=1 only
             line["cpu_baseline"] = (cpu_baseline(cutr, clip_vis, args, scene) if args.cpu_detect_frames > 0 else None)
         emit(line)
     if dist is not None:

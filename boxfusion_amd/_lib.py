@@ -486,8 +486,10 @@ _DS_WS = {}
 
 def depth_workspace(b, h, w, device):
     """zero-filled workspace of bf_depth_standardize / bf_depth_preprocess, one per (device,
-    stream, shape): the kernels leave it zeroed, so it is reused as is.  Graph captures keep
-    their own (the captured kernels own its address)."""
+    stream, shape): the kernels leave it zeroed, so it is reused as is by stream-ordered calls.
+    Not for graph captures: a captured launch keeps the address, so replays on another stream
+    would race the eager users of the cached buffer -- depth_preprocess therefore requires an
+    explicit caller-owned `ws` (new_depth_workspace) while the current stream is capturing."""
     dev = torch.device(device)
     stream = torch.cuda.current_stream(dev).cuda_stream
     key = (dev.index, stream, b, h, w)
@@ -525,6 +527,9 @@ def depth_preprocess(depth, K=None, RT=None, max_depth=10.0, out=None, params=No
         xyz = torch.empty((b, h, w, 3), dtype=torch.float32, device=depth.device) if xyz is None else xyz
         valid = torch.empty((b, h, w), dtype=torch.uint8, device=depth.device) if valid is None else valid
     if ws is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise HipError("bf_depth_preprocess under graph capture needs a caller-owned ws "
+                           "(new_depth_workspace): the per-stream cached workspace is shared")
         ws = depth_workspace(b, h, w, depth.device)
     _check(lib().bf_depth_preprocess(_ptr(depth), c_int(b), c_int(h), c_int(w), _ptr(out), _ptr(params),
                                      _ptr(K) if bp else None, _ptr(RT) if bp else None,
@@ -1034,7 +1039,8 @@ def depth_preprocess(depth, K=None, RT=None, max_depth=10.0, out=None, params=No
     if K is not None:
         xyz = torch.empty((b, h, w, 3), dtype=torch.float32, device=depth.device) if xyz is None else xyz
         valid = torch.empty((b, h, w), dtype=torch.uint8, device=depth.device) if valid is None else valid
-    ws = depth_workspace(b, h, w, depth.device) if ws is None else ws
+    if ws is None and not torch.cuda.is_current_stream_capturing():
+        ws = depth_workspace(b, h, w, depth.device)
     fn = lambda: _depth_preprocess_untimed(depth, K, RT, max_depth, out, params, xyz, valid, ws)
     n = float(b * h * w)
     # algorithmic bytes: read the depth once, write the standardised map (+ xyz and

@@ -33,6 +33,10 @@ from boxfusion_amd.box_fusion import BoxFusion, _warn_hull_once
 from boxfusion_amd.box_manager import BoxManager
 from boxfusion_amd.instances import Instances3D
 
+# last_pred marker of a keyframe without detections: demo.py:206-212 still runs on the last-frame
+# re-entry with an empty pred_instances and records num_record[count] (None = no keyframe yet)
+EMPTY_KEYFRAME = "empty keyframe"
+
 
 class FusionStage:
     """`native` (default: env BF_NATIVE_FUSION, on): the keyframe sequence after the per-box
@@ -214,6 +218,10 @@ class FusionStage:
             preds.project_3d_boxes(self.K_dev, H=self.H, W=self.W)
         if self._select_mode() == "native":
             self._native_batch(counts, poses, preds if n_tot else None, sizes)
+            # the batch's row gathers flag BF_DEV_INDEX_RANGE in the status word (one read per
+            # batch; the sequencer has already waited on the device)
+            if n_tot:
+                _lib.check_status(self.dev)
             return
         off = 0
         for j, c in enumerate(counts):
@@ -248,7 +256,7 @@ class FusionStage:
                 bm.last_fusion_frame.extend([0] for _ in range(n))
                 self._last_pred = (preds, off, n)
             else:
-                self._last_pred = None
+                self._last_pred = EMPTY_KEYFRAME
             bm.num_record[c] = self.box_count
             off += n
 
@@ -268,6 +276,7 @@ class FusionStage:
         n = len(pred) if pred is not None and len(pred._fields) else 0
         pose_np = np.repeat(pose[None], n, 0)
         if n == 0:
+            self._last_pred = EMPTY_KEYFRAME
             bm.num_record[count] = self.box_count
             return
         self._stats["keyframes"] += 1
@@ -387,7 +396,12 @@ class FusionStage:
 
     def finish(self, count, pose, last_was_keyframe):
         """demo.py:200 `count == len(dataset) - 1` re-entry on a non-keyframe last frame."""
-        if last_was_keyframe or not self.stale_last_frame or self.last_pred is None:
+        if last_was_keyframe or not self.stale_last_frame or self._last_pred is None:
+            return
+        if self._last_pred is EMPTY_KEYFRAME:
+            # demo.py:202-212: the re-entry with an empty pred_instances records the count only
+            self.all_kf_pose[count] = np.asarray(pose, np.float32)
+            self._bm.num_record[count] = self.box_count
             return
         if self._mode == "native" and self._stats["keyframes"] == 1:
             # one keyframe so far: the reference's all_pred_box and per_frame_ins ARE that

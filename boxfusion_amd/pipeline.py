@@ -186,6 +186,7 @@ class DetectStage:
         -- one bf_depth_preprocess pass over any number of frames.  Nothing reads the results
         back (in the reference they feed rerun only); they stay in self.last_frames."""
         n = depth.shape[0]
+        self.last_frames = None          # release the previous call's outputs before allocating
         if self.backproject:
             RT = torch.from_numpy(np.ascontiguousarray(poses, np.float32)).to(self.dev, non_blocking=True)
             self.last_frames = _lib.depth_preprocess(depth, self.Kd_dev[:1].expand(n, 3, 3), RT, 10.0)
@@ -279,6 +280,7 @@ class Pipeline:
         self.frames_preprocessed = 0
         for s in range(0, len(kf), B):
             ids = kf[s:s + B]
+            nk_pose = {}           # non-keyframe poses of this batch, logged in frame order below
             if per_frame:
                 nk = [i for i in range(ids[0], min(ids[-1] + self.gap, n_frames)) if i % self.gap != 0]
                 for c in range(0, len(nk), frames_per_call):
@@ -286,8 +288,7 @@ class Pipeline:
                     self.detect.preprocess_frames(depth.contiguous(), poses)
                     self.frames_preprocessed += len(nk[c:c + frames_per_call])
                     if viz is not None:
-                        for j, i in enumerate(nk[c:c + frames_per_call]):
-                            viz.frame(i, poses[j])
+                        nk_pose.update(zip(nk[c:c + frames_per_call], np.asarray(poses)))
             rgb, depth, poses = frames(ids)
             if len(ids) < B:   # ragged tail: pad the batch with the last frame, drop its results
                 pad = B - len(ids)
@@ -298,8 +299,13 @@ class Pipeline:
             for j, i in enumerate(ids):
                 self.fusion.keyframe(i, poses[j], preds[j])
                 if viz is not None:
+                    # demo.py order: keyframe i's frame logs, its boxes after the fusion step, then
+                    # the frames up to the next keyframe (the trajectory grows frame by frame)
                     viz.frame(i, poses[j])
                     viz.boxes(self.fusion.all_pred_box, i)
+                    for f in range(i + 1, min(i + self.gap, n_frames)):
+                        if f in nk_pose:
+                            viz.frame(f, nk_pose[f])
         last = n_frames - 1
         if last % self.gap != 0:
             _, _, p = frames([last])

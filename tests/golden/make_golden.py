@@ -254,15 +254,33 @@ def make_instances(det, H=480, W=640):
     return p
 
 
-def gen_trace(n_keyframes=14, frame_step=25, seed=3, period=400, **scene_kw):
-    cfg = SCANNET_CFG
+def gen_trace(n_keyframes=14, frame_step=25, seed=3, period=400, cfg=None, K=SCANNET_K, H=480, W=640,
+              **scene_kw):
+    """the seeded scene's keyframes (every frame_step-th frame) through run_trace"""
     scene = Scene(seed=seed, period=period, **scene_kw)
-    STUB_STATE["cfg"] = OR.fuse_cfg(cfg, np.eye(4), 480, 640, legacy=False)
-    with quiet():
-        box_manager = BoxManager(cfg)
-        fuser = BoxFusion(cfg)
-    fuser.update_intrinsics((640, 480), SCANNET_K)
-    H, W = 480, 640
+    src = [(k * frame_step, scene.pose(k * frame_step), scene.detections(k * frame_step, K, (W, H)))
+           for k in range(n_keyframes)]
+    return run_trace(src, cfg or SCANNET_CFG, K, H, W)
+
+
+def run_trace(src, cfg, K, H, W):
+    """demo.py:200-305 on the reference's own objects over the keyframes `src` = [(frame, pose,
+    camera-frame detections)], recording every intermediate state.  The trace carries the config
+    it ran with (cfg_json, K, H, W) so a replay can rebuild the same thresholds."""
+    import json
+    import tempfile
+    K = np.asarray(K, np.float32)
+    STUB_STATE["cfg"] = OR.fuse_cfg(cfg, np.eye(4), H, W, legacy=False)
+    with tempfile.TemporaryDirectory() as tmp:
+        if "scannet" not in cfg["data"]["datadir"].lower():
+            # the CA-1M branch of BoxFusion.__init__ reads <datadir>/K_depth.txt (box_fusion.py:44-51)
+            cfg = dict(cfg, data=dict(cfg["data"], datadir=tmp))
+            np.savetxt(os.path.join(tmp, "K_depth.txt"), K.reshape(-1))
+        with quiet():
+            box_manager = BoxManager(cfg)
+            fuser = BoxFusion(cfg)
+    # demo.py:117-118: the image size (W, H) and K of the stream, every frame
+    fuser.update_intrinsics((W, H), K)
     all_pred_box = None
     all_poses = None
     per_frame_ins = None
@@ -279,12 +297,9 @@ def gen_trace(n_keyframes=14, frame_step=25, seed=3, period=400, **scene_kw):
     # behaviour in the reference; the trace holds the exact-hull result there)
     hull_over = []
     OR.hull_overflow()
-    for k in range(n_keyframes):
-        frame = k * frame_step
-        det = scene.detections(frame)
-        pose = scene.pose(frame)
+    for frame, pose, det in src:
         dets.append(det)
-        pred = make_instances(det)
+        pred = make_instances(det, H, W)
         n = len(pred)
         all_kf_pose[frame] = pose
         pose_np = np.repeat(pose[None], n, 0)
@@ -293,7 +308,7 @@ def gen_trace(n_keyframes=14, frame_step=25, seed=3, period=400, **scene_kw):
         pred.init_id = box_count + torch.arange(n)
         pred.valid_num = torch.zeros(n)
         pred.pred_boxes_3d.transform2world(pred.cam_pose)
-        pred.project_3d_boxes(SCANNET_K, H=H, W=W)
+        pred.project_3d_boxes(K, H=H, W=W)
         box_count += n
         rec["frame"].append(frame)
         rec["pose"].append(pose)
@@ -345,7 +360,7 @@ def gen_trace(n_keyframes=14, frame_step=25, seed=3, period=400, **scene_kw):
             with quiet():
                 all_pred_box, all_poses, keep_idx = Instances3D.correspondence_association(
                     cfg, box_manager, cur_keep_idx, cur_success, pred, cur_global, all_pred_box,
-                    all_poses, per_frame_ins.cam_pose, frame, mask, torch.from_numpy(SCANNET_K),
+                    all_poses, per_frame_ins.cam_pose, frame, mask, torch.from_numpy(K),
                     all_kf_pose, threshold=cfg["association"]["small_threshold"], H=H, W=W)
             rec["corr_keep"].append(np.asarray(keep_idx, np.int32))
             rec["corr_valid_num"].append(None)
@@ -367,6 +382,8 @@ def gen_trace(n_keyframes=14, frame_step=25, seed=3, period=400, **scene_kw):
         hull_over.append(OR.hull_overflow())
 
     out = {}
+    out["cfg_json"] = np.array(json.dumps({k: v for k, v in cfg.items() if k != "data"}))
+    out["K"], out["H"], out["W"] = K, np.int32(H), np.int32(W)
     out["hull_over"] = np.asarray([(0, 0)] + hull_over, np.int64)   # keyframe 0 runs no fusion
     # per-frame (cumulative) arrays as the reference left them
     out["pf_tensor"] = per_frame_ins.pred_boxes_3d.tensor.numpy()
@@ -398,6 +415,107 @@ def gen_trace(n_keyframes=14, frame_step=25, seed=3, period=400, **scene_kw):
         f, o = ragged(flat_rows)
         out[key + "_flat"], out[key + "_rowoff"] = f, o
         out[key + "_nrows"] = lens
+    return out
+
+
+CA1M_K = np.array([[360.0, 0.0, 191.5], [0.0, 360.0, 255.5], [0.0, 0.0, 1.0]], np.float32)
+CA1M_CFG = dict(   # config/ca1m.yaml (the stream's image is 384 wide x 512 tall after the H/W swap)
+    dataset="CA1M",
+    data=dict(datadir="/synthetic/ca1m", gap=20),
+    cam=dict(H=384, W=512, png_depth_scale=1000.0),
+    detection=dict(score_thresh=0.4, uv_bound=True, uv_bound_value=0.9, floor_mask=True,
+                   floor_ratio=15, scale_box=1.5),
+    association=dict(small_threshold=0.2, rotation_gap=30, translation_gap=0.8),
+    box_fusion=dict(use=True, iters=20, pst_path=os.path.join(REF, "data/pst_1024_0.tiff"),
+                    pst_size=1024, check_valid=False, nms_threshold=0.1, small_size=0.5,
+                    random_opt=dict(center_init_size=0.1, center_scaling_coefficient=0.1,
+                                    shape_init_size=0.5, shape_scaling_coefficient=0.5)),
+)
+
+
+def _faceon_det(rng, objs, P, K, W, H, noise=1.0):
+    """camera-frame detections (CuTR layout) of world boxes objs = [(centre, lhw, yaw, score,
+    depth_offset)] seen from pose P; depth_offset moves the detected centre along the viewing ray"""
+    from boxfusion_amd.synthetic import box_corners_np, rot_z, _A
+    P = P.astype(np.float64)
+    Rc, tc = P[:3, :3], P[:3, 3]
+    out = dict(scores=[], pred_boxes=[], xyzlhw=[], R=[], proj_xy=[])
+    for c, lhw, yaw, score, dz in objs:
+        xyz = Rc.T @ (np.asarray(c) - tc)
+        xyz = xyz * (1.0 + dz / np.linalg.norm(xyz)) + rng.normal(0, 0.01 * noise, 3)
+        d = np.asarray(lhw) * (1.0 + rng.normal(0, 0.02 * noise, 3))
+        Rcam = Rc.T @ (rot_z(yaw + rng.normal(0, np.deg2rad(0.5))) @ _A)
+        cc = box_corners_np(np.concatenate([xyz, d]), Rcam)
+        assert (cc[:, 2] > 0.3).all()
+        uu = np.clip(K[0, 0] * cc[:, 0] / cc[:, 2] + K[0, 2], 0, W)
+        vv = np.clip(K[1, 1] * cc[:, 1] / cc[:, 2] + K[1, 2], 0, H)
+        out["scores"].append(score)
+        out["pred_boxes"].append([uu.min(), vv.min(), uu.max(), vv.max()])
+        out["xyzlhw"].append(np.concatenate([xyz, d]))
+        out["R"].append(Rcam)
+        out["proj_xy"].append([K[0, 0] * xyz[0] / xyz[2] + K[0, 2], K[1, 1] * xyz[1] / xyz[2] + K[1, 2]])
+    n = len(out["scores"])
+    return dict(scores=np.asarray(out["scores"], np.float32).reshape(n),
+                pred_boxes=np.asarray(out["pred_boxes"], np.float32).reshape(n, 4),
+                xyzlhw=np.asarray(out["xyzlhw"], np.float32).reshape(n, 6),
+                R=np.asarray(out["R"], np.float32).reshape(n, 3, 3),
+                proj_xy=np.asarray(out["proj_xy"], np.float32).reshape(n, 2))
+
+
+def gen_faceon_trace(n_obj=4, n_views=5, seed=13):
+    """The whole keyframe chain pinned to the reference with NO buffer overrun (quirk 13), over
+    n_obj * n_views keyframes.  Keyframe k looks straight at a large face of object k % n_obj
+    (view k // n_obj: the front face from 2.4 / 3.3 / 4.2 m, then the back face -- baselines
+    > 0.8 m or 180 degrees apart, so every revisit joins the object's fusion list and lists of 3, 4
+    and 5 views are fused in turn), from inside the box's slabs like gen_faceon, so every
+    projected hull is the face quadrilateral.  Two small objects (max dim < small_size) show up in
+    two keyframes each (1 and 5, 2 and 6), the second time with the detected centre 0.6 m further
+    along the ray: 3-D IoU 0 with the first sighting, so NMS keeps both and correspondence_association pairs them by
+    their 2-D boxes.  Some keyframes carry a second, lower-scored detection of the object from
+    the same camera (suppressed by NMS without joining the list), and every keyframe a never-seen
+    object, which NMS keeps, so that the keyframe reaches correspondence and boxfusion.  Asserted: no fitness
+    evaluation of any keyframe overruns the reference kernel's buffers."""
+    from boxfusion_amd.synthetic import look_at_pose, rot_z, _A
+    rng = np.random.default_rng(seed)
+    K = SCANNET_K.astype(np.float32)
+    objs = []
+    for j in range(n_obj):
+        a = 2 * np.pi * j / n_obj
+        c = np.array([6.0 * np.cos(a), 6.0 * np.sin(a), rng.uniform(1.0, 1.3)])
+        lhw = np.array([rng.uniform(1.3, 1.7), rng.uniform(1.1, 1.3), rng.uniform(0.4, 0.8)])
+        objs.append((c, lhw, rng.uniform(-np.pi, np.pi)))
+    dists = [2.4, 3.3, 4.2, 2.6, 3.6]
+    src, small = [], {}
+    for k in range(n_obj * n_views):
+        j, v = k % n_obj, k // n_obj
+        c, lhw, yaw = objs[j]
+        R = rot_z(yaw) @ _A
+        lat, nrm = R[:, 0], R[:, 2]
+        side = 1.0 if v < 3 else -1.0                     # front face, then the back face
+        d = dists[v] + lhw[2] / 2
+        eye = (c - side * d * nrm + rng.uniform(-0.06, 0.06) * lat
+               + np.array([0, 0, rng.uniform(-0.05, 0.05)]))
+        P = look_at_pose(eye, eye + side * nrm)
+        seen = [(c, lhw, yaw, np.float32(rng.uniform(0.6, 0.95)), 0.0)]
+        if k % 3 == 1:                                   # duplicate of the object, same camera
+            seen.append((c, lhw, yaw, np.float32(seen[0][3] * rng.uniform(0.7, 0.95)), 0.0))
+        # a never-seen object in front of the camera (max dim > small_size, no correspondence):
+        # NMS keeps it, so the keyframe runs correspondence + boxfusion (demo.py:243-299); its own
+        # list never reaches 3 views
+        off = (0.5 if k % 2 else -0.5) * lat + np.array([0, 0, -0.3])
+        seen.append((eye + 1.6 * side * nrm + off, np.array([0.45, 0.5, 0.42]), yaw + 0.5,
+                     np.float32(rng.uniform(0.45, 0.9)), 0.0))
+        if k in (1, 2, 5, 6):
+            # small objects 0 / 1 beside objects 1 / 2: first seen in keyframes 1 / 2 (view 0),
+            # then from view 1 of the same object (0.9 m further back), 0.6 m deeper along the ray
+            s_ = k % 4 - 1
+            if v == 0:
+                small[s_] = eye + 1.8 * side * nrm + (0.45 if s_ == 0 else -0.45) * lat - np.array([0, 0, 0.25])
+            seen.append((small[s_], np.array([0.25, 0.22, 0.2]), yaw, np.float32(rng.uniform(0.5, 0.9)),
+                         0.6 if v else 0.0))
+        src.append((k * 10, P, _faceon_det(rng, seen, P, K, 640, 480)))
+    out = run_trace(src, SCANNET_CFG, K, 480, 640)
+    assert not out["hull_over"].any(), out["hull_over"]
     return out
 
 
@@ -474,8 +592,17 @@ def gen_faceon(n_obj=8, seed=11):
 
 def main():
     torch.set_num_threads(8)
-    if sys.argv[1:] == ["faceon"]:
+    only = sys.argv[1:]
+    if only == ["faceon"]:
         np.savez_compressed(os.path.join(HERE, "fusion_faceon.npz"), **gen_faceon())
+        return
+    if only == ["traces"]:     # the multi-keyframe traces added in round 4
+        np.savez_compressed(os.path.join(HERE, "fusion_trace_ca1m.npz"),
+                            **gen_trace(n_keyframes=14, frame_step=20, seed=7, period=280, cfg=CA1M_CFG,
+                                        K=CA1M_K, H=512, W=384))
+        print("CA-1M trace done")
+        np.savez_compressed(os.path.join(HERE, "fusion_trace_faceon.npz"), **gen_faceon_trace())
+        print("face-on trace done")
         return
     np.savez_compressed(os.path.join(HERE, "obb_pairs.npz"), **gen_obb_pairs())
     print("obb_pairs done")

@@ -3,7 +3,7 @@ preprocessor.py) on a synthetic 640x480 RGB-D frame with seeded synthetic weight
 boxfusion_amd/weights.py) and record inputs, backbone features and the final instances.
 
 Stand-ins only for absent third-party modules: timm.layers.Mlp (fc1 -> GELU -> fc2, the pinned
-timm 1.0.19 layout) plus the stubs of make_golden.py.  Run: python tests/golden/make_golden_cutr.py
+timm 1.0.19 layout) plus the stubs of make_golden.py.  Run: python tests/golden/make_golden_cutr.py [case.npz ...]
 """
 import os
 import sys
@@ -154,8 +154,34 @@ def run_case(name, dim, frame, seed, H, W, ratio, K, thr, keep_features=False):
     # uniform_queries): the end-to-end GPU test compares these instances one by one
     model_u = make_cubify_transformer(dimension=dim, depth_model=True).eval()
     model_u.load_state_dict(seeded_state_dict(model_u, seed, uniform_queries=True))
-    with torch.no_grad():
-        pu = model_u(packaged)[0]
+    # the encoder's proposal logits (EncoderProposals.get_proposals, cubify_transformer.py:918-943):
+    # query slot q of the decoder is the proposal of top-300 rank q, so an instance whose proposal
+    # sits at the top-300 cut can trade places with the 301st under bf16 rounding
+    from boxfusion.cubify_transformer import EncoderProposals
+    seen = {}
+    orig_gp, orig_inf = EncoderProposals.get_proposals, EncoderProposals.inference_single_image
+
+    def get_proposals(self, *a, **k):
+        enc, inst = orig_gp(self, *a, **k)
+        seen["logits"] = enc[0].pred_logits[..., 0].detach().clone()
+        return enc, inst
+
+    def inference_single_image(self, output, image_size, topk):
+        # the query slot of every instance (the reference takes rows topk_index // 2)
+        idx = torch.topk(output.pred_logits.sigmoid().view(-1), topk)[1]
+        seen["query"] = (idx // output.pred_logits.shape[-1]).clone()
+        return orig_inf(self, output, image_size, topk)
+    EncoderProposals.get_proposals = get_proposals
+    EncoderProposals.inference_single_image = inference_single_image
+    try:
+        with torch.no_grad():
+            pu = model_u(packaged)[0]
+    finally:
+        EncoderProposals.get_proposals = orig_gp
+        EncoderProposals.inference_single_image = orig_inf
+    enc_sorted = torch.sort(seen["logits"], descending=True)[0]
+    out["uq_enc_logits_sorted"] = enc_sorted[:320].numpy()
+    out["uq_query"] = seen["query"].numpy().astype(np.int32)
     out.update(uq_scores=pu.scores.numpy(), uq_pred_classes=pu.pred_classes.numpy(),
                uq_pred_boxes=pu.pred_boxes.numpy(), uq_pred_logits=pu.pred_logits.numpy(),
                uq_boxes3d=pu.pred_boxes_3d.tensor.numpy(), uq_R=pu.pred_boxes_3d.R.numpy(),
@@ -181,14 +207,26 @@ def run_case(name, dim, frame, seed, H, W, ratio, K, thr, keep_features=False):
 CA1M_K = np.array([[360.0, 0.0, 191.5], [0.0, 360.0, 255.5], [0.0, 0.0, 1.0]], np.float32)
 
 
-def main():
+CASES = {
     # ScanNet-shaped frame (640x480, depth at image resolution): the synthetic stream's camera
-    run_case("cutr_vit_t.npz", 192, 7, 0, 480, 640, 1, SCANNET_K, FILTER_CFG["scannet"], keep_features=True)
+    "cutr_vit_t.npz": (192, 7, 0, 480, 640, 1, SCANNET_K, "scannet"),
     # CA-1M-shaped portrait frame (384 wide x 512 tall, ca1m.yaml cam) with a half-resolution depth
-    run_case("cutr_ca1m_r2.npz", 192, 11, 1, 512, 384, 2, CA1M_K, FILTER_CFG["ca1m"], keep_features=True)
+    "cutr_ca1m_r2.npz": (192, 11, 1, 512, 384, 2, CA1M_K, "ca1m"),
     # quarter-resolution depth at 640x480
-    run_case("cutr_r4.npz", 192, 3, 2, 480, 640, 4, SCANNET_K, FILTER_CFG["scannet"], keep_features=True)
+    "cutr_r4.npz": (192, 3, 2, 480, 640, 4, SCANNET_K, "scannet"),
+    # configs[1] as CA1MDataset streams it: depth resized to the image (capture_stream.py:445-459),
+    # i.e. RGB:depth ratio 1 on the 512 x 384 portrait frame
+    "cutr_ca1m_r1.npz": (192, 13, 3, 512, 384, 1, CA1M_K, "ca1m"),
+    # the bench's width: ViT-B (dim 768, 12 x 64 heads, MLP 3072; cubify_transformer.py:1232-1240)
+    "cutr_vitb.npz": (768, 5, 4, 480, 640, 1, SCANNET_K, "scannet"),
+}
+
+
+def main(names=None):
+    for name in (names or CASES):
+        dim, frame, seed, H, W, ratio, K, thr = CASES[name]
+        run_case(name, dim, frame, seed, H, W, ratio, K, FILTER_CFG[thr], keep_features=True)
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

@@ -10,7 +10,9 @@ from oracle import oracle as OR
 from tests import trace_util as TU
 
 
-CASES = ["cutr_vit_t.npz", "cutr_ca1m_r2.npz", "cutr_r4.npz"]
+# dim 192: ScanNet 640x480, CA-1M portrait at RGB:depth 2 and 1 (CA1MDataset's own ratio), 640x480
+# at ratio 4; dim 768: the bench's ViT-B width on the ScanNet frame
+CASES = ["cutr_vit_t.npz", "cutr_ca1m_r2.npz", "cutr_r4.npz", "cutr_ca1m_r1.npz", "cutr_vitb.npz"]
 
 
 @pytest.fixture(scope="module")
@@ -31,6 +33,19 @@ def frame_inputs(g):
     d, params = OR.depth_standardize(depth)
     Tg = camera_to_gravity(Scene().pose(frame))
     return rgb, depth, d, params, Tg
+
+
+def expected_depth_sum(g, params):
+    """the golden's padded standardised-depth sum for depth parameters `params`: torch's f32
+    cascade mean (whose rounding depends on the host's vector width) and the oracle's correctly
+    rounded mean may differ by an ulp (cutr_ca1m_r1: +1 ulp); every valid pixel's standardised
+    value then moves by -dmean/std, so the sum is shifted by that known amount"""
+    params = np.asarray(params, np.float32).reshape(-1)
+    ulp = params.view(np.int32) - g["depth_params"].view(np.int32)
+    assert np.abs(ulp).max() <= 1, ulp
+    _, depth, _, _, _ = frame_inputs(g)
+    shift = float((depth > 0).sum()) * (float(params[0]) - float(g["depth_params"][0])) / float(params[1])
+    return float(g["depth_sum"]) - shift
 
 
 def cpu_frame_batch(g):
@@ -129,8 +144,7 @@ def test_forward_matches_reference(case):
     g = TU.load(case)
     m = model_for(g)
     batch, params = cpu_frame_batch(g)
-    np.testing.assert_allclose(params, g["depth_params"], rtol=2e-6)
-    np.testing.assert_allclose(batch.depth.double().sum().item(), g["depth_sum"], rtol=1e-6)
+    np.testing.assert_allclose(batch.depth.double().sum().item(), expected_depth_sum(g, params), rtol=1e-6)
     np.testing.assert_allclose(batch.image.double().sum().item(), g["image_sum"], rtol=1e-6)
     np.testing.assert_allclose(batch.T_gravity[0].numpy(), g["T_gravity"], atol=1e-6)
     with torch.no_grad():

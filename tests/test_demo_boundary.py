@@ -18,7 +18,7 @@ import torch
 
 from oracle import oracle as OR
 from tests import trace_util as TU
-from tests.test_cutr_golden import CASES, assert_instances, model_for
+from tests.test_cutr_golden import CASES, assert_instances, expected_depth_sum, model_for
 
 
 def oracle_standardize(img, trunc_value=0.1):
@@ -62,7 +62,8 @@ def test_demo_sequence_plumbing(case, monkeypatch):
     np.testing.assert_array_equal(x["K"][0].numpy(), g["K"])
     fb = frame_batch(packaged)
     np.testing.assert_allclose(fb.image.double().sum().item(), g["image_sum"], rtol=1e-6)
-    np.testing.assert_allclose(fb.depth.double().sum().item(), g["depth_sum"], rtol=1e-6)
+    np.testing.assert_allclose(fb.depth.double().sum().item(),
+                               expected_depth_sum(g, x["depth_params"][0].numpy()), rtol=1e-6)
     with pytest.raises(_lib.HipError):          # the model has no CPU path either
         model(packaged)
     with torch.no_grad():

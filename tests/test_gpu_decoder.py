@@ -9,6 +9,8 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+from tests.test_cutr_golden import CASES as CUTR_CASES  # noqa: E402
+
 pytestmark = pytest.mark.gpu
 
 
@@ -174,7 +176,7 @@ def _assert_same(r, t, desc_tol=1e-4):
         np.testing.assert_allclose(a.cpu().numpy()[ok], b.cpu().numpy()[ok], rtol=1e-4, atol=tol)
 
 
-@pytest.mark.parametrize("case", ["cutr_vit_t.npz", "cutr_ca1m_r2.npz", "cutr_r4.npz"])
+@pytest.mark.parametrize("case", CUTR_CASES)
 def test_decoder_engine_vs_reference(L, case):
     """DecoderEngine on the reference's backbone features reproduces the reference's fp32 instances
     (tolerances of the torch decoder's test_demo_sequence_engine_vs_reference)"""

@@ -5,6 +5,8 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+from tests.test_cutr_golden import CASES as CUTR_CASES  # noqa: E402
+
 pytestmark = pytest.mark.gpu
 
 
@@ -239,7 +241,7 @@ def _demo_sequence(g, dev, B=1, uniform_queries=False, model=None):
         return model(packaged)[0], packaged
 
 
-@pytest.mark.parametrize("case", ["cutr_vit_t.npz", "cutr_ca1m_r2.npz", "cutr_r4.npz"])
+@pytest.mark.parametrize("case", CUTR_CASES)
 def test_demo_sequence_engine_vs_reference(dev, case):
     """the HIP CuTR path through the reference's own call sequence (package -> move -> preprocess
     -> model(packaged)), against the REFERENCE's fp32 run on the same frame and seeded weights:
@@ -287,11 +289,12 @@ def test_demo_sequence_engine_vs_reference(dev, case):
                      R_tol=2e-5, desc_tol=5e-3)
 
 
-@pytest.mark.parametrize("case", ["cutr_vit_t.npz", "cutr_ca1m_r2.npz", "cutr_r4.npz"])
+@pytest.mark.parametrize("case", CUTR_CASES)
 def test_demo_sequence_instances_vs_reference(dev, case):
     """END TO END, instance by instance: model(packaged) on the HIP path (bf16 MFMA backbone, f32
     HIP decoder, top-300 / top-100 kernels, 3-D lift) through demo.py:129-136's call sequence,
-    against the REFERENCE's fp32 run of the same frame with the uniform-query weights
+    against the REFERENCE's fp32 run of the same frame with the uniform-query weights (dim 192 on
+    four frame shapes, incl. CA-1M portrait at RGB:depth 1 and 2, and the bench's ViT-B width)
     (weights.uniform_queries: the decoder is then equivariant to the order of its proposal
     queries, so near-tied encoder logits do not swap content rows).  Every reference instance is
     paired with the HIP instance of the same class and 2-D box (<= 0.5 px); per pair: score,
@@ -310,8 +313,14 @@ def test_demo_sequence_instances_vs_reference(dev, case):
     cut = g["scores"][-1]
     print(case, "paired", len(pairs), "unpaired golden ranks", unpaired)
     assert len(pairs) >= 97
+    # an unpaired instance sits at one of the two cuts: the top-100 score cut, or the encoder's
+    # top-300 proposal cut (its query slot's proposal logit within 1e-2 of the 300th logit, where
+    # random-weight logits are spaced ~4e-4 apart; measured at ViT-B: slots 285 / 288, 6e-3 above)
+    enc = g.get("uq_enc_logits_sorted")
     for i in unpaired:
-        assert abs(g["scores"][i] - cut) < 1e-3, (i, g["scores"][i], cut)
+        at_top100 = abs(g["scores"][i] - cut) < 1e-3
+        at_top300 = enc is not None and abs(enc[g["uq_query"][i]] - enc[300]) < 1e-2
+        assert at_top100 or at_top300, (i, g["scores"][i], cut)
     gi = np.array([p[0] for p in pairs])
     hi = np.array([p[1] for p in pairs])
     diffs = {}
@@ -340,7 +349,7 @@ def test_detection_filter_kernel_vs_reference(dev):
     per filter and combined, at the config thresholds and at thresholds splitting every mask"""
     from boxfusion_amd import _lib
     from tests import trace_util as TU
-    for case in ["cutr_vit_t.npz", "cutr_ca1m_r2.npz", "cutr_r4.npz"]:
+    for case in CUTR_CASES:
         g = TU.load(case)
         for suf in ("", "_med"):
             st, ub, fr, lg = g["thr" + suf]

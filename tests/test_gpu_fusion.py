@@ -25,9 +25,8 @@ def L():
     return _lib
 
 
-def nms_cfg(L, cap=CAP):
+def nms_cfg(L, cap=CAP, cfg=TU.SCANNET_CFG):
     c = L.NmsCfg()
-    cfg = TU.SCANNET_CFG
     c.iou_threshold = cfg["box_fusion"]["nms_threshold"]
     c.translation_gap = cfg["association"]["translation_gap"]
     c.rotation_gap = cfg["association"]["rotation_gap"]
@@ -37,26 +36,25 @@ def nms_cfg(L, cap=CAP):
     return c
 
 
-def corr_cfg(L, cap=CAP):
+def corr_cfg(L, cap=CAP, cfg=TU.SCANNET_CFG, W=640, H=480):
     c = L.CorrCfg()
-    cfg = TU.SCANNET_CFG
     c.small_size = cfg["box_fusion"]["small_size"]
     c.threshold = cfg["association"]["small_threshold"]
     c.translation_gap = cfg["association"]["translation_gap"]
     c.rotation_gap = cfg["association"]["rotation_gap"]
-    c.W, c.H = 640.0, 480.0
+    c.W, c.H = float(W), float(H)
     c.max_list = 5
     c.list_capacity = cap
     return c
 
 
-def fuse_cfg(L, legacy):
-    o = OR.fuse_cfg(TU.SCANNET_CFG, np.eye(4), 480, 640, legacy=legacy)
+def fuse_cfg(L, legacy, cfg=TU.SCANNET_CFG, K=TU.SCANNET_K, H=480, W=640):
+    o = OR.fuse_cfg(cfg, np.eye(4), H, W, legacy=legacy)
     c = L.FuseCfg()
     for name, _ in L.FuseCfg._fields_:
         if name == "K":
             K4 = np.eye(4, dtype=np.float32)
-            K4[:3, :3] = [[574.540771, 0.0, 322.522827], [0.0, 577.583740, 238.558853], [0, 0, 1]]
+            K4[:3, :3] = K
             for i in range(16):
                 c.K[i] = float(K4.reshape(-1)[i])
         else:
@@ -65,10 +63,11 @@ def fuse_cfg(L, legacy):
 
 
 class HipBackend:
-    def __init__(self, L, legacy=False):
+    def __init__(self, L, legacy=False, cfg=TU.SCANNET_CFG, K=TU.SCANNET_K, H=480, W=640):
         self.L = L
         self.pst = _t(np.load(TU.GOLDEN + "/../../boxfusion_amd/data/pst_1024_0.npy"))
-        self.fcfg = fuse_cfg(L, legacy)
+        self.fcfg = fuse_cfg(L, legacy, cfg, K, H, W)
+        self.ncfg, self.ccfg = nms_cfg(L, cfg=cfg), corr_cfg(L, cfg=cfg, W=W, H=H)
 
     def corners(self, tensor, R):
         return self.L.box_corners(_t(tensor), _t(R)).cpu().numpy()
@@ -81,7 +80,7 @@ class HipBackend:
         it, ln, vn = _t(items, torch.int32), _t(lens, torch.int32), _t(valid_num)
         keep, succ, ev, cnt = self.L.nms_scan(_t(iou, torch.float64), _t(corners), _t(scores),
                                               _t(init_id, torch.int32), _t(cam_poses), it, ln, vn,
-                                              nms_cfg(self.L))
+                                              self.ncfg)
         c = cnt.cpu().numpy()
         assert c[3] == 0
         return dict(keep=keep.cpu().numpy()[:c[0]], success=succ.cpu().numpy()[:c[1]],
@@ -97,7 +96,7 @@ class HipBackend:
         k, ev, cnt = self.L.corr_assoc(_t(corners), _t(dims), _t(scores), _t(boxes2d),
                                        _t(init_id, torch.int32), _t(cam_poses), _t(pose), _t(K),
                                        n_glo, _t(keep, torch.int32), _t(success, torch.int32),
-                                       it, ln, vn, corr_cfg(self.L))
+                                       it, ln, vn, self.ccfg)
         c = cnt.cpu().numpy()
         assert c[2] == 0
         return dict(keep=k.cpu().numpy()[:c[0]],
@@ -122,12 +121,17 @@ class HipBackend:
         return o
 
 
-@pytest.mark.parametrize("name", ["fusion_trace.npz", "fusion_trace_small.npz"])
+@pytest.mark.parametrize("name", TU.TRACES)
 def test_trace_replay_hip(L, name):
-    """NMS keep/success, fusion lists, association and fused boxes bit-exact vs the reference."""
-    stats = TU.replay(TU.load(name), HipBackend(L, legacy=False))
+    """NMS keep/success, fusion lists, association and fused boxes bit-exact vs the reference
+    (ScanNet scene traces, the CA-1M trace at ca1m.yaml thresholds on 384 x 512 portrait frames,
+    and the overrun-free face-on trace, reference-pinned at every keyframe)."""
+    t = TU.load(name)
+    stats = TU.replay(t, HipBackend(L, False, *TU.trace_setup(t)))
     print(name, stats)
-    assert stats["fused"] > 10 and stats["reference_pinned"] >= 1
+    assert stats["fused"] >= 10 and stats["reference_pinned"] >= 1
+    if "faceon" in name:
+        assert stats["reference_pinned"] == stats["keyframes"] and stats["hull_overflow_keyframes"] == 0
 
 
 def test_faceon_fusion_reference_pinned(L):

@@ -36,27 +36,30 @@ def _inject_geometry(monkeypatch, dev, src):
 
 
 @pytest.mark.parametrize("native", [True, False])
-@pytest.mark.parametrize("name", ["fusion_trace.npz", "fusion_trace_small.npz"])
+@pytest.mark.parametrize("name", TU.TRACES)
 def test_fusion_stage_vs_trace(dev, name, native, monkeypatch):
     """demo.py keyframe state machine on the GPU == the reference's recorded chain, bit for bit,
     given the reference's own world-space boxes and projections (pf_* of the trace).  The trace
     is the reference's control flow with the exact hull wherever its kernel overruns
     convex_inter[8] (recorded per keyframe, hull_over): the keyframes before the first such
     fusion are reference-pinned outright, and BoxFusion's BF_DEV_HULL_OVERFLOW count matches the
-    record keyframe by keyframe.  native: the library's keyframe sequencer (bf_fseq) runs the
-    state machine; else Python drives the same kernels."""
+    record keyframe by keyframe.  fusion_trace_faceon.npz has no overrun anywhere (every keyframe
+    pinned); fusion_trace_ca1m.npz runs ca1m.yaml's thresholds on 384 x 512 portrait frames.
+    native: the library's keyframe sequencer (bf_fseq) runs the state machine; else Python
+    drives the same kernels."""
     from boxfusion_amd.fusion_stage import FusionStage
     from boxfusion_amd.pipeline import scene_instances
-    from boxfusion_amd.synthetic import SCANNET_K
     t = TU.load(name)
+    cfg, K, H, W = TU.trace_setup(t)
     _inject_geometry(monkeypatch, dev, dict(tensor=t["pf_tensor"], R=t["pf_R"], proj=t["pf_proj"]))
-    st = FusionStage(TU.SCANNET_CFG, SCANNET_K, device=dev, legacy_promotion=False, native=native)
+    st = FusionStage(cfg, K, H=H, W=W, device=dev, legacy_promotion=False, native=native)
     nd = t["n_det"]
+    fused = 0
     for k, frame in enumerate(t["frame"]):
         a, b = int(nd[:k].sum()), int(nd[:k + 1].sum())
         det = {key: t["det_" + key][a:b] for key in ["scores", "pred_boxes", "xyzlhw", "R", "proj_xy"]}
         calls = st.fuser.hull_overflow_calls
-        st.keyframe(int(frame), t["pose"][k], scene_instances(det, dev))
+        st.keyframe(int(frame), t["pose"][k], scene_instances(det, dev, H, W))
         got, _ = st.boxes()
         assert st.box_manager.fusion_list == TU._lists(t, "post_fl", k), f"kf {k}"
         assert st.box_manager.already_fusion == TU._lists(t, "fused", k), f"kf {k}"
@@ -65,6 +68,8 @@ def test_fusion_stage_vs_trace(dev, name, native, monkeypatch):
         np.testing.assert_array_equal(got, TU._rows(t, "post_tensor", k), err_msg=f"kf {k}")
         np.testing.assert_array_equal(st.all_pred_box.valid_num.cpu().numpy(),
                                       TU._rows(t, "post_valid_num", k), err_msg=f"kf {k}")
+        fused = len(st.box_manager.already_fusion)
+    assert fused >= 10
 
 
 def test_fusion_stage_own_geometry(dev):
@@ -112,6 +117,35 @@ def test_fusion_stage_vs_oracle_chain_gap1(dev, native, monkeypatch):
         assert st.box_manager.already_fusion == ch.already_fusion, f"frame {f}"
         np.testing.assert_array_equal(st.boxes()[0], ch.g["tensor"], err_msg=f"frame {f}")
     assert len(ch.already_fusion) > 5
+
+
+def test_fusion_stage_empty_last_keyframe_native_vs_python(dev):
+    """The last keyframe has no detections and the stream's last frame is not a keyframe: the
+    re-entry of demo.py:200 sees an empty pred_instances and only records num_record[last]
+    (demo.py:206-212).  Native sequencer and Python-driven stage agree on every list and on
+    num_record."""
+    import copy
+    from boxfusion_amd.fusion_stage import FusionStage
+    from boxfusion_amd.pipeline import scene_instances
+    from boxfusion_amd.synthetic import SCANNET_K, Scene
+    cfg = copy.deepcopy(TU.SCANNET_CFG)
+    cfg["data"] = dict(gap=5)
+    scene = Scene(seed=0)
+    out = {}
+    for native in (True, False):
+        st = FusionStage(cfg, SCANNET_K, device=dev, native=native)
+        for f in range(0, 30, 5):
+            d = scene.detections(f)
+            if f == 25:                      # empty last keyframe
+                d = {k: v[:0] for k, v in d.items()}
+            st.keyframe(f, scene.pose(f), scene_instances(d, dev))
+        st.finish(28, scene.pose(28), False)
+        bm = st.box_manager
+        out[native] = (dict(bm.num_record), bm.fusion_list, bm.already_fusion, st.boxes()[0])
+    assert out[True][0] == out[False][0]
+    assert 28 in out[True][0] and out[True][0][28] == out[True][0][25] == out[True][0][20]
+    assert out[True][1] == out[False][1] and out[True][2] == out[False][2]
+    np.testing.assert_array_equal(out[True][3], out[False][3])
 
 
 def test_detect_stage_filtered(dev):
@@ -467,6 +501,12 @@ def test_pipeline_run_vs_reference_demo_gap25(dev, native, monkeypatch):
     # (demo.py:330), the last of them the final global boxes
     poses = [a for p_, _, k, a in rec.records if p_ == "/world/image" and k == "Transform3D"]
     assert len(poses) == n
+    # frame order (demo.py:108): the pose records are frames 0..n-1 in turn, so the trajectory
+    # strip of the last frame is the positions of every frame before it
+    trans = np.array([a["translation"] for a in poses])
+    np.testing.assert_allclose(trans, np.stack([scene.pose(i)[:3, 3] for i in range(n)]), rtol=0, atol=1e-6)
+    traj = rec.last("/world/trajectory")["strips"][0]
+    np.testing.assert_allclose(traj, trans[:n - 1], rtol=0, atol=1e-6)
     boxes_logged = [a for p_, _, k, a in rec.records if p_ == "/device/wide/pred_instances"]
     assert len(boxes_logged) == len(range(0, n, gap)) + 1
     fin = fusion.all_pred_box

@@ -5,14 +5,14 @@ import pytest
 
 from oracle.chain import OracleChain
 from tests import trace_util as TU
-from boxfusion_amd.synthetic import SCANNET_K
 
 
-@pytest.mark.parametrize("name", ["fusion_trace.npz", "fusion_trace_small.npz"])
+@pytest.mark.parametrize("name", TU.TRACES)
 def test_chain_matches_trace(name):
     t = TU.load(name)
     pst = np.load(TU.GOLDEN + "/../../boxfusion_amd/data/pst_1024_0.npy")
-    ch = OracleChain(TU.SCANNET_CFG, SCANNET_K, pst=pst, legacy=False)
+    cfg, K, H, W = TU.trace_setup(t)
+    ch = OracleChain(cfg, K, H=H, W=W, pst=pst, legacy=False)
     nd = t["n_det"]
     for k, frame in enumerate(t["frame"]):
         a, b = int(nd[:k].sum()), int(nd[:k + 1].sum())

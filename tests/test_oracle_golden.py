@@ -29,9 +29,8 @@ def test_depth_standardize():
         np.testing.assert_allclose(out, g["out"][i], rtol=0, atol=2e-6)
 
 
-def nms_cfg(cap=64):
+def nms_cfg(cap=64, cfg=TU.SCANNET_CFG):
     c = OR.NmsCfg()
-    cfg = TU.SCANNET_CFG
     c.iou_threshold = cfg["box_fusion"]["nms_threshold"]
     c.translation_gap = cfg["association"]["translation_gap"]
     c.rotation_gap = cfg["association"]["rotation_gap"]
@@ -41,34 +40,34 @@ def nms_cfg(cap=64):
     return c
 
 
-def corr_cfg(cap=64):
+def corr_cfg(cap=64, cfg=TU.SCANNET_CFG, W=640, H=480):
     c = OR.CorrCfg()
-    cfg = TU.SCANNET_CFG
     c.small_size = cfg["box_fusion"]["small_size"]
     c.threshold = cfg["association"]["small_threshold"]
     c.translation_gap = cfg["association"]["translation_gap"]
     c.rotation_gap = cfg["association"]["rotation_gap"]
-    c.W, c.H = 640.0, 480.0
+    c.W, c.H = float(W), float(H)
     c.max_list = 5
     c.list_capacity = cap
     return c
 
 
 class OracleBackend:
-    def __init__(self):
+    def __init__(self, cfg=TU.SCANNET_CFG, K=TU.SCANNET_K, H=480, W=640):
         self.pst = np.load(TU.GOLDEN + "/../../boxfusion_amd/data/pst_1024_0.npy")
         K4 = np.eye(4, dtype=np.float32)
-        K4[:3, :3] = [[574.540771, 0.0, 322.522827], [0.0, 577.583740, 238.558853], [0, 0, 1]]
-        self.fcfg = OR.fuse_cfg(TU.SCANNET_CFG, K4, 480, 640, legacy=False)
+        K4[:3, :3] = K
+        self.fcfg = OR.fuse_cfg(cfg, K4, H, W, legacy=False)
+        self.ncfg, self.ccfg = nms_cfg(cfg=cfg), corr_cfg(cfg=cfg, W=W, H=H)
 
     corners = staticmethod(OR.box_corners)
     iou_matrix = staticmethod(OR.obb_iou_matrix)
 
     def nms(self, *a):
-        return OR.nms_scan(*a, nms_cfg())
+        return OR.nms_scan(*a, self.ncfg)
 
     def corr(self, *a):
-        return OR.corr_assoc(*a, corr_cfg())
+        return OR.corr_assoc(*a, self.ccfg)
 
     def fuse(self, views):
         out = []
@@ -81,13 +80,20 @@ class OracleBackend:
         return any(OR.hull_overflow(reset=True))
 
 
-@pytest.mark.parametrize("name", ["fusion_trace.npz", "fusion_trace_small.npz"])
+@pytest.mark.parametrize("name", TU.TRACES)
 def test_trace_replay(name):
-    stats = TU.replay(TU.load(name), OracleBackend())
+    t = TU.load(name)
+    stats = TU.replay(t, OracleBackend(*TU.trace_setup(t)))
     print(name, stats)
-    assert stats["reference_pinned"] >= 1 and stats["hull_overflow_keyframes"] > 0
-    assert stats["suppressions"] > 100
-    assert stats["fused"] > 10
+    assert stats["fused"] >= 10
+    if "faceon" in name:
+        # overrun-free end to end: every keyframe pinned to the reference outright
+        assert stats["hull_overflow_keyframes"] == 0
+        assert stats["reference_pinned"] == stats["keyframes"] == len(t["frame"]) - 1
+        assert stats["corr_changes"] >= 2 and stats["suppressions"] >= 16
+    else:
+        assert stats["reference_pinned"] >= 1 and stats["hull_overflow_keyframes"] > 0
+        assert stats["suppressions"] > 100
     if "small" in name:
         assert stats["corr_changes"] > 5
 

@@ -103,3 +103,66 @@ def test_frame_logger_sequence_and_boxes(tmp_path):
     lines = open(out).read().strip().split("\n")
     assert len(lines) == len(rec.records)
     assert '"kind": "Image"' in lines[3] and '"shape": [480, 640, 3]' in lines[3]
+
+
+def test_pipeline_viz_frame_order():
+    """Pipeline.run(viz=...) logs the frames in frame order for gap > 1 (demo.py:93-197 logs every
+    frame as it arrives, the boxes after each keyframe's fusion): batch [0, g, ...] must not log
+    its non-keyframes before its keyframes, so the trajectory strip of frame c is the poses of
+    frames [0, c)."""
+    import torch
+    from boxfusion_amd.pipeline import Pipeline
+
+    n, gap, B = 23, 4, 2
+    poses_all = np.stack([np.eye(4) for _ in range(n)])
+    poses_all[:, 0, 3] = np.arange(n)
+
+    class Det:
+        def __init__(self):
+            self.B = B
+
+        def preprocess_frames(self, depth, poses):
+            pass
+
+        def __call__(self, rgb, depth, poses):
+            return [None] * len(poses)
+
+    class Fus:
+        all_pred_box = None
+
+        def __init__(self):
+            self.calls = []
+
+        def keyframe(self, i, pose, pred):
+            self.calls.append(("kf", i))
+
+        def finish(self, last, pose, was_kf):
+            self.calls.append(("finish", last))
+
+    class Log:
+        def __init__(self):
+            self.seq = []
+            self.lg = V.FrameLogger(V.Recording(forward=False), np.eye(3), (4, 4))
+
+        def frame(self, i, pose):
+            self.seq.append(("frame", i))
+            self.lg.frame(i, pose)
+
+        def boxes(self, apb, i):
+            self.seq.append(("boxes", i))
+
+    def frames(ids):
+        return (torch.zeros((len(ids), 4, 4, 3), dtype=torch.uint8), torch.zeros((len(ids), 4, 4)),
+                poses_all[list(ids)])
+
+    log, fus = Log(), Fus()
+    Pipeline(Det(), fus, gap).run(frames, n, viz=log)
+    assert [i for k, i in log.seq if k == "frame"] == list(range(n))
+    kfs = list(range(0, n, gap))
+    assert [i for k, i in log.seq if k == "boxes"] == kfs + [n - 1]
+    # each keyframe's boxes come right after its own frame record
+    for i in kfs:
+        assert log.seq[log.seq.index(("frame", i)) + 1] == ("boxes", i)
+    tr = log.lg.rec.last("/world/trajectory")
+    assert np.array_equal(np.asarray(tr["strips"][0])[:, 0], np.arange(n - 1))
+    assert fus.calls == [("kf", i) for i in kfs] + [("finish", n - 1)]

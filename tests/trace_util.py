@@ -2,6 +2,8 @@
 tests/golden/make_golden.py) keyframe by keyframe against a backend (oracle or HIP)."""
 from __future__ import annotations
 
+import copy
+import json
 import os
 
 import numpy as np
@@ -20,6 +22,25 @@ SCANNET_CFG = dict(
                     random_opt=dict(center_init_size=0.1, center_scaling_coefficient=0.1,
                                     shape_init_size=0.5, shape_scaling_coefficient=0.5)),
 )
+
+
+SCANNET_K = np.array([[574.540771, 0.0, 322.522827], [0.0, 577.583740, 238.558853], [0, 0, 1]],
+                     np.float32)
+
+# the fusion-chain traces (make_golden.py): ScanNet scene traces, the CA-1M config trace (ca1m.yaml
+# thresholds, 384 x 512 portrait) and the overrun-free face-on trace
+TRACES = ["fusion_trace.npz", "fusion_trace_small.npz", "fusion_trace_ca1m.npz", "fusion_trace_faceon.npz"]
+
+
+def trace_setup(t):
+    """(cfg, K [3,3], H, W) the trace was generated with; traces without a recorded config ran
+    with SCANNET_CFG on the 640 x 480 ScanNet camera"""
+    if "cfg_json" not in t:
+        return SCANNET_CFG, SCANNET_K, 480, 640
+    cfg = json.loads(str(t["cfg_json"]))
+    cfg["box_fusion"]["pst_path"] = "pst_1024_0"
+    cfg["data"] = dict(gap=1)
+    return cfg, np.asarray(t["K"], np.float32), int(t["H"]), int(t["W"])
 
 
 def load(name):
@@ -117,8 +138,7 @@ def replay(t, backend, fuse_legacy=False):
     control flow with the exact hull where its kernel overruns convex_inter[8] / corners_i[36]
     (box_fusion.py:378-384, undefined behaviour in the reference).
     Returns counters of the exercised paths."""
-    K = np.array([[574.540771, 0.0, 322.522827], [0.0, 577.583740, 238.558853], [0, 0, 1]],
-                 np.float32)
+    _, K, _, _ = trace_setup(t)
     stats = dict(keyframes=0, suppressions=0, corr_changes=0, fused=0, reference_pinned=0,
                  hull_overflow_keyframes=0)
     over_seen = False
