@@ -347,214 +347,11 @@ __device__ __forceinline__ void tile_coords(int tile, int tiles_m, int tiles_n, 
     n0 = (in / rows) * 256;
 }
 
-template <bool OUT_BF16, int ACT>
-__global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256(const u16* __restrict__ A, int lda,
-                                                           const u16* __restrict__ W, int ldw,
-                                                           const float* __restrict__ bias,
-                                                           const float* __restrict__ resid, int ldr,
-                                                           int resid_mod, void* __restrict__ Cv,
-                                                           int ldc, const int32_t* __restrict__ row_map,
-                                                           int M, int N, int K, int tiles_n,
-                                                           int tiles_m, int gm) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char g_smem[];
-    const int t = threadIdx.x;
-    const int lane = t & 63, wave = t >> 6;
-    const int wr = wave >> 2, wc = wave & 3;
-    const int fr = lane & 31, fh = lane >> 5;
-    const int ntiles = tiles_m * tiles_n;
-    const int G = gridDim.x;
-    // XCD-aware slot: blocks b with b % 8 == x share an XCD; give them 32 consecutive tiles
-    const int slot = (G % 8 == 0) ? ((int)blockIdx.x % 8) * (G / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
-    const int my_tiles = ntiles > slot ? (ntiles - slot + G - 1) / G : 0;
-    const int nk = K / GB_K;
-    const int total = my_tiles * nk;             // K-tiles this block walks
-    if (total == 0) return;
-
-    // per-lane staging coordinates (row within the 256-row operand tile, swizzled 16-B chunk)
-    int srow[4], scol[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        srow[i] = (wave * 4 + i) * 8 + (lane >> 3);
-        scol[i] = ((lane & 7) ^ swz_key(srow[i])) * 8;
-    }
-    typedef __attribute__((address_space(3))) void* lds_ptr_t;
-    // issue K-tile g of this block's walk into LDS stage `stage`
-    auto stage_tile = [&](int stage, int g) {
-        const int tile = slot + (g / nk) * G;
-        const int k0 = (g % nk) * GB_K;
-        int m0, n0;
-        tile_coords(tile, tiles_m, tiles_n, gm, m0, n0);
-        unsigned char* sa = g_smem + stage * 65536 + wave * 4096;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const u16* ga = A + (size_t)min(m0 + srow[i], M - 1) * lda + k0 + scol[i];
-            const u16* gw = W + (size_t)min(n0 + srow[i], N - 1) * ldw + k0 + scol[i];
-            __builtin_amdgcn_global_load_lds((const void*)ga, (lds_ptr_t)(sa + i * 1024), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((const void*)gw, (lds_ptr_t)(sa + 32768 + i * 1024), 16, 0, 0);
-        }
-    };
-
-    // v_mfma_f32_16x16x32_bf16: wave tile 128x64 = 8 row blocks x 4 column blocks of 16x16,
-    // K-tile of 64 = 2 k-steps of 32.  Lane l holds A[row l&15][k 8(l>>4)..+7] (16 B) per block.
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[i][j][e] = 0.f;
-
-    const int lr = lane & 15, lq = lane >> 4;     // fragment row / k-quarter
-    bf16x8 fa0[8], fb0[4], fa1[8], fb1[4];
-#define G2_READ(FA, FB, stage, ks)                                                               \
-    {                                                                                            \
-        const unsigned char* sa_ = g_smem + (stage) * 65536;                                     \
-        _Pragma("unroll") for (int i = 0; i < 8; ++i) FA[i] =                                    \
-            *reinterpret_cast<const bf16x8*>(sa_ + swz(wr * 128 + i * 16 + lr, (ks) * 4 + lq));  \
-        _Pragma("unroll") for (int j = 0; j < 4; ++j) FB[j] = *reinterpret_cast<const bf16x8*>(  \
-            sa_ + 32768 + swz(wc * 64 + j * 16 + lr, (ks) * 4 + lq));                            \
-    }
-#define G2_MFMA(FA, FB)                                                                          \
-    _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 4; ++j) \
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA[i], FB[j], acc[i][j], 0, 0, 0);
-
-    stage_tile(0, 0);
-    if (total > 1) stage_tile(1, 1);
-    if (total > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    RAW_BARRIER();
-    G2_READ(fa0, fb0, 0, 0);
-    float* scratch = reinterpret_cast<float*>(g_smem + G2_STAGES_BYTES + wave * 4096);  // [16][64]
-    constexpr int CW = OUT_BF16 ? 8 : 4;            // outputs per 16-B chunk
-    for (int g = 0; g < total; ++g) {
-        const int st = g & 1;
-        G2_READ(fa1, fb1, st, 1);
-        G2_MFMA(fa0, fb0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // K-tile g+1 (the only one in flight)
-        RAW_BARRIER();
-        // second k-step: its 32 MFMAs carry the 8 LDS-DMA issues of K-tile g+2 and the 12
-        // fragment reads of K-tile g+1 (unconditional, clamped past the end)
-        {
-            const int gn = min(g + 2, total - 1);
-            const int tile_n = slot + (gn / nk) * G;
-            const int k0n = (gn % nk) * GB_K;
-            int m0n, n0n;
-            tile_coords(tile_n, tiles_m, tiles_n, gm, m0n, n0n);
-            unsigned char* sa_n = g_smem + st * 65536 + wave * 4096;
-            const unsigned char* sr = g_smem + (st ^ 1) * 65536;
-#pragma unroll
-            for (int q = 0; q < 32; ++q) {
-                const int i = q >> 2, j = q & 3;
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[i], fb1[j], acc[i][j], 0, 0, 0);
-                if ((q & 3) == 0) {
-                    const int si = (q >> 3);
-                    if (((q >> 2) & 1) == 0) {
-                        const u16* ga = A + (size_t)min(m0n + srow[si], M - 1) * lda + k0n + scol[si];
-                        __builtin_amdgcn_global_load_lds((const void*)ga, (lds_ptr_t)(sa_n + si * 1024), 16, 0, 0);
-                    } else {
-                        const u16* gw = W + (size_t)min(n0n + srow[si], N - 1) * ldw + k0n + scol[si];
-                        __builtin_amdgcn_global_load_lds((const void*)gw, (lds_ptr_t)(sa_n + 32768 + si * 1024), 16, 0, 0);
-                    }
-                }
-                if ((q & 1) == 1 && q < 24) {
-                    const int r = q >> 1;     // 0..11
-                    if (r < 8) fa0[r] = *reinterpret_cast<const bf16x8*>(sr + swz(wr * 128 + r * 16 + lr, lq));
-                    else fb0[r - 8] = *reinterpret_cast<const bf16x8*>(sr + 32768 + swz(wc * 64 + (r - 8) * 16 + lr, lq));
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        if (g % nk != nk - 1) continue;
-
-        // ---- epilogue of this tile (wave-private, 16 rows = one row block per pass) ----------
-        const int tile = slot + (g / nk) * G;
-        int m0, n0;
-        tile_coords(tile, tiles_m, tiles_n, gm, m0, n0);
-        m0 += wr * 128; n0 += wc * 64;
-        float bv[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int n = n0 + j * 16 + lr;
-            bv[j] = (bias && n < N) ? bias[min(n, N - 1)] : 0.f;
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            // C/D layout: col = lane&15, row = 4*(lane>>4) + e; rows r and r+4 in other banks
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                f32x2 v01 = {acc[i][j][0] + bv[j], acc[i][j][1] + bv[j]};
-                f32x2 v23 = {acc[i][j][2] + bv[j], acc[i][j][3] + bv[j]};
-                if (ACT == 1) gelu_erf2x2(v01, v23);
-                else if (ACT == 2) {
-                    v01.x = fmaxf(v01.x, 0.f); v01.y = fmaxf(v01.y, 0.f);
-                    v23.x = fmaxf(v23.x, 0.f); v23.y = fmaxf(v23.y, 0.f);
-                }
-                const int rl = 4 * lq;
-                const int col = (j * 16 + lr) ^ (lq << 4);
-                scratch[(rl + 0) * 64 + col] = v01.x;
-                scratch[(rl + 1) * 64 + col] = v01.y;
-                scratch[(rl + 2) * 64 + col] = v23.x;
-                scratch[(rl + 3) * 64 + col] = v23.y;
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int it = 0; it < 16 * (64 / CW) / 64; ++it) {
-                const int id = it * 64 + lane;
-                const int rl = id / (64 / CW), cl = (id % (64 / CW)) * CW;
-                const int m = m0 + i * 16 + rl, n = n0 + cl;
-                const int sw = ((rl >> 2) & 3) << 4;
-                float v[CW];
-#pragma unroll
-                for (int q = 0; q < CW; q += 4) {
-                    const float4 x = *reinterpret_cast<const float4*>(scratch + rl * 64 + ((cl + q) ^ sw));
-                    v[q] = x.x; v[q + 1] = x.y; v[q + 2] = x.z; v[q + 3] = x.w;
-                }
-                if (m < M && n < N) {
-                    const int orow = row_map ? row_map[m] : m;
-                    if (orow >= 0) {
-                        if (resid) {
-                            const int rrow = resid_mod > 0 ? (m % resid_mod) : orow;
-                            const float* rp = resid + (size_t)rrow * ldr + n;
-#pragma unroll
-                            for (int q = 0; q < CW; q += 4) {
-                                const float4 x = *reinterpret_cast<const float4*>(rp + q);
-                                v[q] += x.x; v[q + 1] += x.y; v[q + 2] += x.z; v[q + 3] += x.w;
-                            }
-                        }
-                        if (OUT_BF16) {
-                            U128 o;
-                            o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-                            o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-                            o.z = (uint32_t)f2bf(v[4 % CW]) | ((uint32_t)f2bf(v[5 % CW]) << 16);
-                            o.w = (uint32_t)f2bf(v[6 % CW]) | ((uint32_t)f2bf(v[7 % CW]) << 16);
-                            *reinterpret_cast<U128*>(reinterpret_cast<u16*>(Cv) + (size_t)orow * ldc + n) = o;
-                        } else {
-                            *reinterpret_cast<float4*>(reinterpret_cast<float*>(Cv) + (size_t)orow * ldc + n) =
-                                make_float4(v[0], v[1], v[2], v[3]);
-                        }
-                    }
-                }
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // scratch reads done before reuse
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) acc[i][j][e] = 0.f;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outstanding at exit
-#undef G2_READ
-#undef G2_MFMA
-}
-
 // ------------------------------------------------------------------------------------------
 // Persistent 256x256 kernel, staggered 4-phase schedule (k_gemm256p).
 //
-// Same tile, waves (2 M x 4 N, 128x64 per wave, v_mfma_f32_16x16x32_bf16) and persistent K-tile
-// walk as k_gemm256, but every K-tile (BK = 64) runs as 4 phases, one output quadrant (64x32) of
+// 256x256 tiles, 8 waves (2 M x 4 N, 128x64 per wave, v_mfma_f32_16x16x32_bf16), a persistent
+// K-tile walk (the first form, one MFMA block per K-tile, is in the git history); every K-tile (BK = 64) runs as 4 phases, one output quadrant (64x32) of
 // the wave each:  P1 (0,0)  P2 (0,1)  P3 (1,1)  P4 (1,0).  A phase = memory section (fragment
 // reads + one half-tile of LDS-DMA staging) | s_barrier | 16 MFMAs | s_barrier.  Waves 4-7 run one
 // barrier behind waves 0-3, so on every SIMD one wave's memory section overlaps its partner's
@@ -1407,13 +1204,15 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
 #undef QEPI
 }
 
-// 0: k_gemm256, 1: k_gemm256p (staggered 4-phase schedule), 2: k_gemm256p unstaggered,
+// 1: k_gemm256p (staggered 4-phase schedule), 2: k_gemm256p unstaggered, 3 / 4: k_gemm256p
+// diagnostic builds (no epilogue / no global stores: wrong results, timing ablations only),
 // 5 (default): k_gemm256q for bf16 outputs, k_gemm256p otherwise, 6: k_gemm256q wherever it applies
 static int g_gemm_variant = [] {
     const char* e = getenv("BF_GEMM_VARIANT");
-    return e ? atoi(e) : 5;
+    const int v = e ? atoi(e) : 5;
+    return v >= 1 && v <= 6 ? v : 5;
 }();
-BF_API void bf_gemm_set_variant(int v) { g_gemm_variant = v; }
+BF_API void bf_gemm_set_variant(int v) { g_gemm_variant = v >= 1 && v <= 6 ? v : 5; }
 BF_API int bf_gemm_get_variant(void) { return g_gemm_variant; }
 
 // row panels per tile group (tile_coords); 1 = row-major.  Default 8, env BF_GEMM_GROUP_M.
@@ -1431,21 +1230,14 @@ static void launch_gemm256(int grid, hipStream_t st, const void* A, int lda, con
                            int tiles_m) {
     static bool attr = false;
     if (!attr) {
-        hipFuncSetAttribute((const void*)k_gemm256<OB, AC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            G2_LDS);
         hipFuncSetAttribute((const void*)k_gemm256p<OB, AC>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             G2_LDS);
         attr = true;
     }
-    if (g_gemm_variant >= 1)
-        hipLaunchKernelGGL((k_gemm256p<OB, AC>), dim3(grid), dim3(G2_THREADS), G2_LDS, st, (const u16*)A,
-                           lda, (const u16*)W, ldw, bias, resid, ldr, resid_mod, C, ldc, row_map, M, N,
-                           K, tiles_n, tiles_m, g_gemm_variant == 2 ? 0 : 1, g_group_m,
-                           (g_gemm_variant == 3 || g_gemm_variant == 4) ? g_gemm_variant - 2 : 0);
-    else
-        hipLaunchKernelGGL((k_gemm256<OB, AC>), dim3(grid), dim3(G2_THREADS), G2_LDS, st, (const u16*)A,
-                           lda, (const u16*)W, ldw, bias, resid, ldr, resid_mod, C, ldc, row_map, M, N,
-                           K, tiles_n, tiles_m, g_group_m);
+    hipLaunchKernelGGL((k_gemm256p<OB, AC>), dim3(grid), dim3(G2_THREADS), G2_LDS, st, (const u16*)A,
+                       lda, (const u16*)W, ldw, bias, resid, ldr, resid_mod, C, ldc, row_map, M, N,
+                       K, tiles_n, tiles_m, g_gemm_variant == 2 ? 0 : 1, g_group_m,
+                       (g_gemm_variant == 3 || g_gemm_variant == 4) ? g_gemm_variant - 2 : 0);
 }
 
 static int g_force_small = 0;

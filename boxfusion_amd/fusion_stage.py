@@ -24,6 +24,7 @@ import queue
 import sys
 import threading
 import time
+import warnings
 
 import numpy as np
 import torch
@@ -54,7 +55,11 @@ class FusionStage:
         self.H, self.W = H, W
         self.gap = int(cfg["data"].get("gap", 1)) if "data" in cfg else 1
         self._bm = BoxManager(cfg)
-        self._fuser = BoxFusion(cfg, device=device, legacy_promotion=legacy_promotion)
+        with warnings.catch_warnings():
+            # the CA-1M branch's missing K_depth.txt: the stream's K replaces it right below
+            # (demo.py:117-118 does the same before the first fusion)
+            warnings.filterwarnings("ignore", message="BoxFusion: .*K_depth.txt not found")
+            self._fuser = BoxFusion(cfg, device=device, legacy_promotion=legacy_promotion)
         self._fuser.update_intrinsics((W, H), self.K3)
         self._fuser.update_K_flag = True
         self.stale_last_frame = stale_last_frame

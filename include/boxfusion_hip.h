@@ -346,8 +346,9 @@ int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bi
  * (process-wide): 1 forces the 128x128 kernel, -1 the 256x256 kernel (aligned shapes), 0 the
  * heuristic. */
 void bf_gemm_force_small_tiles(int on);
-/* Persistent 256x256 kernel variant: 0 = k_gemm256 (one barrier per K-tile), 1 = k_gemm256p
- * (staggered 4-phase schedule), 5 = k_gemm256q (k_gemm256p's K loop, epilogue of each 64x32
+/* Persistent 256x256 kernel variant: 1 = k_gemm256p (staggered 4-phase schedule), 2 = k_gemm256p
+ * unstaggered, 3 / 4 = timing ablations of k_gemm256p (no epilogue / no global stores: wrong
+ * results), 5 = k_gemm256q (k_gemm256p's K loop, epilogue of each 64x32
  * quadrant overlapped with the next phases' MFMAs) for bf16 outputs and k_gemm256p for the rest
  * (default; env BF_GEMM_VARIANT), 6 = k_gemm256q for every eligible shape (no row map / broadcast
  * residual, K >= 192, N <= 8192).  Test/benchmark hook; results agree to f32 rounding. */
@@ -356,13 +357,13 @@ int bf_gemm_get_variant(void);
 /* Row panels per tile group of the persistent kernels' tile order (default 8; 1 = row-major).
  * Test/benchmark hook; results are identical in value. */
 void bf_gemm_set_group_m(int g);
-/* 1 if an aligned (16-B rows) problem of this shape runs the 256x256 kernel (k_gemm256), 0 if the
+/* 1 if an aligned (16-B rows) problem of this shape runs a 256x256 kernel (k_gemm256p/q), 0 if the
  * 128x128 one (k_gemm) — lets profilers attribute launches to kernels. */
 int bf_gemm_large_tiles(int M, int N, int K);
 /* Number of CUs the GEMM may assume (sizes the persistent grid); 0 = all CUs of the device.
  * Set when GEMMs launch on a CU-masked stream. */
 void bf_gemm_set_cu_budget(int n);
-/* The budget set above (0 = none); the persistent attention kernels size their grids by it too. */
+/* The budget set above (0 = none). */
 int bf_gemm_get_cu_budget(void);
 /* Persistent-grid sizing of the 256x256 kernel: 1 (default; env BF_GEMM_BALANCED=0 turns it
  * off) launches ceil(tiles / rounds) workgroups so every block walks the same tile count and a
@@ -407,10 +408,8 @@ int bf_attention_fp8out(const void* q, const void* k, const void* v, void* o, in
                         float out_qscale, void* stream);
 /* Attention kernel variant (test/benchmark hook; env BF_ATTN_VARIANT): 6 (default) = k_attn2
  * (deferred-max softmax, row sums from a ones row of V on the MFMA, 9-wave workgroups for short
- * heads), 7 / 8 = k_attn2 with 5 / 3 waves per workgroup, 1 / 2 = k_attn_s (64-key tiles through
- * a double-buffered LDS ring, with / without the XCD block order), 3 = k_attn_r (resident K/V
- * filled by LDS-DMA when all queries fit one workgroup and sk <= 320, else k_attn_s),
- * 4 / 5 = k_attn_s with 5 / 3 waves, 0 = k_attn (first kernel). */
+ * heads, output rows staged in LDS and stored as whole head rows), 27 = the same kernel with
+ * per-lane fragment stores (bit-identical). */
 void bf_attention_set_variant(int v);
 
 /* CuTR decoder cross-attention bias (GlobalCrossAttention.rpe + the logits' bias / clip /

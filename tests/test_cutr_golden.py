@@ -92,20 +92,26 @@ def instance_arrays(r):
 
 
 def match_instances(got, g, box_px=0.5):
-    """pair each golden instance with the got instance of the same class whose 2-D box is nearest
-    (boxes of different proposals sit >= 8 px apart; the same proposal appears at most once per
-    class).  Returns (golden index, got index) pairs and the unpaired golden indices."""
-    pairs, unpaired, used = [], [], set()
-    for i in range(len(g["scores"])):
-        d = np.abs(got["pred_boxes"] - g["pred_boxes"][i]).max(1)
-        d[got["pred_classes"] != g["pred_classes"][i]] = np.inf
-        j = int(np.argmin(d))
-        if d[j] <= box_px and j not in used:
-            pairs.append((i, j))
-            used.add(j)
-        else:
-            unpaired.append(i)
-    return pairs, unpaired
+    """pair golden instances with got instances of the same class whose 2-D box AND projected 3-D
+    centre agree within box_px (random-weight boxes often clamp to the same image-sized 2-D box, so
+    the 2-D box alone is ambiguous; the projected centre separates such proposals), closest pairs
+    first, each instance used once.  Returns (golden index, got index) pairs sorted by golden index
+    and the unpaired golden indices."""
+    d = np.maximum(np.abs(g["pred_boxes"][:, None] - got["pred_boxes"][None]).max(-1),
+                   np.abs(g["pred_proj_xy"][:, None] - got["pred_proj_xy"][None]).max(-1))
+    d[g["pred_classes"][:, None] != got["pred_classes"][None]] = np.inf
+    pairs, used_g, used_h = [], set(), set()
+    for flat in np.argsort(d, axis=None, kind="stable"):
+        i, j = divmod(int(flat), d.shape[1])
+        if d[i, j] > box_px:
+            break
+        if i in used_g or j in used_h:
+            continue
+        pairs.append((i, j))
+        used_g.add(i)
+        used_h.add(j)
+    pairs.sort()
+    return pairs, [i for i in range(len(g["scores"])) if i not in used_g]
 
 
 @pytest.fixture(scope="module")
