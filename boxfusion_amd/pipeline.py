@@ -260,6 +260,14 @@ def scene_instances(det, device, H=480, W=640):
     return p
 
 
+def _viz_images(viz, rgb, depth, j):
+    """(image, depth) of frame j on the host for a FrameLogger that logs images (demo.py:180-190
+    logs the RGB frame and the raw depth of every frame); (None, None) otherwise"""
+    if not getattr(viz, "log_images", False) or rgb is None:
+        return None, None
+    return rgb[j].cpu().numpy(), depth[j].cpu().numpy()
+
+
 class Pipeline:
     """demo.py run() over a stream of (rgb, depth, pose) frames: every frame goes through the
     per-frame preprocessing, keyframes (count % gap == 0) through CuTR + CLIP, and the fusion
@@ -272,9 +280,9 @@ class Pipeline:
         """frames(ids) -> (rgb [b,H,W,3] u8 dev, depth [b,H,W] f32 dev, poses [b,4,4] host).
         per_frame: the frames between keyframes get demo.py:121-131's per-frame work too
         (DetectStage.preprocess_frames, up to `frames_per_call` frames per call).
-        viz: a visualize.FrameLogger -- demo.py's per-frame rerun calls (pose, pinhole, trajectory)
-        for every frame and the global boxes after each keyframe's fusion (host side, after the
-        frame's GPU work; not used by the bench)."""
+        viz: a visualize.FrameLogger -- demo.py's per-frame rerun calls (pose, pinhole, image,
+        depth, trajectory) for every frame in frame order and the global boxes after each
+        keyframe's fusion (host side, after the frame's GPU work; not used by the bench)."""
         B = self.detect.B
         kf = [i for i in range(n_frames) if i % self.gap == 0]
         self.frames_preprocessed = 0
@@ -284,11 +292,12 @@ class Pipeline:
             if per_frame:
                 nk = [i for i in range(ids[0], min(ids[-1] + self.gap, n_frames)) if i % self.gap != 0]
                 for c in range(0, len(nk), frames_per_call):
-                    _, depth, poses = frames(nk[c:c + frames_per_call])
+                    _rgb, depth, poses = frames(nk[c:c + frames_per_call])
                     self.detect.preprocess_frames(depth.contiguous(), poses)
                     self.frames_preprocessed += len(nk[c:c + frames_per_call])
                     if viz is not None:
-                        nk_pose.update(zip(nk[c:c + frames_per_call], np.asarray(poses)))
+                        for j, i in enumerate(nk[c:c + frames_per_call]):
+                            nk_pose[i] = (np.asarray(poses[j]),) + _viz_images(viz, _rgb, depth, j)
             rgb, depth, poses = frames(ids)
             if len(ids) < B:   # ragged tail: pad the batch with the last frame, drop its results
                 pad = B - len(ids)
@@ -301,11 +310,11 @@ class Pipeline:
                 if viz is not None:
                     # demo.py order: keyframe i's frame logs, its boxes after the fusion step, then
                     # the frames up to the next keyframe (the trajectory grows frame by frame)
-                    viz.frame(i, poses[j])
+                    viz.frame(i, poses[j], *_viz_images(viz, rgb, depth, j))
                     viz.boxes(self.fusion.all_pred_box, i)
                     for f in range(i + 1, min(i + self.gap, n_frames)):
                         if f in nk_pose:
-                            viz.frame(f, nk_pose[f])
+                            viz.frame(f, *nk_pose[f])
         last = n_frames - 1
         if last % self.gap != 0:
             _, _, p = frames([last])

@@ -233,7 +233,7 @@ class FrameLogger:
 
     def __init__(self, recording, K_image, image_size, K_depth=None, depth_size=None, fps=30.0,
                  trajectory=True, show_class=False, show_label=True, log_images=True, save_ply=False,
-                 out_dir="./result"):
+                 out_dir="./result", depth_invalid_nan=False):
         self.rec = recording
         self.K_image, self.image_size = np.asarray(K_image, np.float64), list(image_size)
         self.K_depth = None if K_depth is None else np.asarray(K_depth, np.float64)
@@ -242,6 +242,11 @@ class FrameLogger:
         self.trajectory = trajectory
         self.show_class, self.show_label = show_class, show_label
         self.log_images, self.save_ply, self.out_dir = log_images, save_ply, out_dir
+        # depth_invalid_nan: the logged depth with its <= 0 pixels as NaN -- what demo.py:190 logs
+        # on a --device cpu run, where Preprocessor.standardize_depth_map's in-place NaN fill
+        # (preprocessor.py:102) reaches the sample's own depth tensor (on a GPU run the .cpu()
+        # copy keeps the logged depth raw)
+        self.depth_invalid_nan = depth_invalid_nan
         self.traj_xyz = []
 
     def frame(self, count, RT, image=None, depth=None, xyzrgb=None, timestamp=None):
@@ -258,7 +263,10 @@ class FrameLogger:
         r.log("/device/wide/image", cam)
         self.traj_xyz.append(RT[:3, 3].copy())
         if depth is not None and self.log_images and self.K_depth is not None:
-            r.log("/device/wide/depth", DepthImage(image=np.asarray(depth)))
+            depth = np.asarray(depth)
+            if self.depth_invalid_nan:
+                depth = np.where(depth <= 0, np.float32(np.nan), depth).astype(depth.dtype)
+            r.log("/device/wide/depth", DepthImage(image=depth))
             r.log("/device/wide/depth", Pinhole(image_from_camera=self.K_depth, resolution=self.depth_size))
         if xyzrgb is not None:
             xyzrgb = np.asarray(xyzrgb)

@@ -2,8 +2,9 @@
 gap 25 whose last frame is not a keyframe (so the stale last-frame re-fusion of demo.py:200,
 SURVEY §8 quirk 1, fires), recording what run() writes: the global boxes and the framewise
 boxes / class indices / CLIP features (save_box, demo.py:368-387), the box manager's final
-fusion lists, and every box's world-space geometry (transform2world + project_3d_boxes as the
-reference computed them, keyed by init_id).
+fusion lists, every box's world-space geometry (transform2world + project_3d_boxes as the
+reference computed them, keyed by init_id), and every rerun.log call of the run with vis.rerun on
+(demo.py:93-197, 329-330; tools/utils.py:37-96) through a recording rerun stand-in.
 
 run()'s arguments are the only things supplied from outside:
   * model: returns the seeded scene's detections of the next keyframe as Instances3D in the
@@ -49,6 +50,64 @@ for name in ("rerun", "rerun.blueprint", "open_clip"):
     mod.__getattr__ = lambda attr: _Any()
     sys.modules[name] = mod
 sys.modules["rerun"].blueprint = sys.modules["rerun.blueprint"]
+
+# A recording rerun: demo.py's (and tools/utils.visualize_online_boxes's) rerun.log calls become
+# plain records -- entity path, time, archetype and its fields (images as shape + adler32, the
+# trajectory strip as its length, sum and last point) -- in call order.
+RERUN_LOG = []
+_RR_TIME = [None]
+
+
+class _Arch(dict):
+    def __init__(self, kind, **fields):
+        super().__init__(fields)
+        self.kind = kind
+
+    def compress(self, *a, **k):          # rerun.Image(...).compress()
+        return self
+
+
+def _arch(kind):
+    return lambda *a, **k: _Arch(kind, _args=a, **k)
+
+
+def _f(x):
+    return np.asarray(x, np.float64).tolist()
+
+
+def _rr_log(path, arch, *a, **k):
+    import zlib
+    kind = arch.kind
+    rec = {"path": path, "time": _RR_TIME[0], "kind": kind}
+    if kind == "Transform3D":
+        rec.update(translation=_f(arch["translation"]), quaternion_xyzw=_f(arch["rotation"]["xyzw"]))
+    elif kind == "Pinhole":
+        rec.update(image_from_camera=_f(arch["image_from_camera"]), resolution=_f(arch["resolution"]))
+    elif kind in ("Image", "DepthImage"):
+        img = np.ascontiguousarray(np.asarray(arch["_args"][0]))
+        rec.update(shape=list(img.shape), dtype=str(img.dtype), adler32=zlib.adler32(img.tobytes()))
+    elif kind == "LineStrips3D":
+        strip = np.asarray(arch["_args"][0][0], np.float64).reshape(-1, 3)
+        rec.update(n=len(strip), sum=float(strip.sum()), last=_f(strip[-1]) if len(strip) else [],
+                   colors=_f(arch["colors"]))
+    elif kind == "Boxes3D":
+        rec.update(centers=_f(arch["centers"]), sizes=_f(arch["sizes"]),
+                   quaternions_xyzw=[_f(q["xyzw"]) for q in arch["quaternions"]],
+                   colors=[_f(c) for c in arch["colors"]], labels=[str(x) for x in arch["labels"]],
+                   show_labels=bool(arch["show_labels"]))
+    else:
+        rec.update(fields=sorted(arch))
+    RERUN_LOG.append(rec)
+
+
+_rr = sys.modules["rerun"]
+_rr.log = _rr_log
+_rr.set_time_seconds = lambda timeline, t, **k: _RR_TIME.__setitem__(0, [timeline, float(t)])
+_rr.new_recording = lambda *a, **k: _Any()
+_rr.spawn = lambda *a, **k: None
+_rr.Quaternion = lambda xyzw: {"xyzw": np.asarray(xyzw, np.float64)}
+for _kind in ("Transform3D", "Pinhole", "Image", "DepthImage", "Points3D", "LineStrips3D", "Boxes3D"):
+    setattr(_rr, _kind, _arch(_kind))
 # retriev's cv2.resize (tools/utils.py:395): the stand-in CLIP ignores pixels
 sys.modules["cv2"].resize = lambda img, size, *a, **k: np.zeros((size[1], size[0], 3), np.uint8)
 
@@ -76,7 +135,8 @@ def cfg_demo(out_dir):
     c["detection"] = dict(score_thresh=0.5, uv_bound=True, uv_bound_value=0.9, floor_mask=True,
                           floor_ratio=15, scale_box=1.5, class_sim_thres=25.0, size_max_thres=None)
     c["box_fusion"] = dict(c["box_fusion"], clip_sim_coeff=1.0)
-    c["vis"] = dict(rerun=False, show_class=False, show_label=False, trajectory=False)
+    # demo.py's rerun logging on (re_vis=True below; it only gates the log calls), recorded
+    c["vis"] = dict(rerun=True, show_class=False, show_label=False, trajectory=True)
     c["eval"] = True
     return c
 
@@ -178,7 +238,7 @@ def main():
         demo.run(cfg, SceneModel(scene, keyframes), Stream(scene), StubCLIP(text), None, names, text.clone(),
                  Augmentor(("wide/image", "wide/depth")), Preprocessor(),
                  score_thresh=cfg["detection"]["score_thresh"], viz_on_gt_points=False, gap=GAP,
-                 re_vis=False)
+                 re_vis=True)
     # fitness evaluations past the reference kernel's corners_i[36] / convex_inter[8]
     # (box_fusion.py:378-384): the run is the reference's with the exact hull there
     hull_over = np.asarray(MG.OR.hull_overflow(), np.int64)
@@ -199,7 +259,8 @@ def main():
                num_record=np.array([bm.num_record[k] for k in sorted(bm.num_record)], np.int64),
                geom_tensor=np.stack([geom[i][0] for i in range(len(geom))]),
                geom_R=np.stack([geom[i][1] for i in range(len(geom))]),
-               geom_proj=np.stack([geom[i][2] for i in range(len(geom))]), hull_over=hull_over)
+               geom_proj=np.stack([geom[i][2] for i in range(len(geom))]), hull_over=hull_over,
+               rerun_json=np.array(__import__("json").dumps(RERUN_LOG)))
     assert sorted(geom) == list(range(len(geom)))
     np.savez_compressed(os.path.join(HERE, "demo_gap25.npz"), **out)
     print("demo golden:", {k: getattr(v, "shape", v) for k, v in out.items()})

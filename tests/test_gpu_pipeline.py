@@ -5,6 +5,8 @@ given the same world-space boxes and projections.  The GPU transform2world / pro
 the reference's torch-CPU ones by ~1 ulp (test_gpu_fusion.py pins them at 2e-6 / 2e-3 px), and the
 particle search amplifies ulps, so with its own geometry the chain is checked only over the first
 keyframes (test_fusion_stage_own_geometry)."""
+import json
+
 import numpy as np
 import pytest
 import torch
@@ -96,7 +98,8 @@ def test_fusion_stage_own_geometry(dev):
 # first keyframe whose decisions (fusion lists, fused lists) differ from the reference when the
 # chain runs on the GPU's own transform2world / projection (None: identical to the end); measured
 # on MI355X, see DESIGN.md §2
-OWN_GEOMETRY_FIRST_DIVERGENCE = {}
+OWN_GEOMETRY_FIRST_DIVERGENCE = {"fusion_trace.npz": None, "fusion_trace_small.npz": 13,
+                                 "fusion_trace_ca1m.npz": None, "fusion_trace_faceon.npz": None}
 
 
 @pytest.mark.parametrize("name", TU.TRACES)
@@ -107,7 +110,6 @@ def test_fusion_stage_own_geometry_decisions(dev, name):
     until the first divergence, unfused boxes agree within 1e-4 (north_star's box tolerance) and
     the fused boxes' error (the particle search amplifies ulp-level hull differences) is
     reported.  Writes gpurun_out/own_geometry_<trace>.json when that directory exists."""
-    import json
     import os
     from boxfusion_amd.fusion_stage import FusionStage
     from boxfusion_amd.pipeline import scene_instances
@@ -512,6 +514,38 @@ class _DemoDetect:
         return [p]
 
 
+def _assert_rerun_records(got, want):
+    """FrameLogger records (visualize.Recording) vs the reference's recorded rerun.log calls"""
+    import zlib
+    assert len(got) == len(want), (len(got), len(want))
+    for i, ((path, t, kind, a), w) in enumerate(zip(got, want)):
+        msg = f"record {i}: {w['path']} {w['kind']}"
+        assert (path, kind) == (w["path"], w["kind"]), msg
+        assert list(t) == w["time"], msg
+        if kind == "Transform3D":
+            np.testing.assert_allclose(a["translation"], w["translation"], rtol=0, atol=1e-6, err_msg=msg)
+            np.testing.assert_allclose(a["quaternion_xyzw"], w["quaternion_xyzw"], rtol=0, atol=1e-9, err_msg=msg)
+        elif kind == "Pinhole":
+            np.testing.assert_array_equal(np.asarray(a["image_from_camera"], np.float64), w["image_from_camera"], err_msg=msg)
+            np.testing.assert_array_equal(np.asarray(a["resolution"], np.float64), w["resolution"], err_msg=msg)
+        elif kind in ("Image", "DepthImage"):
+            img = np.ascontiguousarray(a["image"])
+            assert [list(img.shape), str(img.dtype), zlib.adler32(img.tobytes())] == \
+                [w["shape"], w["dtype"], w["adler32"]], msg
+        elif kind == "LineStrips3D":
+            strip = np.asarray(a["strips"][0], np.float64).reshape(-1, 3)
+            assert len(strip) == w["n"], msg
+            np.testing.assert_allclose(strip.sum(), w["sum"], rtol=1e-12, atol=1e-9, err_msg=msg)
+            np.testing.assert_array_equal(np.asarray(a["colors"], np.float64), w["colors"], err_msg=msg)
+        elif kind == "Boxes3D":
+            np.testing.assert_allclose(a["centers"], w["centers"], rtol=0, atol=1e-5, err_msg=msg)
+            np.testing.assert_allclose(a["sizes"], w["sizes"], rtol=0, atol=1e-6, err_msg=msg)
+            np.testing.assert_allclose(a["quaternions_xyzw"], w["quaternions_xyzw"], rtol=0, atol=1e-6, err_msg=msg)
+            np.testing.assert_allclose(np.asarray(a["colors"], np.float64).reshape(-1, 3),
+                                       np.asarray(w["colors"]).reshape(-1, 3), rtol=0, atol=1e-12, err_msg=msg)
+            assert a["labels"] == w["labels"] and a["show_labels"] == w["show_labels"], msg
+
+
 @pytest.mark.parametrize("native", [True, False])
 def test_pipeline_run_vs_reference_demo_gap25(dev, native, monkeypatch):
     """Pipeline.run + FusionStage (keyframes every 25 frames, stale re-fusion of the non-keyframe
@@ -551,12 +585,17 @@ def test_pipeline_run_vs_reference_demo_gap25(dev, native, monkeypatch):
 
     from boxfusion_amd.visualize import FrameLogger, Recording
     rec = Recording(forward=False)
-    viz = FrameLogger(rec, SCANNET_K, (640, 480), show_class=True)
+    # the golden run's vis config (make_golden_demo.cfg_demo): trajectory on, no class / id labels
+    # shown; timestamps = frame index (the synthetic stream's meta timestamp); a --device cpu run,
+    # so the logged depth carries the preprocessor's in-place NaN fill
+    viz = FrameLogger(rec, SCANNET_K, (640, 480), K_depth=SCANNET_K, depth_size=(640, 480), fps=1.0,
+                      show_class=False, show_label=False, depth_invalid_nan=True)
     pipe = Pipeline(det, fusion, gap)
     pipe.run(frames, n, viz=viz)
     assert pipe.frames_preprocessed == det.frames_done == n - len(range(0, n, gap))
-    # f4: every frame's pose logged once, the global boxes after each keyframe and the last frame
-    # (demo.py:330), the last of them the final global boxes
+    # f4: the REFERENCE's own rerun.log calls (demo.py:93-197, 329-330, tools/utils.py:37-96,
+    # recorded by make_golden_demo.py) call by call: entity path, time, archetype and its fields
+    _assert_rerun_records(rec.records, json.loads(str(d["rerun_json"])))
     poses = [a for p_, _, k, a in rec.records if p_ == "/world/image" and k == "Transform3D"]
     assert len(poses) == n
     # frame order (demo.py:108): the pose records are frames 0..n-1 in turn, so the trajectory
@@ -569,7 +608,7 @@ def test_pipeline_run_vs_reference_demo_gap25(dev, native, monkeypatch):
     assert len(boxes_logged) == len(range(0, n, gap)) + 1
     fin = fusion.all_pred_box
     np.testing.assert_array_equal(boxes_logged[-1]["centers"], fin.pred_boxes_3d.tensor[:, :3].cpu().numpy())
-    assert boxes_logged[-1]["labels"] == [str(c) for c in fin.categories]
+    assert boxes_logged[-1]["labels"] == [str(i) for i in range(len(fin))]
     bm = fusion.box_manager
     ragged = lambda flat, off: [flat[off[i]:off[i + 1]].tolist() for i in range(len(off) - 1)]
     assert bm.fusion_list == ragged(d["fusion_list_flat"], d["fusion_list_off"])

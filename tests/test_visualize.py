@@ -144,7 +144,7 @@ def test_pipeline_viz_frame_order():
             self.seq = []
             self.lg = V.FrameLogger(V.Recording(forward=False), np.eye(3), (4, 4))
 
-        def frame(self, i, pose):
+        def frame(self, i, pose, *images):
             self.seq.append(("frame", i))
             self.lg.frame(i, pose)
 
