@@ -1,7 +1,8 @@
 """bf_depth_standardize / bf_depth_preprocess timing on the path's shapes (8 and 192 frames of
 480x640, 8 of 256x192) with HIP events, the algorithmic GB/s (read 4 B + write 4 B per pixel;
-+13 B with the back-projection), and an A/B against the round-2 single-workgroup kernel when
-scripts/_ab/libds_old.so exists (params and outputs bit for bit)."""
++13 B with the back-projection), and an A/B against an earlier build of bf_depth.hip when
+scripts/_ab/libds_old.so exists (params and outputs bit for bit; round 4: the 7-launch form,
+built from the previous commit's bf_depth.hip)."""
 import ctypes
 import os
 import sys
@@ -16,13 +17,18 @@ OLD = os.path.join(ROOT, "scripts", "_ab", "libds_old.so")
 old = ctypes.CDLL(OLD) if os.path.exists(OLD) else None
 
 
+_OLD_WS = {}
+
+
 def run_old(d):
     b, h, w = d.shape
     out = torch.empty_like(d)
     p = torch.empty((b, 2), device=d.device)
     st = torch.cuda.current_stream().cuda_stream
+    ws = _OLD_WS.setdefault((b, h, w), _lib.new_depth_workspace(b, h, w, d.device))
     rc = old.bf_depth_standardize(ctypes.c_void_p(d.data_ptr()), b, h, w, ctypes.c_void_p(out.data_ptr()),
-                                  ctypes.c_void_p(p.data_ptr()), None, ctypes.c_void_p(st))
+                                  ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+                                  ctypes.c_void_p(st))
     assert rc == 0
     return out, p
 
