@@ -72,8 +72,8 @@ groups = {"k_gemm256p": [r"k_gemm256p<\w+, \d, 0>", r"k_gemm256q<"],
           "k_gemm256p<true, 1>": [r"k_gemm256p<true, 1, 0>", r"k_gemm256q<true, 1,"],
           "k_gemm256p_fp8": [r"k_gemm256p<\w+, \d, [13]>"],
           "k_attn": ["k_attn"],
-          "k_attn_clip": ["k_attn_clip", "k_attn_s<80", "k_attn_r<80", "k_attn2<80", "k_attn6<80"],
-          "k_attn_cutr": ["k_attn_s<64", "k_attn_w", "k_attn_g", "k_attn2<64"]}
+          "k_attn_clip": ["k_attn2<80"],
+          "k_attn_cutr": ["k_attn2<64"]}
 out = {"round": int(re.match(r"r(\d+)", R).group(1)), "workload": R, "method": (
     "rocprofv3 --pmc FETCH_SIZE --kernel-trace, a separate --pmc WRITE_SIZE pass and an SQ "
     "instruction-count pass over `bench.py --steps 2 --warmup 1 --eager --inflight 1`; per-dispatch "
