@@ -264,14 +264,15 @@ def unpack_records(recs, cnts, dev, clip=None, crops=16, clip_coeff=1.0):
     return p
 
 
-def gather_step(recs, clip, dist, world):
+def gather_step(recs, clip, dist, world, force=False):
     """Exchange of one step: every rank's per-frame records [b, R] (detections, count and camera
     pose) and CLIP rows [b*crops, CLIP_W] are all-gathered with all_gather_into_tensor (RCCL over
     xGMI on the GPU; gloo on CPU tensors in the rehearsal and the tests: the same call sequence)
     so that the fusion owner sees the step's frames in global frame order (rank-major = frame
     order, since rank r holds frames step*b*world + r*b ... + b-1).  On the GPU both collectives
-    are asynchronous device operations: nothing here waits for the detect stream."""
-    if dist is None or world == 1:
+    are asynchronous device operations: nothing here waits for the detect stream.  force: run
+    the collectives at world 1 too (the one-GPU RCCL test)."""
+    if dist is None or (world == 1 and not force):
         return recs, clip
     if recs.is_cuda and dist.get_backend() == "gloo":     # BF_BENCH_REHEARSE=1 (one-GPU rehearsal)
         g_rec, g_clip = gather_step(recs.cpu(), clip.cpu(), dist, world)

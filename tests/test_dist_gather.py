@@ -56,3 +56,44 @@ def test_gather_step_gloo_world2():
         p.join(timeout=60)
     assert res
     assert all(p.exitcode == 0 for p in procs)
+
+
+def _rccl_worker(port, q):
+    """one rank on cuda:0 over RCCL (backend "nccl" = RCCL on ROCm): bench.gather_step's
+    all_gather_into_tensor sequence on device tensors, forced at world size 1"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    import bench
+    from boxfusion_amd.synthetic import Scene
+    scene = Scene(seed=0)
+    frames = list(range(8))
+    recs = torch.from_numpy(bench.pack_records([scene.detections(f) for f in frames],
+                                               np.stack([scene.pose(f) for f in frames]))).to(dev)
+    clip = torch.arange(8 * 16 * bench.CLIP_W, dtype=torch.float32, device=dev).view(8 * 16, -1)
+    g_rec, g_clip = bench.gather_step(recs, clip, dist, 1, force=True)
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(g_rec, recs) and torch.equal(g_clip, clip) and g_rec.data_ptr() != recs.data_ptr())
+    g_rec, g_clip = bench.exchange_step(recs, clip, dist, 1, 8, 8, 16, 0)
+    ok = ok and bool(torch.equal(g_rec, recs))
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put(ok)
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_gather_step_rccl_world1():
+    """the RCCL branch of bench.gather_step on hardware (the 8-GPU run is the driver's)"""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    res = q.get(timeout=120)
+    p.join(timeout=60)
+    assert res and p.exitcode == 0
