@@ -77,7 +77,6 @@ def lib():
         _LIB.bf_obb_iou_workspace_size.restype = c_size_t
         _LIB.bf_obb_iou_workspace_size.argtypes = [c_int]
         _LIB.bf_depth_standardize_workspace_size.restype = c_size_t
-        _LIB.bf_gemm_workspace_size.restype = c_size_t
         _LIB.bf_depth_standardize_workspace_size.argtypes = [c_int, c_int, c_int]
     return _LIB
 
@@ -560,11 +559,9 @@ ACT = {None: 0, "none": 0, "gelu": 1, "relu": 2}
 
 
 def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype=torch.bfloat16,
-         row_map=None, m=None, ws=None):
+         row_map=None, m=None):
     """out[orow(r)] = resid[...] + act(a @ w.T + bias); a bf16 [M,K] (row stride a.stride(0)),
-    w bf16 [N,K]. `out` may be given (its row stride is used).  ws: a split-K workspace
-    (new_gemm_workspace; one per stream of concurrently running GEMMs) lets a partial last round
-    of tiles run split in K."""
+    w bf16 [N,K]. `out` may be given (its row stride is used)."""
     _need(a, torch.bfloat16, "a")
     _need(w, torch.bfloat16, "w")
     M = a.shape[0] if m is None else m
@@ -580,26 +577,14 @@ def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype
         _need(bias, torch.float32, "bias")
     if a.stride(1) != 1 or w.stride(1) != 1 or out.stride(1) != 1:
         raise HipError("gemm operands need unit column stride")
-    if ws is not None and (ws.dtype != torch.uint8 or not ws.is_cuda):
-        raise HipError("gemm ws: a uint8 device tensor from new_gemm_workspace")
-    _check(lib().bf_gemm_bf16_ws(c_void_p(a.data_ptr()), c_int(a.stride(0)), c_void_p(w.data_ptr()),
-                                 c_int(w.stride(0)), _ptr(bias) if bias is not None else None,
-                                 c_void_p(resid.data_ptr()) if resid is not None else None,
-                                 c_int(resid.stride(0) if resid is not None else 0), c_int(resid_mod),
-                                 c_void_p(out.data_ptr()), c_int(out.stride(0)), c_int(c_bf16),
-                                 _ptr(row_map) if row_map is not None else None, c_int(M), c_int(N),
-                                 c_int(K), c_int(ACT[act]),
-                                 c_void_p(ws.data_ptr()) if ws is not None else None,
-                                 ctypes.c_size_t(ws.numel() if ws is not None else 0), _stream()),
-           "bf_gemm_bf16_ws")
+    _check(lib().bf_gemm_bf16(c_void_p(a.data_ptr()), c_int(a.stride(0)), c_void_p(w.data_ptr()),
+                              c_int(w.stride(0)), _ptr(bias) if bias is not None else None,
+                              c_void_p(resid.data_ptr()) if resid is not None else None,
+                              c_int(resid.stride(0) if resid is not None else 0), c_int(resid_mod),
+                              c_void_p(out.data_ptr()), c_int(out.stride(0)), c_int(c_bf16),
+                              _ptr(row_map) if row_map is not None else None, c_int(M), c_int(N),
+                              c_int(K), c_int(ACT[act]), _stream()), "bf_gemm_bf16")
     return out
-
-
-def new_gemm_workspace(device):
-    """a caller-owned zero-filled split-K workspace for gemm(..., ws=) (one per stream of
-    concurrently running GEMMs)"""
-    size = int(lib().bf_gemm_workspace_size())
-    return torch.zeros(size, dtype=torch.uint8, device=device)
 
 
 def attention(q, k, v, o, batch, heads, sq, sk, head_dim, scale, q_bs=None, k_bs=None, v_bs=None,
@@ -943,10 +928,10 @@ _attention_fp8out_untimed = attention_fp8out
 
 
 def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype=torch.bfloat16,
-         row_map=None, m=None, ws=None):
+         row_map=None, m=None):
     t = _timer()
     if t is None:
-        return _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m, ws)
+        return _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m)
     M = a.shape[0] if m is None else m
     N, K = w.shape
     ob = (out.dtype if out is not None else out_dtype) == torch.bfloat16
@@ -956,7 +941,7 @@ def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype
     if resid is not None:
         nbytes += 4.0 * (M * N if not resid_mod else resid_mod * N)
     return t.record(tags, 2.0 * M * N * K, nbytes,
-                    lambda: _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m, ws))
+                    lambda: _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m))
 
 
 def gemm_fp8(a, w, scale, bias=None, act=None, resid=None, out=None, out_dtype=torch.bfloat16,

@@ -334,28 +334,6 @@ __device__ __forceinline__ void glds_buf16(const void* base, int nbytes, void* l
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, vo, so, 0, 0);
 }
 
-// Split-K partials cross XCDs: 16-B vector stores and loads with sc1 (written through, read past the
-// reading XCD's stale lines), signalled by agent-scope atomics after each storing wave's vmcnt(0)
-// (MI355X_MICROARCH.md, hand-off table row 1, per wave).  The loads are asm: the caller's waitcnt
-// below ties their results.
-// four blocks at p + 256 k floats (k = 0..3: immediate offsets, one address pair)
-__device__ __forceinline__ void sk_store16x4(float* p, f32x4 a, f32x4 b, f32x4 c, f32x4 d) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\t"
-                 "global_store_dwordx4 %0, %2, off offset:1024 sc1\n\t"
-                 "global_store_dwordx4 %0, %3, off offset:2048 sc1\n\t"
-                 "global_store_dwordx4 %0, %4, off offset:3072 sc1"
-                 :: "v"(p), "v"(a), "v"(b), "v"(c), "v"(d) : "memory");
-}
-// the same four blocks loaded, one wait for all four
-__device__ __forceinline__ void sk_load16x4(const float* p, f32x4 (&v)[4]) {
-    asm volatile("global_load_dwordx4 %0, %4, off sc1\n\t"
-                 "global_load_dwordx4 %1, %4, off offset:1024 sc1\n\t"
-                 "global_load_dwordx4 %2, %4, off offset:2048 sc1\n\t"
-                 "global_load_dwordx4 %3, %4, off offset:3072 sc1\n\t"
-                 "s_waitcnt vmcnt(0)"
-                 : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]) : "v"(p) : "memory");
-}
-
 // Grouped tile order of the persistent kernels: the linear tile index walks column-major inside
 // groups of `gm` row panels, so the 32 tiles an XCD runs concurrently (consecutive indices) form a
 // gm x (32/gm) patch -- gm A panels and 32/gm W panels per K-step in that XCD's L2 instead of
@@ -440,7 +418,7 @@ __device__ __forceinline__ i32x8 frag32(bf16x8 a, bf16x8 b) {
 // columns per lane, one 8-B store).  The fp8 lane fragment is the bf16 kernel's two k-step
 // fragments (16-B chunks lq and 4+lq of the 128-B row): the MFMA's k order inside a fragment only
 // has to agree between A and B, and the bf16 chunk pattern keeps the LDS reads conflict-free.
-template <bool OUT_BF16, int ACT, int F8 = 0, bool SK = false>
+template <bool OUT_BF16, int ACT, int F8 = 0>
 __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restrict__ A, int lda,
                                                             const u16* __restrict__ W, int ldw,
                                                             const float* __restrict__ bias,
@@ -449,10 +427,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
                                                             int ldc, const int32_t* __restrict__ row_map,
                                                             int M, int N, int K, int tiles_n,
                                                             int tiles_m, int stagger, int gm, int ablate,
-                                                            float csc = 1.f, float oqs = 1.f,
-                                                            int full_tiles = 0, int tail_kt = 0,
-                                                            int* __restrict__ sk_cnt = nullptr,
-                                                            float* __restrict__ sk_slab = nullptr) {
+                                                            float csc = 1.f, float oqs = 1.f) {
     extern __shared__ __attribute__((aligned(16))) unsigned char g_smem[];
 #if GEMM_TACC
     static_assert(F8 == 0, "fp8 operands use the default accumulator layout");
@@ -467,30 +442,10 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
     const int ntiles = tiles_m * tiles_n;
     const int G = gridDim.x;
     const int slot = (G % 8 == 0) ? ((int)blockIdx.x % 8) * (G / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
+    const int my_tiles = ntiles > slot ? (ntiles - slot + G - 1) / G : 0;
     const int nk = K / KTE;
-    // Work of this slot: whole tiles slot, slot + G, ... (data parallel), then -- split-K tail,
-    // sk_cnt != nullptr -- its share [fb, fe) of the last tiles' K-tiles flattened tile-major
-    // (tile full_tiles + u, K-tile k at u*nk + k; the host guarantees tail_kt >= G, so every slot
-    // has at least one K-tile and at most nk, i.e. at most two pieces: A = the end of tile u0 from
-    // K-tile klo, B = the start of tile u0+1).  B runs before A, so a tile's leading piece is done
-    // early and its trailing pieces arrive last.
-    static_assert(!SK || (ACT == 0 && F8 == 0), "split-K tail: linear bf16 GEMMs only");
-    const bool split = SK && sk_cnt != nullptr;
-    const int n_full = split ? full_tiles / G : (ntiles > slot ? (ntiles - slot + G - 1) / G : 0);
-    const long long fb = split ? (long long)slot * tail_kt / G : 0;
-    const long long fe = split ? (long long)(slot + 1) * tail_kt / G : 0;
-    const int u0 = (int)(fb / nk), klo = (int)(fb % nk);
-    const bool two_p = fe > (long long)(u0 + 1) * nk;
-    const int pa_end = two_p ? nk : (int)(fe - (long long)u0 * nk);
-    const int pb_end = two_p ? (int)(fe - (long long)(u0 + 1) * nk) : 0;
-    const int total = n_full * nk + (int)(fe - fb);
+    const int total = my_tiles * nk;
     if (total == 0) return;
-    // segment j of the walk: tile, first and end K-tile
-    auto seg_of = [&](int j, int& tile, int& kb, int& ke) {
-        if (!SK || j < n_full) { tile = slot + j * G; kb = 0; ke = nk; return; }
-        if (two_p && j == n_full) { tile = full_tiles + u0 + 1; kb = 0; ke = pb_end; return; }
-        tile = full_tiles + u0; kb = klo; ke = pa_end;
-    };
 
     // half-tile staging: wave w, instruction i fills local rows (2w+i)*8 + lane/8 of a half.
     // Buffer loads (LDS-DMA form): per-lane 32-bit byte offsets of the rows, computed once per
@@ -512,22 +467,19 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
     // K-tile coordinates of the walk, advanced incrementally (a division only at tile boundaries);
     // past the end of the walk the last K-tile is repeated (same bytes into the same stage)
-    // (kb / kend: the segment's first K element and its end; tile: the tile index)
-    struct KT { int idx, m0, n0, k0, buf, kb, kend, tile; };
-    auto kt_at_seg = [&](int j, int idx) {
-        int tile, kb, ke;
-        seg_of(j, tile, kb, ke);
+    struct KT { int idx, m0, n0, k0, buf; };
+    auto kt_at_tile = [&](int tile_k, int idx) {
+        const int tile = slot + tile_k * G;
         KT r;
-        r.idx = idx; tile_coords(tile, tiles_m, tiles_n, gm, r.m0, r.n0); r.buf = idx & 1;
-        r.k0 = kb * KTE; r.kb = kb * KTE; r.kend = ke * KTE; r.tile = tile;
+        r.idx = idx; tile_coords(tile, tiles_m, tiles_n, gm, r.m0, r.n0); r.k0 = 0; r.buf = idx & 1;
         return r;
     };
-    int seg_ord = 0;        // segment ordinal (within this block's walk) of the newest KT built
+    int tile_ord = 0;       // tile ordinal (within this block's walk) of the newest KT built
     auto kt_next = [&](KT c) {
         if (c.idx >= total - 1) return c;
-        if (c.k0 + KTE < (SK ? c.kend : K)) { c.k0 += KTE; c.idx += 1; c.buf ^= 1; return c; }
-        ++seg_ord;
-        return kt_at_seg(seg_ord, c.idx + 1);
+        if (c.k0 + KTE < K) { c.k0 += KTE; c.idx += 1; c.buf ^= 1; return c; }
+        ++tile_ord;
+        return kt_at_tile(tile_ord, c.idx + 1);
     };
     // per-lane row byte offsets of a K-tile's tile ([0..1] A-half h row i, [2..3] B-half)
     struct VO { int a[2][2], b[2][2]; };
@@ -562,9 +514,9 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
 #if GEMM_TACC
     // transposed accumulators: lane (lr, lq) of block (i, j) holds row m = i*16 + lr, columns
     // n = j*16 + 4*lq + [0,4) -- one 16-B load per block (N % 4 == 0 for residual GEMMs)
-#define ACC_INIT(m0_, n0_, res_)                                                                   \
+#define ACC_INIT(m0_, n0_)                                                                         \
     {                                                                                              \
-        if (acc_init && (res_)) {                                                                  \
+        if (acc_init) {                                                                            \
             _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                       \
                 const float* rp_ = resid + (size_t)min((m0_) + wr * 128 + i * 16 + lr, M - 1) * ldr; \
                 _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                    \
@@ -578,9 +530,9 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
         }                                                                                          \
     }
 #else
-#define ACC_INIT(m0_, n0_, res_)                                                                   \
+#define ACC_INIT(m0_, n0_)                                                                         \
     {                                                                                              \
-        if (acc_init && (res_)) {                                                                  \
+        if (acc_init) {                                                                            \
             const float rc_ = (F8 & 1) ? 1.f / csc : 1.f;                                         \
             _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int e = 0; e < 4; ++e) { \
                 const float* rp_ = resid + (size_t)min((m0_) + wr * 128 + i * 16 + 4 * lq + e, M - 1) * ldr; \
@@ -646,11 +598,11 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
     }
 
     // prologue: K-tile 0 complete, K-tile 1 in flight
-    KT kc = kt_at_seg(0, 0);
+    KT kc = kt_at_tile(0, 0);
     KT k1 = kt_next(kc);
     KT k2 = kt_next(k1);
     VO v2 = vo_of(k2);
-    ACC_INIT(kc.m0, kc.n0, kc.k0 == 0);
+    ACC_INIT(kc.m0, kc.n0);
     {
         const VO v0 = vo_of(kc);
         STAGE_HALF(kc, v0, 2); STAGE_HALF(kc, v0, 0); STAGE_HALF(kc, v0, 3); STAGE_HALF(kc, v0, 1);
@@ -676,7 +628,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
 #endif
     for (int g = 0; g < total; ++g) {
         const int st = g & 1;
-        if (kc.k0 == (SK ? kc.kb : 0)) {  // first K-tile of a segment: its bias columns (loaded well before use)
+        if (kc.k0 == 0) {     // first K-tile of a tile: its bias columns (loaded well before use)
 #if GEMM_TACC
 #pragma unroll
             for (int q = 0; q < CW; ++q) {
@@ -731,72 +683,18 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
         kc = k1; k1 = k2;
         {
             const KT kn = kt_next(k2);
-            if (kn.k0 == (SK ? kn.kb : 0) && kn.idx != k2.idx) v2 = vo_of(kn);   // entered a new segment
+            if (kn.k0 == 0 && kn.idx != k2.idx) v2 = vo_of(kn);   // entered a new tile
             k2 = kn;
         }
-        if (kd.k0 + KTE != (SK ? kd.kend : K)) continue;
+        if (kd.k0 != K - KTE) continue;
         if (ablate == 1) {          // diagnostic: no epilogue at all (keeps acc live)
 #pragma unroll
             for (int i = 0; i < 8; ++i)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) asm volatile("" :: "v"(acc[i][j]));
-            ACC_INIT(kc.m0, kc.n0, kc.k0 == 0);
+            ACC_INIT(kc.m0, kc.n0);
             continue;
         }
-        // ---- split-K tail piece: per wave, the last of the tile's contributors to arrive sums the
-        // others' partials (slab, sc1 stores / loads, counters at agent scope) in slot order and runs
-        // the epilogue; the others store their partial and leave.  No wave waits for a workgroup
-        // that has not arrived, so the protocol cannot deadlock whatever else holds the CUs.
-        // ---- split-K tail piece: per wave, the last of the tile's 2-3 contributors to arrive adds
-        // the others' partials (slab, sc1 stores / loads, counters at agent scope) in slot order
-        // inside the epilogue below; the others store their partial and skip the epilogue.  No
-        // wave waits for a workgroup that has not arrived, so the protocol cannot deadlock whatever
-        // else holds the CUs.
-        bool epi = true;
-        int sk_n = 0, sk_p = 0;              // combiner: contributors, own position in slot order
-        const float* sk_o1 = nullptr;        // combiner: the other partials, in slot order
-        const float* sk_o2 = nullptr;
-        if (split && (kd.kb != 0 || kd.kend != K)) {
-            const int u = kd.tile - full_tiles;
-            const int x0 = u * nk, x1 = x0 + nk;          // (tail_kt * G < 2^31: host check)
-            const int s_first = ((x0 + 1) * G + tail_kt - 1) / tail_kt - 1;
-            const int s_last = (x1 * G + tail_kt - 1) / tail_kt - 1;
-            int* arr = sk_cnt + (u * 8 + wave) * 2;        // [0] arrivals, [1] partials stored
-            int r = 0;
-            if (lane == 0) r = __hip_atomic_fetch_add(arr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            r = __builtin_amdgcn_readfirstlane(r);
-            if (r < s_last - s_first) {
-                // a slot's two pieces keep separate partials (B: 1, A / a single piece: 0)
-                const int pc = (two_p && u == u0 + 1) ? 1 : 0;
-                float* dst = sk_slab + (((size_t)slot * 2 + pc) * 8 + wave) * 8192 + lane * 4;
-#pragma unroll
-                for (int i = 0; i < 8; ++i) sk_store16x4(dst + i * 1024, acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0) __hip_atomic_fetch_add(arr + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                epi = false;
-            } else {
-                if (lane == 0) {
-                    while (__hip_atomic_load(arr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < s_last - s_first)
-                        __builtin_amdgcn_s_sleep(2);
-                    __hip_atomic_store(arr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(arr + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                sk_n = s_last - s_first + 1;
-                sk_p = slot - s_first;
-                const int o1 = sk_p == 0 ? s_first + 1 : s_first;
-                const int o2 = sk_p == 2 ? s_first + 1 : s_first + 2;
-                // contributor o's piece of tile u is its B piece iff o's range starts in tile u - 1
-                // and runs past that tile's end
-                auto piece_of = [&](int o) {
-                    const long long ob = (long long)o * tail_kt / G, oe = (long long)(o + 1) * tail_kt / G;
-                    const int ou = (int)(ob / nk);
-                    return (oe > (long long)(ou + 1) * nk && u == ou + 1) ? 1 : 0;
-                };
-                sk_o1 = sk_slab + (((size_t)o1 * 2 + piece_of(o1)) * 8 + wave) * 8192 + lane * 4;
-                sk_o2 = sk_slab + (((size_t)o2 * 2 + piece_of(o2)) * 8 + wave) * 8192 + lane * 4;
-            }
-        }
-        if (epi) {
 
         // ---- epilogue of this tile (wave-private, 16 rows = one row block per pass) ----------
         // Full in-bounds sub-tiles without a row map or residual loads take the fast path: no
@@ -814,19 +712,6 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
                 *reinterpret_cast<float4*>(scratch + lr * 64 + (((4 * j + lq) ^ lr) << 2)) =
                     make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
 #else
-            if (SK && sk_n > 0) {
-                // the sum in slot order: ((p0 + p1) + p2); commutation makes the own partial's
-                // position 0 or 1 the same sum
-                f32x4 pa[4], pb[4];
-                sk_load16x4(sk_o1 + i * 1024, pa);
-                if (sk_n == 3) sk_load16x4(sk_o2 + i * 1024, pb);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    if (sk_n == 2) acc[i][j] = acc[i][j] + pa[j];
-                    else if (sk_p == 2) acc[i][j] = (pa[j] + pb[j]) + acc[i][j];
-                    else acc[i][j] = (acc[i][j] + pa[j]) + pb[j];
-                }
-            }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 f32x2 v01, v23;
@@ -925,10 +810,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
         }
         // the next tile's accumulator init loads would be ordered behind these stores
         stores_pending = (fast && !acc_init) ? 1 : 0;
-        } else {
-            stores_pending = 0;
-        }
-        ACC_INIT(kc.m0, kc.n0, kc.k0 == 0);   // the next segment (kc is its first K-tile; a repeat past the end)
+        ACC_INIT(kc.m0, kc.n0);    // the next tile (kc is its first K-tile; a repeat past the end)
     }
     if (stagger && wr == 0) PHASE_BARRIER();      // both halves leave with the same barrier count
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outstanding at exit
@@ -1341,94 +1223,21 @@ static int g_group_m = [] {
 }();
 BF_API void bf_gemm_set_group_m(int g) { g_group_m = g; }
 
-// Split-K tail of k_gemm256p (caller-owned workspace): full rounds of whole tiles on every CU, the
-// last partial round's K-tiles spread evenly over all slots, each tile finished by the last of its
-// 2-5 contributors to arrive.  Workspace: per tail tile and wave an {arrivals, stored} counter pair
-// (zero, left zero by every launch) + two 256-KiB partials per slot (a slot's B and A pieces can
-// both end up waiting for a later arrival).
-#define SK_MAX_TAIL 256
-#define SK_CNT_BYTES (SK_MAX_TAIL * 8 * 2 * 4)
-#define SK_SLAB_BYTES (2 * 262144)        // per slot: its two pieces' partials
-struct SplitPlan { int grid = 0, full_tiles = 0, tail_kt = 0; int* cnt = nullptr; float* slab = nullptr; };
-
-static int g_splitk = [] {
-    const char* e = getenv("BF_GEMM_SPLITK");
-    return e ? atoi(e) : 1;
-}();
-// 0: never split; 1 (default): split the tail where it pays (below); 2: whenever the plan is valid
-BF_API void bf_gemm_set_splitk(int on) { g_splitk = on; }
-
-static int gemm_device_cus() {
-    static int n = 0;
-    if (n == 0) {
-        int dev = 0;
-        hipDeviceProp_t prop;
-        n = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-                ? prop.multiProcessorCount : 256;
-    }
-    return n;
-}
-
-BF_API size_t bf_gemm_workspace_size(void) {
-    return SK_CNT_BYTES + (size_t)gemm_device_cus() * SK_SLAB_BYTES;
-}
-
-// t2 tiles of nk K-tiles on n_cu slots.  Valid: a partial last round of at least n_cu / 4 tiles
-// whose even split over the slots gives no tile more than 3 contributors.  Pays (mode 1): the last round at most 80 % full and nk >= 16 (the combine's
-// partial stores and loads cost ~2 K-tiles' time).
-static SplitPlan gemm_split_plan(long long t2, int nk, int n_cu, void* ws, size_t ws_bytes) {
-    SplitPlan p;
-    if (!ws || g_splitk == 0 || n_cu <= 0) return p;
-    const long long rounds = t2 / n_cu, tail = t2 - rounds * n_cu;
-    if (tail == 0 || tail > SK_MAX_TAIL || tail * 4 < n_cu) return p;
-    if (g_splitk == 1 && (tail * 5 > (long long)n_cu * 4 || nk < 16)) return p;
-    if (ws_bytes < SK_CNT_BYTES + (size_t)n_cu * SK_SLAB_BYTES || (uintptr_t)ws % 256) return p;
-    const long long T = tail * nk;
-    if (T * n_cu >= (1LL << 31)) return p;            // the kernel's 32-bit contributor arithmetic
-    // at most 3 contributors per tile (the combine's fixed-order sum): slot ranges [sT/G, (s+1)T/G)
-    for (long long u = 0; u < tail; ++u) {
-        const long long x0 = u * nk, x1 = x0 + nk;
-        const long long s_first = ((x0 + 1) * n_cu + T - 1) / T - 1, s_last = (x1 * n_cu + T - 1) / T - 1;
-        if (s_last - s_first > 2) return p;
-    }
-    p.grid = n_cu;
-    p.full_tiles = (int)(rounds * n_cu);
-    p.tail_kt = (int)T;
-    p.cnt = static_cast<int*>(ws);
-    p.slab = reinterpret_cast<float*>(static_cast<char*>(ws) + SK_CNT_BYTES);
-    return p;
-}
-
 template <bool OB, int AC>
 static void launch_gemm256(int grid, hipStream_t st, const void* A, int lda, const void* W, int ldw,
                            const float* bias, const float* resid, int ldr, int resid_mod, void* C,
                            int ldc, const int32_t* row_map, int M, int N, int K, int tiles_n,
-                           int tiles_m, const SplitPlan& sp) {
+                           int tiles_m) {
     static bool attr = false;
     if (!attr) {
         hipFuncSetAttribute((const void*)k_gemm256p<OB, AC>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             G2_LDS);
         attr = true;
     }
-    const int ablate = (g_gemm_variant == 3 || g_gemm_variant == 4) ? g_gemm_variant - 2 : 0;
-    if constexpr (AC == 0) {
-        if (sp.cnt != nullptr && ablate == 0) {
-            static bool sattr = false;
-            if (!sattr) {
-                hipFuncSetAttribute((const void*)k_gemm256p<OB, 0, 0, true>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
-                sattr = true;
-            }
-            hipLaunchKernelGGL((k_gemm256p<OB, 0, 0, true>), dim3(sp.grid), dim3(G2_THREADS), G2_LDS, st,
-                               (const u16*)A, lda, (const u16*)W, ldw, bias, resid, ldr, resid_mod, C, ldc,
-                               row_map, M, N, K, tiles_n, tiles_m, g_gemm_variant == 2 ? 0 : 1, g_group_m, 0,
-                               1.f, 1.f, sp.full_tiles, sp.tail_kt, sp.cnt, sp.slab);
-            return;
-        }
-    }
     hipLaunchKernelGGL((k_gemm256p<OB, AC>), dim3(grid), dim3(G2_THREADS), G2_LDS, st, (const u16*)A,
                        lda, (const u16*)W, ldw, bias, resid, ldr, resid_mod, C, ldc, row_map, M, N,
-                       K, tiles_n, tiles_m, g_gemm_variant == 2 ? 0 : 1, g_group_m, ablate);
+                       K, tiles_n, tiles_m, g_gemm_variant == 2 ? 0 : 1, g_group_m,
+                       (g_gemm_variant == 3 || g_gemm_variant == 4) ? g_gemm_variant - 2 : 0);
 }
 
 static int g_force_small = 0;
@@ -1489,10 +1298,9 @@ static bool gemm_use_large(int M, int N, int K) {
 
 BF_API int bf_gemm_large_tiles(int M, int N, int K) { return gemm_use_large(M, N, K) ? 1 : 0; }
 
-static int gemm_bf16_impl(const void* A, int lda, const void* W, int ldw, const float* bias,
-                          const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
-                          const int32_t* row_map, int M, int N, int K, int act, void* ws,
-                          size_t ws_bytes, void* stream) {
+BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bias,
+                        const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
+                        const int32_t* row_map, int M, int N, int K, int act, void* stream) {
     if (!A || !W || !C || M < 0 || N <= 0 || K <= 0) return BF_ERR_ARG;
     if (K % GB_K != 0 || lda % 8 != 0 || ldw % 8 != 0) return BF_ERR_UNSUPPORTED;
     if (M == 0) return BF_OK;
@@ -1551,9 +1359,8 @@ static int gemm_bf16_impl(const void* A, int lda, const void* W, int ldw, const 
 #undef GEMMQ
             return bf_check_launch();
         }
-        const SplitPlan sp = act == 0 ? gemm_split_plan(t2, K / 64, n_cu, ws, ws_bytes) : SplitPlan();
 #define GEMM2(OB, AC) launch_gemm256<OB, AC>(grid2, bf_stream(stream), A, lda, W, ldw, bias, \
-                                            resid, ldr, resid_mod, C, ldc, row_map, M, N, K, t2n, t2m, sp)
+                                            resid, ldr, resid_mod, C, ldc, row_map, M, N, K, t2n, t2m)
         if (c_bf16) {
             if (act == 0) GEMM2(true, 0);
             else if (act == 1) GEMM2(true, 1);
@@ -1581,24 +1388,6 @@ static int gemm_bf16_impl(const void* A, int lda, const void* W, int ldw, const 
     }
 #undef GEMM_LAUNCH
     return bf_check_launch();
-}
-
-BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bias,
-                        const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
-                        const int32_t* row_map, int M, int N, int K, int act, void* stream) {
-    return gemm_bf16_impl(A, lda, W, ldw, bias, resid, ldr, resid_mod, C, ldc, c_bf16, row_map, M, N,
-                          K, act, nullptr, 0, stream);
-}
-
-// as bf_gemm_bf16, with a caller-owned split-K workspace (bf_gemm_workspace_size() bytes, 256-B
-// aligned, zero-filled once; every launch leaves it zeroed).  One workspace per stream of
-// concurrently running GEMMs.
-BF_API int bf_gemm_bf16_ws(const void* A, int lda, const void* W, int ldw, const float* bias,
-                           const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
-                           const int32_t* row_map, int M, int N, int K, int act, void* ws,
-                           size_t ws_bytes, void* stream) {
-    return gemm_bf16_impl(A, lda, W, ldw, bias, resid, ldr, resid_mod, C, ldc, c_bf16, row_map, M, N,
-                          K, act, ws, ws_bytes, stream);
 }
 
 // ------------------------------------------------------------------------------------------

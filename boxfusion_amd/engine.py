@@ -58,7 +58,6 @@ class CuTREngine:
         self.model = model.to(dev).eval()
         vit = model.backbone.backbone
         self.dev, self.B, self.H, self.W, self.P = dev, batch, height, width, pad
-        self.gemm_ws = _lib.new_gemm_workspace(dev)     # split-K workspace (this engine's stream)
         self.C, self.heads = vit.embed_dim, vit.num_heads
         self.D = self.C // self.heads
         p = vit.patch_size
@@ -196,7 +195,7 @@ class CuTREngine:
                                else self.win_out)
                 rows = B * T if (last or not joint) else self.rows
                 Xm = X[:rows]
-                _lib.gemm(self.ATT[:rows], *blk["proj"], resid=Xm, out=Xm, ws=self.gemm_ws)
+                _lib.gemm(self.ATT[:rows], *blk["proj"], resid=Xm, out=Xm)
             else:
                 _lib.layernorm(Xr, g1, b1, e1, out=self.LN2[: B * T])
                 qkv = self.QKV[: B * T]
@@ -204,12 +203,12 @@ class CuTREngine:
                 att = self.ATT[: B * T]
                 _lib.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], att, B, self.heads, T, T,
                                self.D, scale)
-                _lib.gemm(att, *blk["proj"], resid=Xr, out=Xr, ws=self.gemm_ws)
+                _lib.gemm(att, *blk["proj"], resid=Xr, out=Xr)
                 rows = B * T
                 Xm = Xr
             _lib.layernorm(Xm, g2, b2, e2, out=self.LN2[:rows])
             _lib.gemm(self.LN2[:rows], *blk["fc1"], act="gelu", out=self.H1[:rows])
-            _lib.gemm(self.H1[:rows], *blk["fc2"], resid=Xm, out=Xm, ws=self.gemm_ws)
+            _lib.gemm(self.H1[:rows], *blk["fc2"], resid=Xm, out=Xm)
         out = Xr
         if self.enc_norm is not None:
             out = _lib.layernorm(Xr, self.enc_norm[0], self.enc_norm[1], self.enc_norm[2], out=self.OUT)
@@ -283,8 +282,6 @@ class CLIPEngine:
         self.visual = visual.to(dev).eval()
         v = visual
         self.dev, self.N = dev, max_crops
-        # split-K workspace of this engine's residual GEMMs (this engine's stream only)
-        self.gemm_ws = _lib.new_gemm_workspace(dev)
         self.width, self.heads = v.width, v.heads
         self.D = self.width // self.heads
         self.np = (v.image_size // v.patch_size) ** 2
@@ -407,7 +404,7 @@ class CLIPEngine:
                                self.D, scale)
                 if stats is not None:
                     stats.append(ATT.abs().amax())
-                _lib.gemm(ATT, *blk["proj"], resid=X, out=X, ws=self.gemm_ws)
+                _lib.gemm(ATT, *blk["proj"], resid=X, out=X)
             if fp8:
                 _lib.layernorm_fp8(X, *blk["n2"][:2], blk["n2"][2], 1.0 / s2, out=LN8)
                 _lib.gemm_fp8(LN8, f18, s2 * wf1, bias=blk["fc1"][1], act="gelu", out=H18,
@@ -420,7 +417,7 @@ class CLIPEngine:
                 _lib.gemm(LN, *blk["fc1"], act="gelu", out=H1)
                 if stats is not None:
                     stats.append(H1.abs().amax())
-                _lib.gemm(H1, *blk["fc2"], resid=X, out=X, ws=self.gemm_ws)
+                _lib.gemm(H1, *blk["fc2"], resid=X, out=X)
         return self._head(X, N)
 
     def _last_block_cls(self, blk, X, LN, QKV, N, fp8, li):

@@ -341,18 +341,6 @@ int bf_backproject(const float* depth, const float* K, const float* RT, int h, i
 int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bias,
                  const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
                  const int32_t* row_map, int M, int N, int K, int act, void* stream);
-/* bf_gemm_bf16 with a caller-owned split-K workspace (bf_gemm_workspace_size() bytes, 256-B aligned,
- * zero-filled once, left zeroed by every call; one per stream of concurrently running GEMMs).  Linear
- * (act 0) problems on the 256x256 kernel whose last round of tiles is partial run that round split in
- * K over every CU: each tile of it is summed from its 2-3 K-pieces in a fixed order by whichever
- * piece finishes last (deterministic for a given CU count; env BF_GEMM_SPLITK=0 / bf_gemm_set_splitk
- * turns it off, 2 forces it wherever the plan is valid). */
-int bf_gemm_bf16_ws(const void* A, int lda, const void* W, int ldw, const float* bias,
-                    const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
-                    const int32_t* row_map, int M, int N, int K, int act, void* ws, size_t ws_bytes,
-                    void* stream);
-size_t bf_gemm_workspace_size(void);
-void bf_gemm_set_splitk(int mode);
 /* Tile selection: large problems (N >= 512, >= 128 tiles of 256x256, 16-B aligned output rows)
  * run the 256x256 8-wave kernel, the rest the 128x128 4-wave kernel.  Test / tuning hook
  * (process-wide): 1 forces the 128x128 kernel, -1 the 256x256 kernel (aligned shapes), 0 the

@@ -421,61 +421,3 @@ def test_gemm_operand_extent_capacity(L):
                             None, None, 0, 0, ctypes.c_void_p(c.data_ptr()), 64, 1, None, 1 << 24, 64,
                             64, 0, None)
     assert rc == -3       # BF_ERR_CAPACITY
-
-
-@pytest.mark.parametrize("shape,mode,kind", [
-    ((32896, 1280, 1280), 1, "resid_inplace"),      # CLIP out_proj: 645 tiles, 133 in the tail
-    ((32896, 1280, 5120), 1, "resid_inplace"),      # CLIP c_proj (fc2)
-    ((12800, 768, 3072), 1, "resid_inplace"),       # CuTR fc2: no full round, 150 tiles split
-    ((3000, 2816, 320), 2, "bf16"),                 # forced: 132 tiles of 5 K-tiles, bf16 out
-    ((20000, 1280, 1280), 2, "resid_rowmap"),       # forced: residual added by the combiner
-    ((32896, 1280, 1280), 1, "budget"),             # 240-CU persistent grid: 165 tail tiles
-])
-def test_gemm_splitk_tail(L, shape, mode, kind):
-    """split-K tail of k_gemm256p (bf_gemm_bf16_ws): full rounds of whole tiles, the partial last
-    round spread in K over every CU and each of its tiles summed from 2-3 pieces in slot order
-    by the last piece to arrive.  Against fp32 torch, bit-identical on a repeat (fixed order,
-    whichever piece arrives last), close to the unsplit kernel, workspace counters left zero."""
-    from boxfusion_amd._lib import lib
-    g = torch.Generator(device="cuda").manual_seed(31)
-    M, N, K = shape
-    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
-    w = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).bfloat16()
-    b = torch.randn(N, device="cuda", generator=g)
-    resid = torch.randn(M, N, device="cuda", generator=g)
-    rmap = None
-    if kind == "resid_rowmap":
-        rmap = torch.randperm(M, device="cuda", generator=g).to(torch.int32)
-    ws = L.new_gemm_workspace("cuda")
-
-    def run(split):
-        lib().bf_gemm_set_splitk(mode if split else 0)
-        if kind == "bf16":
-            return L.gemm(a, w, b, out_dtype=torch.bfloat16, ws=ws)
-        if kind == "resid_rowmap":
-            o = torch.zeros(M, N, device="cuda")
-            return L.gemm(a, w, b, resid=resid, out=o, row_map=rmap, ws=ws)
-        o = resid.clone()
-        return L.gemm(a, w, b, resid=o, out=o, ws=ws)
-
-    if kind == "budget":
-        lib().bf_gemm_set_cu_budget(240)
-    try:
-        o1, o2, o0 = run(True), run(True), run(False)
-        torch.cuda.synchronize()
-    finally:
-        lib().bf_gemm_set_splitk(1)
-        lib().bf_gemm_set_cu_budget(0)
-    y = a.float() @ w.float().T + b
-    if kind == "resid_rowmap":
-        ref = torch.zeros(M, N, device="cuda")
-        ref[rmap.long()] = y + resid[rmap.long()]
-    elif kind == "bf16":
-        ref = y
-    else:
-        ref = y + resid
-    tol = 5e-3 if kind == "bf16" else 1e-5
-    assert rel_err(o1, ref) < tol
-    assert torch.equal(o1, o2)
-    assert rel_err(o1, o0) < (4e-3 if kind == "bf16" else 1e-6)
-    assert int(ws[: 256 * 8 * 2 * 4].view(torch.int32).abs().sum()) == 0
