@@ -756,12 +756,14 @@ def main(argv=None):
         dist.barrier()
     torch.cuda.synchronize()
     timer = _lib.KernelTimer()
+    owner = None
     t0 = time.perf_counter()
     with timer:       # records every eager GEMM / attention launch (graph replays launch none from Python)
         run_steps(args.warmup, total_steps, fusion)
         if not args.sync_fusion:
             worker = fusion
             fusion = fusion.join()
+            owner = (worker.busy_s, fusion.stats["keyframes"])
             if rank == 0:
                 print(f"fusion worker busy {1e3 * worker.busy_s / args.steps:.1f} ms/step "
                       f"({fusion.stats['keyframes']} keyframes)", file=sys.stderr, flush=True)
@@ -910,6 +912,12 @@ def main(argv=None):
         # kernel's convex_inter[8] (box_fusion.py:381: undefined behaviour there; exact hull here)
         line["hull_overflow"] = {"calls": fusion.fuser.hull_overflow_calls,
                                  "fusion_calls": fusion.fuser.fit_calls}
+        if owner is not None and owner[1] > 0:
+            # the fusion owner's worker thread (SURVEY §8e's serial term): time it spent fusing,
+            # host and device waits included, beside the detect streams
+            line["fusion_owner"] = {"busy_ms_per_step": 1e3 * owner[0] / args.steps,
+                                    "keyframes": owner[1],
+                                    "ms_per_keyframe": 1e3 * owner[0] / owner[1]}
         if args.clip_fp8:
             f8 = roofline_obj(timer.summary(lambda t: t["kind"] == "gemm_fp8"),
                               "k_gemm256p<*, *, fp8> (CLIP qkv, fc1 + GELU -> fp8, fc2 + f32 residual; "
