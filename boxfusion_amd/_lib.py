@@ -7,6 +7,7 @@ tensors are not on the GPU, the call raises.
 from __future__ import annotations
 
 import ctypes
+import sys
 import os
 
 import numpy as np
@@ -439,6 +440,8 @@ class FusionSequencer:
 
     def __del__(self):
         h, L = getattr(self, "h", None), getattr(self, "_L", None)
+        if sys.is_finalizing():       # interpreter exit: the process releases the device memory
+            return
         try:
             if h is not None and h.value and L is not None:
                 L.bf_fseq_destroy(h)
