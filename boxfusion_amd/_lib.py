@@ -438,9 +438,9 @@ class FusionSequencer:
                                         _ptr(vn) if n else None, _stream()), "bf_fseq_global")
         return ids[:n], xyz, vn
 
-    def __del__(self):
+    def __del__(self, _finalizing=sys.is_finalizing):
         h, L = getattr(self, "h", None), getattr(self, "_L", None)
-        if sys.is_finalizing():       # interpreter exit: the process releases the device memory
+        if _finalizing():             # interpreter exit: the process releases the device memory
             return
         try:
             if h is not None and h.value and L is not None:
