@@ -15,6 +15,7 @@ across GPUs (bench.py); fusion consumes keyframes strictly in frame order.
 """
 from __future__ import annotations
 
+import inspect
 import os
 
 import numpy as np
@@ -278,6 +279,9 @@ class Pipeline:
 
     def run(self, frames, n_frames, per_frame=True, frames_per_call=64, viz=None):
         """frames(ids) -> (rgb [b,H,W,3] u8 dev, depth [b,H,W] f32 dev, poses [b,4,4] host).
+        A frames callable that takes a `need_rgb` keyword is called with need_rgb=False for the
+        non-keyframes whose RGB nothing reads (their per-frame work uses depth and pose only) and
+        may return None for rgb then.
         per_frame: the frames between keyframes get demo.py:121-131's per-frame work too
         (DetectStage.preprocess_frames, up to `frames_per_call` frames per call).
         viz: a visualize.FrameLogger -- demo.py's per-frame rerun calls (pose, pinhole, image,
@@ -285,6 +289,14 @@ class Pipeline:
         keyframe's fusion (host side, after the frame's GPU work; not used by the bench)."""
         B = self.detect.B
         kf = [i for i in range(n_frames) if i % self.gap == 0]
+        try:
+            lazy_rgb = "need_rgb" in inspect.signature(frames).parameters
+        except (TypeError, ValueError):
+            lazy_rgb = False
+        nk_rgb = viz is not None and getattr(viz, "log_images", False)
+
+        def nk_frames(ids_):
+            return frames(ids_, need_rgb=nk_rgb) if lazy_rgb else frames(ids_)
         self.frames_preprocessed = 0
         for s in range(0, len(kf), B):
             ids = kf[s:s + B]
@@ -292,7 +304,7 @@ class Pipeline:
             if per_frame:
                 nk = [i for i in range(ids[0], min(ids[-1] + self.gap, n_frames)) if i % self.gap != 0]
                 for c in range(0, len(nk), frames_per_call):
-                    _rgb, depth, poses = frames(nk[c:c + frames_per_call])
+                    _rgb, depth, poses = nk_frames(nk[c:c + frames_per_call])
                     self.detect.preprocess_frames(depth.contiguous(), poses)
                     self.frames_preprocessed += len(nk[c:c + frames_per_call])
                     if viz is not None:
@@ -317,7 +329,7 @@ class Pipeline:
                             viz.frame(f, *nk_pose[f])
         last = n_frames - 1
         if last % self.gap != 0:
-            _, _, p = frames([last])
+            _, _, p = nk_frames([last])
             self.fusion.finish(last, p[0], False)
             if viz is not None:        # demo.py:330: the boxes after the last frame's block too
                 viz.boxes(self.fusion.all_pred_box, last)

@@ -170,16 +170,24 @@ def test_pipeline_run_call_order_per_frame_work():
         def finish(self, i, pose, is_kf):
             self.fin.append(i)
 
-    def frames(ids):
+    rgb_reads = []
+
+    def frames(ids, need_rgb=True):
         poses = np.stack([np.eye(4, dtype=np.float32) for _ in ids])
         poses[:, 0, 3] = ids
-        return (torch.zeros(len(ids), 2, 2, 3, dtype=torch.uint8), torch.ones(len(ids), 2, 2), poses)
+        if need_rgb:
+            rgb_reads.extend(ids)
+        rgb = torch.zeros(len(ids), 2, 2, 3, dtype=torch.uint8) if need_rgb else None
+        return (rgb, torch.ones(len(ids), 2, 2), poses)
 
     for n, gap in [(23, 5), (21, 5), (7, 1), (9, 25)]:
         det, fus = Det(), Fus()
         pipe = Pipeline(det, fus, gap)
         pipe.run(frames, n)
         kf = [i for i in range(n) if i % gap == 0]
+        # only the keyframes' RGB is read (no viz)
+        assert sorted(set(rgb_reads)) == kf
+        rgb_reads.clear()
         assert sorted(det.pre) == [i for i in range(n) if i % gap != 0]
         assert pipe.frames_preprocessed == n - len(kf)
         # the batch padding repeats the last keyframe; its results are dropped
