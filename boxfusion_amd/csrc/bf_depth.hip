@@ -40,6 +40,9 @@
 #define DS_NB2 1024
 #define DS_NB3 1024
 #define DS_SEL_T 1024              // LDS scratch sizing of the selects (they run with DS_T threads)
+#ifndef DS_NORM_KV
+#define DS_NORM_KV 1               // float4 groups per thread of the small-batch normalise pass
+#endif
 
 struct DsSel {
     long long m, klo, khi;
@@ -659,7 +662,12 @@ static void ds_launch(const float* depth, int b, int h, int w, float* out, float
         hipLaunchKernelGGL((k_ds_hist3<KV, false>), grid, dim3(DS_T), 0, st, depth, n, ws, params);
         hipLaunchKernelGGL(k_ds_fin, dim3(b), dim3(DS_SEL_T), 0, st, n, CHUNK, ws, params);
     }
-    hipLaunchKernelGGL(k_ds_norm<KV>, grid, dim3(DS_T), 0, st, depth, h, w, params, out, K, RT, max_depth,
+    // the normalise pass carries no per-slice state: small batches run it on 2048-element slices
+    // (four times the workgroups of the histogram passes), which it needs to keep enough stores in
+    // flight across the chip
+    constexpr int KVN = KV <= 4 ? DS_NORM_KV : KV;
+    const dim3 ngrid(ds_slices(n, KVN * 4 * DS_T), b);
+    hipLaunchKernelGGL(k_ds_norm<KVN>, ngrid, dim3(DS_T), 0, st, depth, h, w, params, out, K, RT, max_depth,
                        xyz, valid);
 }
 

@@ -33,6 +33,22 @@ def run_old(d):
     return out, p
 
 
+def run_old_bp(d, K, RT):
+    b, h, w = d.shape
+    out = torch.empty_like(d)
+    p = torch.empty((b, 2), device=d.device)
+    xyz = torch.empty((b, h, w, 3), device=d.device)
+    valid = torch.empty((b, h, w), dtype=torch.uint8, device=d.device)
+    st = torch.cuda.current_stream().cuda_stream
+    ws = _OLD_WS.setdefault((b, h, w), _lib.new_depth_workspace(b, h, w, d.device))
+    P = ctypes.c_void_p
+    rc = old.bf_depth_preprocess(P(d.data_ptr()), b, h, w, P(out.data_ptr()), P(p.data_ptr()),
+                                 P(K.data_ptr()), P(RT.data_ptr()), ctypes.c_float(10.0),
+                                 P(xyz.data_ptr()), P(valid.data_ptr()), P(ws.data_ptr()), P(st))
+    assert rc == 0
+    return out, p, xyz, valid
+
+
 def timed(fn, reps=20):
     for _ in range(3):
         fn()
@@ -61,7 +77,7 @@ def frames(b, h, w, seed, kind="uniform"):
     return d
 
 
-print("shape            new_us   GB/s   frac   old_us  (bp: +back-projection)")
+print("shape            new_us   GB/s   frac   old_us  (bp: +back-projection, new / old)")
 SHAPES = [(8, 480, 640), (192, 480, 640), (8, 256, 192)]
 if os.environ.get("BF_DS_SHAPE"):     # one shape only (per-kernel profiles)
     SHAPES = [tuple(int(v) for v in os.environ["BF_DS_SHAPE"].split("x"))]
@@ -74,10 +90,12 @@ for b, h, w in SHAPES:
     RT = torch.eye(4, device="cuda").expand(b, 4, 4).contiguous()
     t_bp = timed(lambda: _lib.depth_preprocess(d, K, RT, 10.0))
     t_old = timed(lambda: run_old(d)) if old else float("nan")
+    t_bp_old = (timed(lambda: run_old_bp(d, K, RT)) if old is not None and hasattr(old, "bf_depth_preprocess")
+                else float("nan"))
     gbs = 8.0 * n / (t_new * 1e-6) / 1e9
     gbs_bp = 21.0 * n / (t_bp * 1e-6) / 1e9
     print(f"{b:3d}x{h}x{w}  {t_new:8.1f} {gbs:6.0f} {gbs / 8000:6.3f} {t_old:8.1f}   bp {t_bp:7.1f} us "
-          f"{gbs_bp:6.0f} GB/s {gbs_bp / 8000:.3f}", flush=True)
+          f"{gbs_bp:6.0f} GB/s {gbs_bp / 8000:.3f} / old {t_bp_old:7.1f} us", flush=True)
 
 if old:
     bad = 0
@@ -88,6 +106,14 @@ if old:
             o, po = run_old(d)
             same_p = torch.equal(pa, po)
             same_o = torch.equal(a, o)
+            if hasattr(old, "bf_depth_preprocess"):
+                K = torch.tensor([[574.5, 0, 322.5], [0, 577.6, 238.6], [0, 0, 1]], device="cuda").expand(16, 3, 3).contiguous()
+                RT = torch.eye(4, device="cuda").expand(16, 4, 4).contiguous()
+                nb = _lib.depth_preprocess(d, K, RT, 10.0)
+                ob = run_old_bp(d, K, RT)
+                def bits(x):
+                    return x.reshape(-1).view(torch.int32) if x.dtype == torch.float32 else x.reshape(-1).to(torch.uint8)
+                same_o = same_o and all(torch.equal(bits(x), bits(y)) for x, y in zip(nb, ob))
             if not (same_p and same_o):
                 bad += 1
                 dp = (pa - po).abs().max().item()
