@@ -307,6 +307,161 @@ __device__ float iou_hull_lds(const P2* c0in, const P2* ht, int nt, float at, Hu
     return iou;
 }
 
+// ------------------------------------------------------------------------------------------
+// Four lanes per (particle, view) pair (the refinement's terms kernel): the same IoU as
+// iou_hull_lds, with the pair's work split where it is independent.  Each lane projects two of
+// the eight corners; all four run the corner sort and hull(c0) (identical values on identical LDS
+// slots); the candidate tests (hull(c0) vertices in the target, target vertices in hull(c0), the
+// n0 x nt edge crossings) go round-robin over the four lanes and append to the pair's list with
+// an LDS atomic; the list is then ordered by rank (key (x, y), ties by list position -- equal keys
+// are equal points, so every arrival order gives the exchange sort's sequence) with each lane
+// ranking a quarter of it, and all four run the candidate hull's chains and the areas.  Every
+// arithmetic expression is the one iou_hull_lds evaluates, so the terms are bit-identical; the
+// dependent-LDS chain of one lane shrinks to the two hulls' monotone chains.
+// ------------------------------------------------------------------------------------------
+#define G4_PAIRS 16                      // pairs per one-wave workgroup
+struct HullG4 {
+    P2 c0[8 * G4_PAIRS];                 // the projected corners, [j * 16 + pair]
+    P2 lo0[8 * G4_PAIRS];                // hull(c0) chains, [e * 16 + pair]
+    P2 up0[8 * G4_PAIRS];
+    P2 cand[FAST_CAND * G4_PAIRS];       // candidates in arrival order
+    P2 srt[FAST_CAND * G4_PAIRS];        // sorted candidates; then the lower chain in place
+    P2 up[FAST_CAND * G4_PAIRS];         // upper chain of the candidate hull
+    int cnt[G4_PAIRS];
+};
+#define HULL_AT16(lo, up, nl1, i) ((i) < (nl1) ? (lo)[(i) * G4_PAIRS] : (up)[((i) - (nl1)) * G4_PAIRS])
+
+__device__ __forceinline__ bool p2_less(P2 a, P2 b) { return a.x < b.x || (a.x == b.x && a.y < b.y); }
+__device__ __forceinline__ bool p2_equal(P2 a, P2 b) { return a.x == b.x && a.y == b.y; }
+
+// c0in: this pair's 8 projected corners (all four lanes); returns the IoU (all four lanes)
+__device__ float iou_hull_g4(const P2* c0in, const P2* ht, int nt, float at, HullG4& L, int pr,
+                             int g, int* flags) {
+    P2 c[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c[j] = c0in[j];
+    p2_cswap(c[0], c[2]); p2_cswap(c[1], c[3]); p2_cswap(c[4], c[6]); p2_cswap(c[5], c[7]);
+    p2_cswap(c[0], c[4]); p2_cswap(c[1], c[5]); p2_cswap(c[2], c[6]); p2_cswap(c[3], c[7]);
+    p2_cswap(c[0], c[1]); p2_cswap(c[2], c[3]); p2_cswap(c[4], c[5]); p2_cswap(c[6], c[7]);
+    p2_cswap(c[2], c[4]); p2_cswap(c[3], c[5]);
+    p2_cswap(c[1], c[4]); p2_cswap(c[3], c[6]);
+    p2_cswap(c[1], c[2]); p2_cswap(c[3], c[4]); p2_cswap(c[5], c[6]);
+    P2* lo0 = L.lo0 + pr;
+    P2* up0 = L.up0 + pr;
+    int nl = 0, nu = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        while (nl >= 2 && cross2(lo0[(nl - 2) * G4_PAIRS], lo0[(nl - 1) * G4_PAIRS], c[i]) <= 0) nl--;
+        lo0[(nl++) * G4_PAIRS] = c[i];
+    }
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {
+        while (nu >= 2 && cross2(up0[(nu - 2) * G4_PAIRS], up0[(nu - 1) * G4_PAIRS], c[i]) <= 0) nu--;
+        up0[(nu++) * G4_PAIRS] = c[i];
+    }
+    const int nl1 = nl - 1;
+    const int n0 = nl1 + (nu - 1);
+    // candidates, round-robin over the pair's lanes
+    P2* cand = L.cand + pr;
+    int* cnt = L.cnt + pr;
+    if (g == 0) *cnt = 0;
+    __syncthreads();
+    for (int i = g; i < n0; i += 4) {
+        const P2 p = HULL_AT16(lo0, up0, nl1, i);
+        if (point_in_polygon(p, ht, nt)) {
+            const int k = atomicAdd(cnt, 1);
+            if (k < FAST_CAND) cand[k * G4_PAIRS] = p;
+        }
+    }
+    for (int i = g; i < nt; i += 4) {
+        const P2 p = ht[i];
+        bool in = false;
+        for (int k = 0; k < n0; ++k) {
+            const P2 p1 = HULL_AT16(lo0, up0, nl1, k);
+            const P2 p2 = HULL_AT16(lo0, up0, nl1, (k + 1) % n0);
+            if ((p1.y > p.y) != (p2.y > p.y)) {
+                float xi = ((p.y - p1.y) * (p2.x - p1.x) / (p2.y - p1.y)) + p1.x;
+                if (p.x < xi) in = !in;
+            }
+        }
+        if (in) {
+            const int k = atomicAdd(cnt, 1);
+            if (k < FAST_CAND) cand[k * G4_PAIRS] = p;
+        }
+    }
+    for (int q = g; q < n0 * nt; q += 4) {
+        const int i = q / nt, j = q - i * nt;
+        const P2 a1 = HULL_AT16(lo0, up0, nl1, i);
+        const P2 a2 = HULL_AT16(lo0, up0, nl1, (i + 1) % n0);
+        const P2 b1 = ht[j], b2 = ht[(j + 1) % nt];
+        if (seg_boxes_apart(a1, a2, b1, b2)) continue;
+        P2 pt;
+        if (line_intersection(a1, a2, b1, b2, &pt)) {
+            const int k = atomicAdd(cnt, 1);
+            if (k < FAST_CAND) cand[k * G4_PAIRS] = pt;
+        }
+    }
+    __syncthreads();
+    // (the barriers below are reached by every lane: a pair on the scratch path skips the work,
+    // not the barriers)
+    const bool slow = *cnt > FAST_CAND;
+    const int nc = slow ? 0 : *cnt;
+    float iou_slow = 0.f;
+    if (slow && g == 0) {     // scratch path from the original corners (rare): lane 0 of the pair
+        P2 cc[8];
+        for (int j = 0; j < 8; ++j) cc[j] = c0in[j];
+        iou_slow = iou_hull_pre(cc, ht, nt, at, flags);
+    }
+    float a0 = 0.0f;
+    for (int i = 0; i < n0; ++i) {
+        const P2 p1 = HULL_AT16(lo0, up0, nl1, i), p2 = HULL_AT16(lo0, up0, nl1, (i + 1) % n0);
+        a0 += p1.x * p2.y - p2.x * p1.y;
+    }
+    a0 = (float)(fabs((double)a0) / 2.0);
+    // rank order of the candidates (each lane a quarter of them)
+    P2* srt = L.srt + pr;
+    for (int k = g; k < nc; k += 4) {
+        const P2 x = cand[k * G4_PAIRS];
+        int r = 0;
+        for (int m = 0; m < nc; ++m) {
+            const P2 y = cand[m * G4_PAIRS];
+            r += p2_less(y, x) || (m < k && p2_equal(y, x));
+        }
+        srt[r * G4_PAIRS] = x;
+    }
+    __syncthreads();
+    P2* up = L.up + pr;
+    int ni = 0, cl1 = 0;
+    if (nc > 0) {
+        int mu = 0;
+        for (int i = nc - 1; i >= 0; --i) {
+            const P2 x = srt[i * G4_PAIRS];
+            while (mu >= 2 && cross2(up[(mu - 2) * G4_PAIRS], up[(mu - 1) * G4_PAIRS], x) <= 0) mu--;
+            up[(mu++) * G4_PAIRS] = x;
+        }
+        int ml = 0;
+        for (int i = 0; i < nc; ++i) {
+            const P2 x = srt[i * G4_PAIRS];
+            while (ml >= 2 && cross2(srt[(ml - 2) * G4_PAIRS], srt[(ml - 1) * G4_PAIRS], x) <= 0) ml--;
+            srt[(ml++) * G4_PAIRS] = x;
+        }
+        cl1 = ml - 1;
+        ni = cl1 + (mu - 1);
+    }
+    if (slow) return iou_slow;
+    if (ni > 8) *flags |= BF_DEV_HULL_OVERFLOW;
+    float inter = 0.0f;
+    for (int i = 0; i < ni; ++i) {
+        const P2 p1 = HULL_AT16(srt, up, cl1, i), p2 = HULL_AT16(srt, up, cl1, (i + 1) % ni);
+        inter += p1.x * p2.y - p2.x * p1.y;
+    }
+    inter = (float)(fabs((double)inter) / 2.0);
+    float uni = a0 + at - inter;
+    float iou = 0;
+    if (uni > 0) iou = (float)((double)inter / ((double)uni + 0.00001));
+    return iou;
+}
+
 struct FuseViews {
     float pose[FUSE_MAX_VIEWS][16];
     float tc[FUSE_MAX_VIEWS][16];
@@ -511,7 +666,9 @@ __global__ void __launch_bounds__(64) k_fuse_targets(const float* __restrict__ v
     T.area = polygon_area(ht, nt);
 }
 
-#define TERM_THREADS 64   // one wave per workgroup: its hull stacks take 40 KB of LDS
+#define TERM_THREADS 64   // one wave per workgroup (k_fuse_iter: its hull stacks take 40 KB of LDS)
+// one wave = G4_PAIRS (particle, view) pairs x 4 lanes (iou_hull_g4); the pairs of a workgroup
+// share the view (P % 64 == 0)
 __global__ void __launch_bounds__(TERM_THREADS) k_fuse_terms(const float* __restrict__ vpose,
                                                              const TargetHull* __restrict__ th,
                                                              const float* __restrict__ pst,
@@ -522,38 +679,67 @@ __global__ void __launch_bounds__(TERM_THREADS) k_fuse_terms(const float* __rest
     const FuseState& S = states[job];
     if (S.stop) return;                                   // uniform per workgroup
     const int P = cfg.pst_size;                           // multiple of 64
-    const int pair = blockIdx.x * TERM_THREADS + threadIdx.x;
-    const int v = pair / P, p = pair % P;                 // P % 64 == 0: v is uniform per wave
+    const int lane = threadIdx.x;
+    const int pr = lane >> 2, g = lane & 3;
+    const int pair = blockIdx.x * G4_PAIRS + pr;
+    const int v = pair / P, p = pair % P;                 // v uniform per workgroup
     if (v >= S.nv) return;
     __shared__ float s_pose[16];
     __shared__ TargetHull s_th;
-    __shared__ HullLds s_hull;
-    const int lane = threadIdx.x;
+    __shared__ HullG4 s_hull;
     const size_t vi = (size_t)S.off + v;
     if (lane < 16) s_pose[lane] = vpose[vi * 16 + lane];
     else if (lane < 16 + 18) reinterpret_cast<float*>(&s_th)[lane - 16] =
         reinterpret_cast<const float*>(th + (size_t)job * max_views + v)[lane - 16];
-    __syncthreads();
-    float b[6], r[9], ss[6], corners[24];
+    // this lane's two corners of the pair's particle box (particle_corners' expressions)
+    float b[6], r[9], ss[6];
     for (int k = 0; k < 6; ++k) { b[k] = S.box32[k]; ss[k] = S.ss[k]; }
     for (int k = 0; k < 9; ++k) r[k] = S.R[k];
-    particle_corners(b, r, pst + 6 * p, ss, corners);
+    const float* prow = pst + 6 * p;
+    float x = b[0] + prow[0] * ss[0];
+    float y = b[1] + prow[1] * ss[1];
+    float z = b[2] + prow[2] * ss[2];
+    float w = b[5] + prow[5] * ss[5];
+    float h = b[4] + prow[4] * ss[4];
+    float l = b[3] + prow[3] * ss[3];
+    w = fmaxf(w, 0.01f);
+    h = fmaxf(h, 0.01f);
+    l = fmaxf(l, 0.01f);
+    const float xyz[3] = {x, y, z};
+    __syncthreads();
     const float* Pm = s_pose;
-    P2 c0[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        float vx = corners[3 * j] - Pm[3], vy = corners[3 * j + 1] - Pm[7], vz = corners[3 * j + 2] - Pm[11];
+    for (int cc = 0; cc < 2; ++cc) {
+        const int c = 2 * g + cc;
+        const float vv[3] = {bf_vsign_x(c) > 0 ? l / 2 : -l / 2, bf_vsign_y(c) > 0 ? h / 2 : -h / 2,
+                             bf_vsign_z(c) > 0 ? w / 2 : -w / 2};
+        float cn[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            float sacc = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) sacc += r[j * 3 + k] * vv[k];
+            sacc += xyz[j];
+            cn[j] = sacc;
+        }
+        float vx = cn[0] - Pm[3], vy = cn[1] - Pm[7], vz = cn[2] - Pm[11];
         float cx = Pm[0] * vx + Pm[4] * vy + Pm[8] * vz;
         float cy = Pm[1] * vx + Pm[5] * vy + Pm[9] * vz;
         float cz = Pm[2] * vx + Pm[6] * vy + Pm[10] * vz;
         float px = ((cx * cfg.K[0]) / cz + cfg.K[2]);
         float py = ((cy * cfg.K[5]) / cz + cfg.K[6]);
-        c0[j].x = (px > cfg.img_w) ? cfg.img_w : (px < 0) ? 0 : px;
-        c0[j].y = (py > cfg.img_h) ? cfg.img_h : (py < 0) ? 0 : py;
+        P2 q;
+        q.x = (px > cfg.img_w) ? cfg.img_w : (px < 0) ? 0 : px;
+        q.y = (py > cfg.img_h) ? cfg.img_h : (py < 0) ? 0 : py;
+        s_hull.c0[c * G4_PAIRS + pr] = q;
     }
+    __syncthreads();
+    P2 c0[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c0[j] = s_hull.c0[j * G4_PAIRS + pr];
     int flags = 0;
-    const float iou = iou_hull_lds(c0, s_th.h, s_th.n, s_th.area, s_hull, lane, &flags);
-    terms[((size_t)job * max_views + v) * P + p] = fabsf(1 - iou);
+    const float iou = iou_hull_g4(c0, s_th.h, s_th.n, s_th.area, s_hull, pr, g, &flags);
+    if (g == 0) terms[((size_t)job * max_views + v) * P + p] = fabsf(1 - iou);
     if (flags) atomicOr(&states[job].flags, flags);
 }
 
@@ -854,9 +1040,10 @@ BF_API int bf_fusion_fit(const int32_t* view_off, const int32_t* n_views, int n_
                        view_box, view_R, view_score, *cfg, states);
     hipLaunchKernelGGL(k_fuse_targets, dim3(n_jobs), dim3(64), 0, s, view_tc, states, max_views, th);
     const dim3 tgrid((unsigned)bf_cdiv(max_views * P, TERM_THREADS), (unsigned)n_jobs);
+    const dim3 tgrid4((unsigned)bf_cdiv(max_views * P, G4_PAIRS), (unsigned)n_jobs);
     for (int it = 0; it < cfg->iters; ++it) {
 #if FUSE_SPLIT_ITER
-        hipLaunchKernelGGL(k_fuse_terms, tgrid, dim3(TERM_THREADS), 0, s, view_pose, th, pst,
+        hipLaunchKernelGGL(k_fuse_terms, tgrid4, dim3(TERM_THREADS), 0, s, view_pose, th, pst,
                            *cfg, states, terms, max_views);
         hipLaunchKernelGGL(k_fuse_step, dim3(n_jobs), dim3(P), 0, s, pst, *cfg, states, terms,
                            max_views, it, trace);
