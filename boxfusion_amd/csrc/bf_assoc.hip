@@ -291,6 +291,9 @@ __device__ __forceinline__ unsigned long long lanes_lt_mask() {
 // boxes' init ids and their fusion-list entries); a lookup whose slot holds another frame reads
 // the pose from global memory instead, so every pose value is the same either way.
 #define NMS_PC 256
+#ifndef NMS_DIAG_NORECORD
+#define NMS_DIAG_NORECORD 0     // timing diagnostic only (wrong results): the scan without record()
+#endif
 __device__ __forceinline__ const float* nms_pose(const float* poses, const int* ptag, const float* pcache,
                                                  int f) {
     const int slot = f & (NMS_PC - 1);
@@ -429,7 +432,7 @@ __global__ void __launch_bounds__(64) k_nms_scan_w(
             // BoxManager.record(cur=i, fusion_inds=supp)
             const int cur = i;
             const float* ccur = cen + 3 * cur;
-            for (int s = 0; s < nsupp; ++s) {
+            for (int s = 0; s < (NMS_DIAG_NORECORD ? 0 : nsupp); ++s) {
                 const int idx = supp[s];
                 const float* cidx = cen + 3 * idx;
                 float dx = ccur[0] - cidx[0], dy = ccur[1] - cidx[1], dz = ccur[2] - cidx[2];
