@@ -95,15 +95,15 @@ __device__ __forceinline__ void box_center(const float* corners, int i, float* c
 
 // global -> LDS copy with 8 independent loads in flight per lane (a plain strided loop waits for
 // every load before the next: one memory latency per 64 elements)
-template <typename T>
+template <typename T, int F = 8>
 __device__ __forceinline__ void stage_lds(T* dst, const T* __restrict__ src, int count, int t, int nt) {
     int q = t;
-    for (; q + 7 * nt < count; q += 8 * nt) {
-        T v[8];
+    for (; q + (F - 1) * nt < count; q += F * nt) {
+        T v[F];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = src[q + k * nt];
+        for (int k = 0; k < F; ++k) v[k] = src[q + k * nt];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) dst[q + k * nt] = v[k];
+        for (int k = 0; k < F; ++k) dst[q + k * nt] = v[k];
     }
     for (; q < count; q += nt) dst[q] = src[q];
 }
@@ -351,14 +351,28 @@ __global__ void __launch_bounds__(64) k_nms_scan_w(
     int* supp = bufB + n + 1;
     int* keep = supp + n + 1;
     int* succ = keep + n + 2;
-    stage_lds(I, iou, n * n, t, 64);
-    stage_lds(fls, fl, n * cap, t, 64);
     for (int q = t; q < n; q += 64) {
         fll[q] = fl_len[q];
         iid[q] = init_id[q];
         vn[q] = valid_num[q];
         sc[q] = scores[q];
         box_center(corners, q, cen + 3 * q);
+    }
+    stage_lds<double, 16>(I, iou, n * n, t, 64);
+    // the fusion lists: only each row's live entries (the scan never reads past a row's length),
+    // a lane's row loads in flight together
+    for (int r = t; r < n; r += 64) {
+        const int L = min(fl_len[r], cap);
+        const int32_t* src = fl + (size_t)r * cap;
+        int* dst = fls + (size_t)r * cap;
+        for (int e0 = 0; e0 < L; e0 += 8) {
+            int v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = e0 + k < L ? src[e0 + k] : 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (e0 + k < L) dst[e0 + k] = v[k];
+        }
     }
     __syncthreads();
     // pose cache: claim slots with the frames record()'s disparity tests can read (the boxes'
@@ -489,7 +503,8 @@ __global__ void __launch_bounds__(64) k_nms_scan_w(
         for (int k = 0; k < ns; ++k) r += succ[k] < v;
         succ_out[r] = v;
     }
-    for (int q = t; q < n * cap; q += 64) fl[q] = fls[q];
+    for (int r = t; r < n; r += 64)        // the live entries (rows only grow)
+        for (int e = 0; e < fll[r]; ++e) fl[(size_t)r * cap + e] = fls[(size_t)r * cap + e];
     for (int q = t; q < n; q += 64) {
         fl_len[q] = fll[q];
         valid_num[q] = vn[q];
