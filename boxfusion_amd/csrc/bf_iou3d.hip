@@ -221,7 +221,7 @@ __global__ void __launch_bounds__(IOU_THREADS) k_obb_pairs(const BoxPrep* __rest
 //   (k_obb_prep also writes the diagonal and resets the work list: 3 launches per matrix)
 // ------------------------------------------------------------------------------------------
 #ifndef OBB_SPLIT
-#define OBB_SPLIT 8         // (a diagnostic build sets 0: one workgroup per pair, k_obb_pairs)
+#define OBB_SPLIT 2         // (a diagnostic build sets 0: one workgroup per pair, k_obb_pairs)
 #endif
 #define OBB_GRID_WGS 512
 #ifndef OBB_LAST_BLOCK
