@@ -29,6 +29,7 @@ from __future__ import annotations
 import argparse
 import copy
 import json
+import gc
 import os
 import re
 import sys
@@ -434,11 +435,13 @@ def roofline_obj(ks, kernel, bound, pmc_key=None, peak_tflops=PEAK_BF16_TFLOPS):
 
 
 def auto_rank0_batch(B, ranks):
-    """rank 0's detection share when it also fuses `ranks` ranks' frames: its fusion worker must
-    keep pace with ranks * B keyframes per step.  Measured on one MI355X with --sim-ranks 8 and the
-    native keyframe sequencer (worker busy 0.85 ms per keyframe under the detect load): rank 0 on
-    6 / 7 / 8 frames -> 49.2 / 55.0 / 59.9 ms per step against the 54.7-ms N=1 step, i.e. 62/64,
-    63/64 x 54.7/55.0 and 54.7/59.9 = 0.97 / 0.98 / 0.91 of the ideal"""
+    """rank 0's detection share when it also fuses `ranks` ranks' frames.  Measured on one MI355X
+    with --sim-ranks 8 (profiles/r04_fusion_owner_sim8.txt): the fusion worker is busy 16.6 ms per
+    63-keyframe step (0.26 ms per keyframe) on its 32 reserved CUs, so it keeps pace either way;
+    what remains is rank 0's detection on the other 224 CUs: 7 frames 50.5 ms, 8 frames 57.3 ms
+    per step against the 52.2-53.4-ms N=1 step of the other ranks, i.e. 63/64 = 0.98 vs 0.93 of the
+    ideal.  Without the reservation rank 0 detects 8 frames in 53.6 ms (0.975) with the worker at
+    32.5 ms per step beside it."""
     if ranks >= 8:
         return max(1, B - 1)
     return B
@@ -719,8 +722,13 @@ def main(argv=None):
 
                     # the whole step's keyframes as one job: geometry batched, association serial
                     def job(st, r=g_rec, c_=g_clip, k_=counts):
+                        tj = time.perf_counter()
                         p, c = record_meta(r)       # on the worker's stream, after the gather
-                        st.keyframes(k_, p, unpack_records(r, c, dev, c_, args.crops, coeff), c)
+                        u = unpack_records(r, c, dev, c_, args.crops, coeff)
+                        if os.environ.get("BF_FSEQ_PROFILE"):
+                            print(f"job: meta + unpack {1e3 * (time.perf_counter() - tj):.2f} ms",
+                                  file=sys.stderr, flush=True)
+                        st.keyframes(k_, p, u, c)
                     fusion.submit_call(job, ev)
             st_ctx.__exit__(None, None, None)
             if args.breakdown:
@@ -729,7 +737,7 @@ def main(argv=None):
 
     # ---- warmup (own fusion state), then the timed stream from frame 0 ----------------------
     # rank 0 owns the serial fusion state machine; when it fuses more frames than it detects
-    # (N > 1), a few CUs are reserved for it so the persistent GEMMs cannot starve it
+    # (N > 1), 32 CUs (4 per XCD) are reserved for it so the persistent GEMMs cannot starve it
     fusion_cus = args.fusion_cus
     if fusion_cus < 0:
         fusion_cus = 32 if rank == 0 and (world > 1 or args.sim_ranks > 1) else 0
@@ -760,6 +768,11 @@ def main(argv=None):
     run_steps(0, args.warmup, wf)
     if not args.sync_fusion:
         wf.join()
+    # the warm-up sequencer's device / pinned staging buffers go back to their pools, so the timed
+    # sequencer's first keyframes reuse them instead of allocating under the detect load
+    del wf
+    gc.collect()
+    torch.cuda.synchronize()
     fusion = make_fusion()
     brk.update(detect=0.0, fusion=0.0)
     if dist is not None:

@@ -6,6 +6,7 @@ tensors are not on the GPU, the call raises.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import sys
 import os
@@ -262,11 +263,14 @@ def nms_scan(iou, corners, scores, init_id, cam_poses, fl_items, fl_len, valid_n
         succ = torch.empty(n + 1, **i32)
         events = torch.empty((n + 1, 3), **i32)
         counts = torch.zeros(4, **i32)  # n_keep, n_success, n_events, status
-    _check(lib().bf_nms_scan(_ptr(iou), _ptr(corners), _ptr(scores), _ptr(init_id),
-                             _ptr(cam_poses), c_int(n), _ptr(fl_items), _ptr(fl_len),
-                             _ptr(valid_num), _ptr(keep), _ptr(counts[0:1]), _ptr(succ),
-                             _ptr(counts[1:2]), _ptr(events), _ptr(counts[2:3]),
-                             _ptr(counts[3:4]), ctypes.byref(cfg), _stream()), "bf_nms_scan")
+    L = lib()
+    L.bf_nms_scan_workspace_size.restype = ctypes.c_size_t
+    ws = torch.empty(max(int(L.bf_nms_scan_workspace_size(c_int(n))), 8), dtype=torch.uint8, device=dev)
+    _check(L.bf_nms_scan_ws(_ptr(iou), _ptr(corners), _ptr(scores), _ptr(init_id),
+                            _ptr(cam_poses), c_int(n), _ptr(fl_items), _ptr(fl_len),
+                            _ptr(valid_num), _ptr(keep), _ptr(counts[0:1]), _ptr(succ),
+                            _ptr(counts[1:2]), _ptr(events), _ptr(counts[2:3]),
+                            _ptr(counts[3:4]), ctypes.byref(cfg), _ptr(ws), _stream()), "bf_nms_scan_ws")
     return keep, succ, events, counts
 
 
@@ -1083,7 +1087,24 @@ def cu_masked_stream(cus, device=None):
         rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(s), ctypes.c_uint32(len(words)), words)
     if rc != 0:
         raise HipError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+    if not _MASKED_STREAMS:
+        atexit.register(_destroy_masked_streams)
+    _MASKED_STREAMS.append((dev, s.value))
     return torch.cuda.ExternalStream(s.value, device=dev)
+
+
+_MASKED_STREAMS = []
+
+
+def _destroy_masked_streams():
+    """destroy the CU-masked streams while the HIP runtime is still up (interpreter exit, before
+    the runtime's own static teardown: left to that teardown, a profiler's finalisation crashed)"""
+    hip = ctypes.CDLL("libamdhip64.so")
+    while _MASKED_STREAMS:
+        dev, h = _MASKED_STREAMS.pop()
+        with torch.cuda.device(dev):
+            hip.hipStreamSynchronize(ctypes.c_void_p(h))
+            hip.hipStreamDestroy(ctypes.c_void_p(h))
 
 
 def partition_streams(n_reserved, device=None, masked=False):
@@ -1093,21 +1114,28 @@ def partition_streams(n_reserved, device=None, masked=False):
     stream gets high priority for the CUs that free up in between.  masked=True additionally
     confines each stream to its CUs with hipExtStreamCreateWithCUMask."""
     dev = torch.cuda.current_device() if device is None else device
-    n = torch.cuda.get_device_properties(dev).multi_processor_count
-    lib().bf_gemm_set_cu_budget(c_int(n - n_reserved))
+    det, fus = partition_cus(n_reserved, dev)
+    lib().bf_gemm_set_cu_budget(c_int(len(det)))
     if not masked:
         return torch.cuda.current_stream(dev), torch.cuda.Stream(device=dev, priority=-1)
-    det, fus = partition_cus(n_reserved, dev)
     return cu_masked_stream(det, dev), cu_masked_stream(fus, dev)
 
 
+XCDS = 8
+
+
 def partition_cus(n_reserved, device=None):
-    """(detect CUs, fusion CUs): every (n / n_reserved)-th CU goes to the fusion stream"""
+    """(detect CUs, fusion CUs) as CU-mask bit indices.  Mask bit i is CU i // 8 of XCD i % 8, and
+    a mask that leaves an XCD without CUs is not applied at all (the stream then runs on every CU:
+    measured with scripts/diag/cu_probe.py), so the fusion set takes the first n_reserved bits —
+    n_reserved / 8 CUs on every XCD — and detection the rest."""
     dev = torch.cuda.current_device() if device is None else device
     n = torch.cuda.get_device_properties(dev).multi_processor_count
-    step = max(1, n // max(1, n_reserved))
-    fus = [i for i in range(0, n, step)][:n_reserved]
-    det = [i for i in range(n) if i not in set(fus)]
+    k = -(-max(1, n_reserved) // XCDS) * XCDS
+    if k >= n:
+        raise HipError(f"cannot reserve {n_reserved} of {n} CUs for the fusion stream")
+    fus = list(range(k))
+    det = list(range(k, n))
     return det, fus
 
 

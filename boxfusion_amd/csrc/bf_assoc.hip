@@ -319,28 +319,56 @@ __device__ __forceinline__ int nms_count_far(const int* row, int L, const float*
     return cnt;
 }
 
-static size_t nms_fast_lds(int n, int cap) {
+// 64-bit words per row of a threshold bit mask
+__host__ __device__ inline int nms_words(int n) { return (n + 63) / 64; }
+
+static size_t nms_fast_lds(int n, int cap, bool bits) {
     return sizeof(float) * 16 * NMS_PC + sizeof(int) * NMS_PC   // pose cache + tags
-           + sizeof(double) * (size_t)n * n                     // IoU
+           + (bits ? sizeof(unsigned long long) * 2 * (size_t)n * nms_words(n)   // masks
+                   : sizeof(double) * (size_t)n * n)            // IoU
            + sizeof(int) * ((size_t)n * cap + 2 * (size_t)n)     // lists, lengths, init ids
            + sizeof(float) * 5 * (size_t)n                       // valid_num, scores, centres
            + sizeof(int) * (5 * (size_t)n + 8);                  // order x2, supp, keep, succ
 }
 
+// the scan reads the IoU matrix only through the two tests iou <= t (stays in `order`) and
+// iou > t (suppressed; a NaN passes neither and leaves the order), so for large n it runs on
+// these two bit masks, [2][n][words]: row i, word c, bit l <-> column 64c + l
+__global__ void __launch_bounds__(256) k_nms_bits(const double* __restrict__ iou, int n, int words,
+                                                  double thr, unsigned long long* __restrict__ bits) {
+    const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= n * words) return;                                 // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const int i = w / words, c = w % words, j = 64 * c + lane;
+    const bool live = j < n;
+    const double v = live ? iou[(size_t)i * n + j] : 0.0;
+    const unsigned long long r = __ballot(live && v <= thr);
+    const unsigned long long sp = __ballot(live && v > thr);
+    if (lane == 0) {
+        bits[(size_t)i * words + c] = r;
+        bits[(size_t)n * words + (size_t)i * words + c] = sp;
+    }
+}
+
+template <bool BITS>
 __global__ void __launch_bounds__(64) k_nms_scan_w(
     const double* __restrict__ iou, const float* __restrict__ corners,
     const float* __restrict__ scores, const int32_t* __restrict__ init_id,
     const float* __restrict__ poses, int n, int32_t* __restrict__ fl, int32_t* __restrict__ fl_len,
     float* __restrict__ valid_num, int32_t* __restrict__ keep_out, int32_t* __restrict__ n_keep,
     int32_t* __restrict__ succ_out, int32_t* __restrict__ n_succ, int32_t* __restrict__ events,
-    int32_t* __restrict__ n_events, int32_t* __restrict__ status, bf_nms_cfg cfg) {
+    int32_t* __restrict__ n_events, int32_t* __restrict__ status, bf_nms_cfg cfg,
+    const unsigned long long* __restrict__ bits) {
     extern __shared__ __attribute__((aligned(16))) double wsm[];
     const int cap = cfg.list_capacity;
     const int t = threadIdx.x;
+    const int words = nms_words(n);
     float* pcache = reinterpret_cast<float*>(wsm);                // [NMS_PC][16]
     int* ptag = reinterpret_cast<int*>(pcache + 16 * NMS_PC);    // [NMS_PC]
-    double* I = reinterpret_cast<double*>(ptag + NMS_PC);
-    int* fls = reinterpret_cast<int*>(I + (size_t)n * n);
+    double* I = reinterpret_cast<double*>(ptag + NMS_PC);         // IoU matrix, or the masks:
+    unsigned long long* Bm = reinterpret_cast<unsigned long long*>(I);
+    int* fls = BITS ? reinterpret_cast<int*>(Bm + 2 * (size_t)n * words)
+                    : reinterpret_cast<int*>(I + (size_t)n * n);
     int* fll = fls + (size_t)n * cap;
     int* iid = fll + n;
     float* vn = reinterpret_cast<float*>(iid + n);
@@ -358,7 +386,8 @@ __global__ void __launch_bounds__(64) k_nms_scan_w(
         sc[q] = scores[q];
         box_center(corners, q, cen + 3 * q);
     }
-    stage_lds<double, 16>(I, iou, n * n, t, 64);
+    if (BITS) stage_lds<unsigned long long, 16>(Bm, bits, 2 * n * words, t, 64);
+    else stage_lds<double, 16>(I, iou, n * n, t, 64);
     // the fusion lists: only each row's live entries (the scan never reads past a row's length),
     // a lane's row loads in flight together
     for (int r = t; r < n; r += 64) {
@@ -427,9 +456,16 @@ __global__ void __launch_bounds__(64) k_nms_scan_w(
             const int q = base + t;
             const bool live = q < no;
             const int j = order[live ? q : no - 1];
-            const double v = live ? I[(size_t)i * n + j] : 0.0;
-            const bool fr = live && (v <= cfg.iou_threshold);
-            const bool fs = live && (v > cfg.iou_threshold);
+            bool fr, fs;
+            if (BITS) {
+                const size_t wi = (size_t)i * words + (j >> 6);
+                fr = live && ((Bm[wi] >> (j & 63)) & 1ull);
+                fs = live && ((Bm[(size_t)n * words + wi] >> (j & 63)) & 1ull);
+            } else {
+                const double v = live ? I[(size_t)i * n + j] : 0.0;
+                fr = live && (v <= cfg.iou_threshold);
+                fs = live && (v > cfg.iou_threshold);
+            }
             const unsigned long long mr = __ballot(fr), ms = __ballot(fs);
             if (fr) rest[nrest + __popcll(mr & lanes_lt_mask())] = j;
             if (fs) supp[nsupp + __popcll(ms & lanes_lt_mask())] = j;
@@ -517,28 +553,53 @@ __global__ void __launch_bounds__(64) k_nms_scan_w(
     }
 }
 
+BF_API size_t bf_nms_scan_workspace_size(int n) {
+    return n > 0 ? sizeof(unsigned long long) * 2 * (size_t)n * nms_words(n) : 0;
+}
+
 BF_API int bf_nms_scan(const double* iou, const float* corners, const float* scores,
                        const int32_t* init_id, const float* cam_poses, int n, int32_t* fl_items,
                        int32_t* fl_len, float* valid_num, int32_t* keep, int32_t* n_keep,
                        int32_t* success, int32_t* n_success, int32_t* events, int32_t* n_events,
                        int32_t* status, const bf_nms_cfg* cfg, void* stream) {
+    return bf_nms_scan_ws(iou, corners, scores, init_id, cam_poses, n, fl_items, fl_len, valid_num, keep,
+                          n_keep, success, n_success, events, n_events, status, cfg, nullptr, stream);
+}
+
+BF_API int bf_nms_scan_ws(const double* iou, const float* corners, const float* scores,
+                          const int32_t* init_id, const float* cam_poses, int n, int32_t* fl_items,
+                          int32_t* fl_len, float* valid_num, int32_t* keep, int32_t* n_keep,
+                          int32_t* success, int32_t* n_success, int32_t* events, int32_t* n_events,
+                          int32_t* status, const bf_nms_cfg* cfg, void* workspace, void* stream) {
     if (!cfg || n < 0) return BF_ERR_ARG;
     if (n > BF_MAX_BOXES) return BF_ERR_CAPACITY;
     if (n == 0) return BF_OK;
     if (!iou || !corners || !scores || !init_id || !cam_poses || !fl_items || !fl_len ||
         !valid_num || !keep || !n_keep || !success || !n_success || !events || !n_events || !status)
         return BF_ERR_ARG;
-    if (n <= NMS_FAST_N && nms_fast_lds(n, cfg->list_capacity) <= NMS_FAST_LDS_MAX) {
-        static bool attr_w = false;
-        if (!attr_w) {
-            hipFuncSetAttribute((const void*)k_nms_scan_w, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                NMS_FAST_LDS_MAX);
-            attr_w = true;
-        }
-        hipLaunchKernelGGL(k_nms_scan_w, dim3(1), dim3(64), nms_fast_lds(n, cfg->list_capacity),
-                           bf_stream(stream), iou, corners, scores, init_id, cam_poses, n, fl_items,
-                           fl_len, valid_num, keep, n_keep, success, n_success, events, n_events,
-                           status, *cfg);
+    static bool attr_w = false;
+    if (!attr_w) {
+        (void)hipFuncSetAttribute((const void*)k_nms_scan_w<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            NMS_FAST_LDS_MAX);
+        (void)hipFuncSetAttribute((const void*)k_nms_scan_w<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            NMS_FAST_LDS_MAX);
+        attr_w = true;
+    }
+    hipStream_t st = bf_stream(stream);
+    if (n <= NMS_FAST_N && nms_fast_lds(n, cfg->list_capacity, false) <= NMS_FAST_LDS_MAX) {
+        hipLaunchKernelGGL(k_nms_scan_w<false>, dim3(1), dim3(64), nms_fast_lds(n, cfg->list_capacity, false),
+                           st, iou, corners, scores, init_id, cam_poses, n, fl_items, fl_len, valid_num,
+                           keep, n_keep, success, n_success, events, n_events, status, *cfg, nullptr);
+        return bf_check_launch();
+    }
+    if (workspace && NMS_FAST_N > 0 && nms_fast_lds(n, cfg->list_capacity, true) <= NMS_FAST_LDS_MAX) {
+        const int words = nms_words(n);
+        auto* bits = static_cast<unsigned long long*>(workspace);
+        hipLaunchKernelGGL(k_nms_bits, dim3(bf_cdiv(n * words, 4)), dim3(256), 0, st, iou, n, words,
+                           cfg->iou_threshold, bits);
+        hipLaunchKernelGGL(k_nms_scan_w<true>, dim3(1), dim3(64), nms_fast_lds(n, cfg->list_capacity, true),
+                           st, iou, corners, scores, init_id, cam_poses, n, fl_items, fl_len, valid_num,
+                           keep, n_keep, success, n_success, events, n_events, status, *cfg, bits);
         return bf_check_launch();
     }
     size_t lds = sizeof(int) * (size_t)(5 * n + 8) + sizeof(float) * 3 * (size_t)n;

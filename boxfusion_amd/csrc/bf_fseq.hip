@@ -21,8 +21,12 @@
 #include "bf_common.h"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <set>
 #include <string>
 #include <vector>
@@ -97,7 +101,7 @@ struct bf_fseq {
     int cur = 0;                         // g[cur] holds all_pred_box
     int n = 0;                           // its rows
     std::vector<int32_t> ids;            // their init_id (host mirror)
-    DevBuf corners, dims, iou, iou_ws, xch, jobs, packed, views, out_box, fit_ws;
+    DevBuf corners, dims, iou, iou_ws, nms_ws, xch, jobs, packed, views, out_box, fit_ws;
     HostBuf h_in, h_out, h_jobs, h_fit;
     // BoxManager state (box_manager.py:9-20)
     std::vector<std::vector<int32_t>> fusion_list;
@@ -113,6 +117,14 @@ struct bf_fseq {
     long long last_jobs = 0, last_updated = 0, last_iters = 0, last_views = 0;
     int strict_hull = 0;
     std::string err;
+    // BF_FSEQ_PROFILE=1 (diagnostic): per-keyframe host / device phase times, printed every 256
+    // association steps
+    bool used = false;                   // a call has run (s->stream is the caller's)
+    int prof = -1;
+    hipEvent_t pev[6] = {};
+    bool pev_prev = false;
+    double pt[10] = {};
+    long long pn = 0;
 };
 
 namespace {
@@ -140,21 +152,58 @@ int dev_reserve(bf_fseq* s, DevBuf& b, size_t bytes) {
     return BF_OK;
 }
 
-// pinned staging; the stream is drained before an old buffer is released (its copies may be
-// in flight)
+// Pinned staging buffers come from a process-wide pool and go back to it, never to
+// hipHostFree: freeing pinned memory waits for the whole device, i.e. for every detect graph in
+// flight on the other streams (measured: 70-190 ms stalls on the first steps of a fresh
+// sequencer at --sim-ranks 8).  The pool is never torn down (no exit-order dependence).
+struct PinnedPool {
+    std::mutex m;
+    std::multimap<size_t, void*> free;
+};
+
+PinnedPool& pinned_pool() {
+    static PinnedPool* p = new PinnedPool();
+    return *p;
+}
+
+void* pinned_get(size_t bytes, size_t* cap) {
+    PinnedPool& P = pinned_pool();
+    {
+        std::lock_guard<std::mutex> g(P.m);
+        auto it = P.free.lower_bound(bytes);
+        if (it != P.free.end()) {
+            void* q = it->second;
+            *cap = it->first;
+            P.free.erase(it);
+            return q;
+        }
+    }
+    void* q = nullptr;
+    if (hipHostMalloc(&q, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+    *cap = bytes;
+    return q;
+}
+
+void pinned_put(void* q, size_t cap) {
+    if (!q) return;
+    PinnedPool& P = pinned_pool();
+    std::lock_guard<std::mutex> g(P.m);
+    P.free.emplace(cap, q);
+}
+
+// the stream is drained before an old buffer goes back to the pool (its copies may be in flight)
 int host_reserve(bf_fseq* s, HostBuf& b, size_t bytes) {
     if (bytes <= b.cap) return BF_OK;
     size_t nc = std::max(bytes, b.cap * 2);
     nc = std::max(nc, (size_t)16384);
     if (b.p) {
         if (hipStreamSynchronize(s->stream) != hipSuccess) return fail(s, BF_ERR_LAUNCH, "stream sync failed");
-        hipHostFree(b.p);
+        pinned_put(b.p, b.cap);
         b.p = nullptr;
         b.cap = 0;
     }
-    if (hipHostMalloc(&b.p, nc, hipHostMallocDefault) != hipSuccess)
-        return fail(s, BF_ERR_LAUNCH, "hipHostMalloc failed");
-    b.cap = nc;
+    b.p = pinned_get(nc, &b.cap);
+    if (!b.p) return fail(s, BF_ERR_LAUNCH, "hipHostMalloc failed");
     return BF_OK;
 }
 
@@ -341,6 +390,38 @@ int boxfusion(bf_fseq* s, const PerFrame& P, const bf_fuse_cfg* fuse, const floa
     return BF_OK;
 }
 
+double now_us() {
+    return 1e-3 * (double)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                      std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void prof_mark(bf_fseq* s, int k) {
+    if (s->prof > 0) hipEventRecord(s->pev[k], s->stream);
+}
+
+// after the association read-back: device phases of this keyframe (events 0-3), the device gap
+// since the previous keyframe's last launch (event 5 -> 0)
+void prof_collect(bf_fseq* s, double t_entry, double t_sync0, double t_sync1) {
+    float ms[5] = {};
+    for (int k = 0; k < 3; ++k) hipEventElapsedTime(&ms[k], s->pev[k], s->pev[k + 1]);
+    if (s->pev_prev) {
+        hipEventElapsedTime(&ms[3], s->pev[5], s->pev[0]);
+        hipEventElapsedTime(&ms[4], s->pev[4], s->pev[5]);
+    }
+    s->pt[0] += t_sync0 - t_entry;                 // host: prework + enqueue
+    s->pt[1] += t_sync1 - t_sync0;                 // host: wait in hipStreamSynchronize
+    s->pt[2] += 1e3 * ms[0];                       // device: append .. obb matrix
+    s->pt[3] += 1e3 * ms[1];                       // device: nms scan
+    s->pt[4] += 1e3 * ms[2];                       // device: corr assoc + read-back
+    s->pt[5] += 1e3 * ms[3];                       // device: previous keyframe's tail -> this start
+    s->pt[7] += 1e3 * ms[4];                       // device: previous keyframe's gather + fit
+    s->pn += 1;
+    if (s->pn % 256 == 0)
+        fprintf(stderr, "fseq profile (%lld kf, us/kf): host pre %.1f wait %.1f post %.1f | dev obb %.1f nms %.1f "
+                "corr+rb %.1f fit %.1f gap %.1f\n", s->pn, s->pt[0] / s->pn, s->pt[1] / s->pn, s->pt[6] / s->pn,
+                s->pt[2] / s->pn, s->pt[3] / s->pn, s->pt[4] / s->pn, s->pt[7] / s->pn, s->pt[5] / s->pn);
+}
+
 // one keyframe with n > 0 boxes at per-frame rows [base, base + n)
 int keyframe(bf_fseq* s, const bf_fseq_cfg* cfg, const PerFrame& P, long long base, int n,
              const float* K, const float* pst) {
@@ -369,6 +450,13 @@ int keyframe(bf_fseq* s, const bf_fseq_cfg* cfg, const PerFrame& P, long long ba
         s->fusion_list.push_back({(int32_t)(base + i)});
         s->fusion_flag.push_back(0);
     }
+    if (s->prof < 0) {
+        const char* e = getenv("BF_FSEQ_PROFILE");
+        s->prof = e && atoi(e) > 0;
+        if (s->prof > 0)
+            for (hipEvent_t& ev : s->pev) hipEventCreate(&ev);
+    }
+    const double t_entry = s->prof > 0 ? now_us() : 0.0;
     const int n_glo = s->n, n_all = s->n + n;
     if (n_all > BF_MAX_BOXES) return fail(s, BF_ERR_CAPACITY, "more global boxes than BF_MAX_BOXES");
     if ((int)s->fusion_list.size() != n_all)
@@ -381,11 +469,13 @@ int keyframe(bf_fseq* s, const bf_fseq_cfg* cfg, const PerFrame& P, long long ba
     if (!rc) rc = dev_reserve(s, s->corners, (size_t)n_all * 96);
     if (!rc) rc = dev_reserve(s, s->iou, (size_t)n_all * n_all * 8);
     if (!rc) rc = dev_reserve(s, s->iou_ws, std::max(bf_obb_iou_workspace_size(n_all), (size_t)256));
+    if (!rc) rc = dev_reserve(s, s->nms_ws, std::max(bf_nms_scan_workspace_size(n_all), (size_t)256));
     if (!rc) rc = dev_reserve(s, s->xch, x_words * 4);
     if (!rc) rc = host_reserve(s, s->h_in, in_words * 4);
     if (!rc) rc = host_reserve(s, s->h_out, x_words * 4);
     if (rc) return rc;
     Table& G = s->g[s->cur];
+    prof_mark(s, 0);
     // cat(all_pred_box, pred) + dims
     hipLaunchKernelGGL(k_fseq_append, dim3(bf_cdiv(n_all, 64)), dim3(64), 0, s->stream, P.box, P.R,
                        P.score, P.box2d, base, n_glo, n_all, G.field(0), G.field(1), G.field(2),
@@ -396,6 +486,7 @@ int keyframe(bf_fseq* s, const bf_fseq_cfg* cfg, const PerFrame& P, long long ba
     rc = bf_box_corners(G.field(0), G.field(1), n_all, corners, s->stream);
     if (!rc) rc = bf_obb_iou_matrix(corners, n_all, static_cast<double*>(s->iou.p), s->iou_ws.p, s->stream);
     if (rc) return fail(s, rc, "corners / obb iou failed");
+    prof_mark(s, 1);
     // fusion lists in (BoxManager.pack_host), counts zeroed
     int32_t* hi = static_cast<int32_t*>(s->h_in.p);
     for (int i = 0; i < n_all; ++i) {
@@ -425,18 +516,23 @@ int keyframe(bf_fseq* s, const bf_fseq_cfg* cfg, const PerFrame& P, long long ba
     int32_t* ckeep = events + 3 * (n_all + 1);
     int32_t* cevents = ckeep + n_all + 1;
     const int32_t* gid = reinterpret_cast<const int32_t*>(G.field(4));
-    rc = bf_nms_scan(static_cast<double*>(s->iou.p), corners, G.field(2), gid, P.pose, n_all, items, lens,
-                     G.field(5), keep, counts, succ, counts + 1, events, counts + 2, counts + 3, &cfg->nms,
-                     s->stream);
+    rc = bf_nms_scan_ws(static_cast<double*>(s->iou.p), corners, G.field(2), gid, P.pose, n_all, items, lens,
+                        G.field(5), keep, counts, succ, counts + 1, events, counts + 2, counts + 3, &cfg->nms,
+                        s->nms_ws.p, s->stream);
     if (rc) return fail(s, rc, "bf_nms_scan failed");
+    prof_mark(s, 2);
     rc = bf_corr_assoc_chained(corners, static_cast<float*>(s->dims.p), G.field(2), G.field(3), gid, P.pose,
                                P.pose + (size_t)base * 16, K, n_all, n_glo, keep, counts, succ, counts + 1,
                                items, lens, G.field(5), ckeep, ccounts, cevents, ccounts + 1, ccounts + 2,
                                &cfg->corr, s->stream);
     if (rc) return fail(s, rc, "bf_corr_assoc_chained failed");
-    if (hipMemcpyAsync(s->h_out.p, X, x_words * 4, hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
-        hipStreamSynchronize(s->stream) != hipSuccess)
+    if (hipMemcpyAsync(s->h_out.p, X, x_words * 4, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
         return fail(s, BF_ERR_LAUNCH, "association read-back failed");
+    prof_mark(s, 3);
+    const double t_sync0 = s->prof > 0 ? now_us() : 0.0;
+    if (hipStreamSynchronize(s->stream) != hipSuccess) return fail(s, BF_ERR_LAUNCH, "association read-back failed");
+    if (s->prof > 0) prof_collect(s, t_entry, t_sync0, now_us());
+    const double t_post = s->prof > 0 ? now_us() : 0.0;
     s->assoc += 1;
     const int32_t* ho = static_cast<const int32_t*>(s->h_out.p);
     const int32_t* h_items = ho;
@@ -488,28 +584,44 @@ int keyframe(bf_fseq* s, const bf_fseq_cfg* cfg, const PerFrame& P, long long ba
     s->ids.swap(ids);
     s->n = n_keep;
     s->suppressed += hc[1];
-    if (any_cur && cfg->use_fusion) return boxfusion(s, P, &cfg->fuse, pst);
-    return BF_OK;
+    prof_mark(s, 4);
+    if (any_cur && cfg->use_fusion) rc = boxfusion(s, P, &cfg->fuse, pst);
+    if (s->prof > 0) {
+        prof_mark(s, 5);
+        s->pev_prev = true;
+        s->pt[6] += now_us() - t_post;             // host: unpack, gather, fit selection + enqueue
+    }
+    return rc;
 }
 
 }  // namespace
 
 BF_API int bf_fseq_create(bf_fseq** out) {
     if (!out) return BF_ERR_ARG;
+    // keep the stream-ordered pool's memory across synchronisations (a sequencer's buffers are
+    // regrown by doubling; the default threshold 0 returns them to the driver at every sync)
+    int dev = 0;
+    hipMemPool_t mp;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetDefaultMemPool(&mp, dev) == hipSuccess) {
+        uint64_t th = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(mp, hipMemPoolAttrReleaseThreshold, &th);
+    }
+    (void)hipGetLastError();
     *out = new bf_fseq();
     return BF_OK;
 }
 
 BF_API void bf_fseq_destroy(bf_fseq* s) {
     if (!s) return;
-    hipStreamSynchronize(s->stream);
+    if (s->used) hipStreamSynchronize(s->stream);
     for (Table& t : s->g) dev_free(t.mem, s->stream);
-    for (DevBuf* b : {&s->corners, &s->dims, &s->iou, &s->iou_ws, &s->xch, &s->jobs, &s->packed, &s->views,
+    for (DevBuf* b : {&s->corners, &s->dims, &s->iou, &s->iou_ws, &s->nms_ws, &s->xch, &s->jobs, &s->packed, &s->views,
                       &s->out_box, &s->fit_ws})
         dev_free(*b, s->stream);
-    hipStreamSynchronize(s->stream);
-    for (HostBuf* b : {&s->h_in, &s->h_out, &s->h_jobs, &s->h_fit})
-        if (b->p) hipHostFree(b->p);
+    if (s->used) hipStreamSynchronize(s->stream);
+    if (s->prof > 0)
+        for (hipEvent_t ev : s->pev) hipEventDestroy(ev);
+    for (HostBuf* b : {&s->h_in, &s->h_out, &s->h_jobs, &s->h_fit}) pinned_put(b->p, b->cap);
     delete s;
 }
 
@@ -517,10 +629,14 @@ BF_API const char* bf_fseq_error(const bf_fseq* s) { return s ? s->err.c_str() :
 
 static int use_stream(bf_fseq* s, void* stream) {
     hipStream_t st = bf_stream(stream);
-    if (s->stream != st) {      // earlier work (and frees) on the old stream
+    // earlier work (and frees) on the old stream.  Not before the first call: the initial stream
+    // is the null stream, and waiting on it waits for every blocking stream of the process (the
+    // detect streams' graphs: a 90 ms stall on a fresh sequencer's first call at --sim-ranks 8)
+    if (s->used && s->stream != st) {
         if (hipStreamSynchronize(s->stream) != hipSuccess) return fail(s, BF_ERR_LAUNCH, "stream sync failed");
     }
     s->stream = st;
+    s->used = true;
     return BF_OK;
 }
 
@@ -543,6 +659,8 @@ BF_API int bf_fseq_keyframes(bf_fseq* s, const bf_fseq_cfg* cfg, int n_kf, const
     if (cfg->nms.list_capacity != cfg->corr.list_capacity || cfg->nms.list_capacity <= 0)
         return fail(s, BF_ERR_ARG, "list capacities differ");
     const PerFrame P{p_box, p_R, p_score, p_box2d, p_pose, p_proj, p_rows};
+    const bool prof_call = s->prof > 0;
+    const double t_call = prof_call ? now_us() : 0.0;
     long long base = p_base;
     for (int j = 0; j < n_kf; ++j) {
         const int n = sizes[j];
@@ -551,13 +669,20 @@ BF_API int bf_fseq_keyframes(bf_fseq* s, const bf_fseq_cfg* cfg, int n_kf, const
         if (rc) return rc;
         base += n;
     }
+    if (prof_call) {
+        s->pt[8] += now_us() - t_call;
+        s->pt[9] += 1;
+        fprintf(stderr, "fseq call: %d keyframes %.1f us (calls so far %.0f, mean %.1f us)\n", n_kf,
+                now_us() - t_call, s->pt[9], s->pt[8] / s->pt[9]);
+    }
     return BF_OK;
 }
 
 BF_API int bf_fseq_sync(bf_fseq* s) {
     if (!s) return BF_ERR_ARG;
     // (stream may be the null stream: torch's default stream)
-    if (hipStreamSynchronize(s->stream) != hipSuccess) return fail(s, BF_ERR_LAUNCH, "stream sync failed");
+    if (s->used && hipStreamSynchronize(s->stream) != hipSuccess)
+        return fail(s, BF_ERR_LAUNCH, "stream sync failed");
     return resolve_pending(s);
 }
 

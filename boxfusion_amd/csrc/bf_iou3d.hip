@@ -352,6 +352,141 @@ __global__ void __launch_bounds__(IOU_THREADS) k_obb_grid(const BoxPrep* __restr
 
 
 
+
+// ------------------------------------------------------------------------------------------
+// Column form (default, OBB_COLS 1): one lane per grid column (ix, iy), 25 z points each.
+// Along a column x, y and the plane's partial sum S = x*a + y*b are fixed, z_k = linspace(k) is
+// non-decreasing in k, and v(k) = (S + z_k*c) + d is a chain of monotone roundings of z_k*c, so
+// the test v <= 1e-6 holds on a prefix of k (c > 0), a suffix (c < 0) or all / none (c == 0 or
+// NaN: v does not depend on z).  Each of the 12 plane tests is therefore a 5-step binary search
+// for its boundary and the box's inside set on the column is the interval they cut out,
+// intersected with the AABB cull's interval (the same two monotone z tests the point form
+// makes).  Counts: n1 = |I_A|, n2 = |I_B|, n12 = |I_A ∩ I_B| — the point form's counts exactly,
+// in ≈ 140 instead of ≈ 25·12·3 f64 operations per column and box.  A pair whose z step is not
+// >= 0 or whose planes are not all finite takes the point-by-point loop over its 25 z values.
+// ------------------------------------------------------------------------------------------
+#ifndef OBB_COLS
+#define OBB_COLS 1
+#endif
+#define OBB_COL_CHUNKS 10          // 64-column chunks per pair (625 columns)
+
+struct ZLine {
+    double start, step, stop;
+    __device__ __forceinline__ double at(int k) const { return k == 24 ? stop : (double)k * step + start; }
+};
+
+// number of leading k in [0, 25) with pred(k) (pred true on a prefix)
+template <class F>
+__device__ __forceinline__ int lead_true(F pred) {
+    int K = 0;
+#pragma unroll
+    for (int st = 16; st >= 1; st >>= 1)
+        if (K + st <= 25 && pred(K + st - 1)) K += st;
+    return K;
+}
+
+// number of trailing k in [0, 25) with pred(k) (pred true on a suffix)
+template <class F>
+__device__ __forceinline__ int trail_true(F pred) {
+    int T = 0;
+#pragma unroll
+    for (int st = 16; st >= 1; st >>= 1)
+        if (T + st <= 25 && pred(25 - T - st)) T += st;
+    return T;
+}
+
+// the box's inside interval [lo, hi) of z indices on column (x, y) (empty when hi <= lo)
+__device__ __forceinline__ void col_interval(double x, double y, const ZLine& z, const BoxPrep& P,
+                                             int* lo_out, int* hi_out) {
+    const double m = 1e-3;
+    const double lo0 = P.mn[0] - m, lo1 = P.mn[1] - m, lo2 = P.mn[2] - m;
+    const double hi0 = P.mx[0] + m, hi1 = P.mx[1] + m, hi2 = P.mx[2] + m;
+    int lo = 0, hi = 0;
+    if (x >= lo0 && x <= hi0 && y >= lo1 && y <= hi1) {
+        // AABB cull in z: z >= lo2 on a suffix, z <= hi2 on a prefix
+        lo = 25 - trail_true([&](int k) { return z.at(k) >= lo2; });
+        hi = lead_true([&](int k) { return z.at(k) <= hi2; });
+#pragma unroll 1
+        for (int q = 0; q < 12; ++q) {
+            const double a = P.pl[q][0], b = P.pl[q][1], c = P.pl[q][2], d = P.pl[q][3];
+            const double S = x * a + y * b;
+            auto in = [&](int k) { return ((S + z.at(k) * c) + d) <= 1e-6; };
+            if (c > 0) hi = min(hi, lead_true(in));
+            else if (c < 0) lo = max(lo, 25 - trail_true(in));
+            else if (!in(0)) hi = 0;
+        }
+    }
+    *lo_out = lo;
+    *hi_out = hi;
+}
+
+__device__ __forceinline__ bool prep_finite(const BoxPrep& P) {
+    bool f = true;
+#pragma unroll 1
+    for (int q = 0; q < 12; ++q)
+        for (int c = 0; c < 4; ++c) f = f && isfinite(P.pl[q][c]);
+    return f;
+}
+
+// persistent: item = (gated pair, 64-column chunk), one wave per item, 4 waves per workgroup
+__global__ void __launch_bounds__(256) k_obb_cols(const BoxPrep* __restrict__ prep, int n,
+                                                  const ObbWork* __restrict__ w,
+                                                  const int* __restrict__ gated, int* __restrict__ cnt) {
+    const int lane = threadIdx.x & 63;
+    const int items = w->n_gated * OBB_COL_CHUNKS;
+    for (int it = blockIdx.x * 4 + (threadIdx.x >> 6); it < items; it += gridDim.x * 4) {
+        const int slot = it / OBB_COL_CHUNKS, chunk = it % OBB_COL_CHUNKS;
+        int i, j;
+        pair_of((long long)gated[slot], n, &i, &j);
+        const BoxPrep& A = prep[i];
+        const BoxPrep& B = prep[j];
+        // numpy.linspace(f64(min), f64(max), 25) per axis over the union AABB (as k_obb_grid)
+        const ZLine gx{(double)fminf(A.mn[0], B.mn[0]), 0.0, (double)fmaxf(A.mx[0], B.mx[0])};
+        const ZLine gy{(double)fminf(A.mn[1], B.mn[1]), 0.0, (double)fmaxf(A.mx[1], B.mx[1])};
+        ZLine gz{(double)fminf(A.mn[2], B.mn[2]), 0.0, (double)fmaxf(A.mx[2], B.mx[2])};
+        ZLine lx = gx, ly = gy;
+        lx.step = (gx.stop - gx.start) / 24.0;
+        ly.step = (gy.stop - gy.start) / 24.0;
+        gz.step = (gz.stop - gz.start) / 24.0;
+        const int col = chunk * 64 + lane;
+        int n1 = 0, n2 = 0, n12 = 0;
+        if (col < 625) {
+            const double x = lx.at(col / 25), y = ly.at(col % 25);
+            if (gz.step >= 0 && prep_finite(A) && prep_finite(B)) {
+                int la, ha, lb, hb;
+                col_interval(x, y, gz, A, &la, &ha);
+                col_interval(x, y, gz, B, &lb, &hb);
+                n1 = max(ha - la, 0);
+                n2 = max(hb - lb, 0);
+                n12 = max(min(ha, hb) - max(la, lb), 0);
+            } else {
+                const double m = 1e-3;
+#pragma unroll 1
+                for (int k = 0; k < 25; ++k) {
+                    const double z = gz.at(k);
+                    const bool ina = x >= A.mn[0] - m && x <= A.mx[0] + m && y >= A.mn[1] - m &&
+                                     y <= A.mx[1] + m && z >= A.mn[2] - m && z <= A.mx[2] + m;
+                    const bool inb = x >= B.mn[0] - m && x <= B.mx[0] + m && y >= B.mn[1] - m &&
+                                     y <= B.mx[1] + m && z >= B.mn[2] - m && z <= B.mx[2] + m;
+                    const bool a = ina && inside12(x, y, z, A.pl);
+                    const bool b = inb && inside12(x, y, z, B.pl);
+                    n1 += a;
+                    n2 += b;
+                    n12 += (a && b);
+                }
+            }
+        }
+        n1 = bf_wave_sum_i32(n1);
+        n2 = bf_wave_sum_i32(n2);
+        n12 = bf_wave_sum_i32(n12);
+        if (lane == 0) {
+            atomicAdd(&cnt[3 * slot + 0], n1);
+            atomicAdd(&cnt[3 * slot + 1], n2);
+            atomicAdd(&cnt[3 * slot + 2], n12);
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256) k_obb_final(int n, const ObbWork* __restrict__ w,
                                                    const int* __restrict__ gated,
                                                    const int* __restrict__ cnt,
@@ -394,11 +529,17 @@ BF_API int bf_obb_iou_matrix(const float* corners, int n, double* iou, void* wor
         } else {
             hipLaunchKernelGGL(k_obb_gate, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0, s, prep, n,
                                pairs, iou, w, gated, cnt);
-            const unsigned gw = (unsigned)(pairs * (OBB_SPLIT > 0 ? OBB_SPLIT : 1) < OBB_GRID_WGS
-                                               ? pairs * (OBB_SPLIT > 0 ? OBB_SPLIT : 1) : OBB_GRID_WGS);
-            hipLaunchKernelGGL(k_obb_grid, dim3(gw), dim3(IOU_THREADS), 0, s, prep, n, w, gated, cnt,
-                               iou);
-            if (!OBB_LAST_BLOCK)
+            if (OBB_COLS) {
+                const long long waves = pairs * OBB_COL_CHUNKS;
+                const unsigned gw = (unsigned)std::min<long long>((waves + 3) / 4, OBB_GRID_WGS);
+                hipLaunchKernelGGL(k_obb_cols, dim3(gw), dim3(256), 0, s, prep, n, w, gated, cnt);
+            } else {
+                const unsigned gw = (unsigned)(pairs * (OBB_SPLIT > 0 ? OBB_SPLIT : 1) < OBB_GRID_WGS
+                                                   ? pairs * (OBB_SPLIT > 0 ? OBB_SPLIT : 1) : OBB_GRID_WGS);
+                hipLaunchKernelGGL(k_obb_grid, dim3(gw), dim3(IOU_THREADS), 0, s, prep, n, w, gated, cnt,
+                                   iou);
+            }
+            if (OBB_COLS || !OBB_LAST_BLOCK)
                 hipLaunchKernelGGL(k_obb_final, dim3(bf_cdiv((unsigned)pairs, 256)), dim3(256), 0, s, n,
                                    w, gated, cnt, iou);
         }

@@ -143,6 +143,19 @@ int bf_nms_scan(const double* iou, const float* corners, const float* scores,
                 int32_t* events, int32_t* n_events, int32_t* status,
                 const bf_nms_cfg* cfg, void* stream);
 
+/* bf_nms_scan with a caller-owned device workspace of bf_nms_scan_workspace_size(n) bytes
+ * (the same nms_3d + record, instances.py:22-101 / box_manager.py:40-88).  With it, scans too
+ * large for the IoU matrix to sit in LDS (n > 96) run the single-wave scan on the matrix's two
+ * threshold bit masks (iou <= t, iou > t) instead of the 256-thread scan over the f64 matrix in
+ * global memory; results are identical.  workspace may be NULL (= bf_nms_scan). */
+size_t bf_nms_scan_workspace_size(int n);
+int bf_nms_scan_ws(const double* iou, const float* corners, const float* scores,
+                   const int32_t* init_id, const float* cam_poses, int n,
+                   int32_t* fl_items, int32_t* fl_len, float* valid_num,
+                   int32_t* keep, int32_t* n_keep, int32_t* success, int32_t* n_success,
+                   int32_t* events, int32_t* n_events, int32_t* status,
+                   const bf_nms_cfg* cfg, void* workspace, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Cross-view correspondence association for small boxes
  *   Instances3D.correspondence_association (instances.py:411-490) + project_3d_to_2d_box

@@ -1,7 +1,9 @@
 """Host cost of the rank-0 fusion worker per keyframe: the Python-driven FusionStage against the
 native keyframe sequencer (bf_fseq), on the batches rank 0 fuses at N=8 (64 keyframes of
 records per step -> FusionStage.keyframes), 30- and 150-object scenes, GPU otherwise idle.
-Checks that both end in the same state.  Usage: python scripts/fusion_seq_bench.py [steps]"""
+Checks that both end in the same state.  Usage: python scripts/fusion_seq_bench.py [steps]
+BF_SEQ_CUS=32: the fusion runs on a stream confined to the CUs bench.py reserves for rank 0's
+fusion at N>1 (the rest of the chip idle), to separate the CU budget from the detect load."""
 import os
 import sys
 import time
@@ -10,6 +12,7 @@ import numpy as np
 import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
+from boxfusion_amd import _lib  # noqa: E402
 from boxfusion_amd.fusion_stage import FusionStage  # noqa: E402
 from boxfusion_amd.synthetic import SCANNET_K, Scene  # noqa: E402
 
@@ -31,6 +34,9 @@ def run(st, r, base):
 
 OBJS = [int(v) for v in os.environ.get("BF_SEQ_OBJECTS", "30,150").split(",")]
 MODES = [m == "native" for m in os.environ.get("BF_SEQ_MODES", "python,native").split(",")]
+CUS = int(os.environ.get("BF_SEQ_CUS", "0"))
+if CUS:
+    torch.cuda.set_stream(_lib.cu_masked_stream(_lib.partition_cus(CUS)[1]))
 for n_obj in OBJS:
     scene = Scene(seed=0, n_objects=n_obj)
     recs = [records(scene, s) for s in range(steps)]

@@ -197,6 +197,40 @@ def test_obb_iou_matrix_vs_oracle_large(L):
     np.testing.assert_array_equal(got, ref)
 
 
+def test_obb_iou_matrix_vs_oracle_tilted(L):
+    """Fully 3-D rotations (every facet plane has a z component, so the column form's binary
+    searches run on prefixes and suffixes), plus axis-aligned boxes that share faces or are
+    repeated (grid points exactly on a facet), flat boxes (a zero extent: zero z step) and
+    tiny ones: bit-exact vs the oracle's point-by-point count."""
+    rng = np.random.default_rng(11)
+    n = 120
+    xyz = rng.uniform(-1.5, 1.5, (n, 3))
+    xyz[n // 2:] = xyz[:n // 2] + rng.normal(0, 0.15, (n // 2, 3))
+    size = rng.uniform(0.1, 1.2, (n, 3))
+    q = rng.normal(size=(n, 4))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    w, x, y, z = q.T
+    R = np.stack([np.stack([1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)], -1),
+                  np.stack([2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)], -1),
+                  np.stack([2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)], -1)], 1)
+    # axis-aligned face-sharing neighbours, exact repeats, flat and tiny boxes
+    R[:24] = np.eye(3)
+    xyz[:8] = np.array([[0.25 * k, 0.0, 0.0] for k in range(8)])
+    size[:8] = np.array([0.25, 0.5, 0.5])
+    xyz[8:12], size[8:12] = xyz[:4], size[:4]
+    size[12:16, 2] = 0.0
+    size[16:20] *= 1e-3
+    xyz[12:20] = xyz[:8] + 0.01
+    b = np.concatenate([xyz, size], 1).astype(np.float32)
+    R = R.astype(np.float32)
+    corners = OR.box_corners(b, R)
+    np.testing.assert_array_equal(L.box_corners(_t(b), _t(R)).cpu().numpy(), corners)
+    ref = OR.obb_iou_matrix(corners)
+    got = L.obb_iou_matrix(_t(corners)).cpu().numpy()
+    assert (ref[np.triu_indices(n, 1)] > 0).sum() > 50
+    np.testing.assert_array_equal(got, ref)
+
+
 def test_fusion_legacy_promotion_vs_oracle(L):
     """numpy-1.26 (pinned) promotion mode: f64 host scalars, bit-exact vs the oracle."""
     t = TU.load("fusion_trace_small.npz")
