@@ -836,12 +836,16 @@ def main(argv=None):
 
     if rank == 0:
         big = lambda t: t["kind"] == "gemm" and t["large"]
-        r_all = roofline_obj(timer.summary(big), "k_gemm256q / k_gemm256p (persistent bf16 GEMM, every "
-                             "launch: qkv, proj/fc2 + f32 residual, fc1 + GELU of CLIP ViT-H and CuTR)",
+        r_all = roofline_obj(timer.summary(big), "every bf16 linear launch of CLIP ViT-H and CuTR (qkv, "
+                             "proj/fc2 + f32 residual, fc1 + GELU): k_gemm256q / k_gemm256p, or hipBLASLt "
+                             "where it timed faster for the shape (bf_gemm_tune.hip; gemm_choice)",
                              "mfma", pmc_key="k_gemm256p")
+        r_all["gemm_choice"] = _lib.gemm_tune_report()
+        r_all["traffic_note"] = "PMC traffic of the hand-written kernels (hipBLASLt launches not counted)"
         comps = {
             "resid_gemm": roofline_obj(timer.summary(lambda t: big(t) and t["resid"]),
-                                       "k_gemm256p<false, 0> (proj / fc2 + f32 residual)", "mfma",
+                                       "proj / fc2 + f32 residual (hipBLASLt or k_gemm256p<false, 0>, "
+                                       "per shape)", "mfma",
                                        pmc_key="k_gemm256p<false, 0>"),
             "gelu_gemm": roofline_obj(timer.summary(lambda t: big(t) and t["act"] == 1),
                                       "k_gemm256q<true, 1> (fc1 + GELU)", "mfma",

@@ -15,7 +15,46 @@ def L():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     from boxfusion_amd import _lib
-    return _lib
+    # these tests check the hand-written kernels: no per-shape hand-off to hipBLASLt
+    # (test_gemm_tuned_vs_torch turns it back on)
+    _lib.lib().bf_gemm_set_tune(0)
+    yield _lib
+    _lib.lib().bf_gemm_set_tune(1)
+
+
+@pytest.mark.parametrize("M,N,K,out_bf16,resid,bias", [
+    (32896, 1280, 1280, False, "inplace", True),    # CLIP out_proj + residual
+    (4112, 1280, 5120, False, "inplace", True),      # CLIP c_proj + residual (16 crops)
+    (4112, 1280, 1280, False, "separate", True),
+    (4112, 3840, 1280, True, None, True),            # qkv
+    (1000, 768, 768, False, None, False),
+    (257, 1280, 1280, True, None, False)])
+def test_gemm_tuned_vs_torch(L, M, N, K, out_bf16, resid, bias):
+    """bf_gemm_bf16's per-shape choice (hand-written kernel or hipBLASLt, whichever timed faster
+    on this box) against torch fp32, on the residual / plain linear forms it applies to."""
+    L.lib().bf_gemm_set_tune(1)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(M + N + K)
+        a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+        w = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).bfloat16()
+        b = torch.randn(N, device="cuda", generator=g) if bias else None
+        r = torch.randn(M, N, device="cuda", generator=g)
+        ref = a.float() @ w.float().T + (b if bias else 0)
+        if resid:
+            ref = ref + r
+        for _ in range(2):       # the first call of a shape times the candidates, the second uses the choice
+            if resid == "inplace":
+                out = r.clone()
+                L.gemm(a, w, b, resid=out, out=out)
+            elif resid == "separate":
+                out = torch.empty(M, N, device="cuda")
+                L.gemm(a, w, b, resid=r, out=out)
+            else:
+                out = L.gemm(a, w, b, out_dtype=torch.bfloat16 if out_bf16 else torch.float32)
+            torch.cuda.synchronize()
+            assert rel_err(out, ref) < (8e-3 if out_bf16 else 2e-5 * math.sqrt(K / 64) + 1e-5), (M, N, K)
+    finally:
+        L.lib().bf_gemm_set_tune(0)
 
 
 def rel_err(a, b):
