@@ -841,7 +841,8 @@ def main(argv=None):
                              "where it timed faster for the shape (bf_gemm_tune.hip; gemm_choice)",
                              "mfma", pmc_key="k_gemm256p")
         r_all["gemm_choice"] = _lib.gemm_tune_report()
-        r_all["traffic_note"] = "PMC traffic of the hand-written kernels (hipBLASLt launches not counted)"
+        r_all["traffic_note"] = ("PMC bytes per launch averaged over the GEMM family's kernels in "
+                                 "the PMC run: k_gemm256p / k_gemm256q and hipBLASLt's Cijk_*")
         comps = {
             "resid_gemm": roofline_obj(timer.summary(lambda t: big(t) and t["resid"]),
                                        "proj / fc2 + f32 residual (hipBLASLt or k_gemm256p<false, 0>, "
