@@ -24,6 +24,9 @@
 int bf_gemm_bf16_own(const void* A, int lda, const void* W, int ldw, const float* bias, const float* resid,
                      int ldr, int resid_mod, void* C, int ldc, int c_bf16, const int32_t* row_map, int M, int N,
                      int K, int act, void* stream);
+int bf_gemm_f32_own(const float* A, int lda, const int* a_map, const float* W, int ldw, const float* bias,
+                    const float* resid, int ldr, float* C, int ldc, const int* c_map, int M, int N, int K, int act,
+                    void* stream);
 
 namespace {
 
@@ -35,7 +38,8 @@ struct Plan {
     float us_own = 0.f, us_lib = 0.f;
 };
 
-using Key = std::tuple<int, int, int, int, int, int, int, int, int, int>;
+// M, N, K, lda, ldw, ldc, ldr (-1: no residual), output bf16, bias, resid aliases C, f32 operands, act
+using Key = std::tuple<int, int, int, int, int, int, int, int, int, int, int, int>;
 
 std::mutex g_mu;
 std::map<Key, Plan> g_plans;
@@ -55,6 +59,8 @@ struct Args {
     const float *bias, *resid;
     void* C;
     int lda, ldw, ldr, ldc, c_bf16, M, N, K;
+    int f32 = 0;        // f32 A / W (the decoder's bf_gemm_f32) instead of bf16
+    int act = 0;        // 0 none, 2 ReLU (f32 form, no residual)
 };
 
 hipblasStatus_t lib_call(const Plan& p, const Args& a, void* D, hipStream_t st) {
@@ -92,7 +98,8 @@ void make_plan(Plan& p, const Args& a, hipStream_t st) {
     const hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
     hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof ta);
     hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof tb);
-    const uint32_t epi = a.bias ? HIPBLASLT_EPILOGUE_BIAS : HIPBLASLT_EPILOGUE_DEFAULT;
+    const uint32_t epi = a.act == 2 ? (a.bias ? HIPBLASLT_EPILOGUE_RELU_BIAS : HIPBLASLT_EPILOGUE_RELU)
+                                     : (a.bias ? HIPBLASLT_EPILOGUE_BIAS : HIPBLASLT_EPILOGUE_DEFAULT);
     hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof epi);
     if (a.bias) {
         const hipDataType bt = HIP_R_32F;
@@ -101,8 +108,9 @@ void make_plan(Plan& p, const Args& a, hipStream_t st) {
         hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &a.bias, sizeof a.bias);
     }
     const hipDataType dt = a.c_bf16 ? HIP_R_16BF : HIP_R_32F;
-    hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, a.K, a.N, a.ldw);
-    hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, a.K, a.M, a.lda);
+    const hipDataType ot = a.f32 ? HIP_R_32F : HIP_R_16BF;
+    hipblasLtMatrixLayoutCreate(&p.la, ot, a.K, a.N, a.ldw);
+    hipblasLtMatrixLayoutCreate(&p.lb, ot, a.K, a.M, a.lda);
     hipblasLtMatrixLayoutCreate(&p.lc, dt, a.N, a.M, a.resid ? a.ldr : a.ldc);
     hipblasLtMatrixLayoutCreate(&p.ld, dt, a.N, a.M, a.ldc);
     hipblasLtMatmulPreference_t pref;
@@ -121,6 +129,10 @@ void make_plan(Plan& p, const Args& a, hipStream_t st) {
     if (hipMalloc(&D, dbytes) != hipSuccess) { (void)hipGetLastError(); return; }
     const float* resid_in = a.resid;
     p.us_own = time_us([&] {
+        if (a.f32)
+            return bf_gemm_f32_own(static_cast<const float*>(a.A), a.lda, nullptr, static_cast<const float*>(a.W),
+                                   a.ldw, a.bias, resid_in, a.ldr, static_cast<float*>(D), a.ldc, nullptr, a.M, a.N,
+                                   a.K, a.act, st) == BF_OK;
         return bf_gemm_bf16_own(a.A, a.lda, a.W, a.ldw, a.bias, resid_in, a.ldr, 0, D, a.ldc, a.c_bf16, nullptr,
                                 a.M, a.N, a.K, 0, st) == BF_OK;
     }, st, 3);
@@ -141,9 +153,10 @@ void make_plan(Plan& p, const Args& a, hipStream_t st) {
     (void)hipStreamSynchronize(st);
     (void)hipFree(D);
     if (getenv("BF_GEMM_TUNE_LOG"))
-        fprintf(stderr, "bf_gemm tune M=%d N=%d K=%d out=%s resid=%d bias=%d: own %.1f us, hipBLASLt best %.1f us "
-                "(%d candidates) -> %s\n", a.M, a.N, a.K, a.c_bf16 ? "bf16" : "f32", a.resid != nullptr,
-                a.bias != nullptr, p.us_own, p.us_lib, nres, p.choice < 0 ? "own" : "hipBLASLt");
+        fprintf(stderr, "bf_gemm tune %s M=%d N=%d K=%d out=%s resid=%d bias=%d act=%d: own %.1f us, hipBLASLt best "
+                "%.1f us (%d candidates) -> %s\n", a.f32 ? "f32" : "bf16", a.M, a.N, a.K, a.c_bf16 ? "bf16" : "f32",
+                a.resid != nullptr, a.bias != nullptr, a.act, p.us_own, p.us_lib, nres,
+                p.choice < 0 ? "own" : "hipBLASLt");
 }
 
 }  // namespace
@@ -163,9 +176,10 @@ BF_API int bf_gemm_tune_report(char* buf, int cap) {
     for (const auto& kv : g_plans) {
         const Key& k = kv.first;
         const Plan& p = kv.second;
-        snprintf(line, sizeof line, "%dx%dx%d %s%s%s: own %.1f us, hipBLASLt %.1f us -> %s\n", std::get<0>(k),
-                 std::get<1>(k), std::get<2>(k), std::get<7>(k) ? "bf16" : "f32", std::get<6>(k) >= 0 ? " +resid" : "",
-                 std::get<8>(k) ? " +bias" : "", p.us_own, p.us_lib < 1e29f ? p.us_lib : -1.f,
+        snprintf(line, sizeof line, "%s %dx%dx%d %s%s%s%s: own %.1f us, hipBLASLt %.1f us -> %s\n",
+                 std::get<10>(k) ? "f32" : "bf16", std::get<0>(k), std::get<1>(k), std::get<2>(k),
+                 std::get<7>(k) ? "bf16" : "f32", std::get<6>(k) >= 0 ? " +resid" : "", std::get<8>(k) ? " +bias" : "",
+                 std::get<11>(k) == 2 ? " +relu" : "", p.us_own, p.us_lib < 1e29f ? p.us_lib : -1.f,
                  p.choice < 0 ? "own" : "hipBLASLt");
         out += line;
     }
@@ -177,12 +191,13 @@ BF_API int bf_gemm_tune_report(char* buf, int cap) {
     return (int)out.size();
 }
 
-// 1: not handled here (the caller runs the hand-written kernel); otherwise a bf_status
-int bf_gemm_tuned(const void* A, int lda, const void* W, int ldw, const float* bias, const float* resid, int ldr,
-                  void* C, int ldc, int c_bf16, int M, int N, int K, void* stream) {
-    if (!tune_enabled() || (resid && c_bf16)) return 1;
+namespace {
+
+int tuned_call(const Args& a, void* stream) {
+    if (!tune_enabled() || (a.resid && a.c_bf16) || (a.resid && a.act)) return 1;
     hipStream_t st = bf_stream(stream);
-    const Key key{M, N, K, lda, ldw, ldc, resid ? ldr : -1, c_bf16, bias != nullptr, resid == C ? 1 : 0};
+    const Key key{a.M, a.N, a.K, a.lda, a.ldw, a.ldc, a.resid ? a.ldr : -1, a.c_bf16, a.bias != nullptr,
+                  a.resid == a.C ? 1 : 0, a.f32, a.act};
     std::lock_guard<std::mutex> g(g_mu);
     auto it = g_plans.find(key);
     if (it == g_plans.end()) {
@@ -192,14 +207,27 @@ int bf_gemm_tuned(const void* A, int lda, const void* W, int ldw, const float* b
             return 1;                              // no timing inside a capture
         }
         Plan p;
-        const Args a{A, W, bias, resid, C, lda, ldw, ldr, ldc, c_bf16, M, N, K};
         make_plan(p, a, st);
         it = g_plans.emplace(key, p).first;
     }
     Plan& p = it->second;
     if (p.choice < 0) return 1;
-    if (bias)
-        hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof bias);
-    const Args a{A, W, bias, resid, C, lda, ldw, ldr, ldc, c_bf16, M, N, K};
-    return lib_call(p, a, C, st) == HIPBLAS_STATUS_SUCCESS ? BF_OK : BF_ERR_LAUNCH;
+    if (a.bias)
+        hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &a.bias, sizeof a.bias);
+    return lib_call(p, a, a.C, st) == HIPBLAS_STATUS_SUCCESS ? BF_OK : BF_ERR_LAUNCH;
+}
+
+}  // namespace
+
+// 1: not handled here (the caller runs the hand-written kernel); otherwise a bf_status
+int bf_gemm_tuned(const void* A, int lda, const void* W, int ldw, const float* bias, const float* resid, int ldr,
+                  void* C, int ldc, int c_bf16, int M, int N, int K, void* stream) {
+    return tuned_call(Args{A, W, bias, resid, C, lda, ldw, ldr, ldc, c_bf16, M, N, K, 0, 0}, stream);
+}
+
+// the decoder's f32 linears (bf_gemm_f32 without row maps): act 0, or ReLU without a residual
+int bf_gemm_f32_tuned(const float* A, int lda, const float* W, int ldw, const float* bias, const float* resid,
+                      int ldr, float* C, int ldc, int M, int N, int K, int act, void* stream) {
+    if (act != 0 && act != 2) return 1;
+    return tuned_call(Args{A, W, bias, resid, C, lda, ldw, ldr, ldc, 0, M, N, K, 1, act}, stream);
 }
