@@ -1441,9 +1441,30 @@ static void launch_gemm256_f8(int grid, hipStream_t st, const void* A, int lda, 
                        K, tiles_n, tiles_m, 1, g_group_m, 0, csc, oqs);
 }
 
+int bf_gemm_fp8_tuned(const void* A, int lda, const void* W, int ldw, float scale, const float* bias,
+                      const float* resid, int ldr, void* C, int ldc, int out_kind, int M, int N, int K, int act,
+                      void* stream);
+int bf_gemm_fp8_own(const void* A, int lda, const void* W, int ldw, float scale, const float* bias,
+                    const float* resid, int ldr, void* C, int ldc, int out_kind, float out_qscale, int M, int N,
+                    int K, int act, void* stream);
+
+// bf16 / f32 outputs without an activation take the per-shape choice of bf_gemm_tune.hip
 BF_API int bf_gemm_fp8(const void* A, int lda, const void* W, int ldw, float scale,
                        const float* bias, const float* resid, int ldr, void* C, int ldc, int out_kind,
                        float out_qscale, int M, int N, int K, int act, void* stream) {
+    if (A && W && C && scale > 0.f && M > 0 && N > 0 && K > 0 && act == 0 && out_kind <= 1 && out_kind >= 0 &&
+        K % 128 == 0 && lda % 16 == 0 && ldw % 16 == 0 && (!resid || out_kind == 0)) {
+        const int rc = bf_gemm_fp8_tuned(A, lda, W, ldw, scale, bias, resid, ldr, C, ldc, out_kind, M, N, K, act,
+                                         stream);
+        if (rc != 1) return rc;
+    }
+    return bf_gemm_fp8_own(A, lda, W, ldw, scale, bias, resid, ldr, C, ldc, out_kind, out_qscale, M, N, K, act,
+                           stream);
+}
+
+int bf_gemm_fp8_own(const void* A, int lda, const void* W, int ldw, float scale,
+                    const float* bias, const float* resid, int ldr, void* C, int ldc, int out_kind,
+                    float out_qscale, int M, int N, int K, int act, void* stream) {
     if (!A || !W || !C || !(scale > 0.f) || M < 0 || N <= 0 || K <= 0 || act < 0 || act > 1 ||
         out_kind < 0 || out_kind > 2)
         return BF_ERR_ARG;

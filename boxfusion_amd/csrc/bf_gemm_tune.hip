@@ -27,6 +27,9 @@ int bf_gemm_bf16_own(const void* A, int lda, const void* W, int ldw, const float
 int bf_gemm_f32_own(const float* A, int lda, const int* a_map, const float* W, int ldw, const float* bias,
                     const float* resid, int ldr, float* C, int ldc, const int* c_map, int M, int N, int K, int act,
                     void* stream);
+int bf_gemm_fp8_own(const void* A, int lda, const void* W, int ldw, float scale, const float* bias,
+                    const float* resid, int ldr, void* C, int ldc, int out_kind, float out_qscale, int M, int N,
+                    int K, int act, void* stream);
 
 namespace {
 
@@ -59,12 +62,13 @@ struct Args {
     const float *bias, *resid;
     void* C;
     int lda, ldw, ldr, ldc, c_bf16, M, N, K;
-    int f32 = 0;        // f32 A / W (the decoder's bf_gemm_f32) instead of bf16
+    int f32 = 0;        // operands: 0 bf16, 1 f32 (the decoder's bf_gemm_f32), 2 fp8 e4m3 (bf_gemm_fp8)
     int act = 0;        // 0 none, 2 ReLU (f32 form, no residual)
+    float alpha = 1.f;  // fp8: the per-tensor scale product
 };
 
 hipblasStatus_t lib_call(const Plan& p, const Args& a, void* D, hipStream_t st) {
-    const float alpha = 1.f, beta = a.resid ? 1.f : 0.f;
+    const float alpha = a.alpha, beta = a.resid ? 1.f : 0.f;
     const void* Cin = a.resid ? static_cast<const void*>(a.resid) : D;
     return hipblasLtMatmul(g_handle, p.desc, &alpha, a.W, p.la, a.A, p.lb, &beta, Cin, p.lc, D, p.ld, &p.algo,
                            nullptr, 0, st);
@@ -108,7 +112,7 @@ void make_plan(Plan& p, const Args& a, hipStream_t st) {
         hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &a.bias, sizeof a.bias);
     }
     const hipDataType dt = a.c_bf16 ? HIP_R_16BF : HIP_R_32F;
-    const hipDataType ot = a.f32 ? HIP_R_32F : HIP_R_16BF;
+    const hipDataType ot = a.f32 == 1 ? HIP_R_32F : a.f32 == 2 ? HIP_R_8F_E4M3 : HIP_R_16BF;
     hipblasLtMatrixLayoutCreate(&p.la, ot, a.K, a.N, a.ldw);
     hipblasLtMatrixLayoutCreate(&p.lb, ot, a.K, a.M, a.lda);
     hipblasLtMatrixLayoutCreate(&p.lc, dt, a.N, a.M, a.resid ? a.ldr : a.ldc);
@@ -129,6 +133,9 @@ void make_plan(Plan& p, const Args& a, hipStream_t st) {
     if (hipMalloc(&D, dbytes) != hipSuccess) { (void)hipGetLastError(); return; }
     const float* resid_in = a.resid;
     p.us_own = time_us([&] {
+        if (a.f32 == 2)
+            return bf_gemm_fp8_own(a.A, a.lda, a.W, a.ldw, a.alpha, a.bias, resid_in, a.ldr, D, a.ldc,
+                                   a.c_bf16 ? 1 : 0, 1.f, a.M, a.N, a.K, 0, st) == BF_OK;
         if (a.f32)
             return bf_gemm_f32_own(static_cast<const float*>(a.A), a.lda, nullptr, static_cast<const float*>(a.W),
                                    a.ldw, a.bias, resid_in, a.ldr, static_cast<float*>(D), a.ldc, nullptr, a.M, a.N,
@@ -154,7 +161,7 @@ void make_plan(Plan& p, const Args& a, hipStream_t st) {
     (void)hipFree(D);
     if (getenv("BF_GEMM_TUNE_LOG"))
         fprintf(stderr, "bf_gemm tune %s M=%d N=%d K=%d out=%s resid=%d bias=%d act=%d: own %.1f us, hipBLASLt best "
-                "%.1f us (%d candidates) -> %s\n", a.f32 ? "f32" : "bf16", a.M, a.N, a.K, a.c_bf16 ? "bf16" : "f32",
+                "%.1f us (%d candidates) -> %s\n", a.f32 == 2 ? "fp8" : a.f32 ? "f32" : "bf16", a.M, a.N, a.K, a.c_bf16 ? "bf16" : "f32",
                 a.resid != nullptr, a.bias != nullptr, a.act, p.us_own, p.us_lib, nres,
                 p.choice < 0 ? "own" : "hipBLASLt");
 }
@@ -177,7 +184,7 @@ BF_API int bf_gemm_tune_report(char* buf, int cap) {
         const Key& k = kv.first;
         const Plan& p = kv.second;
         snprintf(line, sizeof line, "%s %dx%dx%d %s%s%s%s: own %.1f us, hipBLASLt %.1f us -> %s\n",
-                 std::get<10>(k) ? "f32" : "bf16", std::get<0>(k), std::get<1>(k), std::get<2>(k),
+                 std::get<10>(k) == 2 ? "fp8" : std::get<10>(k) ? "f32" : "bf16", std::get<0>(k), std::get<1>(k), std::get<2>(k),
                  std::get<7>(k) ? "bf16" : "f32", std::get<6>(k) >= 0 ? " +resid" : "", std::get<8>(k) ? " +bias" : "",
                  std::get<11>(k) == 2 ? " +relu" : "", p.us_own, p.us_lib < 1e29f ? p.us_lib : -1.f,
                  p.choice < 0 ? "own" : "hipBLASLt");
@@ -223,6 +230,17 @@ int tuned_call(const Args& a, void* stream) {
 int bf_gemm_tuned(const void* A, int lda, const void* W, int ldw, const float* bias, const float* resid, int ldr,
                   void* C, int ldc, int c_bf16, int M, int N, int K, void* stream) {
     return tuned_call(Args{A, W, bias, resid, C, lda, ldw, ldr, ldc, c_bf16, M, N, K, 0, 0}, stream);
+}
+
+// the fp8 CLIP linears with a bf16 output or an f32 (residual) output and no activation
+// (configs[4]); scale = the activation x weight scale product, hipBLASLt's alpha
+int bf_gemm_fp8_tuned(const void* A, int lda, const void* W, int ldw, float scale, const float* bias,
+                      const float* resid, int ldr, void* C, int ldc, int out_kind, int M, int N, int K, int act,
+                      void* stream) {
+    if (act != 0 || out_kind > 1) return 1;
+    Args a{A, W, bias, resid, C, lda, ldw, ldr, ldc, out_kind == 1 ? 1 : 0, M, N, K, 2, 0};
+    a.alpha = scale;
+    return tuned_call(a, stream);
 }
 
 // the decoder's f32 linears (bf_gemm_f32 without row maps): act 0, or ReLU without a residual
