@@ -132,7 +132,7 @@ void make_plan(Plan& p, const Args& a, hipStream_t st) {
     const size_t dbytes = (size_t)a.M * a.ldc * (a.c_bf16 ? 2 : 4);
     if (hipMalloc(&D, dbytes) != hipSuccess) { (void)hipGetLastError(); return; }
     const float* resid_in = a.resid;
-    p.us_own = time_us([&] {
+    auto own = [&] {
         if (a.f32 == 2)
             return bf_gemm_fp8_own(a.A, a.lda, a.W, a.ldw, a.alpha, a.bias, resid_in, a.ldr, D, a.ldc,
                                    a.c_bf16 ? 1 : 0, 1.f, a.M, a.N, a.K, 0, st) == BF_OK;
@@ -142,17 +142,28 @@ void make_plan(Plan& p, const Args& a, hipStream_t st) {
                                    a.K, a.act, st) == BF_OK;
         return bf_gemm_bf16_own(a.A, a.lda, a.W, a.ldw, a.bias, resid_in, a.ldr, 0, D, a.ldc, a.c_bf16, nullptr,
                                 a.M, a.N, a.K, 0, st) == BF_OK;
-    }, st, 3);
+    };
+    // two passes over every candidate (own kernel first in the first, last in the second: a clock
+    // still ramping up or a neighbour's burst cannot favour one side), the minimum of each kept
+    std::vector<float> lib_us(nres, 1e30f);
+    p.us_own = 1e30f;
+    for (int pass = 0; pass < 2; ++pass) {
+        if (pass == 0) p.us_own = std::min(p.us_own, time_us(own, st, 3));
+        for (int r = 0; r < nres; ++r) {
+            if (res[r].state != HIPBLAS_STATUS_SUCCESS || res[r].workspaceSize != 0) continue;
+            Plan q = p;
+            q.algo = res[r].algo;
+            lib_us[r] = std::min(lib_us[r],
+                                 time_us([&] { return lib_call(q, a, D, st) == HIPBLAS_STATUS_SUCCESS; }, st, 3));
+        }
+        if (pass == 1) p.us_own = std::min(p.us_own, time_us(own, st, 3));
+    }
     float best = p.us_own;
     p.us_lib = 1e30f;
     for (int r = 0; r < nres; ++r) {
-        if (res[r].state != HIPBLAS_STATUS_SUCCESS || res[r].workspaceSize != 0) continue;
-        Plan q = p;
-        q.algo = res[r].algo;
-        const float us = time_us([&] { return lib_call(q, a, D, st) == HIPBLAS_STATUS_SUCCESS; }, st, 3);
-        if (us < p.us_lib) p.us_lib = us;
-        if (us < best) {
-            best = us;
+        if (lib_us[r] < p.us_lib) p.us_lib = lib_us[r];
+        if (lib_us[r] < best) {
+            best = lib_us[r];
             p.choice = r;
             p.algo = res[r].algo;
         }
