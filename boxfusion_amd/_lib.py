@@ -1133,6 +1133,17 @@ def partition_streams(n_reserved, device=None, masked=False):
 XCDS = 8
 
 
+def cu_placement(stream, n_wg=4096, spin=20000):
+    """{(xcc, se, sh, cu)} of the CUs that n_wg probe workgroups ran on when launched on `stream`
+    (bf_cu_probe): what a CU mask really does on this chip"""
+    out = torch.zeros(2 * n_wg, dtype=torch.int32, device=torch.device("cuda", stream.device_index))
+    _check(lib().bf_cu_probe(_ptr(out), c_int(n_wg), c_int(spin), c_void_p(stream.cuda_stream)), "bf_cu_probe")
+    stream.synchronize()
+    v = out.view(-1, 2).cpu().numpy()
+    hw, xcc = v[:, 0], v[:, 1] & 0xF
+    return {(int(x), int((h >> 13) & 7), int((h >> 12) & 1), int((h >> 8) & 0xF)) for h, x in zip(hw, xcc)}
+
+
 def partition_cus(n_reserved, device=None):
     """(detect CUs, fusion CUs) as CU-mask bit indices.  Mask bit i is CU i // 8 of XCD i % 8, and
     a mask that leaves an XCD without CUs is not applied at all (the stream then runs on every CU:

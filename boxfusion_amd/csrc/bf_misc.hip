@@ -67,3 +67,27 @@ BF_API int bf_rows_gather(const bf_rows_field* fields, int n_fields, const void*
                        args, idx, idx_i32, n_out, status);
     return bf_check_launch();
 }
+
+// ------------------------------------------------------------------------------------------
+// placement probe: where the workgroups of a launch on `stream` run.  out[2 b] = the HW_ID
+// register (CU in bits 11:8, SH 12, SE 15:13), out[2 b + 1] = the XCC id; each workgroup spins
+// `spin` cycles so the launch spreads over every CU the stream may use.  Checks CU-mask layouts
+// (bench.py's fusion reservation) on the hardware.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_cu_probe(int* __restrict__ out, int spin) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    const long long t0 = clock64();
+    while (clock64() - t0 < spin) {}
+    if (threadIdx.x == 0) {
+        out[2 * blockIdx.x] = (int)hw;
+        out[2 * blockIdx.x + 1] = (int)xcc;
+    }
+}
+
+BF_API int bf_cu_probe(int* out, int n_wg, int spin, void* stream) {
+    if (!out || n_wg <= 0 || spin < 0) return BF_ERR_ARG;
+    hipLaunchKernelGGL(k_cu_probe, dim3(n_wg), dim3(64), 0, bf_stream(stream), out, spin);
+    return bf_check_launch();
+}

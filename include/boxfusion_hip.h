@@ -597,6 +597,11 @@ int bf_ingest_rgbd(const uint8_t* bgr, int Hc, int Wc, const uint16_t* depth, in
 int bf_cv2_resize_u8(const uint8_t* src, int Hs, int Ws, int cn, int Hd, int Wd, int F, uint8_t* dst,
                      void* stream);
 
+/* placement probe (diagnostic): n_wg workgroups on `stream`, each spinning `spin` cycles, write
+ * out[2b] = HW_ID (CU bits 11:8, SH 12, SE 15:13) and out[2b+1] = XCC id -- which CUs a (CU-masked)
+ * stream really runs on */
+int bf_cu_probe(int* out, int n_wg, int spin, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

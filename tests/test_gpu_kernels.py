@@ -460,3 +460,19 @@ def test_gemm_operand_extent_capacity(L):
                             None, None, 0, 0, ctypes.c_void_p(c.data_ptr()), 64, 1, None, 1 << 24, 64,
                             64, 0, None)
     assert rc == -3       # BF_ERR_CAPACITY
+
+
+def test_cu_partition_placement(L):
+    """the fusion reservation (first 32 mask bits) runs on 4 CUs of every XCD and the detect mask
+    on the other 28 of each; a mask that leaves an XCD without CUs is not applied by the runtime
+    (bench.py's old every-8th-CU set ran on every CU), so the layout is checked on the hardware"""
+    from collections import Counter
+    n = torch.cuda.get_device_properties(0).multi_processor_count
+    if n % L.XCDS:
+        pytest.skip("CU count not a multiple of the XCD count")
+    det, fus = L.partition_cus(32)
+    pf = L.cu_placement(L.cu_masked_stream(fus))
+    pd = L.cu_placement(L.cu_masked_stream(det))
+    assert len(pf) == 32 and len(pd) == n - 32
+    assert not (pf & pd)
+    assert set(Counter(k[0] for k in pf).values()) == {32 // L.XCDS}
