@@ -1144,13 +1144,15 @@ def cu_placement(stream, n_wg=4096, spin=20000):
     return {(int(x), int((h >> 13) & 7), int((h >> 12) & 1), int((h >> 8) & 0xF)) for h, x in zip(hw, xcc)}
 
 
-def partition_cus(n_reserved, device=None):
+def partition_cus(n_reserved, device=None, n_cu=None):
     """(detect CUs, fusion CUs) as CU-mask bit indices.  Mask bit i is CU i // 8 of XCD i % 8, and
     a mask that leaves an XCD without CUs is not applied at all (the stream then runs on every CU:
     measured with scripts/diag/cu_probe.py), so the fusion set takes the first n_reserved bits —
     n_reserved / 8 CUs on every XCD — and detection the rest."""
-    dev = torch.cuda.current_device() if device is None else device
-    n = torch.cuda.get_device_properties(dev).multi_processor_count
+    if n_cu is None:
+        dev = torch.cuda.current_device() if device is None else device
+        n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+    n = n_cu
     k = -(-max(1, n_reserved) // XCDS) * XCDS
     if k >= n:
         raise HipError(f"cannot reserve {n_reserved} of {n} CUs for the fusion stream")
