@@ -67,10 +67,11 @@ for name, ctrs in per.items():
 # (regular expressions over the demangled names; k_gemm256p<OUT_BF16, ACT, F8>)
 # (k_gemm256q, the overlapped-epilogue form, runs the bf16-output GEMMs from round 3 on: it joins
 # the bf16 GEMM groups under the same keys)
-# (round 4: the plain linears a per-shape timing hands to hipBLASLt -- its Cijk_* kernels -- join
-# the bf16 GEMM group, and the residual group, whose members they mostly are)
-groups = {"k_gemm256p": [r"k_gemm256p<\w+, \d, 0>", r"k_gemm256q<", r"^Cijk_"],
-          "k_gemm256p<false, 0>": [r"k_gemm256p<false, 0, 0>", r"k_gemm256q<false, 0, true>", r"^Cijk_"],
+# (round 4: the bf16 linears a per-shape timing hands to hipBLASLt -- its Cijk_*_B[BS]S_BH kernels,
+# bf16 operands; the decoder's f32 ones are Cijk_*_S_B -- join the bf16 GEMM group, the f32-output
+# ones the residual group, whose members they mostly are)
+groups = {"k_gemm256p": [r"k_gemm256p<\w+, \d, 0>", r"k_gemm256q<", r"^Cijk_Alik_Bljk_B[BS]S_BH"],
+          "k_gemm256p<false, 0>": [r"k_gemm256p<false, 0, 0>", r"k_gemm256q<false, 0, true>", r"^Cijk_Alik_Bljk_BSS_BH"],
           "k_gemm256p<true, 1>": [r"k_gemm256p<true, 1, 0>", r"k_gemm256q<true, 1,"],
           "k_gemm256p_fp8": [r"k_gemm256p<\w+, \d, [13]>"],
           "k_attn": ["k_attn"],
