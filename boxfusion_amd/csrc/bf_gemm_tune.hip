@@ -24,9 +24,6 @@
 int bf_gemm_bf16_own(const void* A, int lda, const void* W, int ldw, const float* bias, const float* resid,
                      int ldr, int resid_mod, void* C, int ldc, int c_bf16, const int32_t* row_map, int M, int N,
                      int K, int act, void* stream);
-int bf_gemm_f32_own(const float* A, int lda, const int* a_map, const float* W, int ldw, const float* bias,
-                    const float* resid, int ldr, float* C, int ldc, const int* c_map, int M, int N, int K, int act,
-                    void* stream);
 int bf_gemm_fp8_own(const void* A, int lda, const void* W, int ldw, float scale, const float* bias,
                     const float* resid, int ldr, void* C, int ldc, int out_kind, float out_qscale, int M, int N,
                     int K, int act, void* stream);
@@ -62,8 +59,8 @@ struct Args {
     const float *bias, *resid;
     void* C;
     int lda, ldw, ldr, ldc, c_bf16, M, N, K;
-    int f32 = 0;        // operands: 0 bf16, 1 f32 (the decoder's bf_gemm_f32), 2 fp8 e4m3 (bf_gemm_fp8)
-    int act = 0;        // 0 none, 2 ReLU (f32 form, no residual)
+    int f32 = 0;        // operands: 0 bf16, 2 fp8 e4m3 (bf_gemm_fp8)
+    int act = 0;        // 0 (the only form handed to the library)
     float alpha = 1.f;  // fp8: the per-tensor scale product
 };
 
@@ -102,8 +99,7 @@ void make_plan(Plan& p, const Args& a, hipStream_t st) {
     const hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
     hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof ta);
     hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof tb);
-    const uint32_t epi = a.act == 2 ? (a.bias ? HIPBLASLT_EPILOGUE_RELU_BIAS : HIPBLASLT_EPILOGUE_RELU)
-                                     : (a.bias ? HIPBLASLT_EPILOGUE_BIAS : HIPBLASLT_EPILOGUE_DEFAULT);
+    const uint32_t epi = a.bias ? HIPBLASLT_EPILOGUE_BIAS : HIPBLASLT_EPILOGUE_DEFAULT;
     hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof epi);
     if (a.bias) {
         const hipDataType bt = HIP_R_32F;
@@ -112,7 +108,7 @@ void make_plan(Plan& p, const Args& a, hipStream_t st) {
         hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &a.bias, sizeof a.bias);
     }
     const hipDataType dt = a.c_bf16 ? HIP_R_16BF : HIP_R_32F;
-    const hipDataType ot = a.f32 == 1 ? HIP_R_32F : a.f32 == 2 ? HIP_R_8F_E4M3 : HIP_R_16BF;
+    const hipDataType ot = a.f32 == 2 ? HIP_R_8F_E4M3 : HIP_R_16BF;
     hipblasLtMatrixLayoutCreate(&p.la, ot, a.K, a.N, a.ldw);
     hipblasLtMatrixLayoutCreate(&p.lb, ot, a.K, a.M, a.lda);
     hipblasLtMatrixLayoutCreate(&p.lc, dt, a.N, a.M, a.resid ? a.ldr : a.ldc);
@@ -136,10 +132,6 @@ void make_plan(Plan& p, const Args& a, hipStream_t st) {
         if (a.f32 == 2)
             return bf_gemm_fp8_own(a.A, a.lda, a.W, a.ldw, a.alpha, a.bias, resid_in, a.ldr, D, a.ldc,
                                    a.c_bf16 ? 1 : 0, 1.f, a.M, a.N, a.K, 0, st) == BF_OK;
-        if (a.f32)
-            return bf_gemm_f32_own(static_cast<const float*>(a.A), a.lda, nullptr, static_cast<const float*>(a.W),
-                                   a.ldw, a.bias, resid_in, a.ldr, static_cast<float*>(D), a.ldc, nullptr, a.M, a.N,
-                                   a.K, a.act, st) == BF_OK;
         return bf_gemm_bf16_own(a.A, a.lda, a.W, a.ldw, a.bias, resid_in, a.ldr, 0, D, a.ldc, a.c_bf16, nullptr,
                                 a.M, a.N, a.K, 0, st) == BF_OK;
     };
@@ -172,7 +164,7 @@ void make_plan(Plan& p, const Args& a, hipStream_t st) {
     (void)hipFree(D);
     if (getenv("BF_GEMM_TUNE_LOG"))
         fprintf(stderr, "bf_gemm tune %s M=%d N=%d K=%d out=%s resid=%d bias=%d act=%d: own %.1f us, hipBLASLt best "
-                "%.1f us (%d candidates) -> %s\n", a.f32 == 2 ? "fp8" : a.f32 ? "f32" : "bf16", a.M, a.N, a.K, a.c_bf16 ? "bf16" : "f32",
+                "%.1f us (%d candidates) -> %s\n", a.f32 == 2 ? "fp8" : "bf16", a.M, a.N, a.K, a.c_bf16 ? "bf16" : "f32",
                 a.resid != nullptr, a.bias != nullptr, a.act, p.us_own, p.us_lib, nres,
                 p.choice < 0 ? "own" : "hipBLASLt");
 }
@@ -195,7 +187,7 @@ BF_API int bf_gemm_tune_report(char* buf, int cap) {
         const Key& k = kv.first;
         const Plan& p = kv.second;
         snprintf(line, sizeof line, "%s %dx%dx%d %s%s%s%s: own %.1f us, hipBLASLt %.1f us -> %s\n",
-                 std::get<10>(k) == 2 ? "fp8" : std::get<10>(k) ? "f32" : "bf16", std::get<0>(k), std::get<1>(k), std::get<2>(k),
+                 std::get<10>(k) == 2 ? "fp8" : "bf16", std::get<0>(k), std::get<1>(k), std::get<2>(k),
                  std::get<7>(k) ? "bf16" : "f32", std::get<6>(k) >= 0 ? " +resid" : "", std::get<8>(k) ? " +bias" : "",
                  std::get<11>(k) == 2 ? " +relu" : "", p.us_own, p.us_lib < 1e29f ? p.us_lib : -1.f,
                  p.choice < 0 ? "own" : "hipBLASLt");
@@ -254,9 +246,3 @@ int bf_gemm_fp8_tuned(const void* A, int lda, const void* W, int ldw, float scal
     return tuned_call(a, stream);
 }
 
-// the decoder's f32 linears (bf_gemm_f32 without row maps): act 0, or ReLU without a residual
-int bf_gemm_f32_tuned(const float* A, int lda, const float* W, int ldw, const float* bias, const float* resid,
-                      int ldr, float* C, int ldc, int M, int N, int K, int act, void* stream) {
-    if (act != 0 && act != 2) return 1;
-    return tuned_call(Args{A, W, bias, resid, C, lda, ldw, ldr, ldc, 0, M, N, K, 1, act}, stream);
-}
