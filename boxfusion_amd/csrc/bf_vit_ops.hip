@@ -12,6 +12,10 @@
 
 typedef unsigned short u16;
 
+#ifndef LN_PRELOAD_GB
+#define LN_PRELOAD_GB 1         // 0: gamma / beta read after the reductions (38.9 vs 36.9 us, CLIP 32896 x 1280)
+#endif
+
 __device__ __forceinline__ u16 vf2bf(float f) {
     __bf16 b = (__bf16)f;
     return *reinterpret_cast<u16*>(&b);
@@ -37,11 +41,27 @@ __global__ void __launch_bounds__(256) k_layernorm(const float* __restrict__ x, 
     if (row >= M) return;
     const float* xr = x + (size_t)row * ldx;
     float4 v[NPL];
-    float s = 0.f;
 #pragma unroll
     for (int i = 0; i < NPL; ++i) {
         int c = (lane + 64 * i) * 4;
         v[i] = *reinterpret_cast<const float4*>(xr + min(c, C - 4));   // address always in-row
+    }
+#if LN_PRELOAD_GB
+    // the bf16 form's gamma / beta fetched beside the row, not after the two reductions
+    float4 gpre[OUTK == 0 ? NPL : 1], bpre[OUTK == 0 ? NPL : 1];
+    if (OUTK == 0) {
+#pragma unroll
+        for (int i = 0; i < NPL; ++i) {
+            const int c = min((lane + 64 * i) * 4, C - 4);
+            gpre[i] = *reinterpret_cast<const float4*>(g + c);
+            bpre[i] = *reinterpret_cast<const float4*>(bb + c);
+        }
+    }
+#endif
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+        int c = (lane + 64 * i) * 4;
         if (c >= C) v[i] = make_float4(0, 0, 0, 0);
         s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
     }
@@ -101,8 +121,12 @@ __global__ void __launch_bounds__(256) k_layernorm(const float* __restrict__ x, 
     for (int i = 0; i < NPL; ++i) {
         int c = (lane + 64 * i) * 4;
         if (c < C) {
+#if LN_PRELOAD_GB
+            const float4 gg = gpre[OUTK == 0 ? i : 0], be = bpre[OUTK == 0 ? i : 0];
+#else
             float4 gg = *reinterpret_cast<const float4*>(g + min(c, C - 4));
             float4 be = *reinterpret_cast<const float4*>(bb + min(c, C - 4));
+#endif
             uint32_t lo = (uint32_t)vf2bf((v[i].x - mean) * rstd * gg.x + be.x) |
                           ((uint32_t)vf2bf((v[i].y - mean) * rstd * gg.y + be.y) << 16);
             uint32_t hi = (uint32_t)vf2bf((v[i].z - mean) * rstd * gg.z + be.z) |
