@@ -47,15 +47,13 @@ __global__ void __launch_bounds__(256) k_layernorm(const float* __restrict__ x, 
         v[i] = *reinterpret_cast<const float4*>(xr + min(c, C - 4));   // address always in-row
     }
 #if LN_PRELOAD_GB
-    // the bf16 form's gamma / beta fetched beside the row, not after the two reductions
-    float4 gpre[OUTK == 0 ? NPL : 1], bpre[OUTK == 0 ? NPL : 1];
-    if (OUTK == 0) {
+    // gamma / beta fetched beside the row, not after the two reductions
+    float4 gpre[NPL], bpre[NPL];
 #pragma unroll
-        for (int i = 0; i < NPL; ++i) {
-            const int c = min((lane + 64 * i) * 4, C - 4);
-            gpre[i] = *reinterpret_cast<const float4*>(g + c);
-            bpre[i] = *reinterpret_cast<const float4*>(bb + c);
-        }
+    for (int i = 0; i < NPL; ++i) {
+        const int c = min((lane + 64 * i) * 4, C - 4);
+        gpre[i] = *reinterpret_cast<const float4*>(g + c);
+        bpre[i] = *reinterpret_cast<const float4*>(bb + c);
     }
 #endif
     float s = 0.f;
@@ -88,8 +86,12 @@ __global__ void __launch_bounds__(256) k_layernorm(const float* __restrict__ x, 
         for (int i = 0; i < NPL; ++i) {
             int c = (lane + 64 * i) * 4;
             if (c < C) {
+#if LN_PRELOAD_GB
+                const float4 gg = gpre[i], be = bpre[i];
+#else
                 float4 gg = *reinterpret_cast<const float4*>(g + c);
                 float4 be = *reinterpret_cast<const float4*>(bb + c);
+#endif
                 const float y0 = fminf(fmaxf(((v[i].x - mean) * rstd * gg.x + be.x) * qs, -448.f), 448.f);
                 const float y1 = fminf(fmaxf(((v[i].y - mean) * rstd * gg.y + be.y) * qs, -448.f), 448.f);
                 const float y2 = fminf(fmaxf(((v[i].z - mean) * rstd * gg.z + be.z) * qs, -448.f), 448.f);
@@ -107,8 +109,12 @@ __global__ void __launch_bounds__(256) k_layernorm(const float* __restrict__ x, 
         for (int i = 0; i < NPL; ++i) {
             int c = (lane + 64 * i) * 4;
             if (c < C) {
+#if LN_PRELOAD_GB
+                const float4 gg = gpre[i], be = bpre[i];
+#else
                 float4 gg = *reinterpret_cast<const float4*>(g + c);
                 float4 be = *reinterpret_cast<const float4*>(bb + c);
+#endif
                 *reinterpret_cast<float4*>(yr + c) =
                     make_float4((v[i].x - mean) * rstd * gg.x + be.x, (v[i].y - mean) * rstd * gg.y + be.y,
                                 (v[i].z - mean) * rstd * gg.z + be.z, (v[i].w - mean) * rstd * gg.w + be.w);
@@ -122,7 +128,7 @@ __global__ void __launch_bounds__(256) k_layernorm(const float* __restrict__ x, 
         int c = (lane + 64 * i) * 4;
         if (c < C) {
 #if LN_PRELOAD_GB
-            const float4 gg = gpre[OUTK == 0 ? i : 0], be = bpre[OUTK == 0 ? i : 0];
+            const float4 gg = gpre[i], be = bpre[i];
 #else
             float4 gg = *reinterpret_cast<const float4*>(g + min(c, C - 4));
             float4 be = *reinterpret_cast<const float4*>(bb + min(c, C - 4));
