@@ -394,6 +394,22 @@ def cpu_baseline(cutr, clip_vis, args, scene):
     return out
 
 
+# PMC record keys of the bench line's roofline objects: group names of scripts/profile_round.sh,
+# or "sum:<regex>" over the kernel names of one multi-launch call (every one must match a kernel
+# of the newest committed profiles/r*_pmc.json: tests/test_bench_pmc.py)
+PMC_KEYS = {
+    "gemm": "k_gemm256p",
+    "resid_gemm": "k_gemm256p<false, 0>",
+    "gelu_gemm": "k_gemm256p<true, 1>",
+    "fp8_gemm": "k_gemm256p_fp8",
+    "attention": "k_attn",
+    "attention_clip": "k_attn_clip",
+    "attention_cutr": "k_attn_cutr",
+    # bf_depth_preprocess at a keyframe batch: the three histogram passes + the normalise pass
+    "depth_small": r"sum:k_ds_(hist[123]<\d+, true>|norm<\d+>)",
+}
+
+
 def load_pmc_traffic(kernel):
     """HBM-side bytes per launch of `kernel` from the committed PMC passes (profiles/*_pmc.json,
     newest round); counters cannot be read from inside the run."""
@@ -837,29 +853,27 @@ def main(argv=None):
     if rank == 0:
         big = lambda t: t["kind"] == "gemm" and t["large"]
         r_all = roofline_obj(timer.summary(big), "every bf16 linear launch of CLIP ViT-H and CuTR (qkv, "
-                             "proj/fc2 + f32 residual, fc1 + GELU): k_gemm256q / k_gemm256p, or hipBLASLt "
-                             "where it timed faster for the shape (bf_gemm_tune.hip; gemm_choice)",
-                             "mfma", pmc_key="k_gemm256p")
-        r_all["gemm_choice"] = _lib.gemm_tune_report()
+                             "proj/fc2 + f32 residual, fc1 + GELU): the hand-written k_gemm256q / "
+                             "k_gemm256p, tile height per shape", "mfma", pmc_key=PMC_KEYS["gemm"])
         r_all["traffic_note"] = ("PMC bytes per launch averaged over the GEMM family's kernels in "
-                                 "the PMC run: k_gemm256p / k_gemm256q and hipBLASLt's Cijk_*")
+                                 "the PMC run: k_gemm256p / k_gemm256q")
         comps = {
             "resid_gemm": roofline_obj(timer.summary(lambda t: big(t) and t["resid"]),
-                                       "proj / fc2 + f32 residual (hipBLASLt or k_gemm256p<false, 0>, "
-                                       "per shape)", "mfma",
-                                       pmc_key="k_gemm256p<false, 0>"),
+                                       "proj / fc2 + f32 residual (k_gemm256q at tile heights below 256 "
+                                       "rows, k_gemm256p at 256)", "mfma",
+                                       pmc_key=PMC_KEYS["resid_gemm"]),
             "gelu_gemm": roofline_obj(timer.summary(lambda t: big(t) and t["act"] == 1),
                                       "k_gemm256q<true, 1> (fc1 + GELU)", "mfma",
-                                      pmc_key="k_gemm256p<true, 1>"),
+                                      pmc_key=PMC_KEYS["gelu_gemm"]),
             "attention": roofline_obj(timer.summary(lambda t: t["kind"] == "attn"),
                                       "k_attn_* (every ViT attention launch: CuTR window + global, "
-                                      "CLIP)", "mfma", pmc_key="k_attn"),
+                                      "CLIP)", "mfma", pmc_key=PMC_KEYS["attention"]),
             "attention_clip": roofline_obj(timer.summary(lambda t: t["kind"] == "attn" and t["D"] == 80),
                                            "CLIP ViT-H/14 attention (S=257, D=80)", "mfma",
-                                           pmc_key="k_attn_clip"),
+                                           pmc_key=PMC_KEYS["attention_clip"]),
             "attention_cutr": roofline_obj(timer.summary(lambda t: t["kind"] == "attn" and t["D"] != 80),
                                            "CuTR attention (512-key joint windows, 1600-token global)",
-                                           "mfma", pmc_key="k_attn_cutr"),
+                                           "mfma", pmc_key=PMC_KEYS["attention_cutr"]),
         }
         for v in comps.values():
             v["measured"] = source
@@ -874,7 +888,7 @@ def main(argv=None):
             comps["depth_preprocess"] = roofline_obj(
                 dks, "bf_depth_preprocess (a1 + a13: trimmed depth standardisation + back-projection, "
                      "3-level radix select over the whole chip)", "hbm",
-                pmc_key=r"sum:k_ds_(hist[123]<4, true>|norm<4>)" if small else "k_ds")
+                pmc_key=PMC_KEYS["depth_small"] if small else "k_ds")
             comps["depth_preprocess"]["measured"] = (source if G == 1 else
                                                      "timed region (non-keyframe batches)")
             comps["depth_preprocess"]["frames_per_launch"] = (G - 1) * Bm if G > 1 else Bm
@@ -956,7 +970,7 @@ def main(argv=None):
         if args.clip_fp8:
             f8 = roofline_obj(timer.summary(lambda t: t["kind"] == "gemm_fp8"),
                               "k_gemm256p<*, *, fp8> (CLIP qkv, fc1 + GELU -> fp8, fc2 + f32 residual; "
-                              "block-scaled fp8 MFMA)", "mfma", pmc_key="k_gemm256p_fp8",
+                              "block-scaled fp8 MFMA)", "mfma", pmc_key=PMC_KEYS["fp8_gemm"],
                               peak_tflops=PEAK_FP8_TFLOPS)
             f8["measured"] = source
             comps["bf16_gemm"] = r_all

@@ -774,15 +774,6 @@ FP8_MAX = 448.0
 _FP8_OUT = {torch.float32: 0, torch.bfloat16: 1, FP8: 2}
 
 
-def gemm_tune_report():
-    """bf_gemm_bf16's per-shape choices so far (hand-written kernel or hipBLASLt), one line each"""
-    L = lib()
-    n = L.bf_gemm_tune_report(None, 0)
-    buf = ctypes.create_string_buffer(n + 1)
-    L.bf_gemm_tune_report(buf, n + 1)
-    return [ln for ln in buf.value.decode().splitlines() if ln]
-
-
 def gemm_fp8(a, w, scale, bias=None, act=None, resid=None, out=None, out_dtype=torch.bfloat16,
              out_qscale=1.0):
     """out = resid + act(scale * (a @ w.T) + bias); a fp8 e4m3 [M,K], w fp8 [N,K] (per-tensor

@@ -22,6 +22,15 @@
 #define GEMM_PRIO_MODE 0
 #endif
 
+// gemm_tile_mb1's cost model: a tile of BM rows takes (GEMM_TILE_FIXED + (1 - GEMM_TILE_FIXED) BM / 256)
+// of a 256-row tile's time.  The K loop has a per-K-tile cost that does not shrink with the MFMA
+// count (staging, fragment reads, barriers: scripts/gemm_tile_sweep.py, CuTR 12800 x 768 x 3072 in
+// one round: 160 rows 78.7 us vs 256 rows 82.6; scripts/gemm_l2_probe.py: L2-resident operands
+// take 5-21 % off), so a smaller tile pays only where it saves a round.
+#ifndef GEMM_TILE_FIXED
+#define GEMM_TILE_FIXED 0.7
+#endif
+
 // k_gemm256p accumulator layout: 0 (default) = D[m][n] blocks; 1 = transposed (C^T = W A^T on the
 // MFMA: 16-B residual loads, one ds_write_b128 per block in the epilogue, bias + activation after
 // the LDS transpose).  Both pass the same tests; measured on one box the transposed form was no
@@ -345,12 +354,13 @@ __device__ __forceinline__ void glds_buf16(const void* base, int nbytes, void* l
 // groups of `gm` row panels, so the 32 tiles an XCD runs concurrently (consecutive indices) form a
 // gm x (32/gm) patch -- gm A panels and 32/gm W panels per K-step in that XCD's L2 instead of
 // ~1.6 A panels and every W panel of the problem.  gm <= 1: plain row-major order.
-__device__ __forceinline__ void tile_coords(int tile, int tiles_m, int tiles_n, int gm, int& m0, int& n0) {
-    if (gm <= 1) { m0 = (tile / tiles_n) * 256; n0 = (tile % tiles_n) * 256; return; }
+__device__ __forceinline__ void tile_coords(int tile, int tiles_m, int tiles_n, int gm, int& m0, int& n0,
+                                            int bm = 256) {
+    if (gm <= 1) { m0 = (tile / tiles_n) * bm; n0 = (tile % tiles_n) * 256; return; }
     const int per = gm * tiles_n;
     const int grp = tile / per, in = tile - grp * per;
     const int rows = min(gm, tiles_m - grp * gm);
-    m0 = (grp * gm + in % rows) * 256;
+    m0 = (grp * gm + in % rows) * bm;
     n0 = (in / rows) * 256;
 }
 
@@ -879,7 +889,17 @@ __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
 // F8 (as in k_gemm256p): bit 0 fp8 e4m3 operands (128-element K-tiles, block-scaled MFMA with unit
 // scales, epilogue acc * csc + bias), bit 1 fp8 output (v * oqs saturated to +-448; 8 bytes per lane
 // after the permlane exchange).  Not combined with RES.
-template <bool OUT_BF16, int ACT, bool RES, int F8 = 0>
+//
+// MB1 (1..4): 16-row blocks in the second M-half of a wave, so the tile is BM = 2 (64 + 16 MB1)
+// rows (160 / 192 / 224 / 256) x 256 columns.  The tile height sets the round quantisation of the
+// persistent walk: CLIP's 32896-row GEMMs with N = 1280 run 645 tiles of 256 rows (2.52 rounds of
+// 256 CUs, 0.84 of the chip busy) but 735 of 224 rows (2.87 rounds, 0.96); CuTR's 12800 x 768 runs
+// 150 tiles of 256 rows (one round on 150 CUs) but 240 of 160.  The second A-half then holds 16 MB1
+// valid rows per wave row; its other staging lanes take an out-of-range buffer offset (the LDS-DMA
+// fetches nothing), so every wave still issues the same number of VMEM operations and the counted
+// waits below only change through the per-quadrant store / load counts.  Each output keeps the
+// same K-order MFMA chain, so the tile height never changes a value.
+template <bool OUT_BF16, int ACT, bool RES, int F8 = 0, int MB1 = 4>
 __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restrict__ A, int lda,
                                                             const u16* __restrict__ W, int ldw,
                                                             const float* __restrict__ bias,
@@ -893,8 +913,12 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
     static_assert(!(F8 & 2) || OUT_BF16, "fp8 output takes the narrow store path");
     constexpr int ESZ = (F8 & 1) ? 1 : 2;           // operand bytes
     constexpr int KTE = GB_K * 2 / ESZ;             // K elements per 128-B K-tile row
-    constexpr int S = OUT_BF16 ? 4 : 8;             // stores per quadrant epilogue (per lane)
-    constexpr int R = RES ? 8 : 0;                  // residual loads per quadrant re-init
+    static_assert(MB1 >= 1 && MB1 <= 4, "second M-half of 1..4 row blocks");
+    constexpr int BMH = 64 + 16 * MB1;              // tile rows per wave row (BM = 2 BMH)
+    // per-lane stores of a quadrant epilogue / residual loads of a quadrant re-init, for the
+    // quadrants of the first (4 row blocks) and the second (MB1 row blocks) M-half
+    constexpr int S0 = OUT_BF16 ? 4 : 8, S1 = S0 / 4 * MB1;
+    constexpr int R0 = RES ? 8 : 0, R1 = RES ? 2 * MB1 : 0;
     const int t = threadIdx.x;
     const int lane = t & 63, wave = t >> 6;
     const int wr = wave >> 2, wc = wave & 3;
@@ -918,13 +942,15 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
     }
 
     int a_row[2][2], b_row[2][2], scol[2];
+    bool a1_ok[2];        // this lane's A-half-1 staging row lies inside the tile (MB1 < 4)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int L = (wave * 2 + i) * 8 + (lane >> 3);
         scol[i] = ((lane & 7) ^ swz_key(L)) * 16;
+        a1_ok[i] = (L & 63) < 16 * MB1;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            a_row[h][i] = (L >> 6) * 128 + h * 64 + (L & 63);
+            a_row[h][i] = (L >> 6) * BMH + h * 64 + (L & 63);
             b_row[h][i] = (L >> 5) * 64 + h * 32 + (L & 31);
         }
     }
@@ -934,7 +960,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
     auto kt_at_tile = [&](int tile_k, int idx) {
         const int tile = slot + tile_k * G;
         KT r;
-        r.idx = idx; tile_coords(tile, tiles_m, tiles_n, gm, r.m0, r.n0); r.k0 = 0; r.buf = idx & 1;
+        r.idx = idx; tile_coords(tile, tiles_m, tiles_n, gm, r.m0, r.n0, 2 * BMH); r.k0 = 0; r.buf = idx & 1;
         return r;
     };
     int tile_ord = 0;
@@ -951,7 +977,8 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         for (int h = 0; h < 2; ++h)
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                v.a[h][i] = min(c.m0 + a_row[h][i], M - 1) * lda * ESZ + scol[i];
+                v.a[h][i] = (h == 1 && !a1_ok[i]) ? (int)0x80000000
+                                                  : min(c.m0 + a_row[h][i], M - 1) * lda * ESZ + scol[i];
                 v.b[h][i] = min(c.n0 + b_row[h][i], N - 1) * ldw * ESZ + scol[i];
             }
         return v;
@@ -967,20 +994,22 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         }                                                                                          \
     }
 
-    f32x4 acc[8][4];
+    f32x4 acc[4 + MB1][4];
+    // row blocks of M-half MI
+#define NBLK(MI) ((MI) ? MB1 : 4)
     // quadrant (MI, NI) <- zero or the residual of the tile at (m0_, n0_) (clamped rows / columns:
     // every load is issued, out-of-range values are never stored)
 #define QINIT(MI, NI, m0_, n0_)                                                                    \
     {                                                                                              \
         if constexpr (RES) {                                                                       \
-            _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                       \
-                const float* rp_ = resid + (size_t)min((m0_) + wr * 128 + (MI) * 64 + i * 16 + lr, M - 1) * ldr; \
+            _Pragma("unroll") for (int i = 0; i < NBLK(MI); ++i) {                                \
+                const float* rp_ = resid + (size_t)min((m0_) + wr * BMH + (MI) * 64 + i * 16 + lr, M - 1) * ldr; \
                 _Pragma("unroll") for (int j = 0; j < 2; ++j)                                      \
                     acc[(MI) * 4 + i][(NI) * 2 + j] = *reinterpret_cast<const f32x4*>(            \
                         rp_ + min((n0_) + wc * 64 + (NI) * 32 + j * 16 + 4 * lq, N - 4));          \
             }                                                                                      \
         } else {                                                                                   \
-            _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) \
+            _Pragma("unroll") for (int i = 0; i < NBLK(MI); ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) \
                 acc[(MI) * 4 + i][(NI) * 2 + j] = (f32x4){0.f, 0.f, 0.f, 0.f};                     \
         }                                                                                          \
     }
@@ -990,8 +1019,8 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
 #define QINIT_ASYNC(MI, NI, T_)                                                                    \
     {                                                                                              \
         if constexpr (RES) {                                                                       \
-            _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                       \
-                const float* rp_ = resid + (size_t)min((T_).m0 + wr * 128 + (MI) * 64 + i * 16 + lr, M - 1) * ldr; \
+            _Pragma("unroll") for (int i = 0; i < NBLK(MI); ++i) {                                \
+                const float* rp_ = resid + (size_t)min((T_).m0 + wr * BMH + (MI) * 64 + i * 16 + lr, M - 1) * ldr; \
                 _Pragma("unroll") for (int j = 0; j < 2; ++j)                                      \
                     asm volatile("global_load_dwordx4 %0, %1, off"                                 \
                                  : "=v"(acc[(MI) * 4 + i][(NI) * 2 + j])                           \
@@ -1012,8 +1041,8 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         const int cb_ = (en0_) + wc * 64 + (NI) * 32 + 4 * lq;                                     \
         const f32x4 b0_ = *reinterpret_cast<const f32x4*>(bias_lds + min(cb_, N - 4));            \
         const f32x4 b1_ = *reinterpret_cast<const f32x4*>(bias_lds + min(cb_ + 16, N - 4));       \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                           \
-            const int r_ = (em0_) + wr * 128 + (MI) * 64 + i * 16 + lr;                            \
+        _Pragma("unroll") for (int i = 0; i < NBLK(MI); ++i) {                                    \
+            const int r_ = (em0_) + wr * BMH + (MI) * 64 + i * 16 + lr;                            \
             if constexpr ((F8 & 2) != 0) {                                                         \
                 /* fp8 row segments, one block at a time (fewer live registers): 4 bytes per      \
                    block, exchanged between lane rows -> 8 consecutive bytes */                     \
@@ -1076,13 +1105,13 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
 #define LDS16(off) (*reinterpret_cast<const bf16x8*>(g_smem + (off)))
 #define RD_A(stage, mi)                                                                            \
     if constexpr ((F8 & 1) != 0) {                                                                 \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                            \
+        _Pragma("unroll") for (int i = 0; i < NBLK(mi); ++i) {                                     \
             const int b_ = (stage) * 65536 + (mi) * 16384;                                         \
             ga[i] = frag32(LDS16(b_ + swz(wr * 64 + i * 16 + lr, lq)),                             \
                            LDS16(b_ + swz(wr * 64 + i * 16 + lr, 4 + lq)));                        \
         }                                                                                          \
     } else {                                                                                       \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) \
+        _Pragma("unroll") for (int i = 0; i < NBLK(mi); ++i) _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) \
             fa[i * 2 + ks] = LDS16((stage) * 65536 + (mi) * 16384 + swz(wr * 64 + i * 16 + lr, ks * 4 + lq)); \
     }
 #define RD_B(FB, GB, stage, ni)                                                                    \
@@ -1100,14 +1129,14 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
     {                                                                                              \
         if (GEMM_PRIO_MODE == 0) __builtin_amdgcn_s_setprio(1);                                    \
         if constexpr ((F8 & 1) != 0) {                                                             \
-            _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) \
+            _Pragma("unroll") for (int i = 0; i < NBLK(mi); ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) \
                 acc[(mi) * 4 + i][(ni) * 2 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4( \
                     GB[j], ga[i], acc[(mi) * 4 + i][(ni) * 2 + j], 0, 0, 0, 127, 0, 127);          \
             /* not convergent: pin the results to this phase (see k_gemm256p) */                   \
-            _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) \
+            _Pragma("unroll") for (int i = 0; i < NBLK(mi); ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) \
                 asm volatile("" : "+v"(acc[(mi) * 4 + i][(ni) * 2 + j]));                          \
         } else {                                                                                   \
-            _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i) \
+            _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < NBLK(mi); ++i) \
                 _Pragma("unroll") for (int j = 0; j < 2; ++j) acc[(mi) * 4 + i][(ni) * 2 + j] =    \
                     __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j * 2 + ks], fa[i * 2 + ks],        \
                                                             acc[(mi) * 4 + i][(ni) * 2 + j], 0, 0, 0); \
@@ -1145,7 +1174,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         if (isF) {
             QEPI(1, 0, em0, en0); QINIT_ASYNC(1, 0, kc);
             CBAR();
-            if constexpr (RES) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + 3 * (S + R)) : "memory");  // Q00's residual (L.P2)
+            if constexpr (RES) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + S0 + R0 + 2 * (S1 + R1)) : "memory");  // Q00's residual (L.P2)
         }
         CBAR();
         asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
@@ -1157,7 +1186,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         STAGE_HALF(k2, v2, 2);
         if (isL) { QEPI(0, 0, kc.m0, kc.n0); QINIT_ASYNC(0, 0, k1); }
         if (isF) {
-            if constexpr (RES) { CBAR(); asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + 2 * (S + R)) : "memory"); }  // Q01 (L.P3)
+            if constexpr (RES) { CBAR(); asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + 2 * (S1 + R1)) : "memory"); }  // Q01 (L.P3)
         }
         CBAR();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1169,7 +1198,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         STAGE_HALF(k2, v2, 0);
         if (isL) { QEPI(0, 1, kc.m0, kc.n0); QINIT_ASYNC(0, 1, k1); }
         if (isF) {
-            if constexpr (RES) { CBAR(); asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 + S + R) : "memory"); }      // Q11 (L.P4)
+            if constexpr (RES) { CBAR(); asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 + S1 + R1) : "memory"); }    // Q11 (L.P4)
         }
         CBAR();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1182,11 +1211,11 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         if (isL) {
             QEPI(1, 1, kc.m0, kc.n0); QINIT_ASYNC(1, 1, k1);
             CBAR();
-            asm volatile("s_waitcnt vmcnt(%0)" :: "n"(8 + 3 * (S + R)) : "memory");
+            asm volatile("s_waitcnt vmcnt(%0)" :: "n"(8 + 2 * (S0 + R0) + S1 + R1) : "memory");
             em0 = kc.m0; en0 = kc.n0;
         } else if (isF) {
             // K-tile g+1, and (RES) Q10's residual from P1: 8 younger LDS-DMA
-            asm volatile("s_waitcnt vmcnt(%0)" :: "n"(RES ? 8 : 8 + S) : "memory");
+            asm volatile("s_waitcnt vmcnt(%0)" :: "n"(RES ? 8 : 8 + S1) : "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         }
@@ -1211,6 +1240,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
 #undef QINIT
 #undef QINIT_ASYNC
 #undef QEPI
+#undef NBLK
 }
 
 // 1: k_gemm256p (staggered 4-phase schedule), 2: k_gemm256p unstaggered, 3 / 4: k_gemm256p
@@ -1307,30 +1337,226 @@ static bool gemm_use_large(int M, int N, int K) {
 
 BF_API int bf_gemm_large_tiles(int M, int N, int K) { return gemm_use_large(M, N, K) ? 1 : 0; }
 
-int bf_gemm_tuned(const void* A, int lda, const void* W, int ldw, const float* bias, const float* resid, int ldr,
-                  void* C, int ldc, int c_bf16, int M, int N, int K, void* stream);
+// Persistent grid size for `tiles` tiles: one workgroup per CU, or, when the last round of tiles
+// is at least a quarter full, as many workgroups as the round count needs (every block walks the
+// same number of tiles, +-1): the CUs a partial last round would leave idle at the end are free
+// for the other streams' kernels from the start instead.  A nearly empty last round costs little,
+// and a full-width grid runs the same tiles ~5 % faster alone (measured on CLIP fc1, 2580 tiles).
+static int gemm_grid(long long tiles, int n_cu) {
+    int grid = (int)(tiles < n_cu ? tiles : n_cu);
+    if (gemm_balanced() && tiles > n_cu && (gemm_balanced() == 2 || tiles % n_cu >= n_cu / 4)) {
+        const long long rounds = (tiles + n_cu - 1) / n_cu;
+        const int g = (int)(((tiles + rounds - 1) / rounds + 7) & ~7LL);
+        grid = g < n_cu ? g : n_cu;
+    }
+    return grid;
+}
 
-int bf_gemm_bf16_own(const void* A, int lda, const void* W, int ldw, const float* bias, const float* resid,
-                     int ldr, int resid_mod, void* C, int ldc, int c_bf16, const int32_t* row_map, int M, int N,
-                     int K, int act, void* stream);
+static int g_tile_rows = [] {
+    const char* e = getenv("BF_GEMM_TILE_ROWS");
+    return e ? atoi(e) : 0;
+}();
+// test / measurement hook: force the persistent kernels' tile height (160, 192, 224 or 256 rows);
+// 0 = the per-shape model below
+BF_API void bf_gemm_set_tile_rows(int bm) { g_tile_rows = bm; }
 
-// plain linears (no activation, row map or residual modulus) take the per-shape choice of
-// bf_gemm_tune.hip between this file's kernels and hipBLASLt
+// Tile height of k_gemm256q for an M x N x K problem, from the shape alone (so every box runs the
+// same kernel and summation order): the height with the lowest rounds(BM) x t(BM), rounds =
+// ceil(tiles / CUs), t(BM) the per-tile time model above.  Against the sweep of every path shape
+// (profiles/r05_gemm_tile_sweep.log) it picks the fastest height or one within 1 %: 224 rows for
+// CLIP proj / fc2 (N = 1280) and CuTR's window qkv, 160 for CuTR's N = 768 residual GEMMs, 256
+// elsewhere.
+static int gemm_tile_mb1(int M, int N, int K) {
+    if (g_tile_rows >= 160 && g_tile_rows <= 256 && g_tile_rows % 32 == 0) return (g_tile_rows / 2 - 64) / 16;
+    const int n_cu = gemm_cu_count();
+    const long long tn = (N + 255) / 256;
+    int best = 4;
+    double best_cost = 0.0;
+    for (int mb1 = 4; mb1 >= 1; --mb1) {
+        const int bm = 2 * (64 + 16 * mb1);
+        const long long tiles = ((M + bm - 1) / bm) * tn;
+        const long long rounds = (tiles + n_cu - 1) / n_cu;
+        const double cost = (double)rounds * (GEMM_TILE_FIXED + (1.0 - GEMM_TILE_FIXED) * bm / 256.0);
+        if (mb1 == 4 || cost < best_cost) { best = mb1; best_cost = cost; }
+    }
+    (void)K;
+    return best;
+}
+
+template <bool OB, int AC, bool RS, int F8, int MB1>
+static void gemm256q_attr() {
+    static bool done = false;
+    if (!done) {
+        hipFuncSetAttribute((const void*)k_gemm256q<OB, AC, RS, F8, MB1>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
+        done = true;
+    }
+}
+
+template <bool OB, int AC, bool RS, int F8>
+static int launch_gemm256q(int mb1, int grid, void* stream, const void* A, int lda, const void* W, int ldw,
+                           const float* bias, const float* resid, int ldr, void* C, int ldc, int M, int N, int K,
+                           int tiles_n, int tiles_m, float csc, float oqs) {
+#define GQ(MB)                                                                                              \
+    {                                                                                                       \
+        gemm256q_attr<OB, AC, RS, F8, MB>();                                                                \
+        hipLaunchKernelGGL((k_gemm256q<OB, AC, RS, F8, MB>), dim3(grid), dim3(G2_THREADS), G2_LDS,           \
+                           bf_stream(stream), (const u16*)A, lda, (const u16*)W, ldw, bias, resid, ldr, C,   \
+                           ldc, M, N, K, tiles_n, tiles_m, 1, g_group_m, csc, oqs);                          \
+    }
+    switch (mb1) {
+        case 1: GQ(1); break;
+        case 2: GQ(2); break;
+        case 3: GQ(3); break;
+        default: GQ(4); break;
+    }
+#undef GQ
+    return bf_check_launch();
+}
+
+// ------------------------------------------------------------------------------------------
+// k_gemm_skinny: few-row GEMMs (CLIP's output projection over the 128 class tokens, 128 x 1024 x
+// 1280; the cls-only last block's proj / fc1 / fc2, 128 x {1280, 5120} x {1280, 5120}).  The tiled
+// kernels give those 8-40 workgroups; here a 512-thread workgroup owns a 128-row x 32-column
+// output tile and its 8 waves split K (wave w takes the 32-wide k-steps w, w + 8, ...), so a
+// 128-row problem runs N / 32 workgroups, each reading its 32 weight rows once.  Operands go
+// straight from global memory into MFMA fragments (C^T = W A^T on v_mfma_f32_16x16x32_bf16: lane
+// (lr, lq) of block (i, j) holds row 16i + lr, columns 16j + 4lq + [0, 4)) through a 3-deep
+// register ring, so three k-steps of loads are in flight per wave.  The 8 partial tiles meet in
+// LDS and are summed in wave order (deterministic), then bias / activation / residual / row map
+// as in bf_gemm_bf16.  Needs N % 32 == 0 and K % 256 == 0 (every wave the same k-step count).
+// ------------------------------------------------------------------------------------------
+#define SK_THREADS 512
+#define SK_LDS (8 * 128 * 32 * 4)
+template <bool OUT_BF16, int ACT>
+__global__ void __launch_bounds__(SK_THREADS, 1) k_gemm_skinny(const u16* __restrict__ A, int lda,
+                                                               const u16* __restrict__ W, int ldw,
+                                                               const float* __restrict__ bias,
+                                                               const float* __restrict__ resid, int ldr,
+                                                               int resid_mod, void* __restrict__ Cv, int ldc,
+                                                               const int32_t* __restrict__ row_map, int M,
+                                                               int N, int K) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char g_smem[];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int lr = lane & 15, lq = lane >> 4;
+    const int n0 = blockIdx.x * 32, m0 = blockIdx.y * 128;
+    const int cnt = K / 256;                     // k-steps per wave
+    const u16* ap[8];
+    const u16* wp[2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ap[i] = A + (size_t)min(m0 + 16 * i + lr, M - 1) * lda + 8 * lq + 32 * wave;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) wp[j] = W + (size_t)(n0 + 16 * j + lr) * ldw + 8 * lq + 32 * wave;
+    f32x4 acc[8][2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    bf16x8 ra[3][8], rw[3][2];
+    // k-step s of this wave (clamped: a load past the end re-reads the last step, never used)
+#define SK_LOAD(slot, s)                                                                           \
+    {                                                                                              \
+        const int o_ = 256 * min((s), cnt - 1);                                                    \
+        _Pragma("unroll") for (int i = 0; i < 8; ++i)                                              \
+            ra[slot][i] = *reinterpret_cast<const bf16x8*>(ap[i] + o_);                            \
+        _Pragma("unroll") for (int j = 0; j < 2; ++j)                                              \
+            rw[slot][j] = *reinterpret_cast<const bf16x8*>(wp[j] + o_);                            \
+    }
+#define SK_MFMA(slot)                                                                              \
+    {                                                                                              \
+        _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) \
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rw[slot][j], ra[slot][i], acc[i][j], 0, 0, 0); \
+    }
+    SK_LOAD(0, 0);
+    SK_LOAD(1, 1);
+    SK_LOAD(2, 2);
+    int s = 0;
+    for (; s + 3 <= cnt; s += 3) {
+        SK_MFMA(0); SK_LOAD(0, s + 3);
+        SK_MFMA(1); SK_LOAD(1, s + 4);
+        SK_MFMA(2); SK_LOAD(2, s + 5);
+    }
+    if (s < cnt) SK_MFMA(0);
+    if (s + 1 < cnt) SK_MFMA(1);
+#undef SK_LOAD
+#undef SK_MFMA
+    // partial tiles -> LDS [wave][128][32] f32; rows XOR-swizzled by 16-B slot against the bank rows
+    float* red = reinterpret_cast<float*>(g_smem);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int r = 16 * i + lr, c4 = (4 * j + lq) ^ (r & 7);
+            *reinterpret_cast<f32x4*>(red + wave * 4096 + r * 32 + 4 * c4) = acc[i][j];
+        }
+    __syncthreads();
+    // thread t: row t / 4, columns 8 (t % 4) + [0, 8)
+    const int rl = t >> 2, cq = t & 3;
+    const int m = m0 + rl;
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int c4 = (2 * cq + h) ^ (rl & 7);
+            const f32x4 x = *reinterpret_cast<const f32x4*>(red + w * 4096 + rl * 32 + 4 * c4);
+            v[4 * h] += x.x; v[4 * h + 1] += x.y; v[4 * h + 2] += x.z; v[4 * h + 3] += x.w;
+        }
+    if (m >= M) return;
+    const int orow = row_map ? row_map[m] : m;
+    if (orow < 0) return;
+    const int n = n0 + 8 * cq;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        float x = v[q] + (bias ? bias[n + q] : 0.f);
+        if (ACT == 1) x = gelu_erf(x);
+        else if (ACT == 2) x = fmaxf(x, 0.f);
+        v[q] = x;
+    }
+    if (resid) {
+        const float* rp = resid + (size_t)(resid_mod > 0 ? m % resid_mod : orow) * ldr + n;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] += rp[q];
+    }
+    if (OUT_BF16) {
+        U128 o;
+        o.x = pk_bf16(v[0], v[1]); o.y = pk_bf16(v[2], v[3]);
+        o.z = pk_bf16(v[4], v[5]); o.w = pk_bf16(v[6], v[7]);
+        *reinterpret_cast<U128*>(reinterpret_cast<u16*>(Cv) + (size_t)orow * ldc + n) = o;
+    } else {
+        float* cp = reinterpret_cast<float*>(Cv) + (size_t)orow * ldc + n;
+        *reinterpret_cast<f32x4*>(cp) = (f32x4){v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<f32x4*>(cp + 4) = (f32x4){v[4], v[5], v[6], v[7]};
+    }
+}
+
+// few-row problems: the 128 x 128 kernel would give fewer than half the CUs a workgroup
+static bool gemm_use_skinny(int M, int N, int K, int vec_epi) {
+    if (g_force_small != 0 || !vec_epi || N % 32 != 0 || K % 256 != 0) return false;
+    const long long t1 = (long long)((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N);
+    return t1 < gemm_cu_count() / 2;
+}
+
+template <bool OB, int AC>
+static int launch_gemm_skinny(void* stream, const void* A, int lda, const void* W, int ldw, const float* bias,
+                              const float* resid, int ldr, int resid_mod, void* C, int ldc,
+                              const int32_t* row_map, int M, int N, int K) {
+    static bool attr = false;
+    if (!attr) {
+        hipFuncSetAttribute((const void*)k_gemm_skinny<OB, AC>, hipFuncAttributeMaxDynamicSharedMemorySize, SK_LDS);
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_gemm_skinny<OB, AC>), dim3(N / 32, (M + 127) / 128), dim3(SK_THREADS), SK_LDS,
+                       bf_stream(stream), (const u16*)A, lda, (const u16*)W, ldw, bias, resid, ldr, resid_mod, C,
+                       ldc, row_map, M, N, K);
+    return bf_check_launch();
+}
+
+// The product entry point: hand-written kernels only, chosen from the shape alone.
 BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bias,
                         const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
                         const int32_t* row_map, int M, int N, int K, int act, void* stream) {
-    if (!A || !W || !C || M < 0 || N <= 0 || K <= 0) return BF_ERR_ARG;
-    if (M > 0 && act == 0 && !row_map && resid_mod <= 0 && K % GB_K == 0 && lda % 8 == 0 && ldw % 8 == 0) {
-        const int rc = bf_gemm_tuned(A, lda, W, ldw, bias, resid, ldr, C, ldc, c_bf16, M, N, K, stream);
-        if (rc != 1) return rc;
-    }
-    return bf_gemm_bf16_own(A, lda, W, ldw, bias, resid, ldr, resid_mod, C, ldc, c_bf16, row_map, M, N, K, act,
-                            stream);
-}
-
-int bf_gemm_bf16_own(const void* A, int lda, const void* W, int ldw, const float* bias,
-                     const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
-                     const int32_t* row_map, int M, int N, int K, int act, void* stream) {
     if (!A || !W || !C || M < 0 || N <= 0 || K <= 0) return BF_ERR_ARG;
     if (K % GB_K != 0 || lda % 8 != 0 || ldw % 8 != 0) return BF_ERR_UNSUPPORTED;
     if (M == 0) return BF_OK;
@@ -1350,44 +1576,43 @@ int bf_gemm_bf16_own(const void* A, int lda, const void* W, int ldw, const float
     const int t2m = (M + 255) / 256, t2n = (N + 255) / 256;
     const long long t2 = (long long)t2m * t2n;
     const int n_cu = gemm_cu_count();
-    if (vec_epi && gemm_use_large(M, N, K)) {
-        int grid2 = (int)(t2 < n_cu ? t2 : n_cu);   // persistent: one workgroup per CU
-        if (gemm_balanced() && t2 > n_cu && (gemm_balanced() == 2 || t2 % n_cu >= n_cu / 4)) {
-            // as many workgroups as the round count needs (every block walks the same number
-            // of tiles, +-1): the CUs a partial last round would leave idle at the end are free
-            // for the other streams' kernels from the start instead.  Only for a last round at
-            // least a quarter full: a nearly empty one costs little, and a full-width grid runs
-            // the same tiles ~5 % faster alone (measured on CLIP fc1, 2580 tiles)
-            const long long rounds = (t2 + n_cu - 1) / n_cu;
-            const int g = (int)(((t2 + rounds - 1) / rounds + 7) & ~7LL);
-            grid2 = g < n_cu ? g : n_cu;
+    // 16-B row chunks of C / resid also carry the skinny kernel's epilogue (8 columns per thread)
+    if (gemm_use_skinny(M, N, K, vec_epi && (c_bf16 || N % 8 == 0))) {
+#define GSK(OB, AC) return launch_gemm_skinny<OB, AC>(stream, A, lda, W, ldw, bias, resid, ldr, resid_mod, C, ldc, \
+                                                      row_map, M, N, K)
+        if (c_bf16) {
+            if (act == 0) GSK(true, 0);
+            if (act == 1) GSK(true, 1);
+            GSK(true, 2);
         }
+        if (act == 0) GSK(false, 0);
+        if (act == 1) GSK(false, 1);
+        GSK(false, 2);
+#undef GSK
+    }
+    if (vec_epi && gemm_use_large(M, N, K)) {
+        const int grid2 = gemm_grid(t2, n_cu);
         // the overlapped-epilogue kernel: plain / in-place residual outputs, >= 3 K-tiles, the bias
-        // row fits its LDS slot, 32-bit byte offsets into C and the residual
-        // (variant 5, the default: bf16 outputs only -- the f32 residual GEMMs measured 1-4 % slower
-        // on it than on k_gemm256p; variant 6: every eligible shape)
-        const bool q_ok = (g_gemm_variant == 6 || (g_gemm_variant == 5 && c_bf16)) && row_map == nullptr &&
-                          resid_mod <= 0 && K / 64 >= 3 && N <= G2Q_BIAS_MAX && act <= 1 && !(resid && act) && !(resid && c_bf16) && !(act && !c_bf16) &&
-                          (long long)(M - 1) * ldc * (c_bf16 ? 2 : 4) + (long long)N * 4 < (1LL << 31) &&
-                          (!resid || (long long)(M - 1) * ldr * 4 + (long long)N * 4 < (1LL << 31));
+        // row fits its LDS slot, 32-bit byte offsets into C and the residual.  Variant 5 (default):
+        // bf16 outputs, and the f32 residual GEMMs whose tile height (gemm_tile_rows) is below 256;
+        // at 256 rows those measured 1-4 % slower on it than on k_gemm256p.  Variant 6: every
+        // eligible shape.
+        const int mb1 = gemm_tile_mb1(M, N, K);
+        const bool q_fit = row_map == nullptr && resid_mod <= 0 && K / 64 >= 3 && N <= G2Q_BIAS_MAX && act <= 1 &&
+                           !(resid && act) && !(resid && c_bf16) && !(act && !c_bf16) &&
+                           (long long)(M - 1) * ldc * (c_bf16 ? 2 : 4) + (long long)N * 4 < (1LL << 31) &&
+                           (!resid || (long long)(M - 1) * ldr * 4 + (long long)N * 4 < (1LL << 31));
+        const bool q_ok = q_fit && (g_gemm_variant == 6 || (g_gemm_variant == 5 && (c_bf16 || mb1 < 4)));
         if (q_ok) {
-            static bool qattr = false;
-            if (!qattr) {
-                hipFuncSetAttribute((const void*)k_gemm256q<true, 0, false>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
-                hipFuncSetAttribute((const void*)k_gemm256q<true, 1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
-                hipFuncSetAttribute((const void*)k_gemm256q<false, 0, false>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
-                hipFuncSetAttribute((const void*)k_gemm256q<false, 0, true>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
-                qattr = true;
-            }
-#define GEMMQ(OB, AC, RS) hipLaunchKernelGGL((k_gemm256q<OB, AC, RS>), dim3(grid2), dim3(G2_THREADS), G2_LDS,   \
-                                             bf_stream(stream), (const u16*)A, lda, (const u16*)W, ldw, bias, resid, \
-                                             ldr, C, ldc, M, N, K, t2n, t2m, 1, g_group_m)
-            if (resid) GEMMQ(false, 0, true);
-            else if (!c_bf16) GEMMQ(false, 0, false);
-            else if (act == 0) GEMMQ(true, 0, false);
-            else GEMMQ(true, 1, false);
-#undef GEMMQ
-            return bf_check_launch();
+            const int bm = 2 * (64 + 16 * mb1);
+            const int tqm = (M + bm - 1) / bm;
+            const int gq = gemm_grid(tqm * t2n, n_cu);
+            int rc = 0;
+            if (resid) rc = launch_gemm256q<false, 0, true, 0>(mb1, gq, stream, A, lda, W, ldw, bias, resid, ldr, C, ldc, M, N, K, t2n, tqm, 1.f, 1.f);
+            else if (!c_bf16) rc = launch_gemm256q<false, 0, false, 0>(mb1, gq, stream, A, lda, W, ldw, bias, resid, ldr, C, ldc, M, N, K, t2n, tqm, 1.f, 1.f);
+            else if (act == 0) rc = launch_gemm256q<true, 0, false, 0>(mb1, gq, stream, A, lda, W, ldw, bias, resid, ldr, C, ldc, M, N, K, t2n, tqm, 1.f, 1.f);
+            else rc = launch_gemm256q<true, 1, false, 0>(mb1, gq, stream, A, lda, W, ldw, bias, resid, ldr, C, ldc, M, N, K, t2n, tqm, 1.f, 1.f);
+            return rc;
         }
 #define GEMM2(OB, AC) launch_gemm256<OB, AC>(grid2, bf_stream(stream), A, lda, W, ldw, bias, \
                                             resid, ldr, resid_mod, C, ldc, row_map, M, N, K, t2n, t2m)
@@ -1441,30 +1666,9 @@ static void launch_gemm256_f8(int grid, hipStream_t st, const void* A, int lda, 
                        K, tiles_n, tiles_m, 1, g_group_m, 0, csc, oqs);
 }
 
-int bf_gemm_fp8_tuned(const void* A, int lda, const void* W, int ldw, float scale, const float* bias,
-                      const float* resid, int ldr, void* C, int ldc, int out_kind, int M, int N, int K, int act,
-                      void* stream);
-int bf_gemm_fp8_own(const void* A, int lda, const void* W, int ldw, float scale, const float* bias,
-                    const float* resid, int ldr, void* C, int ldc, int out_kind, float out_qscale, int M, int N,
-                    int K, int act, void* stream);
-
-// bf16 / f32 outputs without an activation take the per-shape choice of bf_gemm_tune.hip
 BF_API int bf_gemm_fp8(const void* A, int lda, const void* W, int ldw, float scale,
                        const float* bias, const float* resid, int ldr, void* C, int ldc, int out_kind,
                        float out_qscale, int M, int N, int K, int act, void* stream) {
-    if (A && W && C && scale > 0.f && M > 0 && N > 0 && K > 0 && act == 0 && out_kind <= 1 && out_kind >= 0 &&
-        K % 128 == 0 && lda % 16 == 0 && ldw % 16 == 0 && (!resid || out_kind == 0)) {
-        const int rc = bf_gemm_fp8_tuned(A, lda, W, ldw, scale, bias, resid, ldr, C, ldc, out_kind, M, N, K, act,
-                                         stream);
-        if (rc != 1) return rc;
-    }
-    return bf_gemm_fp8_own(A, lda, W, ldw, scale, bias, resid, ldr, C, ldc, out_kind, out_qscale, M, N, K, act,
-                           stream);
-}
-
-int bf_gemm_fp8_own(const void* A, int lda, const void* W, int ldw, float scale,
-                    const float* bias, const float* resid, int ldr, void* C, int ldc, int out_kind,
-                    float out_qscale, int M, int N, int K, int act, void* stream) {
     if (!A || !W || !C || !(scale > 0.f) || M < 0 || N <= 0 || K <= 0 || act < 0 || act > 1 ||
         out_kind < 0 || out_kind > 2)
         return BF_ERR_ARG;
@@ -1479,37 +1683,22 @@ int bf_gemm_fp8_own(const void* A, int lda, const void* W, int ldw, float scale,
     const int t2m = (M + 255) / 256, t2n = (N + 255) / 256;
     const long long t2 = (long long)t2m * t2n;
     const int n_cu = gemm_cu_count();
-    int grid = (int)(t2 < n_cu ? t2 : n_cu);
-    if (gemm_balanced() && t2 > n_cu && (gemm_balanced() == 2 || t2 % n_cu >= n_cu / 4)) {
-        const long long rounds = (t2 + n_cu - 1) / n_cu;
-        const int g = (int)(((t2 + rounds - 1) / rounds + 7) & ~7LL);
-        grid = g < n_cu ? g : n_cu;
-    }
+    const int grid = gemm_grid(t2, n_cu);
     // the overlapped-epilogue kernel for the fp8 GEMMs with bf16 outputs (CLIP qkv: 203.0 -> 161.4
     // us); fp8 outputs only under variant 6 (CLIP fc1 + GELU -> fp8 measured 286.7 -> 303.7 us on it:
     // at the fp8 MFMA rate the K loop is short beside that epilogue's VALU work)
     if ((g_gemm_variant == 6 || (g_gemm_variant == 5 && out_kind == 1)) && !resid && out_kind != 0 && K / 128 >= 3 &&
         N <= G2Q_BIAS_MAX && (long long)(M - 1) * ldc * (out_kind == 1 ? 2 : 1) + (long long)N * 2 < (1LL << 31)) {
-        static bool qattr8 = false;
-        if (!qattr8) {
-            hipFuncSetAttribute((const void*)k_gemm256q<true, 0, false, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
-            hipFuncSetAttribute((const void*)k_gemm256q<true, 1, false, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
-            hipFuncSetAttribute((const void*)k_gemm256q<true, 0, false, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
-            hipFuncSetAttribute((const void*)k_gemm256q<true, 1, false, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
-            qattr8 = true;
-        }
-#define GEMMQ8(AC, F8) hipLaunchKernelGGL((k_gemm256q<true, AC, false, F8>), dim3(grid), dim3(G2_THREADS), G2_LDS, \
-                                          bf_stream(stream), (const u16*)A, lda, (const u16*)W, ldw, bias,     \
-                                          (const float*)nullptr, 0, C, ldc, M, N, K, t2n, t2m, 1, g_group_m,   \
-                                          scale, out_qscale)
+        const int mb1 = gemm_tile_mb1(M, N, K);
+        const int bm = 2 * (64 + 16 * mb1);
+        const int tqm = (M + bm - 1) / bm;
+        const int gq = gemm_grid((long long)tqm * t2n, n_cu);
         if (out_kind == 1) {
-            if (act == 0) GEMMQ8(0, 1);
-            else GEMMQ8(1, 1);
-        } else {
-            if (act == 0) GEMMQ8(0, 3);
-            else GEMMQ8(1, 3);
+            if (act == 0) return launch_gemm256q<true, 0, false, 1>(mb1, gq, stream, A, lda, W, ldw, bias, nullptr, 0, C, ldc, M, N, K, t2n, tqm, scale, out_qscale);
+            return launch_gemm256q<true, 1, false, 1>(mb1, gq, stream, A, lda, W, ldw, bias, nullptr, 0, C, ldc, M, N, K, t2n, tqm, scale, out_qscale);
         }
-#undef GEMMQ8
+        if (act == 0) return launch_gemm256q<true, 0, false, 3>(mb1, gq, stream, A, lda, W, ldw, bias, nullptr, 0, C, ldc, M, N, K, t2n, tqm, scale, out_qscale);
+        return launch_gemm256q<true, 1, false, 3>(mb1, gq, stream, A, lda, W, ldw, bias, nullptr, 0, C, ldc, M, N, K, t2n, tqm, scale, out_qscale);
         return bf_check_launch();
     }
 #define GEMM8(OB, AC, F8) launch_gemm256_f8<OB, AC, F8>(grid, bf_stream(stream), A, lda, W, ldw, scale, bias, \

@@ -355,12 +355,13 @@ int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bi
                  const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
                  const int32_t* row_map, int M, int N, int K, int act, void* stream);
 
-/* Plain linears of bf_gemm_bf16 (act 0, no row_map, resid_mod 0) are timed once per shape against
- * hipBLASLt's workspace-free candidates (same D = A W^T + bias [+ resid]) and take the faster;
- * bf_gemm_set_tune(0) (or env BF_GEMM_TUNE=0) keeps the hand-written kernels only. */
-void bf_gemm_set_tune(int on);
-/* the per-shape choices so far as text lines into buf (cap bytes); returns the length needed */
-int bf_gemm_tune_report(char* buf, int cap);
+/* Kernel choice is a function of the shape alone (hand-written kernels only, the same on every
+ * box): few-row problems (the 128 x 128 tiling would feed fewer than half the CUs; N % 32 == 0,
+ * K % 256 == 0) run k_gemm_skinny (8 waves split K, partials summed in wave order); large ones
+ * the persistent kernels with a tile height of 160 / 192 / 224 / 256 rows picked by the round
+ * quantisation of the walk.  Test / measurement hook (process-wide): force that tile height
+ * (env BF_GEMM_TILE_ROWS); 0 = the per-shape model. */
+void bf_gemm_set_tile_rows(int bm);
 /* Tile selection: large problems (N >= 512, >= 128 tiles of 256x256, 16-B aligned output rows)
  * run the 256x256 8-wave kernel, the rest the 128x128 4-wave kernel.  Test / tuning hook
  * (process-wide): 1 forces the 128x128 kernel, -1 the 256x256 kernel (aligned shapes), 0 the

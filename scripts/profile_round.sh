@@ -67,13 +67,11 @@ for name, ctrs in per.items():
 # (regular expressions over the demangled names; k_gemm256p<OUT_BF16, ACT, F8>)
 # (k_gemm256q, the overlapped-epilogue form, runs the bf16-output GEMMs from round 3 on: it joins
 # the bf16 GEMM groups under the same keys)
-# (round 4: the bf16 linears a per-shape timing hands to hipBLASLt -- its Cijk_*_B[BS]S_BH kernels,
-# bf16 operands; the decoder's f32 ones are Cijk_*_S_B -- join the bf16 GEMM group, the f32-output
-# ones the residual group, whose members they mostly are)
-groups = {"k_gemm256p": [r"k_gemm256p<\w+, \d, 0>", r"k_gemm256q<", r"^Cijk_Alik_Bljk_B[BS]S_BH"],
-          "k_gemm256p<false, 0>": [r"k_gemm256p<false, 0, 0>", r"k_gemm256q<false, 0, true>", r"^Cijk_Alik_Bljk_BSS_BH"],
-          "k_gemm256p<true, 1>": [r"k_gemm256p<true, 1, 0>", r"k_gemm256q<true, 1,"],
-          "k_gemm256p_fp8": [r"k_gemm256p<\w+, \d, [13]>"],
+# (round 5: hand-written kernels only; k_gemm256q<OUT_BF16, ACT, RES, F8, MB1> at every tile height)
+groups = {"k_gemm256p": [r"k_gemm256p<\w+, \d, 0>", r"k_gemm256q<\w+, \d, \w+, 0"],
+          "k_gemm256p<false, 0>": [r"k_gemm256p<false, 0, 0>", r"k_gemm256q<false, 0, true"],
+          "k_gemm256p<true, 1>": [r"k_gemm256p<true, 1, 0>", r"k_gemm256q<true, 1, false, 0"],
+          "k_gemm256p_fp8": [r"k_gemm256p<\w+, \d, [13]>", r"k_gemm256q<\w+, \d, \w+, [13]"],
           "k_attn": ["k_attn"],
           "k_attn_clip": ["k_attn2<80"],
           "k_attn_cutr": ["k_attn2<64"]}

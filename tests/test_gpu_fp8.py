@@ -21,40 +21,36 @@ def L():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     from boxfusion_amd import _lib
-    # the kernel tests check the hand-written fp8 GEMM (no per-shape hand-off to hipBLASLt; the
-    # engine test and test_gemm_fp8_tuned turn it back on)
-    _lib.lib().bf_gemm_set_tune(0)
     yield _lib
-    _lib.lib().bf_gemm_set_tune(1)
 
 
+@pytest.mark.parametrize("bm", [0, 160, 192, 224, 256])
 @pytest.mark.parametrize("M,N,K,kind", [(4112, 1280, 5120, "resid"), (4112, 3840, 1280, "bf16"),
                                         (300, 1280, 1280, "f32")])
-def test_gemm_fp8_tuned(L, M, N, K, kind):
-    """bf_gemm_fp8's per-shape choice (hand-written kernel or hipBLASLt) against torch f32 on the
-    same fp8 operands: scale (hipBLASLt's alpha), bias, in-place f32 residual, bf16 output"""
-    L.lib().bf_gemm_set_tune(1)
+def test_gemm_fp8_dispatch(L, M, N, K, kind, bm):
+    """bf_gemm_fp8 at every tile height of the persistent kernels (0 = the per-shape model) against
+    torch f32 on the same fp8 operands: scale, bias, in-place f32 residual, bf16 output"""
+    L.lib().bf_gemm_set_tile_rows(bm)
     try:
         a, w, g = _fp8_pair(M, N, K, 77 + M)
         bias = torch.randn(N, device="cuda", generator=g)
         s = 0.37
         ref = (a.float() @ w.float().T) * s + bias
-        for _ in range(2):
-            if kind == "resid":
-                r = torch.randn(M, N, device="cuda", generator=g)
-                out = r.clone()
-                L.gemm_fp8(a, w, s, bias, resid=out, out=out)
-                want = ref + r
-            elif kind == "bf16":
-                out = L.gemm_fp8(a, w, s, bias, out_dtype=torch.bfloat16)
-                want = ref
-            else:
-                out = L.gemm_fp8(a, w, s, bias, out_dtype=torch.float32)
-                want = ref
-            torch.cuda.synchronize()
-            assert rel(out, want) < (8e-3 if kind == "bf16" else 5e-5), kind
+        if kind == "resid":
+            r = torch.randn(M, N, device="cuda", generator=g)
+            out = r.clone()
+            L.gemm_fp8(a, w, s, bias, resid=out, out=out)
+            want = ref + r
+        elif kind == "bf16":
+            out = L.gemm_fp8(a, w, s, bias, out_dtype=torch.bfloat16)
+            want = ref
+        else:
+            out = L.gemm_fp8(a, w, s, bias, out_dtype=torch.float32)
+            want = ref
+        torch.cuda.synchronize()
+        assert rel(out, want) < (8e-3 if kind == "bf16" else 5e-5), kind
     finally:
-        L.lib().bf_gemm_set_tune(0)
+        L.lib().bf_gemm_set_tile_rows(0)
 
 
 def rel(a, b):
@@ -185,16 +181,8 @@ def _vit(dev, layers, seed=3):
     return init_seeded(VisionTransformer(224, 14, 1280, layers, 16, 1024).eval(), seed=seed).to(dev)
 
 
-@pytest.fixture
-def tuned(L):
-    """the default GEMM dispatch (per-shape choice) for an engine-level test"""
-    L.lib().bf_gemm_set_tune(1)
-    yield
-    L.lib().bf_gemm_set_tune(0)
-
-
 @pytest.mark.parametrize("layers", [4, 32])
-def test_clip_engine_fp8_vs_bf16(L, tuned, layers):
+def test_clip_engine_fp8_vs_bf16(L, layers):
     from boxfusion_amd.engine import CLIPEngine
     from boxfusion_amd.tools_utils import match_features
     from boxfusion_amd.pipeline import load_class_features

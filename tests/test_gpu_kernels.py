@@ -15,24 +15,23 @@ def L():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     from boxfusion_amd import _lib
-    # these tests check the hand-written kernels: no per-shape hand-off to hipBLASLt
-    # (test_gemm_tuned_vs_torch turns it back on)
-    _lib.lib().bf_gemm_set_tune(0)
     yield _lib
-    _lib.lib().bf_gemm_set_tune(1)
 
 
+@pytest.mark.parametrize("bm", [0, 160, 192, 224, 256])
 @pytest.mark.parametrize("M,N,K,out_bf16,resid,bias", [
     (32896, 1280, 1280, False, "inplace", True),    # CLIP out_proj + residual
     (4112, 1280, 5120, False, "inplace", True),      # CLIP c_proj + residual (16 crops)
     (4112, 1280, 1280, False, "separate", True),
     (4112, 3840, 1280, True, None, True),            # qkv
+    (12800, 768, 3072, False, "inplace", True),      # CuTR global fc2 + residual
     (1000, 768, 768, False, None, False),
     (257, 1280, 1280, True, None, False)])
-def test_gemm_tuned_vs_torch(L, M, N, K, out_bf16, resid, bias):
-    """bf_gemm_bf16's per-shape choice (hand-written kernel or hipBLASLt, whichever timed faster
-    on this box) against torch fp32, on the residual / plain linear forms it applies to."""
-    L.lib().bf_gemm_set_tune(1)
+def test_gemm_tile_rows_vs_torch(L, M, N, K, out_bf16, resid, bias, bm):
+    """bf_gemm_bf16 at every tile height of k_gemm256q (0 = the per-shape model; 256 with an f32
+    residual = k_gemm256p) against torch fp32 on the residual / plain linear forms; every height
+    gives the same K-order MFMA chain, so the k_gemm256q heights agree bit for bit."""
+    L.lib().bf_gemm_set_tile_rows(bm)
     try:
         g = torch.Generator(device="cuda").manual_seed(M + N + K)
         a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
@@ -42,19 +41,78 @@ def test_gemm_tuned_vs_torch(L, M, N, K, out_bf16, resid, bias):
         ref = a.float() @ w.float().T + (b if bias else 0)
         if resid:
             ref = ref + r
-        for _ in range(2):       # the first call of a shape times the candidates, the second uses the choice
+        if resid == "inplace":
+            out = r.clone()
+            L.gemm(a, w, b, resid=out, out=out)
+        elif resid == "separate":
+            out = torch.empty(M, N, device="cuda")
+            L.gemm(a, w, b, resid=r, out=out)
+        else:
+            out = L.gemm(a, w, b, out_dtype=torch.bfloat16 if out_bf16 else torch.float32)
+        torch.cuda.synchronize()
+        assert rel_err(out, ref) < (8e-3 if out_bf16 else 2e-5 * math.sqrt(K / 64) + 1e-5), (M, N, K)
+        if bm in (160, 224) and not (resid and bm == 256):
+            L.lib().bf_gemm_set_tile_rows(192)
             if resid == "inplace":
-                out = r.clone()
-                L.gemm(a, w, b, resid=out, out=out)
+                out2 = r.clone()
+                L.gemm(a, w, b, resid=out2, out=out2)
             elif resid == "separate":
-                out = torch.empty(M, N, device="cuda")
-                L.gemm(a, w, b, resid=r, out=out)
+                out2 = torch.empty(M, N, device="cuda")
+                L.gemm(a, w, b, resid=r, out=out2)
             else:
-                out = L.gemm(a, w, b, out_dtype=torch.bfloat16 if out_bf16 else torch.float32)
+                out2 = L.gemm(a, w, b, out_dtype=torch.bfloat16 if out_bf16 else torch.float32)
             torch.cuda.synchronize()
-            assert rel_err(out, ref) < (8e-3 if out_bf16 else 2e-5 * math.sqrt(K / 64) + 1e-5), (M, N, K)
+            assert torch.equal(out, out2), "tile height changed a value"
     finally:
-        L.lib().bf_gemm_set_tune(0)
+        L.lib().bf_gemm_set_tile_rows(0)
+
+
+@pytest.mark.parametrize("M,N,K,act,out_bf16,resid,row_map", [
+    (128, 1024, 1280, None, False, None, False),          # CLIP output projection (class tokens)
+    (128, 5120, 1280, "gelu", True, None, False),         # cls-only last block fc1 + GELU
+    (128, 1280, 5120, None, False, "inplace", True),      # cls-only last block fc2 + residual, row map
+    (100, 1280, 1280, None, False, "separate", True),
+    (200, 512, 768, "relu", True, None, False),
+    (7, 64, 256, None, False, None, False)])
+def test_gemm_skinny_vs_torch(L, M, N, K, act, out_bf16, resid, row_map):
+    """few-row GEMMs (k_gemm_skinny: 8 waves split K, partial tiles summed in wave order)"""
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g)
+    ref = a.float() @ w.float().T + b
+    if act == "gelu":
+        ref = F.gelu(ref)
+    elif act == "relu":
+        ref = F.relu(ref)
+    rows = M + 9 if row_map else M
+    rm = (torch.randperm(rows, device="cuda", generator=g)[:M].int() if row_map else None)
+    r = torch.randn(rows, N, device="cuda", generator=g)
+    dt = torch.bfloat16 if out_bf16 else torch.float32
+    if resid == "inplace":
+        out = r.clone()
+        L.gemm(a, w, b, act=act, resid=out, out=out, row_map=rm)
+    elif resid == "separate":
+        out = torch.zeros(rows, N, device="cuda")
+        L.gemm(a, w, b, act=act, resid=r, out=out, row_map=rm)
+    else:
+        out = torch.zeros(rows, N, device="cuda", dtype=dt)
+        L.gemm(a, w, b, act=act, out=out, row_map=rm)
+    torch.cuda.synchronize()
+    orow = rm.long() if rm is not None else torch.arange(M, device="cuda")
+    want = ref + (r[orow] if resid else 0)
+    assert rel_err(out[orow], want) < (8e-3 if out_bf16 else 2e-5 * math.sqrt(K / 64) + 1e-5)
+    if row_map:      # rows outside the map untouched
+        mask = torch.ones(rows, dtype=torch.bool, device="cuda")
+        mask[orow] = False
+        base = r if resid == "inplace" else torch.zeros_like(out)
+        assert torch.equal(out[mask], base[mask])
+    o1 = out.clone()
+    if resid == "inplace":
+        out = r.clone()
+        L.gemm(a, w, b, act=act, resid=out, out=out, row_map=rm)
+        torch.cuda.synchronize()
+        assert torch.equal(out, o1), "not deterministic"
 
 
 def rel_err(a, b):
