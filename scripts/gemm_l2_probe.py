@@ -12,7 +12,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from boxfusion_amd import _lib  # noqa: E402
 
 SHAPES = [("clip_qkv", 32896, 3840, 1280, 1), ("clip_fc2", 32896, 1280, 5120, 0),
-          ("cutr_w_fc2", 25600, 768, 3072, 0), ("sq8192", 8192, 8192, 8192, 1)]
+          ("clip_fc1", 32896, 5120, 1280, 1), ("clip_proj", 32896, 1280, 1280, 0),
+          ("cutr_w_fc2", 25600, 768, 3072, 0), ("cutr_g_fc2", 12800, 768, 3072, 0), ("sq4096", 4096, 4096, 4096, 1)]
 
 
 def bench(fn, iters=10):
@@ -40,8 +41,11 @@ for name, M, N, K, ob in SHAPES:
                                       None, None, 0, 0, ctypes.c_void_p(out.data_ptr()), N, ob, None, M, N, K, 0, st)
     res = {}
     for rnd in range(3):
-        for tag, lda, ldw in (("real", K, K), ("A_l2", 0, K), ("W_l2", K, 0), ("both_l2", 0, 0)):
+        for tag, lda, ldw, tch in (("real", K, K, 0), ("touch3", K, K, 3), ("touch4", K, K, 4),
+                                   ("touch6", K, K, 6), ("both_l2", 0, 0, 0)):
+            L.bf_gemm_set_touch(tch)
             res.setdefault(tag, []).append(bench(run(lda, ldw)))
+        L.bf_gemm_set_touch(0)
     fl = 2.0 * M * N * K
     print(f"{name:11s} " + " | ".join(f"{t} {sorted(v)[1]:7.1f} us {fl / sorted(v)[1] / 1e6:5.0f} TF"
                                        for t, v in res.items()), flush=True)
