@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import atexit
 import ctypes
+import weakref
 import sys
 import os
 
@@ -394,6 +395,14 @@ class FusionSequencer:
         self.h = c_void_p()
         _check(L.bf_fseq_create(ctypes.byref(self.h)), "bf_fseq_create")
         self._state = np.zeros(FSEQ_STATE_N, np.int64)
+        _LIVE_SEQUENCERS.add(self)
+
+    def close(self):
+        """release the sequencer's device buffers and handle now (idempotent)"""
+        h, L = getattr(self, "h", None), getattr(self, "_L", None)
+        if h is not None and h.value and L is not None:
+            L.bf_fseq_destroy(h)
+        self.h = None
 
     def _rc(self, rc, name):
         if rc != 0:
@@ -443,13 +452,10 @@ class FusionSequencer:
         return ids[:n], xyz, vn
 
     def __del__(self, _finalizing=sys.is_finalizing):
-        h, L = getattr(self, "h", None), getattr(self, "_L", None)
-        if _finalizing():             # interpreter exit: the process releases the device memory
+        if _finalizing():             # interpreter exit: _shutdown() already released it
             return
         try:
-            if h is not None and h.value and L is not None:
-                L.bf_fseq_destroy(h)
-                self.h = None
+            self.close()
         except Exception:  # noqa: BLE001 - interpreter teardown: the process frees everything
             pass
 
@@ -1087,8 +1093,6 @@ def cu_masked_stream(cus, device=None):
         rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(s), ctypes.c_uint32(len(words)), words)
     if rc != 0:
         raise HipError(f"hipExtStreamCreateWithCUMask failed ({rc})")
-    if not _MASKED_STREAMS:
-        atexit.register(_destroy_masked_streams)
     _MASKED_STREAMS.append((dev, s.value))
     return torch.cuda.ExternalStream(s.value, device=dev)
 
@@ -1105,6 +1109,36 @@ def _destroy_masked_streams():
         with torch.cuda.device(dev):
             hip.hipStreamSynchronize(ctypes.c_void_p(h))
             hip.hipStreamDestroy(ctypes.c_void_p(h))
+
+
+# Objects that hold HIP resources past their last use: fusion worker threads (which may still launch
+# on a CU-masked stream) and keyframe sequencers (device buffers, a stored stream).  At interpreter
+# exit they are released in dependency order while the HIP runtime is still up: workers stopped,
+# then sequencers destroyed, then the masked streams.
+_LIVE_WORKERS = weakref.WeakSet()
+_LIVE_SEQUENCERS = weakref.WeakSet()
+
+
+def register_worker(w):
+    """an object with stop(timeout) that runs HIP work on a thread (fusion_stage.AsyncFusion)"""
+    _LIVE_WORKERS.add(w)
+
+
+def _shutdown():
+    for w in list(_LIVE_WORKERS):
+        try:
+            w.stop(timeout=30.0)
+        except Exception:  # noqa: BLE001 - exit path: keep releasing the rest
+            pass
+    for q in list(_LIVE_SEQUENCERS):
+        try:
+            q.close()
+        except Exception:  # noqa: BLE001
+            pass
+    _destroy_masked_streams()
+
+
+atexit.register(_shutdown)
 
 
 def partition_streams(n_reserved, device=None, masked=False):

@@ -15,6 +15,10 @@
 // land on the same XCD (shared L2).
 #include "bf_common.h"
 
+#include <mutex>
+#include <set>
+#include <string>
+
 // wave priority in the K loop: 0 = raise to 1 around every MFMA quadrant (default), 1 = waves 4-7
 // at priority 1 for the whole walk (MI355X_MICROARCH "static priority for the younger half"),
 // 2 = never raised
@@ -1314,20 +1318,15 @@ static int gemm_cu_count() {
     return n_cu;
 }
 
-// Large problems run the persistent 256x256 kernel unless its last round of tiles leaves clearly
-// more of the chip idle than the 128x128 kernel's would (1 block/CU vs 2 blocks/CU); the per-tile
-// advantage of the 256x256 kernel grows with K (measured ~1.04x at K=768, ~1.2x at K>=4096).
+// Large problems (N >= 512, at least half a round of 256x256 tiles) run the persistent kernels:
+// per tile they are 3-4x the 128x128 kernel's rate (CLIP patch embed 32768 x 1280 x 640 with its
+// row map: 240 us on 128x128 tiles, profiles/r05_bench_kernel_stats.csv), which no round
+// quantisation of the 128x128 grid makes up for.
 static bool gemm_large_tiles(int M, int N, int K) {
     const int n_cu = gemm_cu_count();
     const long long t2 = (long long)((M + 255) / 256) * ((N + 255) / 256);
-    const long long t1 = (long long)((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N);
-    const double e2 = (double)t2 / (double)(((t2 + n_cu - 1) / n_cu) * n_cu);
-    const double e1 = (double)t1 / (double)(((t1 + 2 * n_cu - 1) / (2 * n_cu)) * 2 * n_cu);
-    // per-tile advantage of the 256x256 kernel (operand reuse, MFMA density) grows with K;
-    // fitted on the CuTR shapes (scripts/gemm_tiles_probe.py): window qkv K=768 N=2304 and fc2
-    // K=3072 N=768 run faster on 256x256 tiles, proj K=768 N=768 on 128x128
-    const double adv = 1.0 + 0.6 * (double)(K < 4096 ? K : 4096) / 4096.0;
-    return N >= 512 && t2 >= n_cu / 2 && e2 * adv >= e1;
+    (void)K;
+    return N >= 512 && t2 >= n_cu / 2;
 }
 
 // which kernel bf_gemm_bf16 runs for an aligned problem of this shape (1 = 256x256 persistent)
@@ -1553,6 +1552,21 @@ static int launch_gemm_skinny(void* stream, const void* A, int lda, const void* 
     return bf_check_launch();
 }
 
+// BF_GEMM_LOG=1: each distinct (shape, epilogue, kernel) choice of bf_gemm_bf16 once on stderr
+static void gemm_log(int M, int N, int K, int act, int resid, int resid_mod, int row_map, int c_bf16,
+                     const char* kern, int bm) {
+    static const bool on = [] { const char* e = getenv("BF_GEMM_LOG"); return e && e[0] == '1'; }();
+    if (!on) return;
+    // never destroyed: no static destructor runs at process exit (exit order)
+    static std::mutex& mu = *new std::mutex;
+    static std::set<std::string>& seen = *new std::set<std::string>;
+    char buf[256];
+    snprintf(buf, sizeof buf, "bf_gemm M=%d N=%d K=%d act=%d resid=%d resid_mod=%d row_map=%d out=%s -> %s rows=%d",
+             M, N, K, act, resid, resid_mod, row_map, c_bf16 ? "bf16" : "f32", kern, bm);
+    std::lock_guard<std::mutex> g(mu);
+    if (seen.insert(buf).second) fprintf(stderr, "%s\n", buf);
+}
+
 // The product entry point: hand-written kernels only, chosen from the shape alone.
 BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bias,
                         const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
@@ -1578,6 +1592,7 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
     const int n_cu = gemm_cu_count();
     // 16-B row chunks of C / resid also carry the skinny kernel's epilogue (8 columns per thread)
     if (gemm_use_skinny(M, N, K, vec_epi && (c_bf16 || N % 8 == 0))) {
+        gemm_log(M, N, K, act, resid != nullptr, resid_mod, row_map != nullptr, c_bf16, "k_gemm_skinny", 128);
 #define GSK(OB, AC) return launch_gemm_skinny<OB, AC>(stream, A, lda, W, ldw, bias, resid, ldr, resid_mod, C, ldc, \
                                                       row_map, M, N, K)
         if (c_bf16) {
@@ -1607,6 +1622,7 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
             const int bm = 2 * (64 + 16 * mb1);
             const int tqm = (M + bm - 1) / bm;
             const int gq = gemm_grid(tqm * t2n, n_cu);
+            gemm_log(M, N, K, act, resid != nullptr, resid_mod, row_map != nullptr, c_bf16, "k_gemm256q", bm);
             int rc = 0;
             if (resid) rc = launch_gemm256q<false, 0, true, 0>(mb1, gq, stream, A, lda, W, ldw, bias, resid, ldr, C, ldc, M, N, K, t2n, tqm, 1.f, 1.f);
             else if (!c_bf16) rc = launch_gemm256q<false, 0, false, 0>(mb1, gq, stream, A, lda, W, ldw, bias, resid, ldr, C, ldc, M, N, K, t2n, tqm, 1.f, 1.f);
@@ -1614,6 +1630,7 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
             else rc = launch_gemm256q<true, 1, false, 0>(mb1, gq, stream, A, lda, W, ldw, bias, resid, ldr, C, ldc, M, N, K, t2n, tqm, 1.f, 1.f);
             return rc;
         }
+        gemm_log(M, N, K, act, resid != nullptr, resid_mod, row_map != nullptr, c_bf16, "k_gemm256p", 256);
 #define GEMM2(OB, AC) launch_gemm256<OB, AC>(grid2, bf_stream(stream), A, lda, W, ldw, bias, \
                                             resid, ldr, resid_mod, C, ldc, row_map, M, N, K, t2n, t2m)
         if (c_bf16) {
@@ -1628,6 +1645,7 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
 #undef GEMM2
         return bf_check_launch();
     }
+    gemm_log(M, N, K, act, resid != nullptr, resid_mod, row_map != nullptr, c_bf16, "k_gemm", 128);
 #define GEMM_LAUNCH(OB, AC)                                                                       \
     hipLaunchKernelGGL((k_gemm<OB, AC>), dim3(nwg), dim3(G_THREADS), lds, bf_stream(stream),       \
                        (const u16*)A, lda, (const u16*)W, ldw, bias, resid, ldr, resid_mod, C, ldc, \

@@ -458,6 +458,7 @@ class AsyncFusion:
         self.busy_s = 0.0      # wall time the worker spent inside keyframe jobs (after their input was ready)
         self.thread = threading.Thread(target=self._run, name="boxfusion-fusion", daemon=True)
         self.thread.start()
+        _lib.register_worker(self)
 
     def submit(self, count, pose, make_pred, ready=None):
         self.q.put((count, pose, make_pred, ready))
@@ -515,3 +516,17 @@ class AsyncFusion:
         if self.err is not None:
             raise self.err
         return self.stage
+
+    def stop(self, timeout=None):
+        """interpreter exit (_lib._shutdown): drop queued jobs, let the running one finish, and
+        drain the worker's stream before the streams and sequencers it uses are released"""
+        if not self.thread.is_alive():
+            return
+        try:
+            while True:
+                self.q.get_nowait()
+        except queue.Empty:
+            pass
+        self.q.put(None)
+        self.thread.join(timeout)
+        self.stream.synchronize()
