@@ -885,6 +885,9 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
 // in the Infinity Cache).
 // ------------------------------------------------------------------------------------------
 #define G2Q_BIAS_MAX 8192
+#ifndef GEMM_ABL          // diagnostic builds only (wrong results): 1 no K-loop LDS-DMA, 2 no fragment reads
+#define GEMM_ABL 0
+#endif
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2v));
@@ -988,6 +991,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         return v;
     };
 #define STAGE_HALF(c, v, which)                                                                    \
+    if (!(GEMM_ABL & 1) || !in_loop_)                                                              \
     {                                                                                              \
         unsigned char* dst_ = g_smem + (c).buf * 65536 + (which) * 16384 + wave_u * 2048;          \
         _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                         \
@@ -1108,7 +1112,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
     i32x8 ga[4], gb0[2], gb1[2];      // fp8: a lane's two 16-B chunks as one 32-B fragment
 #define LDS16(off) (*reinterpret_cast<const bf16x8*>(g_smem + (off)))
 #define RD_A(stage, mi)                                                                            \
-    if constexpr ((F8 & 1) != 0) {                                                                 \
+    if ((GEMM_ABL & 2) && in_loop_) {} else if constexpr ((F8 & 1) != 0) {                                                                 \
         _Pragma("unroll") for (int i = 0; i < NBLK(mi); ++i) {                                     \
             const int b_ = (stage) * 65536 + (mi) * 16384;                                         \
             ga[i] = frag32(LDS16(b_ + swz(wr * 64 + i * 16 + lr, lq)),                             \
@@ -1119,7 +1123,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
             fa[i * 2 + ks] = LDS16((stage) * 65536 + (mi) * 16384 + swz(wr * 64 + i * 16 + lr, ks * 4 + lq)); \
     }
 #define RD_B(FB, GB, stage, ni)                                                                    \
-    if constexpr ((F8 & 1) != 0) {                                                                 \
+    if ((GEMM_ABL & 2) && in_loop_) {} else if constexpr ((F8 & 1) != 0) {                                                                 \
         _Pragma("unroll") for (int j = 0; j < 2; ++j) {                                            \
             const int b_ = (stage) * 65536 + 32768 + (ni) * 16384;                                 \
             GB[j] = frag32(LDS16(b_ + swz(wc * 32 + j * 16 + lr, lq)),                             \
@@ -1148,6 +1152,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
         if (GEMM_PRIO_MODE == 0) __builtin_amdgcn_s_setprio(0);                                    \
     }
 
+    bool in_loop_ = false;    // GEMM_ABL diagnostics act inside the K loop only
     KT kc = kt_at_tile(0, 0);
     KT k1 = kt_next(kc);
     KT k2 = kt_next(k1);
@@ -1167,6 +1172,8 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
     if (GEMM_PRIO_MODE == 1 && wr == 1) __builtin_amdgcn_s_setprio(1);
 
     int em0 = 0, en0 = 0;     // the tile whose quadrant Q10 is still pending
+    if (GEMM_ABL & 2) { RD_B(fb0, gb0, 0, 0); RD_B(fb1, gb1, 0, 1); RD_A(0, 0); }
+    in_loop_ = true;
     for (int g = 0; g < total; ++g) {
         const int st = g & 1;
         const bool isL = kc.k0 == K - KTE;

@@ -41,11 +41,8 @@ for name, M, N, K, ob in SHAPES:
                                       None, None, 0, 0, ctypes.c_void_p(out.data_ptr()), N, ob, None, M, N, K, 0, st)
     res = {}
     for rnd in range(3):
-        for tag, lda, ldw, tch in (("real", K, K, 0), ("touch3", K, K, 3), ("touch4", K, K, 4),
-                                   ("touch6", K, K, 6), ("both_l2", 0, 0, 0)):
-            L.bf_gemm_set_touch(tch)
+        for tag, lda, ldw in (("real", K, K), ("both_l2", 0, 0)):
             res.setdefault(tag, []).append(bench(run(lda, ldw)))
-        L.bf_gemm_set_touch(0)
     fl = 2.0 * M * N * K
     print(f"{name:11s} " + " | ".join(f"{t} {sorted(v)[1]:7.1f} us {fl / sorted(v)[1] / 1e6:5.0f} TF"
                                        for t, v in res.items()), flush=True)
