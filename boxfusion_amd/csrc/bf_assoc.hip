@@ -379,8 +379,12 @@ __global__ void __launch_bounds__(64) k_nms_scan_w(
     int* supp = bufB + n + 1;
     int* keep = supp + n + 1;
     int* succ = keep + n + 2;
+    // list lengths clamped to the row capacity (a longer input length would read and write past
+    // the row); such an input sets the overflow status bit
+    int in_over = 0;
     for (int q = t; q < n; q += 64) {
-        fll[q] = fl_len[q];
+        fll[q] = min(fl_len[q], cap);
+        in_over |= fl_len[q] > cap;
         iid[q] = init_id[q];
         vn[q] = valid_num[q];
         sc[q] = scores[q];
@@ -446,7 +450,8 @@ __global__ void __launch_bounds__(64) k_nms_scan_w(
     __syncthreads();
     int* order = bufA;
     int* rest = bufB;
-    int no = n, nk = 0, ns = 0, nev = 0, st = 0;   // wave-uniform counters (st: lane 0)
+    int no = n, nk = 0, ns = 0, nev = 0;           // wave-uniform counters (st: lane 0)
+    int st = __any(in_over) ? BF_DEV_FUSION_LIST_OVERFLOW : 0;
     while (no > 0) {
         const int i = order[0];
         if (t == 0) keep[nk] = i;

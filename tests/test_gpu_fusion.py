@@ -445,3 +445,29 @@ def test_nms_scan_large_vs_oracle(L, n_glo, n_new):
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
     assert got["fusion_list"] == ref["fusion_list"]
     assert len(ref["success"]) > 10 and len(ref["events"]) > 10
+
+
+@pytest.mark.parametrize("n", [40, 130])
+def test_nms_scan_input_list_longer_than_capacity(L, n):
+    """an input fusion-list length above the row capacity (a caller error) raises the overflow status
+    bit instead of reading / writing past the row, in the one-wave scan at n <= 96 and the bit-mask
+    scan above it (bf_nms_scan_ws)"""
+    rng = np.random.default_rng(n)
+    b = np.concatenate([rng.uniform(-3, 3, (n, 3)), rng.uniform(0.2, 0.6, (n, 3))], 1).astype(np.float32)
+    R = np.repeat(np.eye(3, dtype=np.float32)[None], n, 0)
+    corners = _t(OR.box_corners(b, R))
+    dev = corners.device
+    cap = 8
+    items = torch.full((n, cap), -1, dtype=torch.int32, device=dev)
+    items[:, 0] = torch.arange(n, dtype=torch.int32, device=dev)
+    lens = torch.ones(n, dtype=torch.int32, device=dev)
+    lens[n // 2] = cap + 5                                   # longer than the row
+    cfg = nms_cfg(L, cap=cap)
+    iou = L.obb_iou_matrix(corners)
+    scores = torch.from_numpy(rng.uniform(0.3, 0.9, n).astype(np.float32)).to(dev)
+    init_id = torch.arange(n, dtype=torch.int32, device=dev)
+    poses = torch.from_numpy(np.repeat(np.eye(4, dtype=np.float32)[None], n, 0)).to(dev)
+    vn = torch.zeros(n, device=dev)
+    keep, succ, events, counts = L.nms_scan(iou, corners, scores, init_id, poses, items, lens, vn, cfg)
+    torch.cuda.synchronize()
+    assert int(counts[3]) & L.BF_DEV_FUSION_LIST_OVERFLOW
