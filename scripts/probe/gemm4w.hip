@@ -5,6 +5,12 @@ typedef unsigned short u16;
 typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
 #define W4_STAGE 32768
 #define W4_LDS (4 * W4_STAGE)
+#ifndef W4_PIPE
+#define W4_PIPE 1
+#endif
+#ifndef W4_NA
+#define W4_NA 32
+#endif
 #ifndef NBJ
 #define NBJ 8
 #endif
@@ -68,10 +74,78 @@ __global__ void __launch_bounds__(256, 1) k_gemm4w(const u16* __restrict__ A, in
 #pragma unroll
         for (int j = 0; j < NBJ; ++j) { acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f}; asm volatile("" : "+a"(acc[i][j])); }
 #define W4_MFMA(SET) { _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < NBJ; ++j) mfma_a(acc[i][j], fb[SET][j], fa[SET][i]); }
+#if W4_PIPE != 2
     stage(0); stage(1); stage(2); stage(3);
     asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
     __syncthreads();
     W4_READ(0, 0);
+#endif
+#if W4_PIPE == 2
+    // register staging: global_load_dwordx4 into VGPRs one K-tile ahead, ds_write_b128 into a 2-slot
+    // ring (the LDS image of the DMA form); part B MFMAs straddle the barrier as in W4_PIPE 1
+    typedef unsigned u32x4r __attribute__((ext_vector_type(4)));
+    u32x4r stg[8];
+    auto gload = [&](int kt) {
+        if (kt < nk) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                stg[i] = *reinterpret_cast<const u32x4r*>(reinterpret_cast<const unsigned char*>(A) + voa[i] + kt * 64);
+                stg[4 + i] = *reinterpret_cast<const u32x4r*>(reinterpret_cast<const unsigned char*>(W) + vow[i] + kt * 64);
+            }
+        }
+    };
+    auto swrite = [&](int kt) {
+        unsigned char* s_ = smem + (kt & 1) * W4_STAGE + wave_u * 4096 + lane * 16;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            *reinterpret_cast<u32x4r*>(s_ + i * 1024) = stg[i];
+            *reinterpret_cast<u32x4r*>(s_ + 16384 + i * 1024) = stg[4 + i];
+        }
+    };
+    auto mf = [&](int set, int idx) { mfma_a(acc[idx / NBJ][idx % NBJ], fb[set][idx % NBJ], fa[set][idx / NBJ]); };
+    gload(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    swrite(0);
+    gload(1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    W4_READ(0, 0);
+    for (int g = 0; g < nk; g += 2) {
+#define W4_RITER(CUR, G) { \
+            _Pragma("unroll") for (int x = 0; x < W4_NA; ++x) mf(CUR, x); \
+            if ((G) + 1 < nk) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); swrite((G) + 1); } \
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); \
+            gload((G) + 2); \
+            { const unsigned char* r_ = smem + (((G) + 1) & 1) * W4_STAGE; \
+              _Pragma("unroll") for (int x = 0; x < 8 * NBJ - W4_NA; ++x) { \
+                  if (x < 8) fa[(CUR) ^ 1][x] = *reinterpret_cast<const bf16x8*>(r_ + (128 * wm + 16 * x + lr) * 64 + rslot * 16); \
+                  else if (x < 8 + NBJ) fb[(CUR) ^ 1][x - 8] = *reinterpret_cast<const bf16x8*>(r_ + 16384 + ((16 * NBJ) * wn + 16 * (x - 8) + lr) * 64 + rslot * 16); \
+                  mf(CUR, W4_NA + x); asm volatile("" ::: "memory"); } } }
+        W4_RITER(0, g);
+        W4_RITER(1, g + 1);
+#undef W4_RITER
+    }
+#elif W4_PIPE
+    // part A: MFMAs 0 .. NA-1 of the current set; barrier; then the next K-tile's DMA and fragment
+    // reads interleaved one for one with MFMAs NA .. 8*NBJ-1 of the current set
+    auto mf = [&](int set, int idx) { mfma_a(acc[idx / NBJ][idx % NBJ], fb[set][idx % NBJ], fa[set][idx / NBJ]); };
+    for (int g = 0; g < nk; g += 2) {
+#define W4_PITER(CUR, G) { \
+            _Pragma("unroll") for (int x = 0; x < W4_NA; ++x) mf(CUR, x); \
+            asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory"); __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); \
+            { unsigned char* s_ = smem + (((G) + 4) & 3) * W4_STAGE + wave_u * 4096; const int kt_ = (G) + 4; const int so_ = kt_ < nk ? kt_ * 64 : 0; \
+              const unsigned char* r_ = smem + (((G) + 1) & 3) * W4_STAGE; \
+              _Pragma("unroll") for (int x = 0; x < 8 * NBJ - W4_NA; ++x) { \
+                  if (x < 8 && (x & 1) == 0) w4_glds(A, bytesA, s_ + (x >> 1) * 1024, kt_ < nk ? voa[x >> 1] : (int)0x80000000, so_); \
+                  if (x < 8 && (x & 1) == 1) w4_glds(W, bytesW, s_ + 16384 + (x >> 1) * 1024, kt_ < nk ? vow[x >> 1] : (int)0x80000000, so_); \
+                  if (x < 8) fa[(CUR) ^ 1][x] = *reinterpret_cast<const bf16x8*>(r_ + (128 * wm + 16 * x + lr) * 64 + rslot * 16); \
+                  else if (x < 8 + NBJ) fb[(CUR) ^ 1][x - 8] = *reinterpret_cast<const bf16x8*>(r_ + 16384 + ((16 * NBJ) * wn + 16 * (x - 8) + lr) * 64 + rslot * 16); \
+                  mf(CUR, W4_NA + x); asm volatile("" ::: "memory"); } } }
+        W4_PITER(0, g);
+        W4_PITER(1, g + 1);
+#undef W4_PITER
+    }
+#else
     for (int g = 0; g < nk; g += 2) {
 #define W4_ITER(CUR, G) { asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory"); __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); \
             stage((G) + 4); W4_READ((CUR) ^ 1, (G) + 1); W4_MFMA(CUR); }
@@ -79,6 +153,7 @@ __global__ void __launch_bounds__(256, 1) k_gemm4w(const u16* __restrict__ A, in
         W4_ITER(1, g + 1);
 #undef W4_ITER
     }
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int i = 0; i < 8; ++i) {

@@ -30,7 +30,8 @@ def bench(fn, iters=10):
 
 
 L = _lib.lib()
-P = ctypes.CDLL(os.path.join(ROOT, "boxfusion_amd/_build/probe/gemm4w_nbj8.so"))
+VARIANTS = sys.argv[1:] or ["na32"]
+PS = {v: ctypes.CDLL(os.path.join(ROOT, f"boxfusion_amd/_build/probe/gemm4w_{v}.so")) for v in VARIANTS}
 vp = ctypes.c_void_p
 for name, M, N, K in SHAPES:
     a = torch.randn(M, K, device="cuda").bfloat16()
@@ -40,17 +41,19 @@ for name, M, N, K in SHAPES:
     st = vp(torch.cuda.current_stream().cuda_stream)
     prod = lambda: L.bf_gemm_bf16(vp(a.data_ptr()), K, vp(w.data_ptr()), K, None, None, 0, 0, vp(o1.data_ptr()), N, 1,
                                   None, M, N, K, 0, st)
-    w4 = lambda: P.gemm4w_launch(vp(a.data_ptr()), K, vp(w.data_ptr()), K, vp(o2.data_ptr()), N, M, N, K, st)
-    assert w4() == 0
+    fns = {"prod": prod}
     prod()
-    torch.cuda.synchronize()
-    ref = (a[:4096].float() @ w.float().T)
-    err = (o2[:4096].float() - ref).abs().max().item()
-    same = torch.equal(o1, o2)
-    res = {"prod": [], "w4": []}
+    same = []
+    for v, P in PS.items():
+        fns[v] = (lambda P=P: P.gemm4w_launch(vp(a.data_ptr()), K, vp(w.data_ptr()), K, vp(o2.data_ptr()), N, M, N, K, st))
+        o2.zero_()
+        assert fns[v]() == 0
+        torch.cuda.synchronize()
+        same.append(f"{v}={'eq' if torch.equal(o1, o2) else 'DIFF'}")
+    res = {k: [] for k in fns}
     for _ in range(3):
-        res["prod"].append(bench(prod))
-        res["w4"].append(bench(w4))
+        for k, f in fns.items():
+            res[k].append(bench(f))
     fl = 2.0 * M * N * K
-    print(f"{name:11s} maxerr {err:.3g} bitequal_prod {same} | " + " | ".join(
+    print(f"{name:11s} {' '.join(same)} | " + " | ".join(
         f"{t} {sorted(v)[1]:7.1f} us {fl / sorted(v)[1] / 1e6:5.0f} TF" for t, v in res.items()), flush=True)
