@@ -30,7 +30,12 @@ def test_pmc_key_resolves_in_newest_round(name):
 
 
 def test_pmc_fp8_key_resolves():
-    assert bench.load_pmc_traffic(bench.PMC_KEYS["fp8_gemm"])
+    """the fp8 line's traffic comes from the fp8 workload's own record of the newest round
+    (profiles/r<N>_fp8_pmc.json), not from an older round's"""
+    d = bench.load_pmc_traffic(bench.PMC_KEYS["fp8_gemm"])
+    assert d
+    n = int(re.match(r"r(\d+)", os.path.basename(_newest_round_pmc())).group(1))
+    assert re.match(rf"profiles/r0*{n}_", d["source"]), d["source"]
 
 
 def test_depth_pmc_sum_covers_every_pass_and_the_writes():
