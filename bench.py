@@ -452,12 +452,14 @@ def roofline_obj(ks, kernel, bound, pmc_key=None, peak_tflops=PEAK_BF16_TFLOPS):
 
 def auto_rank0_batch(B, ranks):
     """rank 0's detection share when it also fuses `ranks` ranks' frames.  Measured on one MI355X
-    with --sim-ranks 8 (profiles/r04_fusion_owner_sim8.txt): the fusion worker is busy 16.6 ms per
-    63-keyframe step (0.26 ms per keyframe) on its 32 reserved CUs, so it keeps pace either way;
-    what remains is rank 0's detection on the other 224 CUs: 7 frames 50.5 ms, 8 frames 57.3 ms
-    per step against the 52.2-53.4-ms N=1 step of the other ranks, i.e. 63/64 = 0.98 vs 0.93 of the
-    ideal.  Without the reservation rank 0 detects 8 frames in 53.6 ms (0.975) with the worker at
-    32.5 ms per step beside it."""
+    with --sim-ranks 8, all arms on one box (scripts/sim8_ab.sh, profiles/r05_bench_sim8.json,
+    DESIGN.md §8): N = 1 step 54.7 ms; rank 0 with its 32 reserved CUs on 7 frames 51.3 ms (the
+    other ranks set the step: 63/64 = 0.984 of the ideal, worker busy 16.2 ms per step); without
+    the reservation on 8 frames 56.0 ms (0.977, worker 36.7 ms); reservation + 8 frames 57.2 ms
+    (0.956).  7 frames with the reservation is kept: it is the fastest arm, and the reserved CUs
+    keep the worker's own time small where scenes are heavier (150 objects: ~33 ms of fusion
+    kernels per 64 keyframes on an idle chip), which it would otherwise spend queued behind the
+    persistent GEMMs that hold every CU."""
     if ranks >= 8:
         return max(1, B - 1)
     return B
