@@ -54,7 +54,12 @@ def match_features(img_features, text_features, sim_thres):
     image features [N, D], max similarity [N])."""
     f = img_features / img_features.norm(dim=-1, keepdim=True)
     text_features /= text_features.norm(dim=-1, keepdim=True)
-    probs = 100.0 * f @ text_features.T
+    if f.is_cuda:
+        # (100 f) @ text^T as the reference groups it, on the f32 MFMA GEMM (bf_gemm_f32)
+        from boxfusion_amd import _lib
+        probs = _lib.gemm_f32((100.0 * f).contiguous(), text_features.contiguous())
+    else:
+        probs = 100.0 * f @ text_features.T
     probs = torch.cat([probs, torch.full_like(probs, float(sim_thres))[..., :1]], dim=-1)
     mx, idx = torch.max(probs, dim=-1)
     return idx, f, mx

@@ -534,3 +534,29 @@ def test_cu_partition_placement(L):
     assert len(pf) == 32 and len(pd) == n - 32
     assert not (pf & pd)
     assert set(Counter(k[0] for k in pf).values()) == {32 // L.XCDS}
+
+
+@pytest.mark.parametrize("n_crops,n_cls", [(128, 473), (16, 200), (1, 1), (37, 33)])
+def test_match_features_on_f32_gemm(L, n_crops, n_cls):
+    """text_prompt's similarity (tools/utils.py:397-401, 486-493) on the device: (100 f) @ text^T on
+    the f32 MFMA GEMM (bf_gemm_f32), then the threshold column and argmax -- against the same
+    formula in float64; the class matches wherever the top two scores are apart, and the in-place
+    text renormalisation still happens."""
+    from boxfusion_amd.tools_utils import match_features
+    g = torch.Generator(device="cuda").manual_seed(n_crops * 1000 + n_cls)
+    img = torch.randn(n_crops, 1024, device="cuda", generator=g)
+    text = torch.randn(n_cls, 1024, device="cuda", generator=g) * 3.0
+    text_in = text.clone()
+    thr = 0.0
+    idx, f, mx = match_features(img, text_in, thr)
+    torch.cuda.synchronize()
+    fd = img.double() / img.double().norm(dim=-1, keepdim=True)
+    td = text.double() / text.double().norm(dim=-1, keepdim=True)
+    pd = 100.0 * fd @ td.T
+    pd = torch.cat([pd, torch.full_like(pd, thr)[..., :1]], dim=-1)
+    mxd, idxd = pd.max(dim=-1)
+    assert torch.allclose(text_in.double(), td, atol=1e-6)      # renormalised in place
+    assert torch.allclose(mx.double(), mxd, atol=2e-4)
+    top2 = pd.topk(min(2, pd.shape[1]), dim=-1).values
+    clear = (top2[:, 0] - top2[:, -1]) > 1e-3 if pd.shape[1] > 1 else torch.ones_like(mxd, dtype=torch.bool)
+    assert torch.equal(idx[clear].cpu(), idxd[clear].cpu())
