@@ -885,7 +885,8 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
 // in the Infinity Cache).
 // ------------------------------------------------------------------------------------------
 #define G2Q_BIAS_MAX 8192
-#ifndef GEMM_ABL          // diagnostic builds only (wrong results): 1 no K-loop LDS-DMA, 2 no fragment reads
+#ifndef GEMM_ABL          // diagnostic builds only (wrong results): 1 no K-loop LDS-DMA, 2 no fragment reads,
+                          // 4 k_gemm256q epilogue stores dropped (out-of-range offsets: same vmcnt counts)
 #define GEMM_ABL 0
 #endif
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
@@ -1069,7 +1070,7 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
                 }                                                                                  \
                 const auto s_ = __builtin_amdgcn_permlane16_swap((uint32_t)XY_[0], (uint32_t)XY_[1], false, false); \
                 const int c_ = (en0_) + wc * 64 + (NI) * 32 + 16 * (lq & 1) + 8 * (lq >> 1);        \
-                const int off_ = (r_ < M && c_ < N) ? (r_ * ldc + c_) : (int)0x80000000;          \
+                const int off_ = (r_ < M && c_ < N && !(GEMM_ABL & 4)) ? (r_ * ldc + c_) : (int)0x80000000; \
                 __builtin_amdgcn_raw_buffer_store_b64((u32x2v){s_[0], s_[1]}, crs, off_, 0, 2);   \
                 continue;                                                                          \
             }                                                                                      \
@@ -1096,12 +1097,12 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
                 const auto s0_ = __builtin_amdgcn_permlane16_swap(X0, Y0, false, false);           \
                 const auto s1_ = __builtin_amdgcn_permlane16_swap(X1, Y1, false, false);           \
                 const int c_ = (en0_) + wc * 64 + (NI) * 32 + 16 * (lq & 1) + 8 * (lq >> 1);        \
-                const int off_ = (r_ < M && c_ < N) ? (r_ * ldc + c_) * 2 : (int)0x80000000;       \
+                const int off_ = (r_ < M && c_ < N && !(GEMM_ABL & 4)) ? (r_ * ldc + c_) * 2 : (int)0x80000000; \
                 __builtin_amdgcn_raw_buffer_store_b128((u32x4v){s0_[0], s1_[0], s0_[1], s1_[1]},   \
                                                        crs, off_, 0, 2);                           \
             } else {                                                                               \
-                const int o0_ = (r_ < M && cb_ < N) ? (r_ * ldc + cb_) * 4 : (int)0x80000000;      \
-                const int o1_ = (r_ < M && cb_ + 16 < N) ? (r_ * ldc + cb_ + 16) * 4 : (int)0x80000000; \
+                const int o0_ = (r_ < M && cb_ < N && !(GEMM_ABL & 4)) ? (r_ * ldc + cb_) * 4 : (int)0x80000000; \
+                const int o1_ = (r_ < M && cb_ + 16 < N && !(GEMM_ABL & 4)) ? (r_ * ldc + cb_ + 16) * 4 : (int)0x80000000; \
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, x0), crs, o0_, 0, 2); \
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, x1), crs, o1_, 0, 2); \
             }                                                                                      \
