@@ -560,3 +560,31 @@ def test_match_features_on_f32_gemm(L, n_crops, n_cls):
     top2 = pd.topk(min(2, pd.shape[1]), dim=-1).values
     clear = (top2[:, 0] - top2[:, -1]) > 1e-3 if pd.shape[1] > 1 else torch.ones_like(mxd, dtype=torch.bool)
     assert torch.equal(idx[clear].cpu(), idxd[clear].cpu())
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_layernorm_forms_sweep(L, seed):
+    """bf_layernorm's forms on the path: row map (the window partition's scatter, < 0 skipped),
+    bf16 / f32 output, a strided input view, ragged M, and a large common offset (the variance
+    must not cancel) -- against torch's layer_norm in float64"""
+    rng = np.random.default_rng(200 + seed)
+    C = int([192, 256, 384, 512, 640, 768, 1024, 1280][seed])
+    M = int(rng.integers(1, 3000))
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    base = torch.randn(M, C + 64, device="cuda", generator=g) * 2.0 + (500.0 if seed % 2 else 0.0)
+    x = base[:, 32:32 + C]                          # row stride C + 64
+    w = torch.randn(C, device="cuda", generator=g)
+    b = torch.randn(C, device="cuda", generator=g)
+    ref = F.layer_norm(x.double(), (C,), w.double(), b.double(), 1e-6)
+    rows = M + 9
+    rm = torch.randperm(rows, device="cuda", generator=g)[:M].int()
+    rm[torch.rand(M, device="cuda", generator=g) < 0.1] = -1
+    for dt, tol in ((torch.bfloat16, 5e-3), (torch.float32, 1e-5)):
+        out = torch.zeros(rows, C, device="cuda", dtype=dt)
+        L.layernorm(x, w, b, 1e-6, out=out, row_map=rm)
+        torch.cuda.synchronize()
+        keep = rm >= 0
+        assert rel_err(out[rm[keep].long()], ref[keep]) < tol, (C, M, dt)
+        untouched = torch.ones(rows, dtype=torch.bool, device="cuda")
+        untouched[rm[keep].long()] = False
+        assert not out[untouched].float().abs().sum().item()
