@@ -471,3 +471,34 @@ def test_nms_scan_input_list_longer_than_capacity(L, n):
     keep, succ, events, counts = L.nms_scan(iou, corners, scores, init_id, poses, items, lens, vn, cfg)
     torch.cuda.synchronize()
     assert int(counts[3]) & L.BF_DEV_FUSION_LIST_OVERFLOW
+
+
+@pytest.mark.parametrize("n_glo,n_new", [(1, 0), (0, 1), (1, 1), (2, 1), (94, 1), (95, 1), (96, 1), (90, 7)])
+def test_nms_scan_small_and_boundary_vs_oracle(L, n_glo, n_new):
+    """the IoU matrix + greedy scan at the smallest counts and around the 96-box switch between
+    the one-wave scan and the block scan: bit-exact against the oracle"""
+    from boxfusion_amd.synthetic import Scene
+    rng = np.random.default_rng(1000 + 17 * n_glo + n_new)
+    n = n_glo + n_new
+    centres = rng.uniform(-2.0, 2.0, (max(1, n // 3), 3))
+    xyz = centres[rng.integers(0, len(centres), n)] + rng.normal(0, 0.04, (n, 3))
+    b = np.concatenate([xyz, rng.uniform(0.2, 0.9, (n, 3))], 1).astype(np.float32)
+    yaw = rng.uniform(-0.2, 0.2, n)
+    R = np.stack([[[np.cos(a), -np.sin(a), 0], [np.sin(a), np.cos(a), 0], [0, 0, 1]]
+                  for a in yaw]).astype(np.float32)
+    corners = OR.box_corners(b, R)
+    scores = rng.permutation(np.linspace(0.3, 0.99, n)).astype(np.float32)
+    init_id = np.arange(n, dtype=np.int32)
+    scene = Scene(seed=2)
+    cam_poses = np.stack([scene.pose(int(f)) for f in rng.integers(0, 1000, n)]).astype(np.float32)
+    fusion_list = [sorted(set([i] + rng.integers(0, max(1, n_glo), rng.integers(0, 3)).tolist()))
+                   if i < n_glo else [i] for i in range(n)]
+    valid_num = rng.integers(0, 3, n).astype(np.float32)
+    iou = L.obb_iou_matrix(_t(corners)).cpu().numpy()
+    np.testing.assert_array_equal(iou, OR.obb_iou_matrix(corners))
+    got = HipBackend(L).nms(iou, corners, scores, init_id, cam_poses, fusion_list, valid_num)
+    ref = OR.nms_scan(iou, corners, scores, init_id, cam_poses, fusion_list, valid_num, nms_cfg(L))
+    assert ref["status"] == 0
+    for k in ("keep", "success", "events", "valid_num"):
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    assert got["fusion_list"] == ref["fusion_list"]
