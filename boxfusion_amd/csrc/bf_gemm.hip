@@ -885,6 +885,15 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256p(const u16* __restric
 // in the Infinity Cache).
 // ------------------------------------------------------------------------------------------
 #define G2Q_BIAS_MAX 8192
+#ifndef GEMM_STAMP        // diagnostic builds only: per-workgroup s_memtime / s_memrealtime stamps of k_gemm256q
+#define GEMM_STAMP 0
+#endif
+#if GEMM_STAMP
+__device__ unsigned long long g_gemm_stamps[4096 * 4];
+BF_API int bf_gemm_read_stamps(unsigned long long* host, int n) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_stamps), (size_t)n * 4 * sizeof(unsigned long long));
+}
+#endif
 #ifndef GEMM_ABL          // diagnostic builds only (wrong results): 1 no K-loop LDS-DMA, 2 no fragment reads,
                           // 4 k_gemm256q epilogue stores dropped (out-of-range offsets: same vmcnt counts)
 #define GEMM_ABL 0
@@ -938,6 +947,10 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
     const int nk = K / KTE;
     const int total = my_tiles * nk;
     if (total == 0) return;
+#if GEMM_STAMP
+    unsigned long long st_t0 = 0, st_r0 = 0;
+    if (t == 0) { st_t0 = __builtin_amdgcn_s_memtime(); st_r0 = __builtin_amdgcn_s_memrealtime(); }
+#endif
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
 
     // bias row -> LDS (retired with K-tile 0 by the prologue's counted wait)
@@ -1244,6 +1257,13 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
     QEPI(1, 0, em0, en0);          // the last tile's Q10
     if (stagger && wr == 0) PHASE_BARRIER();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if GEMM_STAMP
+    if (t == 0 && blockIdx.x < 4096) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        volatile unsigned long long* d = g_gemm_stamps + blockIdx.x * 4;
+        d[0] = st_t0; d[1] = t1; d[2] = st_r0; d[3] = r1;
+    }
+#endif
 #undef RD_A
 #undef RD_B
 #undef LDS16
