@@ -161,8 +161,16 @@ __device__ __forceinline__ void attn2_softmax(f32x16 (&s)[2], bool sub1, bool ma
 // body, tiles past the workgroup's last query are skipped (sq == sk)
 // LSTQ: output rows staged through LDS and stored as whole head rows (the default for non-causal
 // launches; LSTQ = false keeps the per-lane fragment stores)
+// The D = 64 4-wave form (CuTR's windows and global blocks, the text tower) is held to 3 waves per
+// SIMD (163 registers instead of 200 and 64 AGPRs, no spills): 3 workgroups per CU instead of 2
+// take 15-18 % off its shapes (joint windows 105.5-110 -> 86.5-89.8 us, global 97.6-100.5 ->
+// 84.3-84.5; scripts/probe/attn_cutr_probe.py, profiles/r05_attn_cutr_probe.log).  4 waves per
+// SIMD (<= 128 registers) is out of the allocator's reach.  ATTN_WPE64 = 1 rebuilds the old form.
+#ifndef ATTN_WPE64
+#define ATTN_WPE64 3
+#endif
 template <int D, int NW, bool F8O = false, bool CAUSAL = false, bool LSTQ = false>
-__global__ void __launch_bounds__(NW * 64, 1) k_attn2(const u16* __restrict__ Q, const u16* __restrict__ K,
+__global__ void __launch_bounds__(NW * 64, (D == 64 && NW == 4) ? ATTN_WPE64 : 1) k_attn2(const u16* __restrict__ Q, const u16* __restrict__ K,
                                                       const u16* __restrict__ V, u16* __restrict__ O,
                                                       int sq, int sk, int q_rs, int k_rs, int v_rs,
                                                       int o_rs, long long q_bs, long long k_bs,
@@ -184,12 +192,12 @@ __global__ void __launch_bounds__(NW * 64, 1) k_attn2(const u16* __restrict__ Q,
     // LST (the default for one-workgroup short heads): the bf16 output rows go through a per-wave
     // LDS region of their own and leave as whole 2D-byte head rows (16 B per lane along the row)
     // instead of 8-byte fragments of 32 rows per store instruction (CLIP: 122.8 -> 115.8 us)
-    // (9-wave workgroups: an LDS region of their own, free at one workgroup per CU; 4-wave ones
+    // (8- and 9-wave workgroups: an LDS region of their own, free at one workgroup per CU; 4-wave ones
     // reuse the K ring after a barrier, so their occupancy is unchanged)
     constexpr bool LST = LSTQ && !CAUSAL && D % 16 == 0;
     constexpr int EB = F8O ? 1 : 2;                                 // output bytes per element
     constexpr int OROW = ((EB * D + 16) / 32) * 32 + 16;           // bytes per staged row (16-B aligned)
-    constexpr bool OWN = NW == 9;
+    constexpr bool OWN = NW >= 8;
     static_assert(!LST || OWN || NW * 32 * OROW <= NBUF * KTILE * 2, "staged rows fit the K ring");
     __shared__ __attribute__((aligned(16))) unsigned char sO[LST && OWN ? NW * 32 * OROW : 16];
 
@@ -417,7 +425,9 @@ __global__ void __launch_bounds__(NW * 64, 1) k_attn2(const u16* __restrict__ Q,
     }
 }
 // 6 (default): k_attn2 with the LDS-staged whole-row output stores for non-causal launches;
-// 27: the same kernel with the per-lane fragment stores (A/B reference; bit-identical).
+// 27: the same kernel with the per-lane fragment stores (A/B reference; bit-identical);
+// 28 / 29 / 30: 129-256 queries on 9 / 4 / 8 waves for every head dim (A/B references;
+// bit-identical).
 // Env BF_ATTN_VARIANT.
 static int g_attn_variant = [] {
     const char* e = getenv("BF_ATTN_VARIANT");
@@ -439,6 +449,15 @@ BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, v
     const int nw_one = (sq + 31) / 32;
     const bool short_s = nw_one > 4 && nw_one <= 9;
     const bool lst = g_attn_variant != 27;
+    // 129-256 queries (CuTR's rgb-only and last-depth windows: 256): a ninth wave would hold no
+    // query.  D = 64 takes 4-wave workgroups of 128 queries (3 per CU at the form's 3 waves per SIMD:
+    // rgb windows 37.3 -> 28.2 us against 8 waves, last-depth 55.8 -> 43.7), other head dims 8
+    // waves (profiles/r05_attn_cutr_probe.log).  Variants 28 / 29 / 30: 9 / 4 / 8 waves for every D
+    // (A/B references; every form gives the same bits).
+    const int mid = g_attn_variant == 28 ? 9 : g_attn_variant == 29 ? 4 : g_attn_variant == 30 ? 8
+                  : head_dim == 64 ? 4 : 8;
+    const bool eight = short_s && nw_one <= 8 && mid == 8;
+    const bool nine = short_s && (nw_one == 9 || mid == 9);
     const hipStream_t st = bf_stream(stream);
 #define LAUNCH_2(DD, NWV, LS)                                                                     \
     hipLaunchKernelGGL((k_attn2<DD, NWV, false, false, LS>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch), \
@@ -446,7 +465,8 @@ BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, v
                        q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs, o_bs, sl2, o_map, 1.f)
 #define LAUNCH_2D(DD)                                                                             \
     if (nw_one <= 2) { LAUNCH_2(DD, 2, false); }                                                  \
-    else if (short_s) { if (lst) { LAUNCH_2(DD, 9, true); } else { LAUNCH_2(DD, 9, false); } }    \
+    else if (eight) { if (lst) { LAUNCH_2(DD, 8, true); } else { LAUNCH_2(DD, 8, false); } }      \
+    else if (nine) { if (lst) { LAUNCH_2(DD, 9, true); } else { LAUNCH_2(DD, 9, false); } }       \
     else { if (lst) { LAUNCH_2(DD, 4, true); } else { LAUNCH_2(DD, 4, false); } }
     switch (head_dim) {
         case 32: LAUNCH_2D(32); break;
