@@ -169,8 +169,16 @@ __device__ __forceinline__ void attn2_softmax(f32x16 (&s)[2], bool sub1, bool ma
 #ifndef ATTN_WPE64
 #define ATTN_WPE64 3
 #endif
+// The D = 80 4-wave form (CLIP's 257-query heads as three workgroups of 128 / 128 / 1 queries, the
+// last one's three empty waves skipping the MFMA work) takes the same bound (166-168 registers
+// instead of 248): 112.8-116.0 vs 117.6-118.7 us for the 9-wave form; 140 us without the bound.
+// Not the causal instantiation (it spills at 168).
+#ifndef ATTN_WPE80
+#define ATTN_WPE80 3
+#endif
 template <int D, int NW, bool F8O = false, bool CAUSAL = false, bool LSTQ = false>
-__global__ void __launch_bounds__(NW * 64, (D == 64 && NW == 4) ? ATTN_WPE64 : 1) k_attn2(const u16* __restrict__ Q, const u16* __restrict__ K,
+__global__ void __launch_bounds__(NW * 64, (D == 64 && NW == 4) ? ATTN_WPE64 : (D == 80 && NW == 4 && !CAUSAL) ? ATTN_WPE80 : 1)
+k_attn2(const u16* __restrict__ Q, const u16* __restrict__ K,
                                                       const u16* __restrict__ V, u16* __restrict__ O,
                                                       int sq, int sk, int q_rs, int k_rs, int v_rs,
                                                       int o_rs, long long q_bs, long long k_bs,
@@ -206,6 +214,9 @@ __global__ void __launch_bounds__(NW * 64, (D == 64 && NW == 4) ? ATTN_WPE64 : 1
     const int h = blk.h, b = blk.b;
     const int fr = lane & 31, fh = lane >> 5;
     const int q = blk.qb * (NW * 32) + wave * 32 + fr;
+    // a wave whose 32 queries all lie past sq (the last query tile of a head) stages K / V and
+    // meets every barrier but skips the MFMA / softmax work (wave-uniform)
+    const bool idle = blk.qb * (NW * 32) + wave * 32 >= sq;
     const u16* Qb = Q + b * q_bs + h * D;
     const u16* Kb = K + b * k_bs + h * D;
     const u16* Vb = V + b * v_bs + h * D;
@@ -332,11 +343,11 @@ __global__ void __launch_bounds__(NW * 64, (D == 64 && NW == 4) ? ATTN_WPE64 : 1
         for (int tile = 0; tile < nfull; ++tile) {
             const bool more = tile + 1 < ntiles;
             if (more) stage_load((tile + 1) * AT_KT);          // in flight during this tile
-            tile_body(tile, std::false_type{});
+            if (!idle) tile_body(tile, std::false_type{});
             if (more) stage_store((tile + 1) % NBUF);
             __syncthreads();
         }
-        if (nfull < ntiles) tile_body(nfull, std::true_type{});
+        if (nfull < ntiles && !idle) tile_body(nfull, std::true_type{});
     }
     // row sum: the ones row D of O^T (lane half 0, register 8 of block D / 32) or the f32 sum
     float l;
@@ -353,6 +364,7 @@ __global__ void __launch_bounds__(NW * 64, (D == 64 && NW == 4) ? ATTN_WPE64 : 1
     if constexpr (LST) {
         const float inv = 1.0f / l;
         if constexpr (!OWN) __syncthreads();                 // every wave is done with the K ring
+        if (idle) return;
         unsigned char* wreg = (OWN ? sO : reinterpret_cast<unsigned char*>(sK)) + wave * 32 * OROW;
 #pragma unroll
         for (int db = 0; db < DB; ++db)
@@ -426,8 +438,8 @@ __global__ void __launch_bounds__(NW * 64, (D == 64 && NW == 4) ? ATTN_WPE64 : 1
 }
 // 6 (default): k_attn2 with the LDS-staged whole-row output stores for non-causal launches;
 // 27: the same kernel with the per-lane fragment stores (A/B reference; bit-identical);
-// 28 / 29 / 30: 129-256 queries on 9 / 4 / 8 waves for every head dim (A/B references;
-// bit-identical).
+// 28: 129-288 queries on 9 waves (the round-4 dispatch), 29 / 30: 129-256 queries on 4 / 8
+// waves, 31: 129-288 on 4 waves, for every head dim (A/B references; bit-identical).
 // Env BF_ATTN_VARIANT.
 static int g_attn_variant = [] {
     const char* e = getenv("BF_ATTN_VARIANT");
@@ -454,10 +466,14 @@ BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, v
     // rgb windows 37.3 -> 28.2 us against 8 waves, last-depth 55.8 -> 43.7), other head dims 8
     // waves (profiles/r05_attn_cutr_probe.log).  Variants 28 / 29 / 30: 9 / 4 / 8 waves for every D
     // (A/B references; every form gives the same bits).
+    // 257-288 queries (CLIP: 257): 9 waves, at D = 80 4-wave workgroups (ATTN_WPE80 above).
+    // Variant 28 restores 9 waves for all of 129-288, 31 takes 4 waves for all of it.
     const int mid = g_attn_variant == 28 ? 9 : g_attn_variant == 29 ? 4 : g_attn_variant == 30 ? 8
                   : head_dim == 64 ? 4 : 8;
-    const bool eight = short_s && nw_one <= 8 && mid == 8;
-    const bool nine = short_s && (nw_one == 9 || mid == 9);
+    const bool four_all = g_attn_variant == 31;
+    const int top = g_attn_variant == 28 ? 9 : (four_all || head_dim == 80) ? 4 : 9;
+    const bool eight = short_s && nw_one <= 8 && mid == 8 && !four_all;
+    const bool nine = short_s && !four_all && (nw_one <= 8 ? mid == 9 : top == 9);
     const hipStream_t st = bf_stream(stream);
 #define LAUNCH_2(DD, NWV, LS)                                                                     \
     hipLaunchKernelGGL((k_attn2<DD, NWV, false, false, LS>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch), \
@@ -505,8 +521,10 @@ BF_API int bf_attention_fp8out(const void* q, const void* k, const void* v, void
     hipLaunchKernelGGL((k_attn2<DD, NWV, true, false, LS>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch), \
                        dim3(NWV * 64), 0, st, (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, sq, sk, \
                        q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs, o_bs, sl2, (const int32_t*)nullptr, out_qscale)
+    // 257-288 queries at D = 80 (CLIP) on 4-wave workgroups as in bf_attention_bf16 (variant 28: 9)
+    const bool nine = nw_one > 4 && nw_one <= 9 && !(head_dim == 80 && nw_one == 9 && g_attn_variant != 28);
 #define LAUNCH_8D(DD)                                                                             \
-    if (nw_one > 4 && nw_one <= 9) { if (lst) { LAUNCH_8(DD, 9, true); } else { LAUNCH_8(DD, 9, false); } } \
+    if (nine) { if (lst) { LAUNCH_8(DD, 9, true); } else { LAUNCH_8(DD, 9, false); } }             \
     else { if (lst) { LAUNCH_8(DD, 4, true); } else { LAUNCH_8(DD, 4, false); } }
     switch (head_dim) {
         case 64: LAUNCH_8D(64); break;

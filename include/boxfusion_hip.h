@@ -428,11 +428,11 @@ int bf_attention_fp8out(const void* q, const void* k, const void* v, void* o, in
                         long long q_bs, long long k_bs, long long v_bs, long long o_bs, float scale,
                         float out_qscale, void* stream);
 /* Attention kernel variant (test/benchmark hook; env BF_ATTN_VARIANT): 6 (default) = k_attn2
- * (deferred-max softmax, row sums from a ones row of V on the MFMA, 9-wave workgroups for
- * 257-288 queries, 129-256 queries on 4-wave workgroups at head dim 64 and 8-wave ones otherwise,
- * output rows staged in LDS and stored as whole head rows), 27 = the same kernel with per-lane
- * fragment stores, 28 / 29 / 30 = 129-256 queries on 9 / 4 / 8 waves for every head dim (all
- * bit-identical). */
+ * (deferred-max softmax, row sums from a ones row of V on the MFMA; 257-288 queries on 9-wave
+ * workgroups, at head dim 80 on 4-wave ones; 129-256 queries on 4-wave workgroups at head dim 64
+ * and 8-wave ones otherwise; output rows staged in LDS and stored as whole head rows), 27 = the
+ * same kernel with per-lane fragment stores, 28 = 129-288 queries on 9 waves, 29 / 30 = 129-256
+ * queries on 4 / 8 waves, 31 = 129-288 queries on 4 waves, for every head dim (all bit-identical). */
 void bf_attention_set_variant(int v);
 
 /* CuTR decoder cross-attention bias (GlobalCrossAttention.rpe + the logits' bias / clip /

@@ -1,10 +1,11 @@
 """CuTR / CLIP attention shapes: the shipped dispatch (129-256 queries: 4-wave workgroups at D = 64,
-8 waves otherwise) against variants 28 / 29 / 30 (those queries on 9 / 4 / 8 waves for every head
-dim), bit-identity checked; and --
-through BF_LIB_PATH -- a build with -DATTN_WPE64=1 (k_attn2<64, 4> at 200 registers and 2 waves per
-SIMD instead of the shipped 163 and 3):
+8 waves otherwise; 257-288: 4-wave workgroups at D = 80, 9 waves otherwise) against variants 28
+(129-288 queries on 9 waves: the round-4 dispatch), 29 / 30 (129-256 on 4 / 8 waves) and 31
+(129-288 on 4 waves), bit-identity checked; and -- through BF_LIB_PATH -- a build with
+-DATTN_WPE64=1 -DATTN_WPE80=1 (the 4-wave forms at 200 / 248 registers and 2 waves per SIMD
+instead of the shipped 159-168 and 3):
   cd boxfusion_amd && mkdir -p _build/variant &&
-  hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Icsrc -c csrc/bf_attn.hip -o _build/variant/bf_attn_wpe1.o -DATTN_WPE64=1 &&
+  hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Icsrc -c csrc/bf_attn.hip -o _build/variant/bf_attn_wpe1.o -DATTN_WPE64=1 -DATTN_WPE80=1 &&
   hipcc --offload-arch=gfx950 -shared -fPIC -o _build/variant/lib_wpe1.so $(ls _build/*.o | grep -v /bf_attn.o) _build/variant/bf_attn_wpe1.o
 Shapes as engine.py launches them for configs[2] (8 frames of 640x480 -> 40 x 40 tokens, 16 x 16
 windows padded to 48 x 48: 72 windows; ViT-B 12 heads of 64; CLIP 128 crops, 16 heads of 80)."""
@@ -33,7 +34,7 @@ for name, B, H, sq, sk, D in SHAPES:
     f = lambda: _lib.attention(q, k, v, o, B, H, sq, sk, D, D ** -0.5, q_bs=sk * rs, k_bs=sk * rs, v_bs=sk * rs,
                                o_bs=sq * C)
     res = {}
-    for var in (6, 28, 29, 30):
+    for var in (6, 28, 29, 30, 31):
         L.bf_attention_set_variant(var)
         f()
         torch.cuda.synchronize()
@@ -49,8 +50,8 @@ for name, B, H, sq, sk, D in SHAPES:
             best.append(s.elapsed_time(e) / 20 * 1e3)
         res[var] = (min(best), ref)
     L.bf_attention_set_variant(6)
-    same = all(torch.equal(res[6][1], res[v][1]) for v in (28, 29, 30))
+    same = all(torch.equal(res[6][1], res[v][1]) for v in (28, 29, 30, 31))
     fl = 4.0 * B * H * sq * sk * D
     print(f"{name:24s} {os.path.basename(os.environ.get('BF_LIB_PATH', 'in-tree')):12s} default {res[6][0]:7.1f} us "
-          f"({fl / res[6][0] / 1e6:5.0f} TF/s)  9-wave {res[28][0]:7.1f} us  4-wave {res[29][0]:7.1f} us  8-wave {res[30][0]:7.1f} us  "
+          f"({fl / res[6][0] / 1e6:5.0f} TF/s)  r4 9-wave {res[28][0]:7.1f} us  4-wave {res[29][0]:7.1f} us  8-wave {res[30][0]:7.1f} us  4-wave incl. 257-288 {res[31][0]:7.1f} us  "
           f"bit-identical {same}", flush=True)
