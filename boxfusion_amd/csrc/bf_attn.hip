@@ -462,14 +462,15 @@ BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, v
     const bool short_s = nw_one > 4 && nw_one <= 9;
     const bool lst = g_attn_variant != 27;
     // 129-256 queries (CuTR's rgb-only and last-depth windows: 256): a ninth wave would hold no
-    // query.  D = 64 takes 4-wave workgroups of 128 queries (3 per CU at the form's 3 waves per SIMD:
-    // rgb windows 37.3 -> 28.2 us against 8 waves, last-depth 55.8 -> 43.7), other head dims 8
-    // waves (profiles/r05_attn_cutr_probe.log).  Variants 28 / 29 / 30: 9 / 4 / 8 waves for every D
-    // (A/B references; every form gives the same bits).
+    // query.  D = 64 and 80 take 4-wave workgroups of 128 queries (3 per CU at the forms' 3 waves
+    // per SIMD: rgb windows 37.3 -> 28.2 us against 8 waves, last-depth 55.8 -> 43.7, CLIP-shaped
+    // 256-query heads 108 -> 92), other head dims 8 waves (profiles/r05_attn_cutr_probe.log).
+    // Variants 28 / 29 / 30: 9 / 4 / 8 waves for every D (A/B references; every form gives the same
+    // bits).
     // 257-288 queries (CLIP: 257): 9 waves, at D = 80 4-wave workgroups (ATTN_WPE80 above).
     // Variant 28 restores 9 waves for all of 129-288, 31 takes 4 waves for all of it.
     const int mid = g_attn_variant == 28 ? 9 : g_attn_variant == 29 ? 4 : g_attn_variant == 30 ? 8
-                  : head_dim == 64 ? 4 : 8;
+                  : (head_dim == 64 || head_dim == 80) ? 4 : 8;
     const bool four_all = g_attn_variant == 31;
     const int top = g_attn_variant == 28 ? 9 : (four_all || head_dim == 80) ? 4 : 9;
     const bool eight = short_s && nw_one <= 8 && mid == 8 && !four_all;

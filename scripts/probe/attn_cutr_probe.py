@@ -24,7 +24,7 @@ L = _lib.lib()
 torch.manual_seed(0)
 SHAPES = (("cutr joint window", 72, 12, 512, 512, 64), ("cutr rgb window", 72, 12, 256, 256, 64),
           ("cutr last-depth window", 72, 12, 256, 512, 64), ("cutr global", 8, 12, 1600, 1600, 64),
-          ("clip", 128, 16, 257, 257, 80))
+          ("clip", 128, 16, 257, 257, 80), ("clip without query 256", 128, 16, 256, 257, 80))
 for name, B, H, sq, sk, D in SHAPES:
     C = H * D
     qkv = (torch.randn(B * sk, 3 * C, device="cuda") * 0.5).bfloat16()

@@ -1,7 +1,7 @@
 """Seeded random sweep of the attention entry points against torch SDPA in fp32: every dispatch
 branch of bf_attention_bf16 (2-wave workgroups for <= 64 queries, 9-wave one-workgroup heads for
-257..288 queries (4-wave tiles at head dim 80), 8-wave ones (4-wave tiles at head dim 64) for
-129..256, 4-wave 128-query tiles otherwise), head dims 32 / 64 / 80 / 128, sk != sq and ragged
+257..288 queries (4-wave tiles at head dim 80), 8-wave ones (4-wave tiles at head dims 64 and 80)
+for 129..256, 4-wave 128-query tiles otherwise), head dims 32 / 64 / 80 / 128, sk != sq and ragged
 lengths (the masked tail tile), an output row map, the fp8 output and the causal form; and the
 bit-identity of the 4 / 8 / 9-wave forms of the 129..288-query range."""
 import math
