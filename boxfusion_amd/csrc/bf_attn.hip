@@ -439,7 +439,8 @@ k_attn2(const u16* __restrict__ Q, const u16* __restrict__ K,
 // 6 (default): k_attn2 with the LDS-staged whole-row output stores for non-causal launches;
 // 27: the same kernel with the per-lane fragment stores (A/B reference; bit-identical);
 // 28: 129-288 queries on 9 waves (the round-4 dispatch), 29 / 30: 129-256 queries on 4 / 8
-// waves, 31: 129-288 on 4 waves, for every head dim (A/B references; bit-identical).
+// waves, 31: 129-288 on 4 waves, for every head dim; 33: 449-512 queries at D = 64 on 4 waves
+// (A/B references; bit-identical).
 // Env BF_ATTN_VARIANT.
 static int g_attn_variant = [] {
     const char* e = getenv("BF_ATTN_VARIANT");
@@ -475,6 +476,11 @@ BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, v
     const int top = g_attn_variant == 28 ? 9 : (four_all || head_dim == 80) ? 4 : 9;
     const bool eight = short_s && nw_one <= 8 && mid == 8 && !four_all;
     const bool nine = short_s && !four_all && (nw_one <= 8 ? mid == 9 : top == 9);
+    // 449-512 queries at D = 64 (CuTR's joint windows: 512) on two 8-wave workgroups per head
+    // instead of four 4-wave ones: K / V staged twice instead of four times, 76.9-79.0 vs 86.3-89.8
+    // us (the 1600-token global blocks and the 256-query windows are faster on 4 waves).  Variant
+    // 33: the 4-wave form (A/B; the same bits).
+    const bool wide8 = head_dim == 64 && sq > 448 && sq <= 512 && g_attn_variant != 33;
     const hipStream_t st = bf_stream(stream);
 #define LAUNCH_2(DD, NWV, LS)                                                                     \
     hipLaunchKernelGGL((k_attn2<DD, NWV, false, false, LS>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch), \
@@ -484,6 +490,7 @@ BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, v
     if (nw_one <= 2) { LAUNCH_2(DD, 2, false); }                                                  \
     else if (eight) { if (lst) { LAUNCH_2(DD, 8, true); } else { LAUNCH_2(DD, 8, false); } }      \
     else if (nine) { if (lst) { LAUNCH_2(DD, 9, true); } else { LAUNCH_2(DD, 9, false); } }       \
+    else if (wide8) { if (lst) { LAUNCH_2(DD, 8, true); } else { LAUNCH_2(DD, 8, false); } }      \
     else { if (lst) { LAUNCH_2(DD, 4, true); } else { LAUNCH_2(DD, 4, false); } }
     switch (head_dim) {
         case 32: LAUNCH_2D(32); break;

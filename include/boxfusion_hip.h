@@ -430,9 +430,10 @@ int bf_attention_fp8out(const void* q, const void* k, const void* v, void* o, in
 /* Attention kernel variant (test/benchmark hook; env BF_ATTN_VARIANT): 6 (default) = k_attn2
  * (deferred-max softmax, row sums from a ones row of V on the MFMA; 257-288 queries on 9-wave
  * workgroups, at head dim 80 on 4-wave ones; 129-256 queries on 4-wave workgroups at head dims 64
- * and 80 and 8-wave ones otherwise; output rows staged in LDS and stored as whole head rows), 27 = the
+ * and 80 and 8-wave ones otherwise; 449-512 queries at head dim 64 on 8-wave workgroups; output rows staged in LDS and stored as whole head rows), 27 = the
  * same kernel with per-lane fragment stores, 28 = 129-288 queries on 9 waves, 29 / 30 = 129-256
- * queries on 4 / 8 waves, 31 = 129-288 queries on 4 waves, for every head dim (all bit-identical). */
+ * queries on 4 / 8 waves, 31 = 129-288 queries on 4 waves, for every head dim, 33 = 449-512 queries
+ * at head dim 64 on 4 waves (all bit-identical). */
 void bf_attention_set_variant(int v);
 
 /* CuTR decoder cross-attention bias (GlobalCrossAttention.rpe + the logits' bias / clip /

@@ -1,7 +1,8 @@
 """CuTR / CLIP attention shapes: the shipped dispatch (129-256 queries: 4-wave workgroups at D = 64,
-8 waves otherwise; 257-288: 4-wave workgroups at D = 80, 9 waves otherwise) against variants 28
-(129-288 queries on 9 waves: the round-4 dispatch), 29 / 30 (129-256 on 4 / 8 waves) and 31
-(129-288 on 4 waves), bit-identity checked; and -- through BF_LIB_PATH -- a build with
+8 waves otherwise; 257-288: 4-wave workgroups at D = 80, 9 waves otherwise; 449-512 at D = 64: 8
+waves) against variants 28 (129-288 queries on 9 waves: the round-4 dispatch), 29 / 30 (129-256
+on 4 / 8 waves), 31 (129-288 on 4 waves) and 33 (449-512 at D = 64 on 4 waves), bit-identity
+checked; and -- through BF_LIB_PATH -- a build with
 -DATTN_WPE64=1 -DATTN_WPE80=1 (the 4-wave forms at 200 / 248 registers and 2 waves per SIMD
 instead of the shipped 159-168 and 3):
   cd boxfusion_amd && mkdir -p _build/variant &&
@@ -34,24 +35,26 @@ for name, B, H, sq, sk, D in SHAPES:
     f = lambda: _lib.attention(q, k, v, o, B, H, sq, sk, D, D ** -0.5, q_bs=sk * rs, k_bs=sk * rs, v_bs=sk * rs,
                                o_bs=sq * C)
     res = {}
-    for var in (6, 28, 29, 30, 31):
-        L.bf_attention_set_variant(var)
+    VARS = (6, 28, 29, 30, 31, 33)
+    for _ in range(30):                       # warm the clocks before the first timed variant
         f()
-        torch.cuda.synchronize()
-        ref = o.clone()
-        best = []
-        for rep in range(3):
+    for rep in range(4):                      # variants interleaved, best of 4 rounds each
+        for var in VARS if rep % 2 == 0 else VARS[::-1]:
+            L.bf_attention_set_variant(var)
+            f()
+            torch.cuda.synchronize()
+            if rep == 0:
+                res[var] = [float("inf"), o.clone()]
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             for _ in range(20):
                 f()
             e.record()
             torch.cuda.synchronize()
-            best.append(s.elapsed_time(e) / 20 * 1e3)
-        res[var] = (min(best), ref)
+            res[var][0] = min(res[var][0], s.elapsed_time(e) / 20 * 1e3)
     L.bf_attention_set_variant(6)
-    same = all(torch.equal(res[6][1], res[v][1]) for v in (28, 29, 30, 31))
+    same = all(torch.equal(res[6][1], res[v][1]) for v in VARS[1:])
     fl = 4.0 * B * H * sq * sk * D
     print(f"{name:24s} {os.path.basename(os.environ.get('BF_LIB_PATH', 'in-tree')):12s} default {res[6][0]:7.1f} us "
-          f"({fl / res[6][0] / 1e6:5.0f} TF/s)  r4 9-wave {res[28][0]:7.1f} us  4-wave {res[29][0]:7.1f} us  8-wave {res[30][0]:7.1f} us  4-wave incl. 257-288 {res[31][0]:7.1f} us  "
+          f"({fl / res[6][0] / 1e6:5.0f} TF/s)  r4 9-wave {res[28][0]:7.1f} us  4-wave {res[29][0]:7.1f} us  8-wave {res[30][0]:7.1f} us  4-wave incl. 257-288 {res[31][0]:7.1f} us  D64 449-512 on 4 {res[33][0]:7.1f} us  "
           f"bit-identical {same}", flush=True)

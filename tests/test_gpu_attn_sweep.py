@@ -1,7 +1,8 @@
 """Seeded random sweep of the attention entry points against torch SDPA in fp32: every dispatch
 branch of bf_attention_bf16 (2-wave workgroups for <= 64 queries, 9-wave one-workgroup heads for
 257..288 queries (4-wave tiles at head dim 80), 8-wave ones (4-wave tiles at head dims 64 and 80)
-for 129..256, 4-wave 128-query tiles otherwise), head dims 32 / 64 / 80 / 128, sk != sq and ragged
+for 129..256, 8-wave 256-query tiles for 449..512 at head dim 64, 4-wave 128-query tiles
+otherwise), head dims 32 / 64 / 80 / 128, sk != sq and ragged
 lengths (the masked tail tile), an output row map, the fp8 output and the causal form; and the
 bit-identity of the 4 / 8 / 9-wave forms of the 129..288-query range."""
 import math
@@ -108,17 +109,18 @@ def test_attention_fp8out_and_causal_sweep(L, seed):
 
 
 @pytest.mark.parametrize("D,sq,sk", [(64, 256, 256), (64, 256, 512), (80, 200, 333), (32, 129, 129),
-                                     (64, 161, 70), (80, 257, 257), (64, 270, 300), (80, 288, 100)])
+                                     (64, 161, 70), (80, 257, 257), (64, 270, 300), (80, 288, 100),
+                                     (64, 512, 512), (64, 470, 600)])
 def test_attention_workgroup_forms_bit_identical(L, D, sq, sk):
-    """129..288 queries run on 4-, 8- or 9-wave workgroups (bf_attention_set_variant 28 / 29 / 30 /
-    31; the default picks by head dim and query count; a 4-wave tile's empty waves skip the MFMA
+    """129..288 queries (and 449..512 at head dim 64) run on 4-, 8- or 9-wave workgroups
+    (bf_attention_set_variant 28 / 29 / 30 / 31 / 33; the default picks by head dim and query count; a 4-wave tile's empty waves skip the MFMA
     work): every query's key order and tile order is the same, so every form gives the same bits"""
     B, H = 3, 4
     g = torch.Generator(device="cuda").manual_seed(D * 7 + sq + sk)
     q, k, v = _qkv(B, H, sq, sk, D, g, 3.0)
     outs = []
     try:
-        for var in (6, 28, 29, 30, 31):
+        for var in (6, 28, 29, 30, 31, 33):
             L.lib().bf_attention_set_variant(var)
             o = torch.zeros(B * sq, H * D, device="cuda", dtype=torch.bfloat16)
             L.attention(q, k, v, o, B, H, sq, sk, D, D ** -0.5)
