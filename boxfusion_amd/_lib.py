@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import atexit
 import ctypes
+import threading
 import weakref
 import sys
 import os
@@ -571,10 +572,56 @@ def backproject(depth, K, RT, max_depth=10.0):
 ACT = {None: 0, "none": 0, "gelu": 1, "relu": 2}
 
 
+class GemmPlan(ctypes.Structure):
+    """bf_gemm_plan: per-call GEMM options (include/boxfusion_hip.h); all-zero = product defaults"""
+    _fields_ = [("cu_budget", ctypes.c_int32), ("tile_rows", ctypes.c_int32), ("kernel", ctypes.c_int32),
+                ("variant", ctypes.c_int32), ("group_m", ctypes.c_int32), ("balanced", ctypes.c_int32)]
+
+
+# The CU budget a thread's GEMMs pass in their plan (0 = every CU).  Host-side, per thread: the C
+# library keeps no GEMM state; the thread that launches on a CU-masked detect stream sets it
+# (partition_streams), a fusion worker thread keeps 0.
+_TLS = threading.local()
+
+
+def set_cu_budget(n):
+    """CUs the calling thread's GEMMs size their persistent grid for (0 = all)"""
+    _TLS.cu_budget = max(int(n), 0)
+
+
+def cu_budget():
+    return getattr(_TLS, "cu_budget", 0)
+
+
+def set_knobs(**kw):
+    """measurement hooks for scripts/ (not used by the product path): per-thread defaults merged into
+    the bf_gemm_plan of every GEMM call made without a plan (GemmPlan field names) and into every
+    attention call made without a variant (attn_variant=...).  set_knobs() with no arguments clears
+    them."""
+    _TLS.knobs = {**getattr(_TLS, "knobs", {}), **kw} if kw else {}
+
+
+def _knobs():
+    return getattr(_TLS, "knobs", {})
+
+
+def _plan(plan):
+    if plan is None:
+        k = {f: v for f, v in _knobs().items() if f != "attn_variant"}
+        b = cu_budget()
+        if not b and not k:
+            return None
+        plan = GemmPlan(**{"cu_budget": b, **k})
+    elif isinstance(plan, dict):
+        plan = GemmPlan(**{"cu_budget": cu_budget(), **plan})
+    return ctypes.byref(plan)
+
+
 def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype=torch.bfloat16,
-         row_map=None, m=None):
+         row_map=None, m=None, plan=None):
     """out[orow(r)] = resid[...] + act(a @ w.T + bias); a bf16 [M,K] (row stride a.stride(0)),
-    w bf16 [N,K]. `out` may be given (its row stride is used)."""
+    w bf16 [N,K]. `out` may be given (its row stride is used).  plan: None (defaults + the
+    thread's CU budget), a GemmPlan or a dict of its fields (measurement hooks)."""
     _need(a, torch.bfloat16, "a")
     _need(w, torch.bfloat16, "w")
     M = a.shape[0] if m is None else m
@@ -590,20 +637,21 @@ def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype
         _need(bias, torch.float32, "bias")
     if a.stride(1) != 1 or w.stride(1) != 1 or out.stride(1) != 1:
         raise HipError("gemm operands need unit column stride")
-    _check(lib().bf_gemm_bf16(c_void_p(a.data_ptr()), c_int(a.stride(0)), c_void_p(w.data_ptr()),
-                              c_int(w.stride(0)), _ptr(bias) if bias is not None else None,
-                              c_void_p(resid.data_ptr()) if resid is not None else None,
-                              c_int(resid.stride(0) if resid is not None else 0), c_int(resid_mod),
-                              c_void_p(out.data_ptr()), c_int(out.stride(0)), c_int(c_bf16),
-                              _ptr(row_map) if row_map is not None else None, c_int(M), c_int(N),
-                              c_int(K), c_int(ACT[act]), _stream()), "bf_gemm_bf16")
+    _check(lib().bf_gemm_bf16_plan(c_void_p(a.data_ptr()), c_int(a.stride(0)), c_void_p(w.data_ptr()),
+                                   c_int(w.stride(0)), _ptr(bias) if bias is not None else None,
+                                   c_void_p(resid.data_ptr()) if resid is not None else None,
+                                   c_int(resid.stride(0) if resid is not None else 0), c_int(resid_mod),
+                                   c_void_p(out.data_ptr()), c_int(out.stride(0)), c_int(c_bf16),
+                                   _ptr(row_map) if row_map is not None else None, c_int(M), c_int(N),
+                                   c_int(K), c_int(ACT[act]), _plan(plan), _stream()), "bf_gemm_bf16")
     return out
 
 
 def attention(q, k, v, o, batch, heads, sq, sk, head_dim, scale, q_bs=None, k_bs=None, v_bs=None,
-              o_bs=None, o_map=None):
+              o_bs=None, o_map=None, variant=0):
     """q/k/v/o are 2-D token-major views [batch*S, >= heads*head_dim] (any row stride).
-    o_map: int32 [batch*sq] output row of each query (< 0: not stored)."""
+    o_map: int32 [batch*sq] output row of each query (< 0: not stored).  variant: the per-call
+    kernel-variant hook of bf_attention_bf16_ex (0 = default)."""
     for x, n in ((q, "q"), (k, "k"), (v, "v"), (o, "o")):
         _need(x, torch.bfloat16, n)
     q_bs = sq * q.stride(0) if q_bs is None else q_bs
@@ -615,18 +663,19 @@ def attention(q, k, v, o, batch, heads, sq, sk, head_dim, scale, q_bs=None, k_bs
         if o_map.numel() < batch * sq:
             raise HipError(f"o_map has {o_map.numel()} rows < batch*sq = {batch * sq}")
     LL = ctypes.c_longlong
-    _check(lib().bf_attention_bf16_omap(c_void_p(q.data_ptr()), c_void_p(k.data_ptr()),
-                                        c_void_p(v.data_ptr()), c_void_p(o.data_ptr()), c_int(batch),
-                                        c_int(heads), c_int(sq), c_int(sk), c_int(head_dim),
-                                        c_int(q.stride(0)), c_int(k.stride(0)), c_int(v.stride(0)),
-                                        c_int(o.stride(0)), LL(q_bs), LL(k_bs), LL(v_bs), LL(o_bs),
-                                        c_float(scale), _ptr(o_map) if o_map is not None else None,
-                                        _stream()), "bf_attention_bf16_omap")
+    _check(lib().bf_attention_bf16_ex(c_void_p(q.data_ptr()), c_void_p(k.data_ptr()),
+                                      c_void_p(v.data_ptr()), c_void_p(o.data_ptr()), c_int(batch),
+                                      c_int(heads), c_int(sq), c_int(sk), c_int(head_dim),
+                                      c_int(q.stride(0)), c_int(k.stride(0)), c_int(v.stride(0)),
+                                      c_int(o.stride(0)), LL(q_bs), LL(k_bs), LL(v_bs), LL(o_bs),
+                                      c_float(scale), _ptr(o_map) if o_map is not None else None,
+                                      c_int(variant or _knobs().get("attn_variant", 0)), _stream()),
+           "bf_attention_bf16_ex")
     return o
 
 
 def attention_fp8out(q, k, v, o, batch, heads, sq, sk, head_dim, scale, out_qscale, q_bs=None,
-                     k_bs=None, v_bs=None, o_bs=None):
+                     k_bs=None, v_bs=None, o_bs=None, variant=0):
     """attention() with an fp8 e4m3 output o = saturate(softmax(q k^T) v * out_qscale)"""
     for x, n in ((q, "q"), (k, "k"), (v, "v")):
         _need(x, torch.bfloat16, n)
@@ -636,12 +685,13 @@ def attention_fp8out(q, k, v, o, batch, heads, sq, sk, head_dim, scale, out_qsca
     v_bs = sk * v.stride(0) if v_bs is None else v_bs
     o_bs = sq * o.stride(0) if o_bs is None else o_bs
     LL = ctypes.c_longlong
-    _check(lib().bf_attention_fp8out(c_void_p(q.data_ptr()), c_void_p(k.data_ptr()), c_void_p(v.data_ptr()),
-                                     c_void_p(o.data_ptr()), c_int(batch), c_int(heads), c_int(sq),
-                                     c_int(sk), c_int(head_dim), c_int(q.stride(0)), c_int(k.stride(0)),
-                                     c_int(v.stride(0)), c_int(o.stride(0)), LL(q_bs), LL(k_bs), LL(v_bs),
-                                     LL(o_bs), c_float(scale), c_float(out_qscale), _stream()),
-           "bf_attention_fp8out")
+    _check(lib().bf_attention_fp8out_ex(c_void_p(q.data_ptr()), c_void_p(k.data_ptr()), c_void_p(v.data_ptr()),
+                                        c_void_p(o.data_ptr()), c_int(batch), c_int(heads), c_int(sq),
+                                        c_int(sk), c_int(head_dim), c_int(q.stride(0)), c_int(k.stride(0)),
+                                        c_int(v.stride(0)), c_int(o.stride(0)), LL(q_bs), LL(k_bs), LL(v_bs),
+                                        LL(o_bs), c_float(scale), c_float(out_qscale),
+                                        c_int(variant or _knobs().get("attn_variant", 0)), _stream()),
+           "bf_attention_fp8out_ex")
     return o
 
 
@@ -781,7 +831,7 @@ _FP8_OUT = {torch.float32: 0, torch.bfloat16: 1, FP8: 2}
 
 
 def gemm_fp8(a, w, scale, bias=None, act=None, resid=None, out=None, out_dtype=torch.bfloat16,
-             out_qscale=1.0):
+             out_qscale=1.0, plan=None):
     """out = resid + act(scale * (a @ w.T) + bias); a fp8 e4m3 [M,K], w fp8 [N,K] (per-tensor
     scales folded into `scale`); out f32 / bf16 / fp8 (fp8: saturate(value * out_qscale))."""
     _need(a, FP8, "a")
@@ -800,12 +850,13 @@ def gemm_fp8(a, w, scale, bias=None, act=None, resid=None, out=None, out_dtype=t
         _need(bias, torch.float32, "bias")
     if a.stride(1) != 1 or w.stride(1) != 1 or out.stride(1) != 1:
         raise HipError("gemm_fp8 operands need unit column stride")
-    _check(lib().bf_gemm_fp8(c_void_p(a.data_ptr()), c_int(a.stride(0)), c_void_p(w.data_ptr()),
-                             c_int(w.stride(0)), c_float(scale), _ptr(bias) if bias is not None else None,
-                             c_void_p(resid.data_ptr()) if resid is not None else None,
-                             c_int(resid.stride(0) if resid is not None else 0), c_void_p(out.data_ptr()),
-                             c_int(out.stride(0)), c_int(_FP8_OUT[out.dtype]), c_float(out_qscale),
-                             c_int(M), c_int(N), c_int(K), c_int(ACT[act]), _stream()), "bf_gemm_fp8")
+    _check(lib().bf_gemm_fp8_plan(c_void_p(a.data_ptr()), c_int(a.stride(0)), c_void_p(w.data_ptr()),
+                                  c_int(w.stride(0)), c_float(scale), _ptr(bias) if bias is not None else None,
+                                  c_void_p(resid.data_ptr()) if resid is not None else None,
+                                  c_int(resid.stride(0) if resid is not None else 0), c_void_p(out.data_ptr()),
+                                  c_int(out.stride(0)), c_int(_FP8_OUT[out.dtype]), c_float(out_qscale),
+                                  c_int(M), c_int(N), c_int(K), c_int(ACT[act]), _plan(plan), _stream()),
+           "bf_gemm_fp8")
     return out
 
 
@@ -941,10 +992,10 @@ _attention_fp8out_untimed = attention_fp8out
 
 
 def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype=torch.bfloat16,
-         row_map=None, m=None):
+         row_map=None, m=None, plan=None):
     t = _timer()
     if t is None:
-        return _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m)
+        return _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m, plan)
     M = a.shape[0] if m is None else m
     N, K = w.shape
     ob = (out.dtype if out is not None else out_dtype) == torch.bfloat16
@@ -954,41 +1005,41 @@ def gemm(a, w, bias=None, act=None, resid=None, resid_mod=0, out=None, out_dtype
     if resid is not None:
         nbytes += 4.0 * (M * N if not resid_mod else resid_mod * N)
     return t.record(tags, 2.0 * M * N * K, nbytes,
-                    lambda: _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m))
+                    lambda: _gemm_untimed(a, w, bias, act, resid, resid_mod, out, out_dtype, row_map, m, plan))
 
 
 def gemm_fp8(a, w, scale, bias=None, act=None, resid=None, out=None, out_dtype=torch.bfloat16,
-             out_qscale=1.0):
+             out_qscale=1.0, plan=None):
     t = _timer()
     if t is None:
-        return _gemm_fp8_untimed(a, w, scale, bias, act, resid, out, out_dtype, out_qscale)
+        return _gemm_fp8_untimed(a, w, scale, bias, act, resid, out, out_dtype, out_qscale, plan)
     M, K = a.shape
     N = w.shape[0]
     od = out.dtype if out is not None else out_dtype
     tags = dict(kind="gemm_fp8", act=ACT[act], out=str(od), resid=resid is not None, M=M, N=N, K=K)
     nbytes = 1.0 * (M * K + N * K) + M * N * od.itemsize + (4.0 * M * N if resid is not None else 0.0)
     return t.record(tags, 2.0 * M * N * K, nbytes,
-                    lambda: _gemm_fp8_untimed(a, w, scale, bias, act, resid, out, out_dtype, out_qscale))
+                    lambda: _gemm_fp8_untimed(a, w, scale, bias, act, resid, out, out_dtype, out_qscale, plan))
 
 
 def attention(q, k, v, o, batch, heads, sq, sk, head_dim, scale, q_bs=None, k_bs=None, v_bs=None,
-              o_bs=None, o_map=None):
+              o_bs=None, o_map=None, variant=0):
     t = _timer()
     if t is None:
         return _attention_untimed(q, k, v, o, batch, heads, sq, sk, head_dim, scale, q_bs, k_bs, v_bs,
-                                  o_bs, o_map)
+                                  o_bs, o_map, variant)
     tags = dict(kind="attn", D=head_dim, sq=sq, sk=sk, batch=batch, heads=heads)
     bh = float(batch * heads)
     return t.record(tags, 4.0 * bh * sq * sk * head_dim, 2.0 * bh * head_dim * (2 * sq + 2 * sk),
                     lambda: _attention_untimed(q, k, v, o, batch, heads, sq, sk, head_dim, scale,
-                                               q_bs, k_bs, v_bs, o_bs, o_map))
+                                               q_bs, k_bs, v_bs, o_bs, o_map, variant))
 
 
 def attention_fp8out(q, k, v, o, batch, heads, sq, sk, head_dim, scale, out_qscale, q_bs=None,
-                     k_bs=None, v_bs=None, o_bs=None):
+                     k_bs=None, v_bs=None, o_bs=None, variant=0):
     t = _timer()
     fn = lambda: _attention_fp8out_untimed(q, k, v, o, batch, heads, sq, sk, head_dim, scale, out_qscale,
-                                           q_bs, k_bs, v_bs, o_bs)
+                                           q_bs, k_bs, v_bs, o_bs, variant)
     if t is None:
         return fn()
     tags = dict(kind="attn", D=head_dim, sq=sq, sk=sk, batch=batch, heads=heads, fp8out=True)
@@ -1125,11 +1176,16 @@ def register_worker(w):
 
 
 def _shutdown():
+    stuck = False
     for w in list(_LIVE_WORKERS):
         try:
-            w.stop(timeout=30.0)
+            stuck |= w.stop(timeout=30.0) is False
         except Exception:  # noqa: BLE001 - exit path: keep releasing the rest
             pass
+    if stuck:
+        # a worker thread is still launching on the sequencers / masked streams: releasing them
+        # now would be a use-after-free under it, so process teardown reclaims them instead
+        return
     for q in list(_LIVE_SEQUENCERS):
         try:
             q.close()
@@ -1149,7 +1205,7 @@ def partition_streams(n_reserved, device=None, masked=False):
     confines each stream to its CUs with hipExtStreamCreateWithCUMask."""
     dev = torch.cuda.current_device() if device is None else device
     det, fus = partition_cus(n_reserved, dev)
-    lib().bf_gemm_set_cu_budget(c_int(len(det)))
+    set_cu_budget(len(det))
     if not masked:
         return torch.cuda.current_stream(dev), torch.cuda.Stream(device=dev, priority=-1)
     return cu_masked_stream(det, dev), cu_masked_stream(fus, dev)

@@ -203,7 +203,10 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_nms_scan(
                 if (fl_len[idx] == 1) {
                     branch = 1;
                     int cnt = 0;
-                    const int L = fl_len[cur];
+                    // a caller-supplied length past the row capacity reads no further than the
+                    // row (the one-wave scan's clamp) and is reported
+                    const int L = min(fl_len[cur], cap);
+                    if (fl_len[cur] > cap) st |= BF_DEV_FUSION_LIST_OVERFLOW;
                     for (int q = 0; q < L; ++q) {
                         int pi = fl[(size_t)cur * cap + q];
                         float b, a;
@@ -217,7 +220,8 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_nms_scan(
                 } else {
                     branch = 2;
                     int cnt = 0;
-                    const int L = fl_len[idx];
+                    const int L = min(fl_len[idx], cap);
+                    if (fl_len[idx] > cap) st |= BF_DEV_FUSION_LIST_OVERFLOW;
                     for (int q = 0; q < L; ++q) {
                         int pi = fl[(size_t)idx * cap + q];
                         float b, a;
@@ -688,7 +692,8 @@ __device__ int record_corr(int cur, int idx, const int32_t* init_id, const float
     if (fl_len[idx] == 1) {
         branch = 1;
         int cnt = 0;
-        const int L = fl_len[cur];
+        const int L = min(fl_len[cur], cap);
+        if (fl_len[cur] > cap) st |= BF_DEV_FUSION_LIST_OVERFLOW;
         for (int q = 0; q < L; ++q) {
             int pi = fl[(size_t)cur * cap + q];
             float b, a;
@@ -702,7 +707,8 @@ __device__ int record_corr(int cur, int idx, const int32_t* init_id, const float
     } else {
         branch = 2;
         int cnt = 0;
-        const int L = fl_len[idx];
+        const int L = min(fl_len[idx], cap);
+        if (fl_len[idx] > cap) st |= BF_DEV_FUSION_LIST_OVERFLOW;
         for (int q = 0; q < L; ++q) {
             int pi = fl[(size_t)idx * cap + q];
             float b, a;

@@ -436,22 +436,17 @@ k_attn2(const u16* __restrict__ Q, const u16* __restrict__ K,
         }
     }
 }
-// 6 (default): k_attn2 with the LDS-staged whole-row output stores for non-causal launches;
-// 27: the same kernel with the per-lane fragment stores (A/B reference; bit-identical);
-// 28: 129-288 queries on 9 waves (the round-4 dispatch), 29 / 30: 129-256 queries on 4 / 8
-// waves, 31: 129-288 on 4 waves, for every head dim; 33: 449-512 queries at D = 64 on 4 waves
-// (A/B references; bit-identical).
-// Env BF_ATTN_VARIANT.
-static int g_attn_variant = [] {
-    const char* e = getenv("BF_ATTN_VARIANT");
-    return e ? atoi(e) : 6;
-}();
-BF_API void bf_attention_set_variant(int v) { g_attn_variant = v; }
-
-BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, void* o, int batch,
-                                  int heads, int sq, int sk, int head_dim, int q_rs, int k_rs,
-                                  int v_rs, int o_rs, long long q_bs, long long k_bs, long long v_bs,
-                                  long long o_bs, float scale, const int32_t* o_map, void* stream) {
+// Per-call variant (bf_attention_bf16_ex / bf_attention_fp8out_ex; 0 = 6): 6 (default) k_attn2 with
+// the LDS-staged whole-row output stores for non-causal launches; 27 the same kernel with the
+// per-lane fragment stores (A/B reference; bit-identical); 28: 129-288 queries on 9 waves (the
+// round-4 dispatch), 29 / 30: 129-256 queries on 4 / 8 waves, 31: 129-288 on 4 waves, for every
+// head dim; 33: 449-512 queries at D = 64 on 4 waves (A/B references; bit-identical).
+BF_API int bf_attention_bf16_ex(const void* q, const void* k, const void* v, void* o, int batch,
+                                int heads, int sq, int sk, int head_dim, int q_rs, int k_rs,
+                                int v_rs, int o_rs, long long q_bs, long long k_bs, long long v_bs,
+                                long long o_bs, float scale, const int32_t* o_map, int variant,
+                                void* stream) {
+    const int av = variant == 0 ? 6 : variant;
     if (!q || !k || !v || !o || batch <= 0 || heads <= 0 || sq <= 0 || sk <= 0) return BF_ERR_ARG;
     if ((q_rs | k_rs | v_rs) % 8 != 0 || o_rs % 4 != 0) return BF_ERR_UNSUPPORTED;
     const float sl2 = scale * 1.4426950408889634f;
@@ -461,7 +456,7 @@ BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, v
     // only) 2-wave workgroups
     const int nw_one = (sq + 31) / 32;
     const bool short_s = nw_one > 4 && nw_one <= 9;
-    const bool lst = g_attn_variant != 27;
+    const bool lst = av != 27;
     // 129-256 queries (CuTR's rgb-only and last-depth windows: 256): a ninth wave would hold no
     // query.  D = 64 and 80 take 4-wave workgroups of 128 queries (3 per CU at the forms' 3 waves
     // per SIMD: rgb windows 37.3 -> 28.2 us against 8 waves, last-depth 55.8 -> 43.7, CLIP-shaped
@@ -470,17 +465,17 @@ BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, v
     // bits).
     // 257-288 queries (CLIP: 257): 9 waves, at D = 80 4-wave workgroups (ATTN_WPE80 above).
     // Variant 28 restores 9 waves for all of 129-288, 31 takes 4 waves for all of it.
-    const int mid = g_attn_variant == 28 ? 9 : g_attn_variant == 29 ? 4 : g_attn_variant == 30 ? 8
+    const int mid = av == 28 ? 9 : av == 29 ? 4 : av == 30 ? 8
                   : (head_dim == 64 || head_dim == 80) ? 4 : 8;
-    const bool four_all = g_attn_variant == 31;
-    const int top = g_attn_variant == 28 ? 9 : (four_all || head_dim == 80) ? 4 : 9;
+    const bool four_all = av == 31;
+    const int top = av == 28 ? 9 : (four_all || head_dim == 80) ? 4 : 9;
     const bool eight = short_s && nw_one <= 8 && mid == 8 && !four_all;
     const bool nine = short_s && !four_all && (nw_one <= 8 ? mid == 9 : top == 9);
     // 449-512 queries at D = 64 (CuTR's joint windows: 512) on two 8-wave workgroups per head
     // instead of four 4-wave ones: K / V staged twice instead of four times, 76.9-79.0 vs 86.3-89.8
     // us (the 1600-token global blocks and the 256-query windows are faster on 4 waves).  Variant
     // 33: the 4-wave form (A/B; the same bits).
-    const bool wide8 = head_dim == 64 && sq > 448 && sq <= 512 && g_attn_variant != 33;
+    const bool wide8 = head_dim == 64 && sq > 448 && sq <= 512 && av != 33;
     const hipStream_t st = bf_stream(stream);
 #define LAUNCH_2(DD, NWV, LS)                                                                     \
     hipLaunchKernelGGL((k_attn2<DD, NWV, false, false, LS>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch), \
@@ -504,6 +499,14 @@ BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, v
     return bf_check_launch();
 }
 
+BF_API int bf_attention_bf16_omap(const void* q, const void* k, const void* v, void* o, int batch,
+                                  int heads, int sq, int sk, int head_dim, int q_rs, int k_rs,
+                                  int v_rs, int o_rs, long long q_bs, long long k_bs, long long v_bs,
+                                  long long o_bs, float scale, const int32_t* o_map, void* stream) {
+    return bf_attention_bf16_ex(q, k, v, o, batch, heads, sq, sk, head_dim, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs,
+                                v_bs, o_bs, scale, o_map, 0, stream);
+}
+
 BF_API int bf_attention_bf16(const void* q, const void* k, const void* v, void* o, int batch,
                              int heads, int sq, int sk, int head_dim, int q_rs, int k_rs, int v_rs,
                              int o_rs, long long q_bs, long long k_bs, long long v_bs,
@@ -514,23 +517,24 @@ BF_API int bf_attention_bf16(const void* q, const void* k, const void* v, void* 
 
 // the same attention (k_attn2, the default schedule) with an fp8 e4m3 output
 // saturate_448(o * out_qscale); o_rs / o_bs in elements = bytes, o_rs % 4 == 0
-BF_API int bf_attention_fp8out(const void* q, const void* k, const void* v, void* o, int batch,
-                               int heads, int sq, int sk, int head_dim, int q_rs, int k_rs, int v_rs,
-                               int o_rs, long long q_bs, long long k_bs, long long v_bs, long long o_bs,
-                               float scale, float out_qscale, void* stream) {
+BF_API int bf_attention_fp8out_ex(const void* q, const void* k, const void* v, void* o, int batch,
+                                  int heads, int sq, int sk, int head_dim, int q_rs, int k_rs, int v_rs,
+                                  int o_rs, long long q_bs, long long k_bs, long long v_bs, long long o_bs,
+                                  float scale, float out_qscale, int variant, void* stream) {
+    const int av = variant == 0 ? 6 : variant;
     if (!q || !k || !v || !o || batch <= 0 || heads <= 0 || sq <= 0 || sk <= 0 || !(out_qscale > 0.f))
         return BF_ERR_ARG;
     if ((q_rs | k_rs | v_rs) % 8 != 0 || o_rs % 4 != 0 || o_bs % 4 != 0) return BF_ERR_UNSUPPORTED;
     const float sl2 = scale * 1.4426950408889634f;
     const int nw_one = (sq + 31) / 32;
-    const bool lst = g_attn_variant != 27;
+    const bool lst = av != 27;
     const hipStream_t st = bf_stream(stream);
 #define LAUNCH_8(DD, NWV, LS)                                                                     \
     hipLaunchKernelGGL((k_attn2<DD, NWV, true, false, LS>), dim3((sq + NWV * 32 - 1) / (NWV * 32), heads, batch), \
                        dim3(NWV * 64), 0, st, (const u16*)q, (const u16*)k, (const u16*)v, (u16*)o, sq, sk, \
                        q_rs, k_rs, v_rs, o_rs, q_bs, k_bs, v_bs, o_bs, sl2, (const int32_t*)nullptr, out_qscale)
     // 257-288 queries at D = 80 (CLIP) on 4-wave workgroups as in bf_attention_bf16 (variant 28: 9)
-    const bool nine = nw_one > 4 && nw_one <= 9 && !(head_dim == 80 && nw_one == 9 && g_attn_variant != 28);
+    const bool nine = nw_one > 4 && nw_one <= 9 && !(head_dim == 80 && nw_one == 9 && av != 28);
 #define LAUNCH_8D(DD)                                                                             \
     if (nine) { if (lst) { LAUNCH_8(DD, 9, true); } else { LAUNCH_8(DD, 9, false); } }             \
     else { if (lst) { LAUNCH_8(DD, 4, true); } else { LAUNCH_8(DD, 4, false); } }
@@ -542,6 +546,14 @@ BF_API int bf_attention_fp8out(const void* q, const void* k, const void* v, void
 #undef LAUNCH_8D
 #undef LAUNCH_8
     return bf_check_launch();
+}
+
+BF_API int bf_attention_fp8out(const void* q, const void* k, const void* v, void* o, int batch,
+                               int heads, int sq, int sk, int head_dim, int q_rs, int k_rs, int v_rs,
+                               int o_rs, long long q_bs, long long k_bs, long long v_bs, long long o_bs,
+                               float scale, float out_qscale, void* stream) {
+    return bf_attention_fp8out_ex(q, k, v, o, batch, heads, sq, sk, head_dim, q_rs, k_rs, v_rs, o_rs, q_bs, k_bs,
+                                  v_bs, o_bs, scale, out_qscale, 0, stream);
 }
 
 // causal self-attention (sq == sk == s): the CLIP text tower (open_clip TextTransformer's attn_mask,

@@ -1275,28 +1275,50 @@ __global__ void __launch_bounds__(G2_THREADS, 1) k_gemm256q(const u16* __restric
 #undef NBLK
 }
 
-// 1: k_gemm256p (staggered 4-phase schedule), 2: k_gemm256p unstaggered, 3 / 4: k_gemm256p
-// diagnostic builds (no epilogue / no global stores: wrong results, timing ablations only),
-// 5 (default): k_gemm256q for bf16 outputs, k_gemm256p otherwise, 6: k_gemm256q wherever it applies
-static int g_gemm_variant = [] {
-    const char* e = getenv("BF_GEMM_VARIANT");
-    const int v = e ? atoi(e) : 5;
-    return v >= 1 && v <= 6 ? v : 5;
-}();
-BF_API void bf_gemm_set_variant(int v) { g_gemm_variant = v >= 1 && v <= 6 ? v : 5; }
-BF_API int bf_gemm_get_variant(void) { return g_gemm_variant; }
+// Per-call configuration (bf_gemm_plan of the C-ABI; NULL = the defaults): the library keeps no
+// process-wide GEMM state, so concurrent calls on different streams with different plans are
+// independent.  Variant: 1 k_gemm256p (staggered 4-phase schedule), 2 k_gemm256p unstaggered, 3 / 4
+// k_gemm256p timing ablations (no epilogue / no global stores: wrong results), 5 (default)
+// k_gemm256q for bf16 outputs, k_gemm256p otherwise, 6 k_gemm256q wherever it applies.
+struct GemmCfg {
+    int n_cu_dev;    // CUs of the device: every kernel CHOICE is made against this (value-invariant
+                     // across ranks whatever their budgets)
+    int n_cu;        // CUs the persistent grid and the tile-height model assume (the budget)
+    int tile_rows;   // 0 = the per-shape model
+    int kernel;      // 0 = the shape rule, 1 = 128x128 tiles, -1 = the persistent kernels
+    int variant;     // 1..6 (above)
+    int group_m;     // row panels per tile group (tile_coords); 1 = row-major
+    int balanced;    // 0 one workgroup per CU, 1 balanced when the last round is >= 1/4 full, 2 always
+};
 
-// row panels per tile group (tile_coords); 1 = row-major.  Default 8, env BF_GEMM_GROUP_M.
-static int g_group_m = [] {
-    const char* e = getenv("BF_GEMM_GROUP_M");
-    const int g = e ? atoi(e) : 0;
-    return g > 0 ? g : 8;
-}();
-BF_API void bf_gemm_set_group_m(int g) { g_group_m = g; }
+static int gemm_device_cus() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    // per device, cached (read once; never changes)
+    static int cache[64] = {0};
+    if (dev < 0 || dev >= 64) dev = 0;
+    if (cache[dev] == 0) {
+        hipDeviceProp_t prop;
+        cache[dev] = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
+    }
+    return cache[dev];
+}
+
+static GemmCfg gemm_cfg(const bf_gemm_plan* p) {
+    GemmCfg c;
+    c.n_cu_dev = gemm_device_cus();
+    c.n_cu = (p && p->cu_budget > 0 && p->cu_budget < c.n_cu_dev) ? p->cu_budget : c.n_cu_dev;
+    c.tile_rows = (p && p->tile_rows >= 160 && p->tile_rows <= 256 && p->tile_rows % 32 == 0) ? p->tile_rows : 0;
+    c.kernel = p ? (p->kernel > 0 ? 1 : p->kernel < 0 ? -1 : 0) : 0;
+    c.variant = (p && p->variant >= 1 && p->variant <= 6) ? p->variant : 5;
+    c.group_m = (p && p->group_m > 0) ? p->group_m : 8;
+    c.balanced = !p || p->balanced == 0 ? 1 : p->balanced == 2 ? 2 : 0;
+    return c;
+}
 
 template <bool OB, int AC>
-static void launch_gemm256(int grid, hipStream_t st, const void* A, int lda, const void* W, int ldw,
-                           const float* bias, const float* resid, int ldr, int resid_mod, void* C,
+static void launch_gemm256(const GemmCfg& cfg, int grid, hipStream_t st, const void* A, int lda, const void* W,
+                           int ldw, const float* bias, const float* resid, int ldr, int resid_mod, void* C,
                            int ldc, const int32_t* row_map, int M, int N, int K, int tiles_n,
                            int tiles_m) {
     static bool attr = false;
@@ -1307,71 +1329,37 @@ static void launch_gemm256(int grid, hipStream_t st, const void* A, int lda, con
     }
     hipLaunchKernelGGL((k_gemm256p<OB, AC>), dim3(grid), dim3(G2_THREADS), G2_LDS, st, (const u16*)A,
                        lda, (const u16*)W, ldw, bias, resid, ldr, resid_mod, C, ldc, row_map, M, N,
-                       K, tiles_n, tiles_m, g_gemm_variant == 2 ? 0 : 1, g_group_m,
-                       (g_gemm_variant == 3 || g_gemm_variant == 4) ? g_gemm_variant - 2 : 0);
+                       K, tiles_n, tiles_m, cfg.variant == 2 ? 0 : 1, cfg.group_m,
+                       (cfg.variant == 3 || cfg.variant == 4) ? cfg.variant - 2 : 0);
 }
 
-static int g_force_small = 0;
-// test hook: 1 forces the 128x128 kernel for every shape (both kernels stay covered by tests)
-BF_API void bf_gemm_force_small_tiles(int on) { g_force_small = on; }
-
-static int g_balanced = -1;
-// persistent-grid sizing: 1 = balanced (ceil(tiles / rounds) workgroups), 0 = one per CU;
-// default from BF_GEMM_BALANCED (unset: 1)
-BF_API void bf_gemm_set_balanced(int on) { g_balanced = on == 2 ? 2 : on ? 1 : 0; }
-static int gemm_balanced() {
-    if (g_balanced < 0) {
-        const char* e = getenv("BF_GEMM_BALANCED");
-        g_balanced = (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
-    }
-    return g_balanced;
-}
-
-static int g_cu_budget = 0;
-// CUs the GEMMs may assume (persistent grid size); 0 = every CU of the device.  Set it when the
-// launching stream is CU-masked (e.g. part of the chip is reserved for the fusion stream).
-BF_API void bf_gemm_set_cu_budget(int n) { g_cu_budget = n > 0 ? n : 0; }
-// (the persistent attention kernel sizes its grid by the same budget)
-BF_API int bf_gemm_get_cu_budget(void) { return g_cu_budget; }
-
-static int gemm_cu_count() {
-    if (g_cu_budget > 0) return g_cu_budget;
-    static int n_cu = 0;
-    if (n_cu == 0) {
-        int dev = 0;
-        hipDeviceProp_t prop;
-        n_cu = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-                   ? prop.multiProcessorCount : 256;
-    }
-    return n_cu;
-}
-
-// Large problems (N >= 512, at least half a round of 256x256 tiles) run the persistent kernels:
-// per tile they are 3-4x the 128x128 kernel's rate (CLIP patch embed 32768 x 1280 x 640 with its
-// row map: 240 us on 128x128 tiles, profiles/r05_bench_kernel_stats.csv), which no round
-// quantisation of the 128x128 grid makes up for.
-static bool gemm_large_tiles(int M, int N, int K) {
-    const int n_cu = gemm_cu_count();
+// Large problems (N >= 512, at least half a round of 256x256 tiles on the DEVICE's CUs) run the
+// persistent kernels: per tile they are 3-4x the 128x128 kernel's rate (CLIP patch embed 32768 x
+// 1280 x 640 with its row map: 240 us on 128x128 tiles, profiles/r05_bench_kernel_stats.csv), which
+// no round quantisation of the 128x128 grid makes up for.  The rule reads the device's CU count,
+// not a plan's budget, so ranks with different budgets run the same kernels (same bits).
+static bool gemm_large_tiles(int M, int N, int K, int n_cu_dev) {
     const long long t2 = (long long)((M + 255) / 256) * ((N + 255) / 256);
     (void)K;
-    return N >= 512 && t2 >= n_cu / 2;
+    return N >= 512 && t2 >= n_cu_dev / 2;
 }
 
 // which kernel bf_gemm_bf16 runs for an aligned problem of this shape (1 = 256x256 persistent)
-static bool gemm_use_large(int M, int N, int K) {
-    return g_force_small < 0 ? true : g_force_small > 0 ? false : gemm_large_tiles(M, N, K);
+static bool gemm_use_large(int M, int N, int K, const GemmCfg& cfg) {
+    return cfg.kernel < 0 ? true : cfg.kernel > 0 ? false : gemm_large_tiles(M, N, K, cfg.n_cu_dev);
 }
 
-BF_API int bf_gemm_large_tiles(int M, int N, int K) { return gemm_use_large(M, N, K) ? 1 : 0; }
+BF_API int bf_gemm_large_tiles(int M, int N, int K) { return gemm_large_tiles(M, N, K, gemm_device_cus()) ? 1 : 0; }
 
 // Persistent grid size for `tiles` tiles: one workgroup per CU, or, when the last round of tiles
 // is at least a quarter full, as many workgroups as the round count needs (every block walks the
 // same number of tiles, +-1): the CUs a partial last round would leave idle at the end are free
 // for the other streams' kernels from the start instead.  A nearly empty last round costs little,
 // and a full-width grid runs the same tiles ~5 % faster alone (measured on CLIP fc1, 2580 tiles).
-static int gemm_grid(long long tiles, int n_cu) {
+static int gemm_grid(long long tiles, const GemmCfg& cfg) {
+    const int n_cu = cfg.n_cu;
     int grid = (int)(tiles < n_cu ? tiles : n_cu);
-    if (gemm_balanced() && tiles > n_cu && (gemm_balanced() == 2 || tiles % n_cu >= n_cu / 4)) {
+    if (cfg.balanced && tiles > n_cu && (cfg.balanced == 2 || tiles % n_cu >= n_cu / 4)) {
         const long long rounds = (tiles + n_cu - 1) / n_cu;
         const int g = (int)(((tiles + rounds - 1) / rounds + 7) & ~7LL);
         grid = g < n_cu ? g : n_cu;
@@ -1379,23 +1367,15 @@ static int gemm_grid(long long tiles, int n_cu) {
     return grid;
 }
 
-static int g_tile_rows = [] {
-    const char* e = getenv("BF_GEMM_TILE_ROWS");
-    return e ? atoi(e) : 0;
-}();
-// test / measurement hook: force the persistent kernels' tile height (160, 192, 224 or 256 rows);
-// 0 = the per-shape model below
-BF_API void bf_gemm_set_tile_rows(int bm) { g_tile_rows = bm; }
-
-// Tile height of k_gemm256q for an M x N x K problem, from the shape alone (so every box runs the
-// same kernel and summation order): the height with the lowest rounds(BM) x t(BM), rounds =
-// ceil(tiles / CUs), t(BM) the per-tile time model above.  Against the sweep of every path shape
-// (profiles/r05_gemm_tile_sweep.log) it picks the fastest height or one within 1 %: 224 rows for
-// CLIP proj / fc2 (N = 1280) and CuTR's window qkv, 160 for CuTR's N = 768 residual GEMMs, 256
-// elsewhere.
-static int gemm_tile_mb1(int M, int N, int K) {
-    if (g_tile_rows >= 160 && g_tile_rows <= 256 && g_tile_rows % 32 == 0) return (g_tile_rows / 2 - 64) / 16;
-    const int n_cu = gemm_cu_count();
+// Tile height of k_gemm256q for an M x N x K problem, from the shape (and the grid's CU count):
+// the height with the lowest rounds(BM) x t(BM), rounds = ceil(tiles / CUs), t(BM) the per-tile
+// time model above.  Against the sweep of every path shape (profiles/r05_gemm_tile_sweep.log) it
+// picks the fastest height or one within 1 %: 224 rows for CLIP proj / fc2 (N = 1280) and CuTR's
+// window qkv, 160 for CuTR's N = 768 residual GEMMs, 256 elsewhere.  Every height gives the same
+// K-order MFMA chain per output, so this choice never changes a value.
+static int gemm_tile_mb1(int M, int N, int K, const GemmCfg& cfg) {
+    if (cfg.tile_rows) return (cfg.tile_rows / 2 - 64) / 16;
+    const int n_cu = cfg.n_cu;
     const long long tn = (N + 255) / 256;
     int best = 4;
     double best_cost = 0.0;
@@ -1420,7 +1400,7 @@ static void gemm256q_attr() {
 }
 
 template <bool OB, int AC, bool RS, int F8>
-static int launch_gemm256q(int mb1, int grid, void* stream, const void* A, int lda, const void* W, int ldw,
+static int launch_gemm256q(int mb1, int gm, int grid, void* stream, const void* A, int lda, const void* W, int ldw,
                            const float* bias, const float* resid, int ldr, void* C, int ldc, int M, int N, int K,
                            int tiles_n, int tiles_m, float csc, float oqs) {
 #define GQ(MB)                                                                                              \
@@ -1428,7 +1408,7 @@ static int launch_gemm256q(int mb1, int grid, void* stream, const void* A, int l
         gemm256q_attr<OB, AC, RS, F8, MB>();                                                                \
         hipLaunchKernelGGL((k_gemm256q<OB, AC, RS, F8, MB>), dim3(grid), dim3(G2_THREADS), G2_LDS,           \
                            bf_stream(stream), (const u16*)A, lda, (const u16*)W, ldw, bias, resid, ldr, C,   \
-                           ldc, M, N, K, tiles_n, tiles_m, 1, g_group_m, csc, oqs);                          \
+                           ldc, M, N, K, tiles_n, tiles_m, 1, gm, csc, oqs);                                 \
     }
     switch (mb1) {
         case 1: GQ(1); break;
@@ -1559,10 +1539,11 @@ __global__ void __launch_bounds__(SK_THREADS, 1) k_gemm_skinny(const u16* __rest
 }
 
 // few-row problems: the 128 x 128 kernel would give fewer than half the CUs a workgroup
-static bool gemm_use_skinny(int M, int N, int K, int vec_epi) {
-    if (g_force_small != 0 || !vec_epi || N % 32 != 0 || K % 256 != 0) return false;
+// (the device's CU count, as gemm_large_tiles: a rank's budget never changes the kernel)
+static bool gemm_use_skinny(int M, int N, int K, int vec_epi, const GemmCfg& cfg) {
+    if (cfg.kernel != 0 || !vec_epi || N % 32 != 0 || K % 256 != 0) return false;
     const long long t1 = (long long)((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N);
-    return t1 < gemm_cu_count() / 2;
+    return t1 < cfg.n_cu_dev / 2;
 }
 
 template <bool OB, int AC>
@@ -1595,10 +1576,13 @@ static void gemm_log(int M, int N, int K, int act, int resid, int resid_mod, int
     if (seen.insert(buf).second) fprintf(stderr, "%s\n", buf);
 }
 
-// The product entry point: hand-written kernels only, chosen from the shape alone.
-BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bias,
-                        const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
-                        const int32_t* row_map, int M, int N, int K, int act, void* stream) {
+// The product entry point: hand-written kernels only, chosen from the shape alone; the plan (NULL =
+// defaults) sizes the persistent grid and carries the measurement hooks, per call.
+BF_API int bf_gemm_bf16_plan(const void* A, int lda, const void* W, int ldw, const float* bias,
+                             const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
+                             const int32_t* row_map, int M, int N, int K, int act, const bf_gemm_plan* plan,
+                             void* stream) {
+    const GemmCfg cfg = gemm_cfg(plan);
     if (!A || !W || !C || M < 0 || N <= 0 || K <= 0) return BF_ERR_ARG;
     if (K % GB_K != 0 || lda % 8 != 0 || ldw % 8 != 0) return BF_ERR_UNSUPPORTED;
     if (M == 0) return BF_OK;
@@ -1617,9 +1601,8 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
                         (!resid || (((uintptr_t)resid % 16 == 0) && (ldr % 4 == 0)));
     const int t2m = (M + 255) / 256, t2n = (N + 255) / 256;
     const long long t2 = (long long)t2m * t2n;
-    const int n_cu = gemm_cu_count();
     // 16-B row chunks of C / resid also carry the skinny kernel's epilogue (8 columns per thread)
-    if (gemm_use_skinny(M, N, K, vec_epi && (c_bf16 || N % 8 == 0))) {
+    if (gemm_use_skinny(M, N, K, vec_epi && (c_bf16 || N % 8 == 0), cfg)) {
         gemm_log(M, N, K, act, resid != nullptr, resid_mod, row_map != nullptr, c_bf16, "k_gemm_skinny", 128);
 #define GSK(OB, AC) return launch_gemm_skinny<OB, AC>(stream, A, lda, W, ldw, bias, resid, ldr, resid_mod, C, ldc, \
                                                       row_map, M, N, K)
@@ -1633,33 +1616,33 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
         GSK(false, 2);
 #undef GSK
     }
-    if (vec_epi && gemm_use_large(M, N, K)) {
-        const int grid2 = gemm_grid(t2, n_cu);
+    if (vec_epi && gemm_use_large(M, N, K, cfg)) {
+        const int grid2 = gemm_grid(t2, cfg);
         // the overlapped-epilogue kernel: plain / in-place residual outputs, >= 3 K-tiles, the bias
         // row fits its LDS slot, 32-bit byte offsets into C and the residual.  Variant 5 (default):
         // bf16 outputs, and the f32 residual GEMMs whose tile height (gemm_tile_rows) is below 256;
         // at 256 rows those measured 1-4 % slower on it than on k_gemm256p.  Variant 6: every
         // eligible shape.
-        const int mb1 = gemm_tile_mb1(M, N, K);
+        const int mb1 = gemm_tile_mb1(M, N, K, cfg);
         const bool q_fit = row_map == nullptr && resid_mod <= 0 && K / 64 >= 3 && N <= G2Q_BIAS_MAX && act <= 1 &&
                            !(resid && act) && !(resid && c_bf16) && !(act && !c_bf16) &&
                            (long long)(M - 1) * ldc * (c_bf16 ? 2 : 4) + (long long)N * 4 < (1LL << 31) &&
                            (!resid || (long long)(M - 1) * ldr * 4 + (long long)N * 4 < (1LL << 31));
-        const bool q_ok = q_fit && (g_gemm_variant == 6 || (g_gemm_variant == 5 && (c_bf16 || mb1 < 4)));
+        const bool q_ok = q_fit && (cfg.variant == 6 || (cfg.variant == 5 && (c_bf16 || mb1 < 4)));
         if (q_ok) {
             const int bm = 2 * (64 + 16 * mb1);
             const int tqm = (M + bm - 1) / bm;
-            const int gq = gemm_grid(tqm * t2n, n_cu);
+            const int gq = gemm_grid((long long)tqm * t2n, cfg);
             gemm_log(M, N, K, act, resid != nullptr, resid_mod, row_map != nullptr, c_bf16, "k_gemm256q", bm);
             int rc = 0;
-            if (resid) rc = launch_gemm256q<false, 0, true, 0>(mb1, gq, stream, A, lda, W, ldw, bias, resid, ldr, C, ldc, M, N, K, t2n, tqm, 1.f, 1.f);
-            else if (!c_bf16) rc = launch_gemm256q<false, 0, false, 0>(mb1, gq, stream, A, lda, W, ldw, bias, resid, ldr, C, ldc, M, N, K, t2n, tqm, 1.f, 1.f);
-            else if (act == 0) rc = launch_gemm256q<true, 0, false, 0>(mb1, gq, stream, A, lda, W, ldw, bias, resid, ldr, C, ldc, M, N, K, t2n, tqm, 1.f, 1.f);
-            else rc = launch_gemm256q<true, 1, false, 0>(mb1, gq, stream, A, lda, W, ldw, bias, resid, ldr, C, ldc, M, N, K, t2n, tqm, 1.f, 1.f);
+            if (resid) rc = launch_gemm256q<false, 0, true, 0>(mb1, cfg.group_m, gq, stream, A, lda, W, ldw, bias, resid, ldr, C, ldc, M, N, K, t2n, tqm, 1.f, 1.f);
+            else if (!c_bf16) rc = launch_gemm256q<false, 0, false, 0>(mb1, cfg.group_m, gq, stream, A, lda, W, ldw, bias, resid, ldr, C, ldc, M, N, K, t2n, tqm, 1.f, 1.f);
+            else if (act == 0) rc = launch_gemm256q<true, 0, false, 0>(mb1, cfg.group_m, gq, stream, A, lda, W, ldw, bias, resid, ldr, C, ldc, M, N, K, t2n, tqm, 1.f, 1.f);
+            else rc = launch_gemm256q<true, 1, false, 0>(mb1, cfg.group_m, gq, stream, A, lda, W, ldw, bias, resid, ldr, C, ldc, M, N, K, t2n, tqm, 1.f, 1.f);
             return rc;
         }
         gemm_log(M, N, K, act, resid != nullptr, resid_mod, row_map != nullptr, c_bf16, "k_gemm256p", 256);
-#define GEMM2(OB, AC) launch_gemm256<OB, AC>(grid2, bf_stream(stream), A, lda, W, ldw, bias, \
+#define GEMM2(OB, AC) launch_gemm256<OB, AC>(cfg, grid2, bf_stream(stream), A, lda, W, ldw, bias, \
                                             resid, ldr, resid_mod, C, ldc, row_map, M, N, K, t2n, t2m)
         if (c_bf16) {
             if (act == 0) GEMM2(true, 0);
@@ -1698,7 +1681,7 @@ BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const fl
 // 1: bf16 C, 2: fp8 C = sat448(value * out_qscale).  The persistent 256x256 kernel only.
 // ------------------------------------------------------------------------------------------
 template <bool OB, int AC, int F8>
-static void launch_gemm256_f8(int grid, hipStream_t st, const void* A, int lda, const void* W, int ldw,
+static void launch_gemm256_f8(int gm, int grid, hipStream_t st, const void* A, int lda, const void* W, int ldw,
                               float csc, const float* bias, const float* resid, int ldr, void* C,
                               int ldc, float oqs, int M, int N, int K, int tiles_n, int tiles_m) {
     static bool attr = false;
@@ -1709,12 +1692,14 @@ static void launch_gemm256_f8(int grid, hipStream_t st, const void* A, int lda, 
     }
     hipLaunchKernelGGL((k_gemm256p<OB, AC, F8>), dim3(grid), dim3(G2_THREADS), G2_LDS, st, (const u16*)A,
                        lda, (const u16*)W, ldw, bias, resid, ldr, 0, C, ldc, (const int32_t*)nullptr, M, N,
-                       K, tiles_n, tiles_m, 1, g_group_m, 0, csc, oqs);
+                       K, tiles_n, tiles_m, 1, gm, 0, csc, oqs);
 }
 
-BF_API int bf_gemm_fp8(const void* A, int lda, const void* W, int ldw, float scale,
-                       const float* bias, const float* resid, int ldr, void* C, int ldc, int out_kind,
-                       float out_qscale, int M, int N, int K, int act, void* stream) {
+BF_API int bf_gemm_fp8_plan(const void* A, int lda, const void* W, int ldw, float scale,
+                            const float* bias, const float* resid, int ldr, void* C, int ldc, int out_kind,
+                            float out_qscale, int M, int N, int K, int act, const bf_gemm_plan* plan,
+                            void* stream) {
+    const GemmCfg cfg = gemm_cfg(plan);
     if (!A || !W || !C || !(scale > 0.f) || M < 0 || N <= 0 || K <= 0 || act < 0 || act > 1 ||
         out_kind < 0 || out_kind > 2)
         return BF_ERR_ARG;
@@ -1728,26 +1713,24 @@ BF_API int bf_gemm_fp8(const void* A, int lda, const void* W, int ldw, float sca
         return BF_ERR_CAPACITY;
     const int t2m = (M + 255) / 256, t2n = (N + 255) / 256;
     const long long t2 = (long long)t2m * t2n;
-    const int n_cu = gemm_cu_count();
-    const int grid = gemm_grid(t2, n_cu);
+    const int grid = gemm_grid(t2, cfg);
     // the overlapped-epilogue kernel for the fp8 GEMMs with bf16 outputs (CLIP qkv: 203.0 -> 161.4
     // us); fp8 outputs only under variant 6 (CLIP fc1 + GELU -> fp8 measured 286.7 -> 303.7 us on it:
     // at the fp8 MFMA rate the K loop is short beside that epilogue's VALU work)
-    if ((g_gemm_variant == 6 || (g_gemm_variant == 5 && out_kind == 1)) && !resid && out_kind != 0 && K / 128 >= 3 &&
+    if ((cfg.variant == 6 || (cfg.variant == 5 && out_kind == 1)) && !resid && out_kind != 0 && K / 128 >= 3 &&
         N <= G2Q_BIAS_MAX && (long long)(M - 1) * ldc * (out_kind == 1 ? 2 : 1) + (long long)N * 2 < (1LL << 31)) {
-        const int mb1 = gemm_tile_mb1(M, N, K);
+        const int mb1 = gemm_tile_mb1(M, N, K, cfg);
         const int bm = 2 * (64 + 16 * mb1);
         const int tqm = (M + bm - 1) / bm;
-        const int gq = gemm_grid((long long)tqm * t2n, n_cu);
+        const int gq = gemm_grid((long long)tqm * t2n, cfg);
         if (out_kind == 1) {
-            if (act == 0) return launch_gemm256q<true, 0, false, 1>(mb1, gq, stream, A, lda, W, ldw, bias, nullptr, 0, C, ldc, M, N, K, t2n, tqm, scale, out_qscale);
-            return launch_gemm256q<true, 1, false, 1>(mb1, gq, stream, A, lda, W, ldw, bias, nullptr, 0, C, ldc, M, N, K, t2n, tqm, scale, out_qscale);
+            if (act == 0) return launch_gemm256q<true, 0, false, 1>(mb1, cfg.group_m, gq, stream, A, lda, W, ldw, bias, nullptr, 0, C, ldc, M, N, K, t2n, tqm, scale, out_qscale);
+            return launch_gemm256q<true, 1, false, 1>(mb1, cfg.group_m, gq, stream, A, lda, W, ldw, bias, nullptr, 0, C, ldc, M, N, K, t2n, tqm, scale, out_qscale);
         }
-        if (act == 0) return launch_gemm256q<true, 0, false, 3>(mb1, gq, stream, A, lda, W, ldw, bias, nullptr, 0, C, ldc, M, N, K, t2n, tqm, scale, out_qscale);
-        return launch_gemm256q<true, 1, false, 3>(mb1, gq, stream, A, lda, W, ldw, bias, nullptr, 0, C, ldc, M, N, K, t2n, tqm, scale, out_qscale);
-        return bf_check_launch();
+        if (act == 0) return launch_gemm256q<true, 0, false, 3>(mb1, cfg.group_m, gq, stream, A, lda, W, ldw, bias, nullptr, 0, C, ldc, M, N, K, t2n, tqm, scale, out_qscale);
+        return launch_gemm256q<true, 1, false, 3>(mb1, cfg.group_m, gq, stream, A, lda, W, ldw, bias, nullptr, 0, C, ldc, M, N, K, t2n, tqm, scale, out_qscale);
     }
-#define GEMM8(OB, AC, F8) launch_gemm256_f8<OB, AC, F8>(grid, bf_stream(stream), A, lda, W, ldw, scale, bias, \
+#define GEMM8(OB, AC, F8) launch_gemm256_f8<OB, AC, F8>(cfg.group_m, grid, bf_stream(stream), A, lda, W, ldw, scale, bias, \
                                                          resid, ldr, C, ldc, out_qscale, M, N, K, t2n, t2m)
     if (out_kind == 0) {
         if (act != 0) return BF_ERR_UNSUPPORTED;   // (f32 GELU output: not on the path)
@@ -1761,4 +1744,18 @@ BF_API int bf_gemm_fp8(const void* A, int lda, const void* W, int ldw, float sca
     }
 #undef GEMM8
     return bf_check_launch();
+}
+
+BF_API int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bias,
+                        const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
+                        const int32_t* row_map, int M, int N, int K, int act, void* stream) {
+    return bf_gemm_bf16_plan(A, lda, W, ldw, bias, resid, ldr, resid_mod, C, ldc, c_bf16, row_map, M, N, K, act,
+                             nullptr, stream);
+}
+
+BF_API int bf_gemm_fp8(const void* A, int lda, const void* W, int ldw, float scale,
+                       const float* bias, const float* resid, int ldr, void* C, int ldc, int out_kind,
+                       float out_qscale, int M, int N, int K, int act, void* stream) {
+    return bf_gemm_fp8_plan(A, lda, W, ldw, scale, bias, resid, ldr, C, ldc, out_kind, out_qscale, M, N, K, act,
+                            nullptr, stream);
 }

@@ -521,7 +521,7 @@ class AsyncFusion:
         """interpreter exit (_lib._shutdown): drop queued jobs, let the running one finish, and
         drain the worker's stream before the streams and sequencers it uses are released"""
         if not self.thread.is_alive():
-            return
+            return True
         try:
             while True:
                 self.q.get_nowait()
@@ -529,4 +529,12 @@ class AsyncFusion:
             pass
         self.q.put(None)
         self.thread.join(timeout)
+        if self.thread.is_alive():
+            # still launching (a long batch): its sequencers and CU-masked streams must outlive it,
+            # so _shutdown leaves them to process teardown instead of releasing them under it
+            import warnings
+            warnings.warn("fusion worker still running at exit: its HIP resources are not released",
+                          RuntimeWarning)
+            return False
         self.stream.synchronize()
+        return True

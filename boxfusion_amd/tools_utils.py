@@ -57,7 +57,15 @@ def match_features(img_features, text_features, sim_thres):
     if f.is_cuda:
         # (100 f) @ text^T as the reference groups it, on the f32 MFMA GEMM (bf_gemm_f32)
         from boxfusion_amd import _lib
-        probs = _lib.gemm_f32((100.0 * f).contiguous(), text_features.contiguous())
+        a, t = (100.0 * f).contiguous(), text_features.contiguous()
+        K = a.shape[-1]
+        if K % 4 or a.data_ptr() % 16 or t.data_ptr() % 16:
+            # bf_gemm_f32 wants 16-B aligned rows: zero-pad K to a multiple of 4 in fresh (aligned)
+            # buffers -- the added products are exact zeros, so the sums are unchanged
+            K4 = (K + 3) // 4 * 4
+            a = torch.nn.functional.pad(a, (0, K4 - K))
+            t = torch.nn.functional.pad(t, (0, K4 - K))
+        probs = _lib.gemm_f32(a, t)
     else:
         probs = 100.0 * f @ text_features.T
     probs = torch.cat([probs, torch.full_like(probs, float(sim_thres))[..., :1]], dim=-1)

@@ -4,12 +4,15 @@
  *
  * Conventions (every entry point):
  *   - All data pointers are CALLER-OWNED DEVICE pointers (e.g. torch tensors' data_ptr()),
- *     contiguous, with the dtype named in the signature.  Nothing here allocates device memory.
+ *     contiguous, with the dtype named in the signature.  Nothing here allocates device memory
+ *     (except the keyframe sequencer bf_fseq_*, which owns its rows: see its section).
  *   - `stream` is a hipStream_t passed as void* (NULL = the legacy default stream).
  *   - Every call is asynchronous on `stream` and returns a bf_status (0 = ok, < 0 = error).
  *     Device-side capacity problems are reported through an int32 device status word where the
  *     signature has one (BF_DEV_* flags); the caller reads it after synchronising.
- *   - Functions are stateless and reentrant; concurrent calls on different streams are safe.
+ *   - Functions keep no process-wide state (per-call options travel in caller-owned structs such
+ *     as bf_gemm_plan) and are reentrant; concurrent calls on different streams are safe.  The
+ *     one stateful object is a bf_fseq sequencer, owned by its caller.
  *
  * Each function cites the reference interface it replaces (paths relative to the reference
  * repository pliam1105/BoxFusion).
@@ -355,44 +358,44 @@ int bf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bi
                  const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
                  const int32_t* row_map, int M, int N, int K, int act, void* stream);
 
-/* Kernel choice is a function of the shape alone (hand-written kernels only, the same on every
- * box): few-row problems (the 128 x 128 tiling would feed fewer than half the CUs; N % 32 == 0,
- * K % 256 == 0) run k_gemm_skinny (8 waves split K, partials summed in wave order); large ones
- * the persistent kernels with a tile height of 160 / 192 / 224 / 256 rows picked by the round
- * quantisation of the walk.  Test / measurement hook (process-wide): force that tile height
- * (env BF_GEMM_TILE_ROWS); 0 = the per-shape model. */
-void bf_gemm_set_tile_rows(int bm);
-/* Tile selection: large problems (N >= 512, >= 128 tiles of 256x256, 16-B aligned output rows)
- * run the 256x256 8-wave kernel, the rest the 128x128 4-wave kernel.  Test / tuning hook
- * (process-wide): 1 forces the 128x128 kernel, -1 the 256x256 kernel (aligned shapes), 0 the
- * heuristic. */
-void bf_gemm_force_small_tiles(int on);
-/* Persistent 256x256 kernel variant: 1 = k_gemm256p (staggered 4-phase schedule), 2 = k_gemm256p
- * unstaggered, 3 / 4 = timing ablations of k_gemm256p (no epilogue / no global stores: wrong
- * results), 5 = k_gemm256q (k_gemm256p's K loop, epilogue of each 64x32
- * quadrant overlapped with the next phases' MFMAs) for bf16 outputs and k_gemm256p for the rest
- * (default; env BF_GEMM_VARIANT), 6 = k_gemm256q for every eligible shape (no row map / broadcast
- * residual, K >= 192, N <= 8192).  Test/benchmark hook; results agree to f32 rounding. */
-void bf_gemm_set_variant(int v);
-int bf_gemm_get_variant(void);
-/* Row panels per tile group of the persistent kernels' tile order (default 8; 1 = row-major).
- * Test/benchmark hook; results are identical in value. */
-void bf_gemm_set_group_m(int g);
-/* 1 if an aligned (16-B rows) problem of this shape runs a 256x256 kernel (k_gemm256p/q), 0 if the
- * 128x128 one (k_gemm) — lets profilers attribute launches to kernels. */
+/* Kernel choice is a function of the shape and the DEVICE's CU count alone (hand-written kernels
+ * only, the same on every box and every rank): few-row problems (the 128 x 128 tiling would feed
+ * fewer than half the CUs; N % 32 == 0, K % 256 == 0) run k_gemm_skinny (8 waves split K, partials
+ * summed in wave order); large ones the persistent kernels with a tile height of 160 / 192 / 224 /
+ * 256 rows picked by the round quantisation of the walk (the height never changes a value).
+ *
+ * bf_gemm_plan: caller-owned, per-call configuration (no process-wide GEMM state exists; NULL or an
+ * all-zero plan = the product defaults):
+ *   cu_budget  CUs the persistent grid may assume (0 = every CU of the device): a GEMM launched on a
+ *              CU-masked stream passes that stream's CU count.  Sizes the grid and the tile-height
+ *              model only, so results are bit-identical under any budget.
+ *   tile_rows  0 = the per-shape model; 160 / 192 / 224 / 256 force the height (value-invariant).
+ *   The remaining fields are measurement / test hooks (0 = product default):
+ *   kernel     1 forces the 128x128 kernel, -1 the persistent kernels (aligned shapes);
+ *   variant    persistent kernel variant: 1 = k_gemm256p (staggered 4-phase schedule), 2 = k_gemm256p
+ *              unstaggered, 3 / 4 = timing ablations (no epilogue / no global stores: wrong
+ *              results), 5 = default (k_gemm256q for bf16 outputs and sub-256-row residual tiles,
+ *              k_gemm256p otherwise), 6 = k_gemm256q for every eligible shape;
+ *   group_m    row panels per tile group of the persistent tile order (default 8; 1 = row-major);
+ *   balanced   0 = default (ceil(tiles / rounds) workgroups when the last round is at least a
+ *              quarter full), 1 = one workgroup per CU, 2 = balanced for every multi-round problem.
+ * bf_gemm_bf16(...) == bf_gemm_bf16_plan(..., NULL, stream). */
+typedef struct {
+    int32_t cu_budget;
+    int32_t tile_rows;
+    int32_t kernel;
+    int32_t variant;
+    int32_t group_m;
+    int32_t balanced;
+} bf_gemm_plan;
+int bf_gemm_bf16_plan(const void* A, int lda, const void* W, int ldw, const float* bias,
+                      const float* resid, int ldr, int resid_mod, void* C, int ldc, int c_bf16,
+                      const int32_t* row_map, int M, int N, int K, int act, const bf_gemm_plan* plan,
+                      void* stream);
+/* 1 if an aligned (16-B rows) problem of this shape runs a 256-column persistent kernel
+ * (k_gemm256p/q) under the default plan, 0 if the 128x128 one (k_gemm) -- lets profilers
+ * attribute launches to kernels. */
 int bf_gemm_large_tiles(int M, int N, int K);
-/* Number of CUs the GEMM may assume (sizes the persistent grid); 0 = all CUs of the device.
- * Set when GEMMs launch on a CU-masked stream. */
-void bf_gemm_set_cu_budget(int n);
-/* The budget set above (0 = none). */
-int bf_gemm_get_cu_budget(void);
-/* Persistent-grid sizing of the 256x256 kernel: 1 (default; env BF_GEMM_BALANCED=0 turns it
- * off) launches ceil(tiles / rounds) workgroups so every block walks the same tile count and a
- * partial last round (when at least a quarter full) leaves its idle CUs to concurrent streams
- * from the start; 2 = balanced for every multi-round problem (measured: same bench, CLIP fc1
- * slower alone); 0 = one per CU.
- * Results are identical in value. */
-void bf_gemm_set_balanced(int on);
 
 /* fp8 e4m3 (OCP) GEMM of the CLIP ViT-H fp8 path (BASELINE configs[4]; the same open_clip
  * in_proj / c_fc / c_proj linears as bf_gemm_bf16, tools/utils.py:383-403):
@@ -405,6 +408,10 @@ void bf_gemm_set_balanced(int on);
 int bf_gemm_fp8(const void* A, int lda, const void* W, int ldw, float scale, const float* bias,
                 const float* resid, int ldr, void* C, int ldc, int out_kind, float out_qscale,
                 int M, int N, int K, int act, void* stream);
+/* the same with a per-call plan (cu_budget / tile_rows / variant / group_m / balanced as above) */
+int bf_gemm_fp8_plan(const void* A, int lda, const void* W, int ldw, float scale, const float* bias,
+                     const float* resid, int ldr, void* C, int ldc, int out_kind, float out_qscale,
+                     int M, int N, int K, int act, const bf_gemm_plan* plan, void* stream);
 
 /* softmax(Q K^T * scale) V per (batch, head); X(b,h,s,d) at X + b*x_bs + s*x_rs + h*D + d,
  * bf16 in/out, head_dim in {32, 64, 80, 128}.  Replaces vit.py Attention.forward (:170-203,
@@ -427,14 +434,22 @@ int bf_attention_fp8out(const void* q, const void* k, const void* v, void* o, in
                         int sq, int sk, int head_dim, int q_rs, int k_rs, int v_rs, int o_rs,
                         long long q_bs, long long k_bs, long long v_bs, long long o_bs, float scale,
                         float out_qscale, void* stream);
-/* Attention kernel variant (test/benchmark hook; env BF_ATTN_VARIANT): 6 (default) = k_attn2
- * (deferred-max softmax, row sums from a ones row of V on the MFMA; 257-288 queries on 9-wave
- * workgroups, at head dim 80 on 4-wave ones; 129-256 queries on 4-wave workgroups at head dims 64
- * and 80 and 8-wave ones otherwise; 449-512 queries at head dim 64 on 8-wave workgroups; output rows staged in LDS and stored as whole head rows), 27 = the
- * same kernel with per-lane fragment stores, 28 = 129-288 queries on 9 waves, 29 / 30 = 129-256
- * queries on 4 / 8 waves, 31 = 129-288 queries on 4 waves, for every head dim, 33 = 449-512 queries
- * at head dim 64 on 4 waves (all bit-identical). */
-void bf_attention_set_variant(int v);
+/* bf_attention_bf16_omap / bf_attention_fp8out with a per-call kernel variant (a test / benchmark
+ * hook; 0 or 6 = the default the plain entry points run): 6 = k_attn2 (deferred-max softmax, row
+ * sums from a ones row of V on the MFMA; 257-288 queries on 9-wave workgroups, at head dim 80 on
+ * 4-wave ones; 129-256 queries on 4-wave workgroups at head dims 64 and 80 and 8-wave ones
+ * otherwise; 449-512 queries at head dim 64 on 8-wave workgroups; output rows staged in LDS and
+ * stored as whole head rows), 27 = the same kernel with per-lane fragment stores, 28 = 129-288
+ * queries on 9 waves, 29 / 30 = 129-256 queries on 4 / 8 waves, 31 = 129-288 queries on 4 waves,
+ * for every head dim, 33 = 449-512 queries at head dim 64 on 4 waves (all bit-identical). */
+int bf_attention_bf16_ex(const void* q, const void* k, const void* v, void* o, int batch, int heads,
+                         int sq, int sk, int head_dim, int q_rs, int k_rs, int v_rs, int o_rs,
+                         long long q_bs, long long k_bs, long long v_bs, long long o_bs, float scale,
+                         const int32_t* o_map, int variant, void* stream);
+int bf_attention_fp8out_ex(const void* q, const void* k, const void* v, void* o, int batch, int heads,
+                           int sq, int sk, int head_dim, int q_rs, int k_rs, int v_rs, int o_rs,
+                           long long q_bs, long long k_bs, long long v_bs, long long o_bs, float scale,
+                           float out_qscale, int variant, void* stream);
 
 /* CuTR decoder cross-attention bias (GlobalCrossAttention.rpe + the logits' bias / clip /
  * softmax, cubify_transformer.py:93-190 of the reference), f32:

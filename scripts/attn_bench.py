@@ -1,5 +1,5 @@
 """Attention microbenchmark on the path's shapes (TFLOP/s of 4*Sq*Sk*D per head), kernel variants
-(bf_attention_set_variant) interleaved in one process, vs torch SDPA; max |err| vs SDPA in fp32."""
+(_lib.set_knobs(attn_variant=...)) interleaved in one process, vs torch SDPA; max |err| vs SDPA in fp32."""
 import os
 import sys
 import torch
@@ -40,11 +40,11 @@ for name, B, H, S, D in SHAPES:
     times = {vv_: [] for vv_ in variants}
     for rnd in range(3):
         for var in variants:
-            L.bf_attention_set_variant(var)
+            _lib.set_knobs(attn_variant=var)
             times[var].append(timeit(f))
     first = None
     for var in variants:
-        L.bf_attention_set_variant(var)
+        _lib.set_knobs(attn_variant=var)
         o.zero_()
         f()
         torch.cuda.synchronize()

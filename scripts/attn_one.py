@@ -7,7 +7,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from boxfusion_amd import _lib
 B, H, S, D, var = (int(x) for x in sys.argv[1:6])
 iters = int(sys.argv[6]) if len(sys.argv) > 6 else 10
-_lib.lib().bf_attention_set_variant(var)
+_lib.set_knobs(attn_variant=var)
 qkv = torch.randn(B * S, 3 * H * D, device="cuda").bfloat16()
 o = torch.empty(B * S, H * D, device="cuda", dtype=torch.bfloat16)
 q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]

@@ -25,7 +25,7 @@ def timeit(f, iters=30):
 
 
 for var in [int(v) for v in sys.argv[1:]] or [6]:
-    L.bf_attention_set_variant(var)
+    _lib.set_knobs(attn_variant=var)
     for B in (16, 32, 64, 128, 256):
         qkv = torch.randn(B * S, 3 * H * D, device="cuda").bfloat16()
         o = torch.empty(B * S, H * D, device="cuda", dtype=torch.bfloat16)

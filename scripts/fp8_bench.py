@@ -43,13 +43,13 @@ def main():
         o8 = torch.empty(M, N, device=dev, dtype=od)
         msg = f"{name:4s} M={M} N={N} K={K}:"
         for var in VARIANTS:
-            _lib.lib().bf_gemm_set_variant(var)
+            _lib.set_knobs(variant=var)
             t16 = timeit(lambda: _lib.gemm(a16, w16, b, act=act, resid=x if res else None, out=x if res else o16))
             t8 = timeit(lambda: _lib.gemm_fp8(a8, w8, 0.05, bias=b, act=act, resid=x if res else None,
                                               out=x if res else o8, out_qscale=0.1))
             msg += (f" | v{var} bf16 {t16:7.1f} us {fl / t16 / 1e6:7.1f} TF/s, "
                     f"fp8 {t8:7.1f} us {fl / t8 / 1e6:7.1f} TF/s ({t16 / t8:.2f}x)")
-        _lib.lib().bf_gemm_set_variant(5)
+        _lib.set_knobs(variant=5)
         print(msg, flush=True)
     from boxfusion_amd.clip import VisionTransformer
     from boxfusion_amd.engine import CLIPEngine

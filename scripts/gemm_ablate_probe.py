@@ -30,9 +30,9 @@ for name, N, K, act in [("qkv", 3840, 1280, None), ("fc1", 5120, 1280, "gelu"), 
     tiles = ((M + 255) // 256) * ((N + 255) // 256)
     msg = f"{name:8s} N={N} K={K} tiles={tiles}:"
     for var, lab in [(1, "full"), (4, "nostore"), (3, "noepi")]:
-        L.bf_gemm_set_variant(var)
+        _lib.set_knobs(variant=var)
         t = timeit(lambda: _lib.gemm(a, w, b, act=act, out=o))
         rounds = (tiles + 255) // 256
         msg += f" {lab} {t:7.1f} us ({t / rounds:5.1f} us/round)"
-    L.bf_gemm_set_variant(1)
+    _lib.set_knobs(variant=1)
     print(msg, flush=True)

@@ -56,8 +56,8 @@ for name, M, N, K, act, ob, use_resid in SHAPES:
     for rnd in range(3):
         for v in variants:
             vv, _, gm = v.partition(":")
-            L.bf_gemm_set_variant(int(vv))
-            L.bf_gemm_set_group_m(int(gm or 4))
+            _lib.set_knobs(variant=int(vv))
+            _lib.set_knobs(group_m=int(gm or 4))
             times[v].append(bench(lambda: _lib.gemm(a, w, bias, act=act, resid=resid, out=out)))
             if rnd == 0:
                 out.zero_()

@@ -13,8 +13,8 @@ iters = int(sys.argv[3]) if len(sys.argv) > 3 else 20
 _, M, N, K, act, ob, use_resid = [s for s in SHAPES if s[0] == name][0]
 L = _lib.lib()
 vv, _, gm = v.partition(":")
-L.bf_gemm_set_variant(int(vv))
-L.bf_gemm_set_group_m(int(gm or 4))
+_lib.set_knobs(variant=int(vv))
+_lib.set_knobs(group_m=int(gm or 4))
 dev = torch.device("cuda")
 a = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16()
 w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).bfloat16()

@@ -26,8 +26,8 @@ for K in (1280, 5120):
         x = torch.randn(M, 1280, device=dev)
         tiles = ((M + 255) // 256) * 5
         for bal in (1, 0):
-            _lib.lib().bf_gemm_set_balanced(bal)
+            _lib.set_knobs(balanced={1: 0, 0: 1, 2: 2}[bal])
             t = timeit(lambda: _lib.gemm(a, w, b, resid=x, out=x))
             print(f"K={K} M={M} tiles={tiles} balanced={bal}: {t:7.1f} us  {t / tiles * 256:6.1f} us per 256 tiles "
                   f"{2 * M * 1280 * K / t / 1e6:7.1f} TF/s", flush=True)
-        _lib.lib().bf_gemm_set_balanced(1)
+        _lib.set_knobs(balanced={1: 0, 0: 1, 2: 2}[1])

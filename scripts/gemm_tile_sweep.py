@@ -69,7 +69,7 @@ def main():
         ref = None
         for rnd in range(3):
             for h in heights:
-                L.bf_gemm_set_tile_rows(h)
+                _lib.set_knobs(tile_rows=h)
                 times[h].append(bench(fn))
                 if rnd == 0 and resid is None:
                     fn()
@@ -78,7 +78,7 @@ def main():
                         ref = out.clone()
                     elif not torch.equal(ref, out):
                         print(f"  {name}: tile height {h} changed the output", flush=True)
-        L.bf_gemm_set_tile_rows(0)
+        _lib.set_knobs(tile_rows=0)
         t_lib = (bench(lambda: torch.nn.functional.linear(a, w)) if not fp8 and "--auto-only" not in sys.argv
                  else float("nan"))
         fl = 2.0 * M * N * K

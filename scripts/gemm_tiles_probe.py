@@ -1,4 +1,4 @@
-"""128x128 vs 256x256 kernel on the CuTR / CLIP shapes (bf_gemm_force_small_tiles 1 / -1)."""
+"""128x128 vs 256x256 kernel on the CuTR / CLIP shapes (_lib.set_knobs(kernel=1 / -1))."""
 import os
 import sys
 import torch
@@ -23,8 +23,8 @@ for name, M, N, K, act, ob, use_resid in SHAPES + extra:
     resid = torch.rand((M, N), device=dev) if use_resid else None
     res = []
     for f in (1, -1, 0):
-        L.bf_gemm_force_small_tiles(f)
+        _lib.set_knobs(kernel=f)
         t = min(bench(lambda: _lib.gemm(a, w, bias, act=act, resid=resid, out=out)) for _ in range(3))
         res.append(f"{ {1: 'small', -1: 'large', 0: 'auto'}[f]} {t * 1e3:6.1f} us {2 * M * N * K / t / 1e9:5.0f} TF")
-    L.bf_gemm_force_small_tiles(0)
+    _lib.set_knobs(kernel=0)
     print(f"{name:14s} M={M} N={N} K={K} | " + " | ".join(res), flush=True)

@@ -40,7 +40,7 @@ for name, B, H, sq, sk, D in SHAPES:
         f()
     for rep in range(4):                      # variants interleaved, best of 4 rounds each
         for var in VARS if rep % 2 == 0 else VARS[::-1]:
-            L.bf_attention_set_variant(var)
+            _lib.set_knobs(attn_variant=var)
             f()
             torch.cuda.synchronize()
             if rep == 0:
@@ -52,7 +52,7 @@ for name, B, H, sq, sk, D in SHAPES:
             e.record()
             torch.cuda.synchronize()
             res[var][0] = min(res[var][0], s.elapsed_time(e) / 20 * 1e3)
-    L.bf_attention_set_variant(6)
+    _lib.set_knobs(attn_variant=6)
     same = all(torch.equal(res[6][1], res[v][1]) for v in VARS[1:])
     fl = 4.0 * B * H * sq * sk * D
     print(f"{name:24s} {os.path.basename(os.environ.get('BF_LIB_PATH', 'in-tree')):12s} default {res[6][0]:7.1f} us "

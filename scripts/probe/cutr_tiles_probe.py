@@ -1,5 +1,5 @@
 """CuTR's K = 768 GEMMs: the per-shape tile height (auto) against forced 256 / 160 rows and the 128x128
-kernel (bf_gemm_force_small_tiles), in rotating order (auto measured last in odd rounds)."""
+kernel (_lib.set_knobs(kernel=...)), in rotating order (auto measured last in odd rounds)."""
 import math
 import os
 import sys
@@ -39,10 +39,10 @@ for name, M, N, K, act in SHAPES:
     keys = list(modes)
     for rnd in range(4):
         for k in (keys if rnd % 2 == 0 else keys[::-1]):
-            L.bf_gemm_set_tile_rows(modes[k][0])
-            L.bf_gemm_force_small_tiles(modes[k][1])
+            _lib.set_knobs(tile_rows=modes[k][0])
+            _lib.set_knobs(kernel=modes[k][1])
             res[k].append(bench(fn))
-    L.bf_gemm_set_tile_rows(0)
-    L.bf_gemm_force_small_tiles(0)
+    _lib.set_knobs(tile_rows=0)
+    _lib.set_knobs(kernel=0)
     ref = (a.float() @ w.float().T)
     print(f"{name:11s} " + " | ".join(f"{k} {sorted(v)[1]:6.1f} ({min(v):.1f}-{max(v):.1f})" for k, v in res.items()), flush=True)

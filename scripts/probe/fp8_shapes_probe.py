@@ -54,9 +54,9 @@ for name, N, K in (("qkv", 3840, 1280), ("proj", 1280, 1280), ("fc1", 5120, 1280
                  "bf16 out": lambda: _lib.gemm_fp8(a, w, sc, bias=bias, out=ob)}
     fl = 2.0 * M * N * K
     for v in (5, 6):
-        L.bf_gemm_set_variant(v)
+        _lib.set_knobs(variant=v)
         for k, f in forms.items():
             ts = sorted(bench(f) for _ in range(3))
             print(f"{name:5s} variant {v} {k:22s} {ts[1]:7.1f} us {fl / ts[1] / 1e6:6.0f} TF  frac {fl / ts[1] / 1e6 / 5000:.3f}",
                   flush=True)
-    L.bf_gemm_set_variant(5)
+    _lib.set_knobs(variant=5)

@@ -28,3 +28,22 @@ def test_library_exports_all_symbols():
     assert not missing, missing
     lib.bf_version.restype = ctypes.c_char_p
     assert b"gfx950" in lib.bf_version()
+
+
+def test_gemm_abi_is_stateless():
+    """no process-wide GEMM / attention knobs in the product ABI (round-5 verdict item 6): the
+    options travel per call in bf_gemm_plan / the _ex variant argument, and the library no longer
+    exports the old setters"""
+    src = open(HEADER).read()
+    assert not re.search(r"\bbf_(gemm|attention)_(set|get|force)_\w*\s*\(", src)
+    lib = ctypes.CDLL(B.build())
+    for gone in ["bf_gemm_set_variant", "bf_gemm_set_tile_rows", "bf_gemm_force_small_tiles",
+                 "bf_gemm_set_group_m", "bf_gemm_set_balanced", "bf_gemm_set_cu_budget",
+                 "bf_gemm_get_cu_budget", "bf_gemm_get_variant", "bf_attention_set_variant"]:
+        assert not hasattr(lib, gone), gone
+    # the Python mirror of bf_gemm_plan has the header's layout (six int32 fields)
+    from boxfusion_amd import _lib
+    body = re.search(r"typedef struct \{([^}]*)\} bf_gemm_plan;", src).group(1)
+    fields = re.findall(r"int32_t\s+(\w+);", body)
+    assert [f for f, _ in _lib.GemmPlan._fields_] == fields
+    assert ctypes.sizeof(_lib.GemmPlan) == 4 * len(fields)

@@ -113,21 +113,17 @@ def test_attention_fp8out_and_causal_sweep(L, seed):
                                      (64, 512, 512), (64, 470, 600)])
 def test_attention_workgroup_forms_bit_identical(L, D, sq, sk):
     """129..288 queries (and 449..512 at head dim 64) run on 4-, 8- or 9-wave workgroups
-    (bf_attention_set_variant 28 / 29 / 30 / 31 / 33; the default picks by head dim and query count; a 4-wave tile's empty waves skip the MFMA
+    (bf_attention_bf16_ex variants 28 / 29 / 30 / 31 / 33; the default picks by head dim and query count; a 4-wave tile's empty waves skip the MFMA
     work): every query's key order and tile order is the same, so every form gives the same bits"""
     B, H = 3, 4
     g = torch.Generator(device="cuda").manual_seed(D * 7 + sq + sk)
     q, k, v = _qkv(B, H, sq, sk, D, g, 3.0)
     outs = []
-    try:
-        for var in (6, 28, 29, 30, 31, 33):
-            L.lib().bf_attention_set_variant(var)
-            o = torch.zeros(B * sq, H * D, device="cuda", dtype=torch.bfloat16)
-            L.attention(q, k, v, o, B, H, sq, sk, D, D ** -0.5)
-            torch.cuda.synchronize()
-            outs.append(o)
-    finally:
-        L.lib().bf_attention_set_variant(6)
+    for var in (6, 28, 29, 30, 31, 33):
+        o = torch.zeros(B * sq, H * D, device="cuda", dtype=torch.bfloat16)
+        L.attention(q, k, v, o, B, H, sq, sk, D, D ** -0.5, variant=var)
+        torch.cuda.synchronize()
+        outs.append(o)
     assert rel_err(outs[0], _ref(q, k, v, B, H, sq, sk, D)) < 1e-2
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
@@ -141,14 +137,10 @@ def test_attention_fp8out_forms_bit_identical(L, D):
     g = torch.Generator(device="cuda").manual_seed(D)
     q, k, v = _qkv(B, H, s, s, D, g, 3.0)
     outs = []
-    try:
-        for var in (6, 28):
-            L.lib().bf_attention_set_variant(var)
-            o8 = torch.zeros(B * s, H * D, device="cuda", dtype=L.FP8)
-            L.attention_fp8out(q, k, v, o8, B, H, s, s, D, D ** -0.5, 16.0)
-            torch.cuda.synchronize()
-            outs.append(o8.view(torch.uint8))
-    finally:
-        L.lib().bf_attention_set_variant(6)
+    for var in (6, 28):
+        o8 = torch.zeros(B * s, H * D, device="cuda", dtype=L.FP8)
+        L.attention_fp8out(q, k, v, o8, B, H, s, s, D, D ** -0.5, 16.0, variant=var)
+        torch.cuda.synchronize()
+        outs.append(o8.view(torch.uint8))
     assert rel_err(outs[0].view(L.FP8).float() / 16.0, _ref(q, k, v, B, H, s, s, D)) < 6e-2
     assert torch.equal(outs[0], outs[1])

@@ -30,27 +30,24 @@ def L():
 def test_gemm_fp8_dispatch(L, M, N, K, kind, bm):
     """bf_gemm_fp8 at every tile height of the persistent kernels (0 = the per-shape model) against
     torch f32 on the same fp8 operands: scale, bias, in-place f32 residual, bf16 output"""
-    L.lib().bf_gemm_set_tile_rows(bm)
-    try:
-        a, w, g = _fp8_pair(M, N, K, 77 + M)
-        bias = torch.randn(N, device="cuda", generator=g)
-        s = 0.37
-        ref = (a.float() @ w.float().T) * s + bias
-        if kind == "resid":
-            r = torch.randn(M, N, device="cuda", generator=g)
-            out = r.clone()
-            L.gemm_fp8(a, w, s, bias, resid=out, out=out)
-            want = ref + r
-        elif kind == "bf16":
-            out = L.gemm_fp8(a, w, s, bias, out_dtype=torch.bfloat16)
-            want = ref
-        else:
-            out = L.gemm_fp8(a, w, s, bias, out_dtype=torch.float32)
-            want = ref
-        torch.cuda.synchronize()
-        assert rel(out, want) < (8e-3 if kind == "bf16" else 5e-5), kind
-    finally:
-        L.lib().bf_gemm_set_tile_rows(0)
+    pl = dict(tile_rows=bm)
+    a, w, g = _fp8_pair(M, N, K, 77 + M)
+    bias = torch.randn(N, device="cuda", generator=g)
+    s = 0.37
+    ref = (a.float() @ w.float().T) * s + bias
+    if kind == "resid":
+        r = torch.randn(M, N, device="cuda", generator=g)
+        out = r.clone()
+        L.gemm_fp8(a, w, s, bias, resid=out, out=out, plan=pl)
+        want = ref + r
+    elif kind == "bf16":
+        out = L.gemm_fp8(a, w, s, bias, out_dtype=torch.bfloat16, plan=pl)
+        want = ref
+    else:
+        out = L.gemm_fp8(a, w, s, bias, out_dtype=torch.float32, plan=pl)
+        want = ref
+    torch.cuda.synchronize()
+    assert rel(out, want) < (8e-3 if kind == "bf16" else 5e-5), kind
 
 
 def rel(a, b):
@@ -242,9 +239,5 @@ def test_attention_fp8_output(L, B, H, S, D):
     assert bool(((dec - ref).abs() <= tol).all())
     # the LDS-staged fp8 rows (default) == the per-lane fragment stores (variant 27)
     o8b = torch.full_like(o8.view(torch.uint8), 0x7F).view(L.FP8)
-    L.lib().bf_attention_set_variant(27)
-    try:
-        L.attention_fp8out(q, k, v, o8b, B, H, S, S, D, D ** -0.5, qs)
-    finally:
-        L.lib().bf_attention_set_variant(6)
+    L.attention_fp8out(q, k, v, o8b, B, H, S, S, D, D ** -0.5, qs, variant=27)
     assert torch.equal(o8.view(torch.uint8), o8b.view(torch.uint8))

@@ -31,8 +31,8 @@ def test_gemm_tile_rows_vs_torch(L, M, N, K, out_bf16, resid, bias, bm):
     """bf_gemm_bf16 at every tile height of k_gemm256q (0 = the per-shape model; 256 with an f32
     residual = k_gemm256p) against torch fp32 on the residual / plain linear forms; every height
     gives the same K-order MFMA chain, so the k_gemm256q heights agree bit for bit."""
-    L.lib().bf_gemm_set_tile_rows(bm)
-    try:
+    pl = dict(tile_rows=bm)
+    if True:
         g = torch.Generator(device="cuda").manual_seed(M + N + K)
         a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
         w = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).bfloat16()
@@ -43,28 +43,26 @@ def test_gemm_tile_rows_vs_torch(L, M, N, K, out_bf16, resid, bias, bm):
             ref = ref + r
         if resid == "inplace":
             out = r.clone()
-            L.gemm(a, w, b, resid=out, out=out)
+            L.gemm(a, w, b, resid=out, out=out, plan=pl)
         elif resid == "separate":
             out = torch.empty(M, N, device="cuda")
-            L.gemm(a, w, b, resid=r, out=out)
+            L.gemm(a, w, b, resid=r, out=out, plan=pl)
         else:
-            out = L.gemm(a, w, b, out_dtype=torch.bfloat16 if out_bf16 else torch.float32)
+            out = L.gemm(a, w, b, out_dtype=torch.bfloat16 if out_bf16 else torch.float32, plan=pl)
         torch.cuda.synchronize()
         assert rel_err(out, ref) < (8e-3 if out_bf16 else 2e-5 * math.sqrt(K / 64) + 1e-5), (M, N, K)
         if bm in (160, 224) and not (resid and bm == 256):
-            L.lib().bf_gemm_set_tile_rows(192)
+            p2 = dict(tile_rows=192)
             if resid == "inplace":
                 out2 = r.clone()
-                L.gemm(a, w, b, resid=out2, out=out2)
+                L.gemm(a, w, b, resid=out2, out=out2, plan=p2)
             elif resid == "separate":
                 out2 = torch.empty(M, N, device="cuda")
-                L.gemm(a, w, b, resid=r, out=out2)
+                L.gemm(a, w, b, resid=r, out=out2, plan=p2)
             else:
-                out2 = L.gemm(a, w, b, out_dtype=torch.bfloat16 if out_bf16 else torch.float32)
+                out2 = L.gemm(a, w, b, out_dtype=torch.bfloat16 if out_bf16 else torch.float32, plan=p2)
             torch.cuda.synchronize()
             assert torch.equal(out, out2), "tile height changed a value"
-    finally:
-        L.lib().bf_gemm_set_tile_rows(0)
 
 
 @pytest.mark.parametrize("M,N,K,act,out_bf16,resid,row_map", [
@@ -175,23 +173,20 @@ def test_gemm_large_tiles(L, small, shape, act, out_bf16, use_resid):
         y = F.gelu(y)
     elif act == "relu":
         y = F.relu(y)
-    lib().bf_gemm_force_small_tiles(1 if small else 0)
-    try:
-        if use_resid:
-            resid = torch.randn(M + 40, N, device="cuda", generator=g)
-            perm = torch.randperm(M + 40, device="cuda", generator=g)[:M].int()
-            perm[::5] = -1
-            out = resid.clone()
-            L.gemm(a, w, b, act=act, resid=out, out=out, row_map=perm)
-            ref = resid.clone()
-            keep = perm >= 0
-            ref[perm[keep].long()] += y[keep]
-            assert rel_err(out, ref) < 1e-5
-        else:
-            out = L.gemm(a, w, b, act=act, out_dtype=torch.bfloat16 if out_bf16 else torch.float32)
-            assert rel_err(out, y) < (5e-3 if out_bf16 else 1e-5)
-    finally:
-        lib().bf_gemm_force_small_tiles(0)
+    pl = dict(kernel=1 if small else 0)
+    if use_resid:
+        resid = torch.randn(M + 40, N, device="cuda", generator=g)
+        perm = torch.randperm(M + 40, device="cuda", generator=g)[:M].int()
+        perm[::5] = -1
+        out = resid.clone()
+        L.gemm(a, w, b, act=act, resid=out, out=out, row_map=perm, plan=pl)
+        ref = resid.clone()
+        keep = perm >= 0
+        ref[perm[keep].long()] += y[keep]
+        assert rel_err(out, ref) < 1e-5
+    else:
+        out = L.gemm(a, w, b, act=act, out_dtype=torch.bfloat16 if out_bf16 else torch.float32, plan=pl)
+        assert rel_err(out, y) < (5e-3 if out_bf16 else 1e-5)
 
 
 @pytest.mark.parametrize("variant", [1, 2])
@@ -208,21 +203,17 @@ def test_gemm_resid_persistent(L, variant, shape, inplace, out_bf16):
     b = torch.randn(N, device="cuda", generator=g)
     resid = torch.randn(M, N, device="cuda", generator=g)
     ref = resid + a.float() @ w.float().T + b
-    prev = lib().bf_gemm_get_variant()
-    lib().bf_gemm_set_variant(variant)
-    try:
-        if inplace:
-            out = resid.clone()
-            L.gemm(a, w, b, resid=out, out=out)
-        else:
-            out = L.gemm(a, w, b, resid=resid, out_dtype=torch.bfloat16 if out_bf16 else torch.float32)
-        assert rel_err(out, ref) < (5e-3 if out_bf16 else 1e-5)
-        # a second call on the same output buffer (persistent walk state must not leak)
-        if not inplace:
-            out2 = L.gemm(a, w, b, resid=resid, out_dtype=out.dtype)
-            assert torch.equal(out2, out)
-    finally:
-        lib().bf_gemm_set_variant(prev)
+    pl = dict(variant=variant)
+    if inplace:
+        out = resid.clone()
+        L.gemm(a, w, b, resid=out, out=out, plan=pl)
+    else:
+        out = L.gemm(a, w, b, resid=resid, out_dtype=torch.bfloat16 if out_bf16 else torch.float32, plan=pl)
+    assert rel_err(out, ref) < (5e-3 if out_bf16 else 1e-5)
+    # a second call on the same output buffer (persistent walk state must not leak)
+    if not inplace:
+        out2 = L.gemm(a, w, b, resid=resid, out_dtype=out.dtype, plan=pl)
+        assert torch.equal(out2, out)
 
 
 @pytest.mark.parametrize("shape", [(3000, 2816, 320), (8292, 1280, 640), (600, 384, 192),
@@ -248,21 +239,16 @@ def test_gemm_overlapped_epilogue(L, shape, kind):
         y = y + resid
     od = torch.bfloat16 if kind in ("bf16", "gelu", "nobias") else torch.float32
 
-    prev = lib().bf_gemm_get_variant()
-
     def run(variant):
-        lib().bf_gemm_set_variant(variant)
-        try:
-            if kind == "resid_inplace":
-                out = resid.clone()
-                L.gemm(a, w, b, resid=out, out=out)
-            else:
-                out = torch.full((M, N), float("nan"), device="cuda", dtype=od)
-                L.gemm(a, w, b, act=act, resid=resid, out=out)
-            torch.cuda.synchronize()
-            return out
-        finally:
-            lib().bf_gemm_set_variant(prev)
+        pl = dict(variant=variant)
+        if kind == "resid_inplace":
+            out = resid.clone()
+            L.gemm(a, w, b, resid=out, out=out, plan=pl)
+        else:
+            out = torch.full((M, N), float("nan"), device="cuda", dtype=od)
+            L.gemm(a, w, b, act=act, resid=resid, out=out, plan=pl)
+        torch.cuda.synchronize()
+        return out
     out_q, out_p = run(6), run(1)
     assert torch.isfinite(out_q).all(), "rows / columns left unwritten"
     tol = 5e-3 if od == torch.bfloat16 else 1e-5
@@ -271,11 +257,7 @@ def test_gemm_overlapped_epilogue(L, shape, kind):
     # out-of-range rows / columns untouched: a padded output view keeps its sentinels
     if kind == "bf16":
         big = torch.full((M + 3, N + 8), 7.0, device="cuda", dtype=od)
-        lib().bf_gemm_set_variant(6)
-        try:
-            L.gemm(a, w, b, out=big[:M, :N])
-        finally:
-            lib().bf_gemm_set_variant(prev)
+        L.gemm(a, w, b, out=big[:M, :N], plan=dict(variant=6))
         assert torch.equal(big[:M, :N], out_q)
         assert (big[M:] == 7.0).all() and (big[:, N:] == 7.0).all()
 
@@ -299,11 +281,7 @@ def test_attention(L, B, H, S, D, variant):
     q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
     o = torch.empty(B * S, H * D, device="cuda", dtype=torch.bfloat16)
     scale = D ** -0.5
-    L.lib().bf_attention_set_variant(variant)
-    try:
-        L.attention(q, k, v, o, B, H, S, S, D, scale)
-    finally:
-        L.lib().bf_attention_set_variant(6)
+    L.attention(q, k, v, o, B, H, S, S, D, scale, variant=variant)
     ref = _attn_ref(q, k, v, B, H, S, D, scale)
     assert rel_err(o, ref) < 1e-2
 
@@ -319,11 +297,7 @@ def test_attention_short_heads_row_stores(L, B, H, S, D):
     outs = {}
     for var in (6, 27):
         o = torch.full((B * S, H * D), float("nan"), device="cuda", dtype=torch.bfloat16)
-        L.lib().bf_attention_set_variant(var)
-        try:
-            L.attention(q, k, v, o, B, H, S, S, D, D ** -0.5)
-        finally:
-            L.lib().bf_attention_set_variant(6)
+        L.attention(q, k, v, o, B, H, S, S, D, D ** -0.5, variant=var)
         outs[var] = o
     assert torch.equal(outs[27], outs[6])
     assert rel_err(outs[6], _attn_ref(q, k, v, B, H, S, D, D ** -0.5)) < 1e-2
@@ -346,11 +320,7 @@ def test_attention_row_stores_equal_fragment_stores(L, B, H, S, D, scatter):
     outs = []
     for var in (27, 6):
         o = torch.full((B * S, H * D), float("nan"), device="cuda", dtype=torch.bfloat16)
-        L.lib().bf_attention_set_variant(var)
-        try:
-            L.attention(q, k, v, o, B, H, S, S, D, D ** -0.5, o_map=om)
-        finally:
-            L.lib().bf_attention_set_variant(6)
+        L.attention(q, k, v, o, B, H, S, S, D, D ** -0.5, o_map=om, variant=var)
         outs.append(o)
     assert torch.equal(outs[1].nan_to_num(7.0), outs[0].nan_to_num(7.0))
 
@@ -448,7 +418,7 @@ def test_crop_resize_im2col(L):
 @pytest.mark.parametrize("act,use_resid", [("gelu", False), (None, True)])
 def test_gemm_balanced_grid(L, act, use_resid):
     """360 tiles of 256x256 (a last round 104/256 full) launch the balanced persistent grid
-    (bf_gemm_set_balanced): every tile is computed the same way whichever workgroup walks it, so
+    (bf_gemm_plan.balanced): every tile is computed the same way whichever workgroup walks it, so
     the output is bit-identical to the one-block-per-CU grid, and matches the fp32 reference"""
     from boxfusion_amd._lib import lib
     g = torch.Generator(device="cuda").manual_seed(23)
@@ -458,18 +428,15 @@ def test_gemm_balanced_grid(L, act, use_resid):
     b = torch.randn(N, device="cuda", generator=g)
     resid = torch.randn(M, N, device="cuda", generator=g) if use_resid else None
     outs = []
-    try:
-        for bal in (1, 0):
-            lib().bf_gemm_set_balanced(bal)
-            if use_resid:
-                o = resid.clone()
-                L.gemm(a, w, b, resid=o, out=o)
-            else:
-                o = L.gemm(a, w, b, act=act, out_dtype=torch.bfloat16)
-            torch.cuda.synchronize()
-            outs.append(o)
-    finally:
-        lib().bf_gemm_set_balanced(1)
+    for bal in (0, 1):          # 0: the default balanced grid, 1: one workgroup per CU
+        pl = dict(balanced=bal)
+        if use_resid:
+            o = resid.clone()
+            L.gemm(a, w, b, resid=o, out=o, plan=pl)
+        else:
+            o = L.gemm(a, w, b, act=act, out_dtype=torch.bfloat16, plan=pl)
+        torch.cuda.synchronize()
+        outs.append(o)
     assert torch.equal(outs[0], outs[1])
     y = a.float() @ w.float().T + b
     if act == "gelu":
@@ -492,18 +459,61 @@ def test_gemm_stem_rowmap_broadcast_resid(L, force):
     pos = torch.randn(npch, W, device="cuda", generator=g)
     row_map = (torch.arange(crops, device="cuda", dtype=torch.int32)[:, None] * S + 1
                + torch.arange(npch, device="cuda", dtype=torch.int32)[None]).reshape(-1)
-    lib().bf_gemm_force_small_tiles(force)        # -1: the persistent 256x256 kernel, 1: 128x128
-    assert bool(lib().bf_gemm_large_tiles(crops * npch, W, K)) == (force < 0)
-    try:
-        X = torch.full((crops * S, W), 7.0, device="cuda")
-        L.gemm(a, w, resid=pos, resid_mod=npch, out=X, row_map=row_map)
-    finally:
-        lib().bf_gemm_force_small_tiles(0)
+    # kernel -1: the persistent 256x256 kernel (the default for this shape), 1: 128x128
+    assert bool(lib().bf_gemm_large_tiles(crops * npch, W, K))
+    X = torch.full((crops * S, W), 7.0, device="cuda")
+    L.gemm(a, w, resid=pos, resid_mod=npch, out=X, row_map=row_map, plan=dict(kernel=force))
     ref = torch.full((crops * S, W), 7.0, device="cuda")
     P = a.float() @ w.float().T
     ref.view(crops, S, W)[:, 1:] = (P.view(crops, npch, W) + pos[None])
     assert rel_err(X, ref) < 1e-5
     assert torch.all(X.view(crops, S, W)[:, 0] == 7.0)      # class-token rows untouched
+
+
+@pytest.mark.parametrize("shape", [(32896, 1280, 1280), (32896, 3840, 1280), (12800, 768, 3072), (128, 5120, 1280)])
+def test_gemm_plan_budgets_two_streams(L, shape):
+    """the GEMM ABI keeps no process-wide state: two streams launch the same problem concurrently
+    with different CU budgets in their per-call plans (224: a rank-0 detect stream beside the
+    fusion reservation; 0: every CU).  The kernel choice follows the device's CU count, only the
+    persistent grid / tile height follow the budget, so both outputs are bit-identical -- and
+    identical to the plan-less bf_gemm_bf16."""
+    M, N, K = shape
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g)
+    r = torch.randn(M, N, device="cuda", generator=g)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    torch.cuda.synchronize()
+    for st, budget in ((s1, 224), (s2, 0), (s1, 96), (s2, 255)):
+        o = r.clone()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(st):
+            L.gemm(a, w, b, resid=o, out=o, plan=L.GemmPlan(cu_budget=budget))
+        outs.append(o)
+    torch.cuda.synchronize()
+    ref = r.clone()
+    L.gemm(a, w, b, resid=ref, out=ref)
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o, ref)
+    assert rel_err(ref, a.float() @ w.float().T + b + r) < 2e-5 * math.sqrt(K / 64) + 1e-5
+    # the thread-local budget of the Python wrapper goes into the plan, and is per thread
+    L.set_cu_budget(160)
+    try:
+        o = r.clone()
+        L.gemm(a, w, b, resid=o, out=o)
+        torch.cuda.synchronize()
+        assert torch.equal(o, ref)
+        import threading
+        seen = []
+        th = threading.Thread(target=lambda: seen.append(L.cu_budget()))
+        th.start()
+        th.join()
+        assert seen == [0] and L.cu_budget() == 160
+    finally:
+        L.set_cu_budget(0)
 
 
 def test_gemm_operand_extent_capacity(L):
