@@ -126,6 +126,11 @@ def parse(argv=None):
     p.add_argument("--depth-ratio", type=int, default=1, choices=(1, 2, 4),
                    help="RGB:depth resolution ratio of the stream (--dataset ca1m: 2 / 4 = a lower-"
                         "resolution depth sensor through the CuTR depth grid; not what CA1MDataset streams)")
+    p.add_argument("--png-depth", action="store_true",
+                   help="every frame's depth arrives as a 16-bit PNG file (bytes resident in HBM) and is "
+                        "decoded on the GPU inside the timed region (bf_png_decode_depth: cv2.imread "
+                        "IMREAD_UNCHANGED + astype(f32) / depth_scale, capture_stream.py:197-203); the "
+                        "line gains a `decode` object with the host PIL decode rate beside it")
     p.add_argument("--cpu-rehearsal", action="store_true",
                    help="CPU/gloo rehearsal of the N-rank control flow (no kernels; test harness)")
     return p.parse_args(argv)
@@ -465,6 +470,66 @@ def auto_rank0_batch(B, ranks):
     return B
 
 
+def png_pool(n, H, W, level=6):
+    """n distinct 16-bit depth PNGs (mm) of the synthetic scene's frames as PIL writes them
+    (adaptive row filters, zlib level 6), the kind of file a ScanNet / CA-1M depth directory holds"""
+    import io
+    from PIL import Image
+    from boxfusion_amd.synthetic import frame_rgbd
+    out = []
+    for f in range(n):
+        d = np.clip(frame_rgbd(f * 5, H, W)[1] * 1000.0, 0, 65535).astype(np.uint16)
+        b = io.BytesIO()
+        Image.fromarray(d).save(b, format="PNG", compress_level=level)
+        out.append(b.getvalue())
+    return out
+
+
+def host_png_rate(pool, threads, seconds=3.0):
+    """PIL decode of the pool on `threads` host threads for ~`seconds` (frames/s): the host decode
+    wall a CPU loader would hit (PIL releases the GIL inside the zlib / unfilter code)"""
+    import io
+    from concurrent.futures import ThreadPoolExecutor
+    from PIL import Image
+
+    def dec(b):
+        return np.asarray(Image.open(io.BytesIO(b)))
+    rep = pool * max(1, -(-4 * threads // len(pool)))
+    n = 0
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(dec, pool))
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            list(ex.map(dec, rep))
+            n += len(rep)
+        return n / (time.perf_counter() - t0)
+
+
+def host_jpeg_rate(threads, seconds=2.0):
+    """PIL decode of a ScanNet-sized colour JPEG (1296 x 968, quality 90: the synthetic scene frame
+    upsampled) on `threads` host threads (frames/s) -- the colour half of cv2.imread
+    (capture_stream.py:194), which stays on the host: only keyframes need their colour image"""
+    import io
+    from concurrent.futures import ThreadPoolExecutor
+    from PIL import Image
+    from boxfusion_amd.synthetic import frame_rgbd
+    img = Image.fromarray(frame_rgbd(3, 480, 640)[0]).resize((1296, 968), Image.BILINEAR)
+    b = io.BytesIO()
+    img.save(b, format="JPEG", quality=90)
+    blob = b.getvalue()
+
+    def dec(_):
+        return np.asarray(Image.open(io.BytesIO(blob)).convert("RGB"))
+    n = 0
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(dec, range(threads)))
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            list(ex.map(dec, range(4 * threads)))
+            n += 4 * threads
+        return n / (time.perf_counter() - t0), len(blob)
+
+
 def emit(line):
     print(json.dumps(line), flush=True)
 
@@ -675,6 +740,24 @@ def main(argv=None):
         # one workspace per in-flight detect stream (the steps on two streams overlap)
         nk_ws = [_lib.new_depth_workspace((G - 1) * Bm, FH // FRAME["r"], FW // FRAME["r"], dev)
                  for _ in range(n_inflight)]
+    png_in = None
+    if args.png_depth:
+        # every frame's depth file of every step (keyframes first, then the non-keyframes in
+        # stream order), bytes resident in HBM before timing; decoded per step in the timed region
+        from boxfusion_amd.capture_stream import upload_files
+        Hd_, Wd_ = FH // FRAME["r"], FW // FRAME["r"]
+        pool = png_pool(16, Hd_, Wd_)
+        png_in = {"pool": pool, "steps": [], "H": Hd_, "W": Wd_}
+        for s_ in range(total_steps):
+            kf = my_frames(s_)
+            ids = list(kf) + [f + o for f in kf for o in range(1, G)]
+            png_in["steps"].append(upload_files([pool[f % len(pool)] for f in ids], dev))
+        nfile = G * Bm
+        tot = max(int(o[2][-1]) for o in png_in["steps"])
+        png_in["work"] = [torch.empty(_lib.png_workspace_bytes(nfile, Hd_, Wd_, tot), dtype=torch.uint8, device=dev)
+                          for _ in range(n_inflight)]
+        png_in["out"] = [torch.empty((nfile, Hd_, Wd_), dtype=torch.float32, device=dev) for _ in range(n_inflight)]
+        png_in["bytes_per_frame"] = float(np.mean([len(pool[f % len(pool)]) for f in range(nfile)]))
     poses_all = np.stack([scene.pose(f) for f in all_mine]).astype(np.float32)
     dets_mine = [scene.detections(f, Kf, (FW, FH)) for f in all_mine]
     rec_all = torch.from_numpy(pack_records(dets_mine, poses_all)).to(dev)
@@ -709,9 +792,17 @@ def main(argv=None):
             st_ctx = torch.cuda.stream(det_streams[k])
             st_ctx.__enter__()      # this step's detect, gather and fusion hand-off on its stream
             det = detects[k]
+            kf_depth = depth_all[sl]
+            if png_in is not None:            # the step's depth files -> f32 depth (GPU decode)
+                files, offs, offs_h = png_in["steps"][s]
+                dec = png_in["out"][k]
+                _lib.png_decode_u16(files, offs, png_in["H"], png_in["W"], out=dec, offsets_host=offs_h,
+                                    depth_scale=CFG["cam"].get("png_depth_scale", 1000.0), work=png_in["work"][k], check=False)
+                kf_depth = dec[:Bm]
             if nk_depth is not None:          # the step's non-keyframes: per-frame work only
-                _lib.depth_preprocess(nk_depth[s], nk_K, nk_RT[s], 10.0, ws=nk_ws[k])
-            det(rgb_all[sl], depth_all[sl], poses_all[sl], return_instances=False,
+                _lib.depth_preprocess(dec[Bm:] if png_in is not None else nk_depth[s], nk_K, nk_RT[s], 10.0,
+                                      ws=nk_ws[k])
+            det(rgb_all[sl], kf_depth, poses_all[sl], return_instances=False,
                 crop_boxes=crops_all[s * Bm * args.crops:(s + 1) * Bm * args.crops])
             if args.breakdown:
                 torch.cuda.synchronize()
@@ -986,6 +1077,39 @@ def main(argv=None):
                         "bf16 peak; the GEMM family is roofline_components.gemm")
         line["roofline"] = head
         line["roofline_components"] = comps
+        if png_in is not None:
+            # the GPU decode alone: one step's files (keyframes + non-keyframes), HIP events, after
+            # the timed region; and PIL on 16 host threads over the same files
+            files, offs, offs_h = png_in["steps"][args.warmup]
+            dec, wk = png_in["out"][0], png_in["work"][0]
+            nfile = len(offs_h) - 1
+            for _ in range(2):
+                _lib.png_decode_u16(files, offs, png_in["H"], png_in["W"], out=dec, offsets_host=offs_h,
+                                    depth_scale=1000.0, work=wk, check=False)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                _lib.png_decode_u16(files, offs, png_in["H"], png_in["W"], out=dec, offsets_host=offs_h,
+                                    depth_scale=1000.0, work=wk, check=False)
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / 5
+            _, st = _lib.png_decode_u16(files, offs, png_in["H"], png_in["W"], out=dec, offsets_host=offs_h,
+                                        depth_scale=1000.0, work=wk, check=True)
+            thr = min(16, os.cpu_count() or 1)
+            line["decode"] = {
+                "kernel": "bf_png_decode_depth (k_png_parse + k_png_gather + k_png_inflate + k_png_unfilter)",
+                "files_per_step": nfile, "bytes_per_file": png_in["bytes_per_frame"],
+                "gpu_ms_per_step": ms, "gpu_frames_per_s": nfile / (ms * 1e-3),
+                "host_pil_frames_per_s": host_png_rate(png_in["pool"], thr), "host_threads": thr,
+                "host_jpeg_keyframes_per_s": None, "jpeg_bytes": None,
+                "note": ("depth files: the synthetic scene's 640x480 depth in mm written by PIL (adaptive "
+                         "filters, zlib level 6); gpu = one step's files decoded alone (HIP events, mean of "
+                         "5); host = PIL on the pool over ~3 s")}
+            jr, jb = host_jpeg_rate(thr)
+            line["decode"].update(host_jpeg_keyframes_per_s=jr, jpeg_bytes=jb,
+                                  keyframes_per_s_needed=line["value"] / G)
+            line["config"]["depth_input"] = "16-bit PNG bytes in HBM, decoded on the GPU in the timed region"
         if args.breakdown:
             line["breakdown_ms_per_step"] = {k: 1e3 * v / args.steps for k, v in brk.items()}
         if not args.no_cpu_baseline and N == 1:   # rank 0 at N=1 only

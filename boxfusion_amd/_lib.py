@@ -808,6 +808,65 @@ def ingest_rgbd(bgr, depth_u16, depth_scale, rot_k=0, rgb_out=None, depth_out=No
     return rgb_out, depth_out
 
 
+PNG_STATUS = {1: "bad signature", 2: "bad IHDR", 4: "unsupported PNG kind", 8: "bad chunk list",
+              16: "bad zlib / deflate stream", 32: "Adler-32 mismatch", 64: "bad row filter", 128: "size mismatch"}
+
+
+def png_decode_u16(files, offsets, H, W, out=None, offsets_host=None, check=True, depth_scale=None, work=None):
+    """cv2.imread(path, IMREAD_UNCHANGED) for F 16-bit greyscale PNGs (capture_stream.py:197/:405):
+    files u8 [total] device bytes of the files back to back, offsets int64 [F+1] device (and the
+    same offsets on the host, `offsets_host`, to size the launch) -> out u16 [F,H,W] and the int32
+    status word per file.  depth_scale given: out f32 [F,H,W] = sample / depth_scale
+    (capture_stream.py:203, bf_png_decode_depth).  check=True synchronises and raises on any file
+    that did not decode."""
+    _need(files, torch.uint8, "files")
+    _need(offsets, torch.int64, "offsets")
+    if offsets_host is None:
+        offsets_host = offsets.cpu()
+    oh = [int(v) for v in offsets_host]
+    F_ = len(oh) - 1
+    if F_ < 0 or offsets.numel() != F_ + 1:
+        raise HipError("png_decode_u16: offsets [F+1]")
+    total = oh[-1] if F_ >= 0 else 0
+    if total > files.numel():
+        raise HipError("png_decode_u16: offsets run past the file bytes")
+    mx = max((oh[i + 1] - oh[i] for i in range(F_)), default=0)
+    wb = png_workspace_bytes(F_, H, W, total)
+    if work is None or work.numel() < wb:
+        work = torch.empty(max(wb, 1), dtype=torch.uint8, device=files.device)
+    dt = torch.uint16 if depth_scale is None else torch.float32
+    if out is None:
+        out = torch.empty((F_, H, W), dtype=dt, device=files.device)
+    _need(out, dt, "out")
+    if out.numel() != F_ * H * W:
+        raise HipError("png_decode_u16: out [F,H,W]")
+    status = torch.zeros(max(F_, 1), dtype=torch.int32, device=files.device)
+    if depth_scale is None:
+        rc = lib().bf_png_decode_u16(_ptr(files), _ptr(offsets), c_int(F_), c_int(H), c_int(W), ctypes.c_longlong(total),
+                                     ctypes.c_longlong(mx), _ptr(out), _ptr(work), c_size_t(wb), _ptr(status),
+                                     _stream())
+    else:
+        rc = lib().bf_png_decode_depth(_ptr(files), _ptr(offsets), c_int(F_), c_int(H), c_int(W),
+                                       ctypes.c_longlong(total), ctypes.c_longlong(mx), c_float(depth_scale),
+                                       _ptr(out), _ptr(work), c_size_t(wb), _ptr(status), _stream())
+    _check(rc, "bf_png_decode")
+    if check and F_:
+        st = status[:F_].cpu()
+        bad = torch.nonzero(st).flatten().tolist()
+        if bad:
+            f = bad[0]
+            why = ", ".join(v for k, v in PNG_STATUS.items() if int(st[f]) & k)
+            raise HipError(f"png_decode_u16: {len(bad)} of {F_} files did not decode (file {f}: {why})")
+    return out, status[:F_]
+
+
+def png_workspace_bytes(F, H, W, total_file_bytes):
+    L = lib()
+    L.bf_png_workspace_bytes.restype = c_size_t
+    L.bf_png_workspace_bytes.argtypes = [c_int, c_int, c_int, ctypes.c_longlong]
+    return int(L.bf_png_workspace_bytes(F, H, W, total_file_bytes))
+
+
 def cv2_resize_u8(src, Wd, Hd, out=None):
     """cv2.resize(src, (Wd, Hd)) (u8 INTER_LINEAR) of u8 images [H,W], [H,W,cn] or [F,H,W,cn]"""
     _need(src, torch.uint8, "src")

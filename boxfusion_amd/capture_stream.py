@@ -7,7 +7,8 @@ depth infos, T_gravity = camera -> gravity rotation, RT = identity) and the `gt`
 camera -> world pose), the frame rotated to the upright orientation first (torch.rot90 on
 whatever device the frame is on).  `make_sample_decoded` / `DecodedFrameStream` take decoded
 colour + 16-bit depth frames and run the rest of the streams' per-frame work on the GPU
-(bf_ingest_rgbd: cvtColor, cv2.resize, depth scaling, rotation).  Image decode stays on the host.
+(bf_ingest_rgbd: cvtColor, cv2.resize, depth scaling, rotation); the 16-bit depth PNGs are decoded on the
+GPU too (bf_png_decode_u16), colour images on the host.
 """
 from __future__ import annotations
 
@@ -104,30 +105,68 @@ def make_sample_decoded(bgr, depth_u16, depth_scale, K, pose, video_id=0, index=
             "meta": dict(video_id=video_id, timestamp=index), "sensor_info": si}
 
 
+def upload_files(blobs, device="cuda"):
+    """file bytes -> (device u8 [total] of the files back to back, device int64 offsets [F+1],
+    host offsets): one pinned staging copy and one host-to-device transfer per batch"""
+    offs = np.zeros(len(blobs) + 1, np.int64)
+    offs[1:] = np.cumsum([len(b) for b in blobs])
+    host = torch.empty(max(int(offs[-1]), 1), dtype=torch.uint8).pin_memory()
+    hv = host.numpy()
+    for b, o in zip(blobs, offs[:-1]):
+        hv[o:o + len(b)] = np.frombuffer(b, np.uint8)
+    dev = host.to(device, non_blocking=True)
+    return dev, torch.from_numpy(offs).to(device, non_blocking=True), offs
+
+
+def decode_depth_pngs(blobs, H, W, device="cuda"):
+    """cv2.imread(p, IMREAD_UNCHANGED) (capture_stream.py:197/:405) for a batch of 16-bit depth
+    PNG files (their bytes), decoded on the GPU (bf_png_decode_u16) -> u16 [F, H, W] on device;
+    raises if any file does not decode"""
+    from boxfusion_amd import _lib
+    files, offs, offs_h = upload_files(blobs, device)
+    out, _ = _lib.png_decode_u16(files, offs, H, W, offsets_host=offs_h)
+    return out
+
+
 class DecodedFrameStream:
     """a ScanNet / CA-1M style frame directory as demo.py's dataset: colour JPEG / PNG and 16-bit
-    depth PNG paths plus camera -> world poses; files are decoded on the host (PIL: the image
-    decoder is not part of the GPU path, and cv2 is absent here) and everything after decode runs
-    in bf_ingest_rgbd on `device`."""
+    depth PNG paths plus camera -> world poses.  Depth PNGs are decoded on the GPU
+    (bf_png_decode_u16, `batch` files per launch); colour images on the host (PIL: cv2 is absent
+    here).  Everything after decode runs in bf_ingest_rgbd on `device`."""
 
-    def __init__(self, color_paths, depth_paths, poses, K, depth_scale, device="cuda", video_id=0):
+    def __init__(self, color_paths, depth_paths, poses, K, depth_scale, device="cuda", video_id=0, batch=16):
         if not (len(color_paths) == len(depth_paths) == len(poses)):
             raise ValueError("one colour image, depth map and pose per frame")
         self.color, self.depth, self.poses = list(color_paths), list(depth_paths), list(poses)
         self.K, self.scale, self.dev, self.video_id = np.asarray(K, np.float32), float(depth_scale), device, video_id
+        self.batch = max(1, int(batch))
 
     def __len__(self):
         return len(self.color)
 
+    def _depth_size(self, path):
+        with open(path, "rb") as fh:
+            head = fh.read(24)
+        if head[:8] != b"\x89PNG\r\n\x1a\n" or head[12:16] != b"IHDR":
+            raise ValueError(f"{path}: not a PNG")
+        return int.from_bytes(head[20:24], "big"), int.from_bytes(head[16:20], "big")
+
     def __iter__(self):
         from PIL import Image
-        for i, (cp, dp) in enumerate(zip(self.color, self.depth)):
-            rgb = np.asarray(Image.open(cp).convert("RGB"))
-            dep = np.asarray(Image.open(dp)).astype(np.uint16)
-            rgb_t = torch.from_numpy(np.ascontiguousarray(rgb)).to(self.dev, non_blocking=True)
-            dep_t = torch.from_numpy(dep.view(np.int16)).to(self.dev, non_blocking=True)
-            yield make_sample_decoded(rgb_t, dep_t, self.scale, self.K, self.poses[i], video_id=self.video_id,
-                                      index=i, src_bgr=False)
+        for b0 in range(0, len(self), self.batch):
+            idx = range(b0, min(len(self), b0 + self.batch))
+            H, W = self._depth_size(self.depth[b0])
+            blobs = []
+            for i in idx:
+                with open(self.depth[i], "rb") as fh:
+                    blobs.append(fh.read())
+            deps = decode_depth_pngs(blobs, H, W, self.dev)
+            for j, i in enumerate(idx):
+                rgb = np.asarray(Image.open(self.color[i]).convert("RGB"))
+                rgb_t = torch.from_numpy(np.ascontiguousarray(rgb)).to(self.dev, non_blocking=True)
+                yield make_sample_decoded(rgb_t, deps[j].view(torch.int16), self.scale, self.K, self.poses[i],
+                                          video_id=self.video_id, index=i, src_bgr=False)
+
 
 class SyntheticDataset:
     """the seeded synthetic RGB-D stream (boxfusion_amd.synthetic) as demo.py's dataset:

@@ -616,6 +616,33 @@ int bf_ingest_rgbd(const uint8_t* bgr, int Hc, int Wc, const uint16_t* depth, in
 int bf_cv2_resize_u8(const uint8_t* src, int Hs, int Ws, int cn, int Hd, int Wd, int F, uint8_t* dst,
                      void* stream);
 
+/* ---- depth PNG decode (reference: cv2.imread(depth_path, cv2.IMREAD_UNCHANGED),
+ * capture_stream.py:197 ScanNet / :405 CA-1M) ----
+ * F PNG files, back to back in device memory: file f = files[offsets[f] .. offsets[f+1]) (offsets
+ * int64 [F+1], device; total_file_bytes = offsets[F], max_file_bytes = the largest file, both as the
+ * host uploaded them) -> out u16 [F,H,W], the sample values in native order (what cv2 returns).
+ * 16-bit greyscale, non-interlaced files of exactly H x W; status int32 [F] (device) gets the
+ * BF_PNG_* bits of a file that did not decode (its out rows are then undefined).  The zlib Adler-32
+ * is verified; chunk CRCs are not.  work: bf_png_workspace_bytes(F, H, W, total_file_bytes) bytes,
+ * caller-owned device memory. */
+#define BF_PNG_BAD_SIGNATURE 1
+#define BF_PNG_BAD_HEADER 2      /* IHDR missing / invalid */
+#define BF_PNG_UNSUPPORTED 4     /* not 16-bit greyscale non-interlaced, or an unknown critical chunk */
+#define BF_PNG_BAD_CHUNK 8       /* truncated chunk, no IDAT, a zlib stream of 2 GiB or more */
+#define BF_PNG_BAD_ZLIB 16       /* invalid zlib header / deflate block / code / distance */
+#define BF_PNG_BAD_ADLER 32
+#define BF_PNG_BAD_FILTER 64     /* row filter type > 4 */
+#define BF_PNG_SIZE 128          /* IHDR size != (W, H) or inflated length != H x (2W + 1) */
+size_t bf_png_workspace_bytes(int F, int H, int W, long long total_file_bytes);
+int bf_png_decode_u16(const uint8_t* files, const int64_t* offsets, int F, int H, int W,
+                      long long total_file_bytes, long long max_file_bytes, uint16_t* out, void* work,
+                      size_t work_bytes, int32_t* status, void* stream);
+/* the same decode fused with the streams' depth scaling (capture_stream.py:203 / :410,
+ * depth_data.astype(np.float32) / depth_scale, IEEE f32 division): depth_out f32 [F,H,W] */
+int bf_png_decode_depth(const uint8_t* files, const int64_t* offsets, int F, int H, int W,
+                        long long total_file_bytes, long long max_file_bytes, float depth_scale,
+                        float* depth_out, void* work, size_t work_bytes, int32_t* status, void* stream);
+
 /* placement probe (diagnostic): n_wg workgroups on `stream`, each spinning `spin` cycles, write
  * out[2b] = HW_ID (CU bits 11:8, SH 12, SE 15:13) and out[2b+1] = XCC id -- which CUs a (CU-masked)
  * stream really runs on */

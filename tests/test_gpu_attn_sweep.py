@@ -67,6 +67,19 @@ def test_attention_dispatch_sweep(L, B, H, sq, sk, D, mult):
     assert rel_err(o, _ref(q, k, v, B, H, sq, sk, D)) < 1e-2, (B, H, sq, sk, D, mult)
 
 
+@pytest.mark.parametrize("sq", [2304, 3136, 4096])
+def test_attention_large_global_blocks(L, sq):
+    """CuTR global blocks at square pads 768 / 896 / 1024 (preprocessor.py:86, vit.py:482):
+    (pad / 16)^2 tokens, 12 heads of 64; B = 2 frames"""
+    B, H, D = 2, 12, 64
+    g = torch.Generator(device="cuda").manual_seed(sq)
+    q, k, v = _qkv(B, H, sq, sq, D, g, 3.0)
+    o = torch.zeros(B * sq, H * D, device="cuda", dtype=torch.bfloat16)
+    L.attention(q, k, v, o, B, H, sq, sq, D, D ** -0.5)
+    torch.cuda.synchronize()
+    assert rel_err(o, _ref(q, k, v, B, H, sq, sq, D)) < 1e-2, sq
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_attention_omap_sweep(L, seed):
     """output rows through o_map (the window attention's token-order write-back, pad queries

@@ -189,7 +189,8 @@ def test_xattn_kernel_vs_torch(dev, B, Nq, q0, h, w):
 
 @pytest.mark.parametrize("H,W,ratio,depth_model", [(480, 640, 2, True), (480, 640, 4, True),
                                                   (512, 384, 2, True), (512, 384, 1, True),
-                                                  (480, 640, 1, False)])
+                                                  (480, 640, 1, False), (576, 768, 2, True),
+                                                  (720, 896, 2, True), (768, 1024, 4, True)])
 def test_cutr_backbone_shapes_vs_fp32(dev, H, W, ratio, depth_model):
     """depth at 1/2 and 1/4 of the image resolution (joint windows of 256 + 64 / 256 + 16 tokens),
     the CA-1M portrait frame (512 square, 2x2 windows) and the RGB-only model (windows without

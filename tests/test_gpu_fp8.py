@@ -119,16 +119,12 @@ def test_gemm_fp8_overlapped_epilogue_vs_serial(L, M, N, K, act):
     if act == "gelu":
         ref = F.gelu(ref)
     oqs = 448.0 / float(ref.abs().max()) * 0.5
-    prev = L.lib().bf_gemm_get_variant()
     outs = {}
-    try:
-        for var in (6, 1):
-            L.lib().bf_gemm_set_variant(var)
-            outs[var] = (L.gemm_fp8(a, w, scale, bias=bias, act=act, out_dtype=torch.bfloat16),
-                         L.gemm_fp8(a, w, scale, bias=bias, act=act, out_dtype=L.FP8, out_qscale=oqs))
-            torch.cuda.synchronize()
-    finally:
-        L.lib().bf_gemm_set_variant(prev)
+    for var in (6, 1):          # per-call bf_gemm_plan.variant
+        outs[var] = (L.gemm_fp8(a, w, scale, bias=bias, act=act, out_dtype=torch.bfloat16, plan={"variant": var}),
+                     L.gemm_fp8(a, w, scale, bias=bias, act=act, out_dtype=L.FP8, out_qscale=oqs,
+                                plan={"variant": var}))
+        torch.cuda.synchronize()
     (bq, fq), (bp, fp) = outs[6], outs[1]
     assert rel(bq, ref) < 5e-3 and rel(bq, bp) < 2e-3
     dq, dp = fq.float() / oqs, fp.float() / oqs
