@@ -22,6 +22,9 @@
 #define PNG_FB 11                 // primary Huffman table bits (longer codes: the bit-serial path)
 #define PNG_RING (1 << 16)        // LDS output window (deflate needs the last 32 KiB)
 #define PNG_FLUSH (1 << 14)
+#ifndef PNG_HALVES
+#define PNG_HALVES 2              // candidate token starts per round: 64 per half (one per lane)
+#endif
 
 struct PngSegTable {              // per file, in the workspace
     uint32_t nseg, zlen, width, height;
@@ -509,87 +512,113 @@ __global__ void __launch_bounds__(64) k_png_inflate(const uint8_t* __restrict__ 
         // longer than PNG_FB bits (or invalid) ends the round and goes through the bit-serial
         // decoder.
         bool eob = false;
-        // the 160-bit window at P (5 words; the next round's is loaded as soon as its P is known,
-        // so the scalar loads fly while this round stores its output)
-        uint32_t Wd[5];
+        // the window at P: 64 * PNG_HALVES + 48 bits of candidate tokens (+ 31 of alignment); the
+        // next round's is loaded as soon as its P is known, so the scalar loads fly while this round
+        // stores its output
+        constexpr int NW = 3 + 2 * PNG_HALVES;
+        uint32_t Wd[NW];
 #pragma unroll
-        for (int k = 0; k < 5; ++k) Wd[k] = z[min((P >> 5) + k, lim)];
+        for (int k = 0; k < NW; ++k) Wd[k] = z[min((P >> 5) + k, lim)];
         while (!eob) {
-            const uint32_t o = (P & 31u) + (uint32_t)lane;
-            const uint32_t kk = o >> 5, sh = o & 31u;
-            const uint32_t d0 = kk == 0 ? Wd[0] : (kk == 1 ? Wd[1] : Wd[2]);
-            const uint32_t d1 = kk == 0 ? Wd[1] : (kk == 1 ? Wd[2] : Wd[3]);
-            const uint32_t d2 = kk == 0 ? Wd[2] : (kk == 1 ? Wd[3] : Wd[4]);
-            uint64_t bits = ((((uint64_t)d1) << 32) | d0) >> sh;
-            if (sh) bits |= ((uint64_t)d2) << (64 - sh);
-            const uint32_t e = L.lit[(uint32_t)bits & ((1u << PNG_FB) - 1u)];
-            const uint32_t len1 = e & 15u, sym = e >> 4;
-            // length code (meaningful for 257..285)
-            const uint32_t c = sym - 257u;
-            const uint32_t eb = (c < 8u || c == 28u) ? 0u : ((c - 4u) >> 2);
-            const uint32_t base = c < 8u ? 3u + c : (c == 28u ? 258u : ((4u + (c & 3u)) << eb) + 3u);
-            uint64_t b2 = bits >> len1;
-            const uint32_t mlen = base + ((uint32_t)b2 & ((1u << eb) - 1u));
-            b2 >>= eb;
-            const uint32_t e2 = L.dist[(uint32_t)b2 & ((1u << PNG_FB) - 1u)];
-            const uint32_t len2 = e2 & 15u, dsy = e2 >> 4;
-            b2 >>= len2;
-            const uint32_t deb = dsy < 4u ? 0u : (dsy >> 1) - 1u;
-            const uint32_t dbase = dsy < 4u ? dsy + 1u : ((2u + (dsy & 1u)) << deb) + 1u;
-            const uint32_t dist = dbase + ((uint32_t)b2 & ((1u << deb) - 1u));
-            const bool is_lit = len1 != 0 && sym < 256u;
-            const bool is_eob = len1 != 0 && sym == 256u;
-            const bool is_match = len1 != 0 && sym > 256u && c <= 28u && len2 != 0 && dsy <= 29u;
-            const uint32_t T = len1 + (is_match ? eb + len2 + deb : 0u);
-            // next token start: lane + T (< 112), end of block 256 + lane + T, bit-serial path
-            // 512 + lane.  The walk stops at the first start >= 64; the lanes it passed are the
-            // round's tokens (an end-of-block or bit-serial lane among them has size 0)
-            const uint32_t nxt = is_lit || is_match ? (uint32_t)lane + T
-                                                    : (is_eob ? 256u + (uint32_t)lane + T : 512u + (uint32_t)lane);
-            const uint32_t sz = is_lit ? 1u : (is_match ? mlen : 0u);
-            // the chain of real token starts (scalar)
-            uint32_t at = 0;
-            uint64_t mem = 0;
-            do {
-                mem |= 1ull << at;
-                at = __builtin_amdgcn_readlane(nxt, at);
-            } while (at < 64u);
-            const bool slow = at >= 512u;
-            if (slow) at -= 512u;
-            else if (at >= 256u) {
-                eob = true;
-                at -= 256u;
+            // candidate token at bit P + 64 h + lane (half h): literal, length + distance with their
+            // extra bits, end of block, or "bit-serial" (a code longer than PNG_FB bits / invalid)
+            uint32_t nxt[PNG_HALVES], sz[PNG_HALVES], lit[PNG_HALVES], mlen[PNG_HALVES], dist[PNG_HALVES];
+            bool is_lit[PNG_HALVES], is_match[PNG_HALVES];
+#pragma unroll
+            for (int h = 0; h < PNG_HALVES; ++h) {
+                const uint32_t o = (P & 31u) + (uint32_t)lane + 64u * h;
+                const uint32_t kk = o >> 5, sh = o & 31u;          // kk in 2h .. 2h + 2
+                const uint32_t d0 = kk == 2 * h ? Wd[2 * h] : (kk == 2 * h + 1 ? Wd[2 * h + 1] : Wd[2 * h + 2]);
+                const uint32_t d1 = kk == 2 * h ? Wd[2 * h + 1] : (kk == 2 * h + 1 ? Wd[2 * h + 2] : Wd[2 * h + 3]);
+                const uint32_t d2 = kk == 2 * h ? Wd[2 * h + 2] : (kk == 2 * h + 1 ? Wd[2 * h + 3] : Wd[2 * h + 4]);
+                uint64_t bits = ((((uint64_t)d1) << 32) | d0) >> sh;
+                if (sh) bits |= ((uint64_t)d2) << (64 - sh);
+                const uint32_t e = L.lit[(uint32_t)bits & ((1u << PNG_FB) - 1u)];
+                const uint32_t len1 = e & 15u, sym = e >> 4;
+                const uint32_t c = sym - 257u;                        // length code (257..285)
+                const uint32_t eb = (c < 8u || c == 28u) ? 0u : ((c - 4u) >> 2);
+                const uint32_t base = c < 8u ? 3u + c : (c == 28u ? 258u : ((4u + (c & 3u)) << eb) + 3u);
+                uint64_t b2 = bits >> len1;
+                mlen[h] = base + ((uint32_t)b2 & ((1u << eb) - 1u));
+                b2 >>= eb;
+                const uint32_t e2 = L.dist[(uint32_t)b2 & ((1u << PNG_FB) - 1u)];
+                const uint32_t len2 = e2 & 15u, dsy = e2 >> 4;
+                b2 >>= len2;
+                const uint32_t deb = dsy < 4u ? 0u : (dsy >> 1) - 1u;
+                const uint32_t dbase = dsy < 4u ? dsy + 1u : ((2u + (dsy & 1u)) << deb) + 1u;
+                dist[h] = dbase + ((uint32_t)b2 & ((1u << deb) - 1u));
+                is_lit[h] = len1 != 0 && sym < 256u;
+                const bool is_eob = len1 != 0 && sym == 256u;
+                is_match[h] = len1 != 0 && sym > 256u && c <= 28u && len2 != 0 && dsy <= 29u;
+                const uint32_t T = len1 + (is_match[h] ? eb + len2 + deb : 0u);
+                // next token start (position 64 h + lane + T), end of block 1024 + start, bit-serial
+                // 2048 + position.  The walk stops at the first start >= 64 * PNG_HALVES
+                const uint32_t me = 64u * h + (uint32_t)lane;
+                nxt[h] = is_lit[h] || is_match[h] ? me + T : (is_eob ? 1024u + me + T : 2048u + me);
+                sz[h] = is_lit[h] ? 1u : (is_match[h] ? mlen[h] : 0u);
+                lit[h] = sym;
             }
-            const bool member = (mem >> lane) & 1ull;
+            // the chain of real token starts (scalar), through the halves in order
+            uint32_t at = 0;
+            uint64_t mem[PNG_HALVES];
+#pragma unroll
+            for (int h = 0; h < PNG_HALVES; ++h) mem[h] = 0;
+#pragma unroll
+            for (int h = 0; h < PNG_HALVES; ++h) {
+                while (at < 64u * (h + 1)) {
+                    mem[h] |= 1ull << (at - 64u * h);
+                    at = __builtin_amdgcn_readlane(nxt[h], at - 64u * h);
+                }
+            }
+            const bool slow = at >= 2048u;
+            if (slow) at -= 2048u;
+            else if (at >= 1024u) {
+                eob = true;
+                at -= 1024u;
+            }
 #ifdef PNG_STATS
             ++n_rounds;
-            n_tok += __popcll(mem);
             n_slow += slow;
-            n_match += __popcll(__ballot(member && is_match));
+#pragma unroll
+            for (int h = 0; h < PNG_HALVES; ++h) {
+                n_tok += __popcll(mem[h]);
+                n_match += __popcll(__ballot(((mem[h] >> lane) & 1ull) && is_match[h]));
+            }
 #endif
             P += at;
             if (!slow) {
 #pragma unroll
-                for (int k = 0; k < 5; ++k) Wd[k] = z[min((P >> 5) + k, lim)];
+                for (int k = 0; k < NW; ++k) Wd[k] = z[min((P >> 5) + k, lim)];
             }
-            // output offsets of the round's tokens: exclusive scan of their sizes in lane order
-            const uint32_t msz = member ? sz : 0u;
-            const uint32_t incl = png_wave_scan(msz);
-            const uint32_t offv = incl - msz;
-            const uint32_t run = __builtin_amdgcn_readlane(incl, 63);
+            // output offsets of the round's tokens: exclusive scan of their sizes in position order
+            uint32_t offv[PNG_HALVES], run = 0;
+            bool member[PNG_HALVES];
+#pragma unroll
+            for (int h = 0; h < PNG_HALVES; ++h) {
+                member[h] = (mem[h] >> lane) & 1ull;
+                const uint32_t msz = member[h] ? sz[h] : 0u;
+                const uint32_t incl = png_wave_scan(msz);
+                offv[h] = run + incl - msz;
+                run += __builtin_amdgcn_readlane(incl, 63);
+            }
             if (run > total - pos) { st |= BF_PNG_SIZE; break; }
-            if (member && is_lit) L.ring[(pos + offv) & (PNG_RING - 1)] = (uint8_t)sym;
-            uint64_t mm = __ballot(member && is_match);
-            while (mm) {
-                const uint32_t j = (uint32_t)__builtin_ctzll(mm);
-                mm &= mm - 1;
-                const uint32_t len = __builtin_amdgcn_readlane(mlen, j);
-                const uint32_t d = __builtin_amdgcn_readlane(dist, j);
-                const uint32_t dst = pos + __builtin_amdgcn_readlane(offv, j);
-                if (d > dst) { st |= BF_PNG_BAD_ZLIB; break; }
-                for (uint32_t k = (uint32_t)lane; k < len; k += 64) {
-                    const uint32_t oo = d >= len ? k : k % d;
-                    L.ring[(dst + k) & (PNG_RING - 1)] = L.ring[(dst - d + oo) & (PNG_RING - 1)];
+#pragma unroll
+            for (int h = 0; h < PNG_HALVES; ++h)
+                if (member[h] && is_lit[h]) L.ring[(pos + offv[h]) & (PNG_RING - 1)] = (uint8_t)lit[h];
+#pragma unroll
+            for (int h = 0; h < PNG_HALVES; ++h) {
+                uint64_t mm = __ballot(member[h] && is_match[h]);
+                while (mm) {
+                    const uint32_t j = (uint32_t)__builtin_ctzll(mm);
+                    mm &= mm - 1;
+                    const uint32_t len = __builtin_amdgcn_readlane(mlen[h], j);
+                    const uint32_t d = __builtin_amdgcn_readlane(dist[h], j);
+                    const uint32_t dst = pos + __builtin_amdgcn_readlane(offv[h], j);
+                    if (d > dst) { st |= BF_PNG_BAD_ZLIB; break; }
+                    for (uint32_t k = (uint32_t)lane; k < len; k += 64) {
+                        const uint32_t oo = d >= len ? k : k % d;
+                        L.ring[(dst + k) & (PNG_RING - 1)] = L.ring[(dst - d + oo) & (PNG_RING - 1)];
+                    }
                 }
             }
             if (st) break;
@@ -621,7 +650,7 @@ __global__ void __launch_bounds__(64) k_png_inflate(const uint8_t* __restrict__ 
                 }
                 P = t.P;
 #pragma unroll
-                for (int k = 0; k < 5; ++k) Wd[k] = z[min((P >> 5) + k, lim)];
+                for (int k = 0; k < NW; ++k) Wd[k] = z[min((P >> 5) + k, lim)];
             }
             if (pos - flushed >= PNG_FLUSH) {
                 const uint32_t to = pos & ~15u;
@@ -691,23 +720,40 @@ __global__ void __launch_bounds__(64) k_png_unfilter(const uint8_t* __restrict__
         bad |= ft > 4;
         uint32_t mine = 0, up_prev = 0;          // (hi << 8 | lo) of this lane's last pixel / last row-above pixel
         // the filtered pixels of a chunk of 8 steps are loaded one chunk ahead
+        // every lane loads every step (address clamped into the row, the value selected after), so
+        // the 8 loads of a chunk issue back to back instead of one branch and wait each
+        auto ld = [&](int x) -> uint32_t {
+            const int xc = x < 0 ? 0 : (x >= W ? W - 1 : x);
+            // the sample's two bytes as one (unaligned: rows are 2W + 1 bytes) 16-bit load, byte-swapped at use
+            return (uint32_t)*reinterpret_cast<const uint16_t*>(row + 1 + 2 * xc);
+        };
+        // the raw loads go through an empty asm at their use (the next chunk), so the compiler
+        // can neither sink them into a branch nor wait for them early
+        auto fix = [&](uint32_t (&v)[8], int x0) {
+            asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+                         "+v"(v[7]));
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int x = x0 + j;
+                v[j] = (valid && x >= 0 && x < W) ? (((v[j] & 255u) << 8) | (v[j] >> 8)) : 0u;
+            }
+        };
         uint32_t cur[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int x = j - lane;
-            cur[j] = (valid && x >= 0 && x < W) ? ((uint32_t)row[1 + 2 * x] << 8) | row[2 + 2 * x] : 0u;
-        }
+        for (int j = 0; j < 8; ++j) cur[j] = ld(j - lane);
+        fix(cur, -lane);
         for (int t0 = 0; t0 < W + 63; t0 += 8) {
             uint32_t nxt[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int x = t0 + 8 + j - lane;
-                nxt[j] = (valid && x >= 0 && x < W) ? ((uint32_t)row[1 + 2 * x] << 8) | row[2 + 2 * x] : 0u;
-            }
+            for (int j = 0; j < 8; ++j) nxt[j] = ld(t0 + 8 + j - lane);     // fixed up next chunk
             // lane 0's row above for the chunk (the previous band's last row), read ahead of the chain
             uint32_t pv[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) pv[j] = (lane == 0 && b0 > 0 && t0 + j < W) ? prev[t0 + j] : 0u;
+            for (int j = 0; j < 8; ++j) pv[j] = prev[t0 + j < W ? t0 + j : 0];
+            asm volatile("" : "+v"(pv[0]), "+v"(pv[1]), "+v"(pv[2]), "+v"(pv[3]), "+v"(pv[4]), "+v"(pv[5]),
+                         "+v"(pv[6]), "+v"(pv[7]));
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pv[j] = (b0 > 0 && t0 + j < W) ? pv[j] : 0u;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int x = t0 + j - lane;
@@ -731,6 +777,7 @@ __global__ void __launch_bounds__(64) k_png_unfilter(const uint8_t* __restrict__
             }
 #pragma unroll
             for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
+            fix(cur, t0 + 8 - lane);
         }
         __syncthreads();
     }

@@ -30,11 +30,11 @@ def main():
         cyc, rt, rounds, tok, slow, match = a[:, 0], a[:, 1] * 10.0, a[:, 2], a[:, 3], a[:, 4], a[:, 5]
         ucyc, urt = a[:, 6], a[:, 7] * 10.0
         print(f"{name}: {F} files, {np.mean([len(b) for b in blobs]) / 1e3:.0f} KB")
-        print(f"  inflate: {rt.mean() / 1e3:.2f} ms/file (max {rt.max() / 1e3:.2f}), clock {np.mean(cyc / rt) * 1e3:.0f} MHz, "
+        print(f"  inflate: {rt.mean() / 1e6:.2f} ms/file (max {rt.max() / 1e6:.2f}), clock {np.mean(cyc / rt) * 1e3:.0f} MHz, "
               f"{rounds.mean():.0f} rounds, {tok.mean():.0f} tokens ({tok.mean() / rounds.mean():.2f}/round), "
               f"{slow.mean():.0f} bit-serial, {match.mean():.0f} matches; "
               f"{cyc.mean() / rounds.mean():.0f} cycles/round, {cyc.mean() / tok.mean():.0f} cycles/token")
-        print(f"  unfilter: {urt.mean() / 1e3:.2f} ms/file, clock {np.mean(ucyc / urt) * 1e3:.0f} MHz, "
+        print(f"  unfilter: {urt.mean() / 1e6:.2f} ms/file, clock {np.mean(ucyc / urt) * 1e3:.0f} MHz, "
               f"{ucyc.mean() / (480 / 64 * (640 + 63)):.0f} cycles/step")
 
 
