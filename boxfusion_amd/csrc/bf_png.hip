@@ -530,32 +530,42 @@ __global__ void __launch_bounds__(64) k_png_inflate(const uint8_t* __restrict__ 
                 const uint32_t kk = o >> 5, sh = o & 31u;          // kk in 2h .. 2h + 2
                 const uint32_t d0 = kk == 2 * h ? Wd[2 * h] : (kk == 2 * h + 1 ? Wd[2 * h + 1] : Wd[2 * h + 2]);
                 const uint32_t d1 = kk == 2 * h ? Wd[2 * h + 1] : (kk == 2 * h + 1 ? Wd[2 * h + 2] : Wd[2 * h + 3]);
-                const uint32_t d2 = kk == 2 * h ? Wd[2 * h + 2] : (kk == 2 * h + 1 ? Wd[2 * h + 3] : Wd[2 * h + 4]);
-                uint64_t bits = ((((uint64_t)d1) << 32) | d0) >> sh;
-                if (sh) bits |= ((uint64_t)d2) << (64 - sh);
-                const uint32_t e = L.lit[(uint32_t)bits & ((1u << PNG_FB) - 1u)];
+                // the first 32 bits at the candidate start (a literal / length code is <= 15 bits)
+                const uint32_t b32 = __builtin_amdgcn_alignbit(d1, d0, sh);
+                const uint32_t e = L.lit[b32 & ((1u << PNG_FB) - 1u)];
                 const uint32_t len1 = e & 15u, sym = e >> 4;
-                const uint32_t c = sym - 257u;                        // length code (257..285)
-                const uint32_t eb = (c < 8u || c == 28u) ? 0u : ((c - 4u) >> 2);
-                const uint32_t base = c < 8u ? 3u + c : (c == 28u ? 258u : ((4u + (c & 3u)) << eb) + 3u);
-                uint64_t b2 = bits >> len1;
-                mlen[h] = base + ((uint32_t)b2 & ((1u << eb) - 1u));
-                b2 >>= eb;
-                const uint32_t e2 = L.dist[(uint32_t)b2 & ((1u << PNG_FB) - 1u)];
-                const uint32_t len2 = e2 & 15u, dsy = e2 >> 4;
-                b2 >>= len2;
-                const uint32_t deb = dsy < 4u ? 0u : (dsy >> 1) - 1u;
-                const uint32_t dbase = dsy < 4u ? dsy + 1u : ((2u + (dsy & 1u)) << deb) + 1u;
-                dist[h] = dbase + ((uint32_t)b2 & ((1u << deb) - 1u));
                 is_lit[h] = len1 != 0 && sym < 256u;
                 const bool is_eob = len1 != 0 && sym == 256u;
-                is_match[h] = len1 != 0 && sym > 256u && c <= 28u && len2 != 0 && dsy <= 29u;
-                const uint32_t T = len1 + (is_match[h] ? eb + len2 + deb : 0u);
+                bool mt = false;
+                uint32_t T = len1;
+                mlen[h] = 0;
+                dist[h] = 0;
+                // length + distance decode only when some lane of the half decoded a length symbol
+                // (literal-heavy streams -- noisy depth -- rarely have one at any of the 64 starts)
+                if (__any(len1 != 0 && sym > 256u)) {
+                    const uint32_t d2 = kk == 2 * h ? Wd[2 * h + 2] : (kk == 2 * h + 1 ? Wd[2 * h + 3] : Wd[2 * h + 4]);
+                    const uint64_t bits = ((uint64_t)__builtin_amdgcn_alignbit(d2, d1, sh) << 32) | b32;
+                    const uint32_t c = sym - 257u;                    // length code (257..285)
+                    const uint32_t eb = (c < 8u || c == 28u) ? 0u : ((c - 4u) >> 2);
+                    const uint32_t base = c < 8u ? 3u + c : (c == 28u ? 258u : ((4u + (c & 3u)) << eb) + 3u);
+                    uint64_t b2 = bits >> len1;
+                    mlen[h] = base + ((uint32_t)b2 & ((1u << eb) - 1u));
+                    b2 >>= eb;
+                    const uint32_t e2 = L.dist[(uint32_t)b2 & ((1u << PNG_FB) - 1u)];
+                    const uint32_t len2 = e2 & 15u, dsy = e2 >> 4;
+                    b2 >>= len2;
+                    const uint32_t deb = dsy < 4u ? 0u : (dsy >> 1) - 1u;
+                    const uint32_t dbase = dsy < 4u ? dsy + 1u : ((2u + (dsy & 1u)) << deb) + 1u;
+                    dist[h] = dbase + ((uint32_t)b2 & ((1u << deb) - 1u));
+                    mt = len1 != 0 && sym > 256u && c <= 28u && len2 != 0 && dsy <= 29u;
+                    if (mt) T = len1 + eb + len2 + deb;
+                }
+                is_match[h] = mt;
                 // next token start (position 64 h + lane + T), end of block 1024 + start, bit-serial
                 // 2048 + position.  The walk stops at the first start >= 64 * PNG_HALVES
                 const uint32_t me = 64u * h + (uint32_t)lane;
-                nxt[h] = is_lit[h] || is_match[h] ? me + T : (is_eob ? 1024u + me + T : 2048u + me);
-                sz[h] = is_lit[h] ? 1u : (is_match[h] ? mlen[h] : 0u);
+                nxt[h] = is_lit[h] || mt ? me + T : (is_eob ? 1024u + me + T : 2048u + me);
+                sz[h] = is_lit[h] ? 1u : (mt ? mlen[h] : 0u);
                 lit[h] = sym;
             }
             // the chain of real token starts (scalar), through the halves in order

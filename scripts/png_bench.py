@@ -15,11 +15,17 @@ from PIL import Image
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
 
-def make_pngs(n_distinct=16, H=480, W=640, level=6):
+def make_pngs(n_distinct=16, H=480, W=640, level=6, smooth=False):
+    """smooth=True: the same frames with the sensor noise box-filtered away (5 x 5) before the
+    mm quantisation -- a more compressible file (longer matches), closer to a filtered depth map"""
     from boxfusion_amd.synthetic import frame_rgbd
     out = []
     for f in range(n_distinct):
-        d = np.clip(frame_rgbd(f * 5, H, W)[1] * 1000.0, 0, 65535).astype(np.uint16)
+        d = frame_rgbd(f * 5, H, W)[1].astype(np.float64)
+        if smooth:
+            from scipy.ndimage import uniform_filter
+            d = np.where(d > 0, uniform_filter(d, 5), 0.0)
+        d = np.clip(d * 1000.0, 0, 65535).astype(np.uint16)
         b = io.BytesIO()
         Image.fromarray(d).save(b, format="PNG", compress_level=level)
         out.append(b.getvalue())

@@ -19,7 +19,9 @@ def main():
     from scripts.png_bench import make_pngs
     L = _lib.lib()
     pool = make_pngs()
-    for name, blobs in (("pil_level6_noisy", [pool[i % len(pool)] for i in range(F)]),):
+    pool_s = make_pngs(smooth=True)
+    for name, blobs in (("pil_level6_noisy", [pool[i % len(pool)] for i in range(F)]),
+                        ("pil_level6_smoothed", [pool_s[i % len(pool_s)] for i in range(F)])):
         files, offs, offs_h = upload_files(blobs, "cuda")
         for rep in range(2):
             out, st = _lib.png_decode_u16(files, offs, 480, 640, offsets_host=offs_h, depth_scale=1000.0)
