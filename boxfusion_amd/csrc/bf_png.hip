@@ -702,8 +702,17 @@ __device__ __forceinline__ uint32_t png_paeth(uint32_t a, uint32_t b, uint32_t c
     return (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
 }
 
+// branch-free: every candidate computed, the row's filter type selects by masks (a divergent
+// switch became jumps to far blocks, several per step of the unfilter's serial chain)
+__device__ __forceinline__ uint32_t png_sel(bool c, uint32_t x, uint32_t y) { return y ^ ((x ^ y) & (0u - (uint32_t)c)); }
 __device__ __forceinline__ uint32_t png_pred(uint32_t ft, uint32_t a, uint32_t b, uint32_t c) {
-    return ft == 1 ? a : ft == 2 ? b : ft == 3 ? ((a + b) >> 1) : ft == 4 ? png_paeth(a, b, c) : 0u;
+    const int p = (int)a + (int)b - (int)c;
+    const int pa = abs(p - (int)a), pb = abs(p - (int)b), pc = abs(p - (int)c);
+    const uint32_t pth = png_sel(pa <= pb && pa <= pc, a, png_sel(pb <= pc, b, c));
+    uint32_t r = png_sel(ft == 1, a, 0u);
+    r = png_sel(ft == 2, b, r);
+    r = png_sel(ft == 3, (a + b) >> 1, r);
+    return png_sel(ft == 4, pth, r);
 }
 
 // OutT uint16_t: the samples (cv2.imread IMREAD_UNCHANGED); float: sample / depth_scale in IEEE
