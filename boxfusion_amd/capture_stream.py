@@ -134,12 +134,19 @@ class DecodedFrameStream:
     (bf_png_decode_u16, `batch` files per launch); colour images on the host (PIL: cv2 is absent
     here).  Everything after decode runs in bf_ingest_rgbd on `device`."""
 
-    def __init__(self, color_paths, depth_paths, poses, K, depth_scale, device="cuda", video_id=0, batch=16):
+    def __init__(self, color_paths, depth_paths, poses, K, depth_scale, device="cuda", video_id=0, batch=16,
+                 depth_decode="gpu", host_threads=16):
+        """depth_decode "gpu": bf_png_decode_u16 on `batch` files per launch; "host": PIL on
+        `host_threads` threads (the faster choice when a GPU's share of host cores decodes more
+        files per second than the GPU path, DESIGN.md §4 "Depth PNG decode")"""
         if not (len(color_paths) == len(depth_paths) == len(poses)):
             raise ValueError("one colour image, depth map and pose per frame")
+        if depth_decode not in ("gpu", "host"):
+            raise ValueError("depth_decode: 'gpu' or 'host'")
         self.color, self.depth, self.poses = list(color_paths), list(depth_paths), list(poses)
         self.K, self.scale, self.dev, self.video_id = np.asarray(K, np.float32), float(depth_scale), device, video_id
         self.batch = max(1, int(batch))
+        self.depth_decode, self.host_threads = depth_decode, max(1, int(host_threads))
 
     def __len__(self):
         return len(self.color)
@@ -156,11 +163,17 @@ class DecodedFrameStream:
         for b0 in range(0, len(self), self.batch):
             idx = range(b0, min(len(self), b0 + self.batch))
             H, W = self._depth_size(self.depth[b0])
-            blobs = []
-            for i in idx:
-                with open(self.depth[i], "rb") as fh:
-                    blobs.append(fh.read())
-            deps = decode_depth_pngs(blobs, H, W, self.dev)
+            if self.depth_decode == "gpu":
+                blobs = []
+                for i in idx:
+                    with open(self.depth[i], "rb") as fh:
+                        blobs.append(fh.read())
+                deps = decode_depth_pngs(blobs, H, W, self.dev)
+            else:
+                from concurrent.futures import ThreadPoolExecutor
+                with ThreadPoolExecutor(self.host_threads) as ex:
+                    arrs = list(ex.map(lambda i: np.asarray(Image.open(self.depth[i])).astype(np.uint16), idx))
+                deps = torch.from_numpy(np.stack(arrs).view(np.int16)).to(self.dev).view(torch.uint16)
             for j, i in enumerate(idx):
                 rgb = np.asarray(Image.open(self.color[i]).convert("RGB"))
                 rgb_t = torch.from_numpy(np.ascontiguousarray(rgb)).to(self.dev, non_blocking=True)

@@ -203,11 +203,12 @@ def test_decoded_frame_stream_reads_png_files(L, tmp_path):
     up = np.eye(4, dtype=np.float32)
     up[1:3, :3] = [[0, 0, 1], [0, -1, 0]]           # camera y down the world z: the upright roll
     poses = [up] * 5
-    stream = DecodedFrameStream(cps, dps, poses, SCANNET_K, 1000.0, device="cuda", batch=2)
-    n = 0
-    for i, s in enumerate(stream):
-        dep = s["wide"]["depth"]
-        want = torch.from_numpy(deps[i].astype(np.float32) / np.float32(1000.0))
-        torch.testing.assert_close(dep.reshape(480, 640).cpu(), want, rtol=0, atol=0)
-        n += 1
-    assert n == 5
+    for mode in ("gpu", "host"):
+        stream = DecodedFrameStream(cps, dps, poses, SCANNET_K, 1000.0, device="cuda", batch=2, depth_decode=mode)
+        n = 0
+        for i, s in enumerate(stream):
+            dep = s["wide"]["depth"]
+            want = torch.from_numpy(deps[i].astype(np.float32) / np.float32(1000.0))
+            torch.testing.assert_close(dep.reshape(480, 640).cpu(), want, rtol=0, atol=0)
+            n += 1
+        assert n == 5, mode
