@@ -867,6 +867,48 @@ def png_workspace_bytes(F, H, W, total_file_bytes):
     return int(L.bf_png_workspace_bytes(F, H, W, total_file_bytes))
 
 
+JPEG_STATUS = {1: "bad / missing marker segment", 2: "unsupported JPEG kind (not baseline 1/3-component h2v2/h2v1/h1v1)",
+               4: "size mismatch", 8: "corrupt entropy-coded data"}
+
+
+def jpeg_decode_rgb(files, offsets, H, W, out=None, check=True, work=None):
+    """cv2.imread(color_path) for F baseline JPEGs (capture_stream.py:194/:402), in RGB order (the
+    cvtColor(BGR2RGB) of the streams folded in): files u8 [total] device bytes back to back, offsets
+    int64 [F+1] device -> out u8 [F,H,W,3] and the int32 status word per file (BF_JPG_* bits).
+    check=True synchronises and raises on any file that did not decode."""
+    _need(files, torch.uint8, "files")
+    _need(offsets, torch.int64, "offsets")
+    F_ = offsets.numel() - 1
+    if F_ < 0:
+        raise HipError("jpeg_decode_rgb: offsets [F+1]")
+    wb = jpeg_workspace_bytes(F_, H, W)
+    if work is None or work.numel() < wb:
+        work = torch.empty(max(wb, 1), dtype=torch.uint8, device=files.device)
+    if out is None:
+        out = torch.empty((F_, H, W, 3), dtype=torch.uint8, device=files.device)
+    _need(out, torch.uint8, "out")
+    if out.numel() != F_ * H * W * 3:
+        raise HipError("jpeg_decode_rgb: out [F,H,W,3]")
+    status = torch.zeros(max(F_, 1), dtype=torch.int32, device=files.device)
+    _check(lib().bf_jpeg_decode_rgb(_ptr(files), _ptr(offsets), c_int(F_), c_int(H), c_int(W), _ptr(out), _ptr(work),
+                                    c_size_t(wb), _ptr(status), _stream()), "bf_jpeg_decode_rgb")
+    if check and F_:
+        st = status[:F_].cpu()
+        bad = torch.nonzero(st).flatten().tolist()
+        if bad:
+            f = bad[0]
+            why = ", ".join(v for k, v in JPEG_STATUS.items() if int(st[f]) & k)
+            raise HipError(f"jpeg_decode_rgb: {len(bad)} of {F_} files did not decode (file {f}: {why})")
+    return out, status[:F_]
+
+
+def jpeg_workspace_bytes(F, H, W):
+    L = lib()
+    L.bf_jpeg_workspace_bytes.restype = c_size_t
+    L.bf_jpeg_workspace_bytes.argtypes = [c_int, c_int, c_int]
+    return int(L.bf_jpeg_workspace_bytes(F, H, W))
+
+
 def cv2_resize_u8(src, Wd, Hd, out=None):
     """cv2.resize(src, (Wd, Hd)) (u8 INTER_LINEAR) of u8 images [H,W], [H,W,cn] or [F,H,W,cn]"""
     _need(src, torch.uint8, "src")

@@ -28,6 +28,7 @@ SOURCES = {
     "bf_dec_native.hip": EXACT,
     "bf_ingest.hip": EXACT,
     "bf_png.hip": EXACT,
+    "bf_jpeg.hip": EXACT,
     "bf_fseq.hip": EXACT,
 }
 EXTRA = [s for s in sorted(os.listdir(CSRC)) if s.endswith(".hip") and s not in SOURCES]

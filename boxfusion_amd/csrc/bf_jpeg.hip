@@ -1,0 +1,572 @@
+// bf_jpeg.hip — baseline JPEG decode on the GPU (the colour half of frame
+// ingestion): cv2.imread(color_path) of the reference's capture streams (capture_stream.py:194
+// ScanNet, :402 CA-1M), i.e. libjpeg(-turbo)'s default decompression of a sequential Huffman JPEG:
+// entropy decode (ITU T.81 F.2), dequantisation and the accurate integer IDCT (jidctint.c "islow"),
+// fancy (triangle) upsampling of 4:2:0 / 4:2:2 chroma (jdsample.c, context rows replicated at the
+// image edges) and the fixed-point YCbCr -> RGB tables of jdcolor.c.  Every step is integer
+// arithmetic, so the result is checked for equality (oracle/jpeg.py, pinned to PIL's libjpeg-turbo).
+//
+// Four launches per batch of F files (device bytes back to back + F+1 offsets), all H x W:
+//   k_jpeg_parse    one wave per file: markers (DQT, SOF0/1, DHT, DRI, SOS), the frame and scan
+//                   layout, the entropy-coded segment's extent
+//   k_jpeg_entropy  one wave per file: the lanes un-stuff the entropy bytes (FF 00 -> FF, RSTn
+//                   dropped) into an LDS ring 64 bytes per step; the Huffman walk runs wave-uniform
+//                   (10-bit primary tables in LDS, a 16-bit canonical slow path), each block's
+//                   coefficients gathered in LDS and stored by the 64 lanes (one int16 per lane)
+//   k_jpeg_idct     one thread per 8 x 8 block: dequantise, islow IDCT, post-IDCT range limit
+//   k_jpeg_color    one thread per pixel: fancy upsampling of the chroma planes + ycc -> RGB (u8 HWC)
+#include "bf_common.h"
+
+#define JPG_FB 10
+#define JPG_RING 4096
+
+struct JpegInfo {                 // per file, in the workspace (written by k_jpeg_parse)
+    uint32_t nc, hmax, vmax, mcux, mcuy, dri, ent_off, ent_len;
+    uint32_t h[3], v[3], tq[3], td[3], ta[3], bw[3], bh[3], coff[3];   // coff: block offset of the comp's grid
+    uint16_t q[4][64];            // natural order
+    uint8_t dht[8][16 + 256];     // DC 0-3, AC 4-7: counts[16], values
+    uint32_t dht_mask, q_mask;
+};
+
+static inline size_t jpg_align(size_t v, size_t a) { return (v + a - 1) / a * a; }
+__host__ __device__ inline uint32_t jpg_blocks_cap(int H, int W) {
+    return 3u * (2u * (((uint32_t)H + 15) / 16)) * (2u * (((uint32_t)W + 15) / 16));
+}
+
+__device__ __forceinline__ uint32_t jrfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__constant__ uint8_t jpg_zigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                                       12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                                       35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                                       58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+// ---- markers ----------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_jpeg_parse(const uint8_t* __restrict__ files, const int64_t* __restrict__ offs,
+                                                   int F, int H, int W, JpegInfo* __restrict__ infos,
+                                                   int32_t* __restrict__ status) {
+    const int f = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (f >= F) return;
+    const uint8_t* p = files + offs[f];
+    const long long n = offs[f + 1] - offs[f];
+    JpegInfo* I = infos + f;
+    int st = 0;
+    bool frame = false, scan = false;
+    uint32_t dht_mask = 0, q_mask = 0;
+    if (n < 4 || p[0] != 0xFF || p[1] != 0xD8) st |= BF_JPG_BAD_MARKER;
+    if (lane == 0) {
+        I->dri = 0;
+        I->nc = 0;
+    }
+    long long pos = 2;
+    while (!st && !scan) {
+        while (pos < n && p[pos] == 0xFF && pos + 1 < n && p[pos + 1] == 0xFF) ++pos;   // fill bytes
+        if (pos + 4 > n || p[pos] != 0xFF) { st |= BF_JPG_BAD_MARKER; break; }
+        const uint32_t m = p[pos + 1];
+        if (m == 0xD9) { st |= BF_JPG_BAD_MARKER; break; }                              // EOI before SOS
+        const uint32_t len = ((uint32_t)p[pos + 2] << 8) | p[pos + 3];
+        if (len < 2 || pos + 2 + len > n) { st |= BF_JPG_BAD_MARKER; break; }
+        const uint8_t* s = p + pos + 4;
+        const uint32_t sl = len - 2;
+        if (m == 0xDB) {                                                                 // DQT
+            uint32_t i = 0;
+            while (i < sl) {
+                const uint32_t pq = s[i] >> 4, t = s[i] & 15;
+                if (t > 3 || pq > 1 || i + 1 + (pq ? 128u : 64u) > sl) { st |= BF_JPG_BAD_MARKER; break; }
+                const uint32_t zz = jpg_zigzag[lane];
+                const uint32_t val = pq ? (((uint32_t)s[i + 1 + 2 * lane] << 8) | s[i + 2 + 2 * lane]) : s[i + 1 + lane];
+                I->q[t][zz] = (uint16_t)val;
+                q_mask |= 1u << t;
+                i += 1 + (pq ? 128 : 64);
+            }
+        } else if (m == 0xC0 || m == 0xC1) {                                             // SOF0 / SOF1
+            if (sl < 6) { st |= BF_JPG_BAD_MARKER; break; }
+            const uint32_t prec = s[0], hh = ((uint32_t)s[1] << 8) | s[2], ww = ((uint32_t)s[3] << 8) | s[4], nc = s[5];
+            if (prec != 8 || (nc != 1 && nc != 3) || sl < 6 + 3 * nc) { st |= BF_JPG_UNSUPPORTED; break; }
+            if ((int)hh != H || (int)ww != W) st |= BF_JPG_SIZE;
+            // a single-component scan is non-interleaved: one block per MCU whatever the factors say
+            auto fh = [&](uint32_t c) -> uint32_t { return nc == 1 ? 1u : (uint32_t)(s[7 + 3 * c] >> 4); };
+            auto fv = [&](uint32_t c) -> uint32_t { return nc == 1 ? 1u : (uint32_t)(s[7 + 3 * c] & 15); };
+            uint32_t hm = 1, vm = 1;
+            for (uint32_t c = 0; c < nc; ++c) {
+                const uint32_t h = fh(c), v = fv(c), tq = s[8 + 3 * c];
+                if (h < 1 || h > 2 || v < 1 || v > 2 || tq > 3) st |= BF_JPG_UNSUPPORTED;
+                if (lane == 0) { I->h[c] = h; I->v[c] = v; I->tq[c] = tq; }
+                hm = max(hm, h);
+                vm = max(vm, v);
+            }
+            // luma at full resolution, chroma at full or half (h2v2 / h2v1 / h1v1 upsampling only)
+            for (uint32_t c = 0; c < nc; ++c) {
+                const uint32_t h = fh(c), v = fv(c);
+                if (h == 0 || v == 0 || hm % h || vm % v || (vm / v == 2 && hm / h != 2)) st |= BF_JPG_UNSUPPORTED;
+                if (c == 0 && (h != hm || v != vm)) st |= BF_JPG_UNSUPPORTED;
+            }
+            if (lane == 0) {
+                I->nc = nc; I->hmax = hm; I->vmax = vm;
+                I->mcux = (ww + 8 * hm - 1) / (8 * hm);
+                I->mcuy = (hh + 8 * vm - 1) / (8 * vm);
+                uint32_t off = 0;
+                for (uint32_t c = 0; c < nc; ++c) {
+                    const uint32_t h = fh(c), v = fv(c);
+                    I->bw[c] = I->mcux * h;
+                    I->bh[c] = I->mcuy * v;
+                    I->coff[c] = off;
+                    off += I->bw[c] * I->bh[c];
+                }
+            }
+            frame = true;
+        } else if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {       // progressive, lossless, arithmetic
+            st |= BF_JPG_UNSUPPORTED;
+        } else if (m == 0xC4) {                                                          // DHT
+            uint32_t i = 0;
+            while (i + 17 <= sl) {
+                const uint32_t tc = s[i] >> 4, th = s[i] & 15;
+                if (tc > 1 || th > 3) { st |= BF_JPG_BAD_MARKER; break; }
+                uint32_t cnt = 0;
+                for (int k = 0; k < 16; ++k) cnt += s[i + 1 + k];
+                if (cnt > 256 || i + 17 + cnt > sl) { st |= BF_JPG_BAD_MARKER; break; }
+                uint8_t* d = I->dht[tc * 4 + th];
+                for (uint32_t k = lane; k < 16 + cnt; k += 64) d[k] = s[i + 1 + k];
+                for (uint32_t k = 16 + cnt + lane; k < 16 + 256; k += 64) d[k] = 0;
+                dht_mask |= 1u << (tc * 4 + th);
+                i += 17 + cnt;
+            }
+        } else if (m == 0xDD) {                                                          // DRI
+            if (sl < 2) { st |= BF_JPG_BAD_MARKER; break; }
+            if (lane == 0) I->dri = ((uint32_t)s[0] << 8) | s[1];
+        } else if (m == 0xDA) {                                                          // SOS
+            if (!frame || sl < 1) { st |= BF_JPG_BAD_MARKER; break; }
+            const uint32_t ns = s[0];
+            uint32_t nc = 0;
+            // one interleaved scan of every component (sequential JPEG as libjpeg / PIL write it)
+            if (sl < 4 + 2 * ns) { st |= BF_JPG_BAD_MARKER; break; }
+            nc = I->nc;
+            if (ns != nc) { st |= BF_JPG_UNSUPPORTED; break; }
+            for (uint32_t k = 0; k < ns; ++k) {
+                const uint32_t td = s[2 + 2 * k] >> 4, ta = s[2 + 2 * k] & 15;
+                if (td > 3 || ta > 3) st |= BF_JPG_BAD_MARKER;
+                if (lane == 0) { I->td[k] = td; I->ta[k] = ta; }
+            }
+            const uint32_t ss = s[1 + 2 * ns], se = s[2 + 2 * ns], ahal = s[3 + 2 * ns];
+            if (ss != 0 || se != 63 || ahal != 0) st |= BF_JPG_UNSUPPORTED;
+            // entropy data: up to the first marker that is not RSTn or a stuffed FF
+            long long e = pos + 2 + len, j = e;
+            while (j + 1 < n) {
+                if (p[j] == 0xFF && p[j + 1] != 0 && !(p[j + 1] >= 0xD0 && p[j + 1] <= 0xD7)) break;
+                ++j;
+            }
+            if (j + 1 >= n) j = n;
+            if (lane == 0) { I->ent_off = (uint32_t)e; I->ent_len = (uint32_t)(j - e); }
+            scan = true;
+        }
+        pos += 2 + len;
+    }
+    if (!st && !scan) st |= BF_JPG_BAD_MARKER;
+    if (lane == 0) {
+        I->dht_mask = dht_mask;
+        I->q_mask = q_mask;
+        if (frame && scan) {
+            if (!st) {
+                for (uint32_t c = 0; c < I->nc; ++c)
+                    if (!((q_mask >> I->tq[c]) & 1) || !((dht_mask >> I->td[c]) & 1) || !((dht_mask >> (4 + I->ta[c])) & 1))
+                        st |= BF_JPG_BAD_MARKER;
+            }
+        }
+        status[f] = st;
+    }
+}
+
+// ---- entropy decode -----------------------------------------------------------------------------
+struct JpegLds {
+    uint16_t fast[8][1 << JPG_FB];    // (len << 8) | value for codes <= JPG_FB bits, 0 otherwise
+    int32_t maxcode[8][18];           // jdhuff.c: largest code of each length (-1: none), [17] sentinel
+    int32_t valoff[8][17];
+    uint8_t vals[8][256];
+    int16_t blk[64];
+    __attribute__((aligned(16))) uint8_t ring[JPG_RING];
+};
+
+// canonical table (T.81 Annex C / jdhuff.c jpeg_make_d_derived_tbl) from counts + values
+__device__ bool jpg_build(JpegLds& L, int t, const uint8_t* dht) {
+    const int lane = threadIdx.x;
+    for (int i = lane; i < (1 << JPG_FB); i += 64) L.fast[t][i] = 0;
+    for (int i = lane; i < 256; i += 64) L.vals[t][i] = dht[16 + i];
+    __syncthreads();
+    bool ok = true;
+    {
+        int code = 0;                 // over-subscribed tables (jdhuff.c "Bogus Huffman table") are refused
+        for (int l = 1; l <= 16; ++l) {
+            code += dht[l - 1];
+            if (code > (1 << l)) ok = false;
+            code <<= 1;
+        }
+    }
+    if (lane == 0 && ok) {
+        int code = 0, p = 0;
+        for (int l = 1; l <= 16; ++l) {
+            const int c = dht[l - 1];
+            if (c) {
+                L.valoff[t][l] = p - code;
+                for (int k = 0; k < c; ++k, ++p, ++code) {
+                    if (l <= JPG_FB) {
+                        const int base = code << (JPG_FB - l);
+                        for (int j = 0; j < (1 << (JPG_FB - l)); ++j)
+                            L.fast[t][base + j] = (uint16_t)((l << 8) | dht[16 + p]);
+                    }
+                }
+                L.maxcode[t][l] = code - 1;
+            } else {
+                L.maxcode[t][l] = -1;
+                L.valoff[t][l] = 0;
+            }
+            code <<= 1;
+        }
+        L.maxcode[t][17] = 0x7fffffff;
+    }
+    __syncthreads();
+    return ok;
+}
+
+struct JpgBits {                  // MSB-first bit buffer over the un-stuffed LDS ring
+    uint64_t buf;                 // valid bits left-aligned at bit 63
+    int nb;
+    uint32_t rp;                  // next ring byte to load
+};
+
+// the entropy-decode kernel: one wave per file
+__global__ void __launch_bounds__(64) k_jpeg_entropy(const uint8_t* __restrict__ files, const int64_t* __restrict__ offs,
+                                                     const JpegInfo* __restrict__ infos, int16_t* __restrict__ coef,
+                                                     uint32_t blocks_cap, int32_t* __restrict__ status) {
+    __shared__ JpegLds L;
+    const int f = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (status[f]) return;
+    const JpegInfo* I = infos + f;
+    const uint8_t* ent = files + offs[f] + I->ent_off;
+    const uint32_t elen = I->ent_len;
+    const uint32_t nc = I->nc;
+    int16_t* out = coef + (size_t)f * blocks_cap * 64;
+    bool tables_ok = true;
+    for (int t = 0; t < 8; ++t)
+        if ((I->dht_mask >> t) & 1) tables_ok &= jpg_build(L, t, I->dht[t]);
+    if (!tables_ok) {
+        if (lane == 0) status[f] |= BF_JPG_BAD_MARKER;
+        return;
+    }
+
+    // producer state: source byte position, bytes produced into the ring, last source byte
+    uint32_t sp = 0, prod = 0, prev = 0, real_end = 0xffffffffu;
+    bool ended = false;
+    auto produce = [&]() {        // 64 source bytes -> the ring, stuffing and RSTn removed
+        if (ended) {
+            // past the end of the segment: zeros (as libjpeg feeds zeros after a marker)
+            L.ring[(prod + lane) & (JPG_RING - 1)] = 0;
+            prod += 64;
+            return;
+        }
+        const uint32_t i = sp + lane;
+        const uint32_t b = i < elen ? ent[i] : 0u;
+        // the shuffles run on all 64 lanes (a lane masked off during one reads back garbage)
+        const uint32_t bu = (uint32_t)__shfl_up((int)b, 1, 64);
+        const uint32_t bp = lane == 0 ? prev : bu;
+        const uint32_t bn = (uint32_t)__shfl_down((int)b, 1, 64);
+        const uint32_t bnext = lane == 63 ? (i + 1 < elen ? ent[i + 1] : 0u) : bn;
+        // drop: the 00 after an FF, an RSTn (FF Dx: both bytes); bytes past the segment end
+        const bool is_rst_ff = b == 0xFF && bnext >= 0xD0 && bnext <= 0xD7 && i + 1 < elen;
+        const bool is_rst_d = bp == 0xFF && b >= 0xD0 && b <= 0xD7 && i < elen && i > 0;
+        const bool keep = i < elen && !(bp == 0xFF && b == 0 && i > 0) && !is_rst_ff && !is_rst_d;
+        const unsigned long long km = __ballot(keep);
+        const uint32_t o = (uint32_t)bf_lanes_below(km);
+        if (keep) L.ring[(prod + o) & (JPG_RING - 1)] = (uint8_t)b;
+        prod += (uint32_t)__popcll(km);
+        prev = jrfl((uint32_t)__shfl((int)b, 63, 64));
+        __builtin_amdgcn_wave_barrier();
+        sp += 64;
+        if (sp >= elen) {
+            ended = true;
+            real_end = prod;                                       // un-stuffed bytes of real data
+        }
+    };
+    while (prod < 1024) produce();
+    JpgBits br{0, 0, 0};
+    auto refill = [&]() {         // keep >= 32 bits in the buffer
+        while (br.nb <= 32) {
+            if (br.rp + 8 > prod) { while (br.rp + 1024 > prod) produce(); }
+            const uint32_t byte = jrfl(L.ring[br.rp & (JPG_RING - 1)]);
+            br.buf |= (uint64_t)byte << (56 - br.nb);
+            br.nb += 8;
+            ++br.rp;
+        }
+    };
+    auto getb = [&](int s) -> uint32_t {        // s <= 16 bits
+        if (s == 0) return 0u;
+        refill();
+        const uint32_t v = (uint32_t)(br.buf >> (64 - s));
+        br.buf <<= s;
+        br.nb -= s;
+        return v;
+    };
+    auto decode = [&](int t, int& err) -> uint32_t {
+        refill();
+        const uint32_t e = jrfl(L.fast[t][(uint32_t)(br.buf >> (64 - JPG_FB))]);
+        if (e) {
+            const int l = (int)(e >> 8);
+            br.buf <<= l;
+            br.nb -= l;
+            return e & 255u;
+        }
+        const uint32_t w = (uint32_t)(br.buf >> 48);                   // 16 bits
+        for (int l = JPG_FB + 1; l <= 16; ++l) {
+            const int code = (int)(w >> (16 - l));
+            const int mc = (int)jrfl((uint32_t)L.maxcode[t][l]);
+            if (code <= mc) {
+                br.buf <<= l;
+                br.nb -= l;
+                return jrfl(L.vals[t][(code + (int)jrfl((uint32_t)L.valoff[t][l])) & 255]);
+            }
+        }
+        err = 1;
+        return 0u;
+    };
+    int err = 0;
+    int pred[3] = {0, 0, 0};
+    const uint32_t nmcu = I->mcux * I->mcuy, dri = I->dri;
+    uint32_t td[3], ta[3], hh[3], vv[3], bw[3], coff[3];
+    for (uint32_t c = 0; c < 3; ++c) {
+        const bool in = c < nc;
+        td[c] = in ? I->td[c] : 0; ta[c] = in ? I->ta[c] : 0; hh[c] = in ? I->h[c] : 0; vv[c] = in ? I->v[c] : 0;
+        bw[c] = in ? I->bw[c] : 0; coff[c] = in ? I->coff[c] : 0;
+    }
+    bool insufficient = false;
+    for (uint32_t mcu = 0; mcu < nmcu && !err; ++mcu) {
+        if (dri && mcu && mcu % dri == 0) {
+            // restart interval: byte-align (the RSTn bytes are gone from the ring), reset predictors
+            const int drop = br.nb & 7;
+            br.buf <<= drop;
+            br.nb -= drop;
+            pred[0] = pred[1] = pred[2] = 0;
+        }
+        // jdhuff.c: once a decode has needed bits past the end of the data, the rest of the MCUs
+        // are left zero (uniform grey), not decoded from the zero fill
+        if ((uint64_t)br.rp * 8 - (uint64_t)br.nb > (uint64_t)real_end * 8) insufficient = true;
+        const uint32_t my = mcu / I->mcux, mx = mcu - my * I->mcux;
+        if (insufficient) {
+            for (uint32_t c = 0; c < nc; ++c)
+                for (uint32_t v = 0; v < vv[c]; ++v)
+                    for (uint32_t h = 0; h < hh[c]; ++h) {
+                        const size_t blk_i = (size_t)coff[c] + (size_t)(my * vv[c] + v) * bw[c] + mx * hh[c] + h;
+                        out[blk_i * 64 + lane] = 0;
+                    }
+            continue;
+        }
+        for (uint32_t c = 0; c < nc && !err; ++c) {
+            for (uint32_t v = 0; v < vv[c] && !err; ++v)
+                for (uint32_t h = 0; h < hh[c] && !err; ++h) {
+                    L.blk[lane] = 0;
+                    const uint32_t s = decode(td[c], err);
+                    if (err || s > 11) { err = 1; break; }
+                    uint32_t r = getb((int)s);
+                    int diff = (int)r;
+                    if (s && r < (1u << (s - 1))) diff = (int)r - (1 << s) + 1;
+                    pred[c] += diff;
+                    if (lane == 0) L.blk[0] = (int16_t)pred[c];
+                    for (int k = 1; k < 64;) {
+                        const uint32_t rs = decode(4 + ta[c], err);
+                        if (err) break;
+                        const int run = (int)(rs >> 4), sz = (int)(rs & 15);
+                        if (sz) {
+                            k += run;
+                            if (k > 63) { err = 1; break; }
+                            const uint32_t bits = getb(sz);
+                            int val = (int)bits;
+                            if (bits < (1u << (sz - 1))) val = (int)bits - (1 << sz) + 1;
+                            if (lane == 0) L.blk[jpg_zigzag[k]] = (int16_t)val;
+                            ++k;
+                        } else if (run == 15) {
+                            k += 16;
+                        } else {
+                            break;
+                        }
+                    }
+                    if (err) break;
+                    const uint32_t by = my * vv[c] + v, bx = mx * hh[c] + h;
+                    const size_t blk_i = (size_t)coff[c] + (size_t)by * bw[c] + bx;
+                    __builtin_amdgcn_wave_barrier();
+                    out[blk_i * 64 + lane] = L.blk[lane];
+                }
+        }
+    }
+    if (err && lane == 0) status[f] |= BF_JPG_BAD_DATA;
+}
+
+// ---- IDCT (jidctint.c jpeg_idct_islow) ----------------------------------------------------------
+#define JI_CB 13
+#define JI_P1 2
+#define JFIX(x) ((int)((x) * (1 << JI_CB) + 0.5))
+
+// the post-IDCT range-limit table of jdmaster.c, indexed by v & 1023 (v centred at 0)
+__device__ __forceinline__ uint32_t jpg_range(int v) {
+    const int i = v & 1023;
+    return i < 128 ? (uint32_t)(i + 128) : (i < 512 ? 255u : (i < 896 ? 0u : (uint32_t)(i - 896)));
+}
+
+__device__ __forceinline__ void jpg_idct_1d(const long long z[8], long long o[8]) {
+    // even part
+    const long long z1e = (z[2] + z[6]) * JFIX(0.541196100);
+    const long long t2 = z1e + z[6] * (-JFIX(1.847759065));
+    const long long t3 = z1e + z[2] * JFIX(0.765366865);
+    const long long t0 = (z[0] + z[4]) * (1 << JI_CB);
+    const long long t1 = (z[0] - z[4]) * (1 << JI_CB);
+    const long long t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
+    // odd part
+    long long o0 = z[7], o1 = z[5], o2 = z[3], o3 = z[1];
+    long long zz1 = o0 + o3, zz2 = o1 + o2, zz3 = o0 + o2, zz4 = o1 + o3;
+    const long long zz5 = (zz3 + zz4) * JFIX(1.175875602);
+    o0 *= JFIX(0.298631336);
+    o1 *= JFIX(2.053119869);
+    o2 *= JFIX(3.072711026);
+    o3 *= JFIX(1.501321110);
+    zz1 *= -JFIX(0.899976223);
+    zz2 *= -JFIX(2.562915447);
+    zz3 = zz3 * (-JFIX(1.961570560)) + zz5;
+    zz4 = zz4 * (-JFIX(0.390180644)) + zz5;
+    o0 += zz1 + zz3;
+    o1 += zz2 + zz4;
+    o2 += zz2 + zz3;
+    o3 += zz1 + zz4;
+    o[0] = t10 + o3; o[7] = t10 - o3;
+    o[1] = t11 + o2; o[6] = t11 - o2;
+    o[2] = t12 + o1; o[5] = t12 - o1;
+    o[3] = t13 + o0; o[4] = t13 - o0;
+}
+
+__global__ void __launch_bounds__(256) k_jpeg_idct(const JpegInfo* __restrict__ infos, const int16_t* __restrict__ coef,
+                                                   uint32_t blocks_cap, int F, uint8_t* __restrict__ planes,
+                                                   const int32_t* __restrict__ status) {
+    const int f = blockIdx.y;
+    if (f >= F || status[f]) return;
+    const JpegInfo* I = infos + f;
+    const uint32_t nc = I->nc;
+    uint32_t total = 0;
+    for (uint32_t c = 0; c < nc; ++c) total += I->bw[c] * I->bh[c];
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= total) return;
+    uint32_t c = 0;
+    while (c + 1 < nc && b >= I->coff[c + 1]) ++c;
+    const uint32_t local = b - I->coff[c], by = local / I->bw[c], bx = local - by * I->bw[c];
+    const int16_t* src = coef + ((size_t)f * blocks_cap + b) * 64;
+    const uint16_t* q = I->q[I->tq[c]];
+    int ws[64];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {                      // pass 1: columns
+        long long z[8], o[8];
+#pragma unroll
+        for (int v = 0; v < 8; ++v) z[v] = (int)src[v * 8 + u] * (int)q[v * 8 + u];
+        jpg_idct_1d(z, o);
+#pragma unroll
+        for (int v = 0; v < 8; ++v) ws[v * 8 + u] = (int)((o[v] + (1 << (JI_CB - JI_P1 - 1))) >> (JI_CB - JI_P1));
+    }
+    uint8_t* plane = planes + ((size_t)f * blocks_cap + I->coff[c]) * 64;   // the comp's plane: bh*8 x bw*8
+    const uint32_t pw = I->bw[c] * 8;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {                      // pass 2: rows
+        long long z[8], o[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) z[u] = ws[v * 8 + u];
+        jpg_idct_1d(z, o);
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t s = jpg_range((int)((o[u] + (1 << (JI_CB + JI_P1 + 3 - 1))) >> (JI_CB + JI_P1 + 3)));
+            if (u < 4) lo |= s << (8 * u); else hi |= s << (8 * (u - 4));
+        }
+        uint2* dst = reinterpret_cast<uint2*>(plane + (size_t)(by * 8 + v) * pw + bx * 8);
+        *dst = make_uint2(lo, hi);
+    }
+}
+
+// ---- upsampling + colour conversion ----------------------------------------------------------
+// chroma sample of the fancy upsampler (jdsample.c h2v2 / h2v1; fullsize copy) at output (x, y)
+__device__ __forceinline__ int jpg_chroma(const uint8_t* pl, uint32_t pw, int cw, int ch, int rx, int ry, int x, int y) {
+    if (rx == 1 && ry == 1) return pl[(size_t)y * pw + x];
+    const int c = x >> 1, e = x & 1;
+    auto S = [&](int col, int row) -> int { return pl[(size_t)row * pw + col]; };
+    if (ry == 1) {                                      // h2v1_fancy_upsample
+        const int row = y;
+        if (cw == 1) return S(0, row);
+        if (c == 0 && e == 0) return S(0, row);
+        if (c == cw - 1 && e == 1) return S(cw - 1, row);
+        const int m = S(c, row) * 3;
+        return e == 0 ? (m + S(c - 1, row) + 1) >> 2 : (m + S(c + 1, row) + 2) >> 2;
+    }
+    // h2v2_fancy_upsample: column sums with the row above (even output row) or below (odd)
+    const int r = y >> 1, d = y & 1;
+    const int rn = d == 0 ? (r > 0 ? r - 1 : 0) : (r + 1 < ch ? r + 1 : ch - 1);
+    auto colsum = [&](int col) -> int { return S(col, r) * 3 + S(col, rn); };
+    const int s = colsum(c);
+    if (cw == 1) return e == 0 ? (s * 4 + 8) >> 4 : (s * 4 + 7) >> 4;
+    if (e == 0) return c == 0 ? (s * 4 + 8) >> 4 : (s * 3 + colsum(c - 1) + 8) >> 4;
+    return c == cw - 1 ? (s * 4 + 7) >> 4 : (s * 3 + colsum(c + 1) + 7) >> 4;
+}
+
+__global__ void __launch_bounds__(256) k_jpeg_color(const JpegInfo* __restrict__ infos, const uint8_t* __restrict__ planes,
+                                                    uint32_t blocks_cap, int F, int H, int W, uint8_t* __restrict__ rgb,
+                                                    const int32_t* __restrict__ status) {
+    const int f = blockIdx.y;
+    if (f >= F || status[f]) return;
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= (uint32_t)H * W) return;
+    const int y = (int)(p / W), x = (int)(p - (uint32_t)y * W);
+    const JpegInfo* I = infos + f;
+    const uint8_t* base = planes + (size_t)f * blocks_cap * 64;
+    uint8_t* o = rgb + ((size_t)f * H * W + p) * 3;
+    const int Y = base[(size_t)I->coff[0] * 64 + (size_t)y * (I->bw[0] * 8) + x];
+    if (I->nc == 1) {
+        o[0] = o[1] = o[2] = (uint8_t)Y;
+        return;
+    }
+    int cc[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t c = 1 + k;
+        const int rx = (int)(I->hmax / I->h[c]), ry = (int)(I->vmax / I->v[c]);
+        const int cw = (int)((W * I->h[c] + I->hmax - 1) / I->hmax), ch = (int)((H * I->v[c] + I->vmax - 1) / I->vmax);
+        cc[k] = jpg_chroma(base + (size_t)I->coff[c] * 64, I->bw[c] * 8, cw, ch, rx, ry, x, y);
+    }
+    // jdcolor.c ycc_rgb_convert, SCALEBITS 16
+    const int cb = cc[0] - 128, cr = cc[1] - 128;
+    const int half = 1 << 15;
+    const int r = Y + ((91881 * cr + half) >> 16);                  // FIX(1.40200) = 91881
+    const int g = Y + (((-22554) * cb + half + (-46802) * cr) >> 16); // FIX(0.34414) = 22554, FIX(0.71414) = 46802
+    const int b = Y + ((116130 * cb + half) >> 16);                 // FIX(1.77200) = 116130
+    o[0] = (uint8_t)min(max(r, 0), 255);
+    o[1] = (uint8_t)min(max(g, 0), 255);
+    o[2] = (uint8_t)min(max(b, 0), 255);
+}
+
+BF_API size_t bf_jpeg_workspace_bytes(int F, int H, int W) {
+    if (F < 0 || H <= 0 || W <= 0) return 0;
+    const size_t cap = jpg_blocks_cap(H, W);
+    return jpg_align((size_t)F * sizeof(JpegInfo), 256) + jpg_align((size_t)F * cap * 64 * 2, 256) +
+           jpg_align((size_t)F * cap * 64, 256);
+}
+
+BF_API int bf_jpeg_decode_rgb(const uint8_t* files, const int64_t* offsets, int F, int H, int W, uint8_t* rgb,
+                              void* work, size_t work_bytes, int32_t* status, void* stream) {
+    if (!files || !offsets || !rgb || !work || !status || F < 0 || H <= 0 || W <= 0) return BF_ERR_ARG;
+    if (H > 16384 || W > 16384) return BF_ERR_UNSUPPORTED;
+    if (work_bytes < bf_jpeg_workspace_bytes(F, H, W)) return BF_ERR_CAPACITY;
+    if (F == 0) return BF_OK;
+    const uint32_t cap = jpg_blocks_cap(H, W);
+    uint8_t* w = static_cast<uint8_t*>(work);
+    JpegInfo* infos = reinterpret_cast<JpegInfo*>(w);
+    int16_t* coef = reinterpret_cast<int16_t*>(w + jpg_align((size_t)F * sizeof(JpegInfo), 256));
+    uint8_t* planes = w + jpg_align((size_t)F * sizeof(JpegInfo), 256) + jpg_align((size_t)F * cap * 64 * 2, 256);
+    hipStream_t s = bf_stream(stream);
+    hipLaunchKernelGGL(k_jpeg_parse, dim3(F), dim3(64), 0, s, files, offsets, F, H, W, infos, status);
+    hipLaunchKernelGGL(k_jpeg_entropy, dim3(F), dim3(64), 0, s, files, offsets, infos, coef, cap, status);
+    hipLaunchKernelGGL(k_jpeg_idct, dim3((cap + 255) / 256, F), dim3(256), 0, s, infos, coef, cap, F, planes, status);
+    const unsigned gp = (unsigned)(((size_t)H * W + 255) / 256);
+    hipLaunchKernelGGL(k_jpeg_color, dim3(gp, F), dim3(256), 0, s, infos, planes, cap, F, H, W, rgb, status);
+    return bf_check_launch();
+}

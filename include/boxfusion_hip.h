@@ -643,6 +643,22 @@ int bf_png_decode_depth(const uint8_t* files, const int64_t* offsets, int F, int
                         long long total_file_bytes, long long max_file_bytes, float depth_scale,
                         float* depth_out, void* work, size_t work_bytes, int32_t* status, void* stream);
 
+/* ---- colour JPEG decode (reference: cv2.imread(color_path), capture_stream.py:194 ScanNet /
+ * :402 CA-1M -- libjpeg's default decompression, which PIL's decoder reproduces) ----
+ * F baseline (sequential Huffman, 8-bit) JPEG files, back to back in device memory as for the PNG
+ * decode, each exactly H x W, 1 or 3 components, chroma at full or half resolution (4:4:4, 4:2:2,
+ * 4:2:0), restart markers allowed -> rgb u8 [F,H,W,3] (RGB order; grey files replicated).  islow
+ * integer IDCT, fancy upsampling, jdcolor fixed-point YCbCr -> RGB: bit-exact to libjpeg's
+ * defaults.  status int32 [F] gets the BF_JPG_* bits of a file that did not decode (its rows are
+ * then undefined).  work: bf_jpeg_workspace_bytes(F, H, W) bytes of caller-owned device memory. */
+#define BF_JPG_BAD_MARKER 1      /* no SOI, truncated / invalid marker segment, missing tables */
+#define BF_JPG_UNSUPPORTED 2     /* progressive / arithmetic / 12-bit / 2 or 4 components / other sampling / multi-scan */
+#define BF_JPG_SIZE 4            /* frame size != (W, H) */
+#define BF_JPG_BAD_DATA 8        /* invalid Huffman code or coefficient index in the entropy data */
+size_t bf_jpeg_workspace_bytes(int F, int H, int W);
+int bf_jpeg_decode_rgb(const uint8_t* files, const int64_t* offsets, int F, int H, int W, uint8_t* rgb,
+                       void* work, size_t work_bytes, int32_t* status, void* stream);
+
 /* placement probe (diagnostic): n_wg workgroups on `stream`, each spinning `spin` cycles, write
  * out[2b] = HW_ID (CU bits 11:8, SH 12, SE 15:13) and out[2b+1] = XCC id -- which CUs a (CU-masked)
  * stream really runs on */
