@@ -149,14 +149,10 @@ __global__ void __launch_bounds__(64) k_jpeg_parse(const uint8_t* __restrict__ f
             }
             const uint32_t ss = s[1 + 2 * ns], se = s[2 + 2 * ns], ahal = s[3 + 2 * ns];
             if (ss != 0 || se != 63 || ahal != 0) st |= BF_JPG_UNSUPPORTED;
-            // entropy data: up to the first marker that is not RSTn or a stuffed FF
-            long long e = pos + 2 + len, j = e;
-            while (j + 1 < n) {
-                if (p[j] == 0xFF && p[j + 1] != 0 && !(p[j + 1] >= 0xD0 && p[j + 1] <= 0xD7)) break;
-                ++j;
-            }
-            if (j + 1 >= n) j = n;
-            if (lane == 0) { I->ent_off = (uint32_t)e; I->ent_len = (uint32_t)(j - e); }
+            // entropy data: the rest of the file (the decode stops at the first marker that is
+            // neither RSTn nor a stuffed FF)
+            const long long e = pos + 2 + len;
+            if (lane == 0) { I->ent_off = (uint32_t)e; I->ent_len = (uint32_t)(n - e); }
             scan = true;
         }
         pos += 2 + len;
@@ -177,13 +173,38 @@ __global__ void __launch_bounds__(64) k_jpeg_parse(const uint8_t* __restrict__ f
 }
 
 // ---- entropy decode -----------------------------------------------------------------------------
+// One wave per file.  The lanes un-stuff the entropy bytes into an LDS ring (JPG_SUB x 64 source
+// bytes per refill, all loads in flight together; FF 00 -> FF, RSTn dropped, the first other
+// marker ends the segment).  Decoding is speculative, as in the PNG inflate: each round, lane l
+// decodes the token (Huffman code + its extra bits) that would start at bit P + l, once with each
+// table a component of the scan uses (DC and AC); the scalar walk then follows the chain of real
+// token starts through the per-lane results with v_readlane, across block and MCU boundaries, and
+// ends the round at the first token starting past the 64 lanes.  A block's coefficients build up
+// in one VGPR (lane i = natural index i) and are stored by the 64 lanes at its end.
+#define JPG_SUB 8
+
+#ifdef JPG_STATS
+// diagnostic build (scripts/build_var.py jpg_stats -DJPG_STATS=1 bf_jpeg.hip): per file, the entropy
+// kernel's shader-clock and 100-MHz stamps, rounds, tokens, slow tokens, refills, refill cycles, blocks
+#define JPG_NSTAT 10
+__device__ unsigned long long jpg_stats[4096 * JPG_NSTAT];
+BF_API int bf_jpeg_read_stats(unsigned long long* dst, int n) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(jpg_stats), sizeof(unsigned long long) * JPG_NSTAT * n) == hipSuccess
+               ? BF_OK : BF_ERR_LAUNCH;
+}
+#define JST(...) __VA_ARGS__
+#else
+#define JST(...)
+#endif
+
 struct JpegLds {
     uint16_t fast[8][1 << JPG_FB];    // (len << 8) | value for codes <= JPG_FB bits, 0 otherwise
     int32_t maxcode[8][18];           // jdhuff.c: largest code of each length (-1: none), [17] sentinel
     int32_t valoff[8][17];
     uint8_t vals[8][256];
-    int16_t blk[64];
-    __attribute__((aligned(16))) uint8_t ring[JPG_RING];
+    uint32_t ring[JPG_RING / 4];      // un-stuffed entropy bytes (byte writes, dword reads)
+    int16_t blk[64];                  // the block being decoded, natural order
+    uint8_t zz[80];                   // zigzag -> natural (64..79: 63, libjpeg's guard entries)
 };
 
 // canonical table (T.81 Annex C / jdhuff.c jpeg_make_d_derived_tbl) from counts + values
@@ -227,13 +248,73 @@ __device__ bool jpg_build(JpegLds& L, int t, const uint8_t* dht) {
     return ok;
 }
 
-struct JpgBits {                  // MSB-first bit buffer over the un-stuffed LDS ring
-    uint64_t buf;                 // valid bits left-aligned at bit 63
-    int nb;
-    uint32_t rp;                  // next ring byte to load
-};
+// 32 stream bits starting at bit q of the un-stuffed stream, MSB first
+__device__ __forceinline__ uint32_t jpg_peek32(const JpegLds& L, uint32_t q) {
+    const uint32_t d = (q >> 5) & (JPG_RING / 4 - 1);
+    const uint32_t w0 = __builtin_bswap32(L.ring[d]);
+    const uint32_t w1 = __builtin_bswap32(L.ring[(d + 1) & (JPG_RING / 4 - 1)]);
+    return (uint32_t)((((uint64_t)w0 << 32) | w1) >> (32 - (q & 31)));
+}
 
-// the entropy-decode kernel: one wave per file
+// the token at the head of `bits` with table t: packed (value int16 << 16) | flags | size << 9 |
+// run << 5 | total bits (code + extra bits).  DC tokens: run 0, size = the magnitude category.
+// jpg_token_fast answers from the 10-bit table only: a longer code gives JT_SLOW, decoded by the
+// walk with jpg_token_slow if (rarely) the chain reaches that lane.
+#define JT_BAD (1u << 13)
+#define JT_SLOW (1u << 14)
+__device__ __forceinline__ uint32_t jpg_pack(uint32_t bits, uint32_t len, uint32_t sym, bool dc) {
+    const uint32_t run = dc ? 0u : (sym >> 4), sz = dc ? sym : (sym & 15u);
+    if (sz > (dc ? 11u : 15u)) return JT_BAD;
+    int val = 0;
+    if (sz) {
+        const uint32_t r = (bits << len) >> (32 - sz);
+        val = r < (1u << (sz - 1)) ? (int)r - (1 << sz) + 1 : (int)r;
+    }
+    return ((uint32_t)val << 16) | (sz << 9) | (run << 5) | (len + sz);
+}
+
+__device__ __forceinline__ uint32_t jpg_token_fast(const JpegLds& L, int t, uint32_t bits, bool dc) {
+    const uint32_t e = L.fast[t][bits >> (32 - JPG_FB)];
+    return e ? jpg_pack(bits, e >> 8, e & 255u, dc) : JT_SLOW;
+}
+
+__device__ __noinline__ uint32_t jpg_token_slow(const JpegLds& L, int t, uint32_t bits, bool dc) {
+    for (int l = JPG_FB + 1; l <= 16; ++l) {
+        const int code = (int)(bits >> (32 - l));
+        if (code <= L.maxcode[t][l]) return jpg_pack(bits, (uint32_t)l, L.vals[t][(code + L.valoff[t][l]) & 255], dc);
+    }
+    return JT_BAD;
+}
+
+// per-lane words of the walk from the 10-bit table entries of one component's DC (ed) / AC (ea) table:
+//   dw  DC token: the jpg_pack word (JT_SLOW when the code is longer than JPG_FB bits)
+//   aw  AC chain word: next token start (lane + bits, < 128) | (run + 1) << 8; EOB: 128 | next; slow: 255
+//   av  AC coefficient: value << 16 | run << 1 | (size != 0)
+__device__ __forceinline__ void jpg_lane_words(uint32_t bits, uint32_t lane, uint32_t ed, uint32_t ea, uint32_t& dw,
+                                               uint32_t& aw, uint32_t& av) {
+    dw = ed ? jpg_pack(bits, ed >> 8, ed & 255u, true) : JT_SLOW;
+    const uint32_t len = ea >> 8, run = (ea >> 4) & 15u, sz = ea & 15u;
+    uint32_t val = 0;
+    if (sz) {
+        const uint32_t r = (bits << len) >> (32 - sz);
+        val = r < (1u << (sz - 1)) ? r - (1u << sz) + 1u : r;
+    }
+    const uint32_t nxt = lane + len + sz;
+    aw = !ea ? 255u : (sz == 0 && run != 15) ? (128u | nxt) : (((run + 1) << 8) | nxt);
+    av = (val << 16) | (run << 1) | (sz != 0);
+}
+
+// inclusive prefix sum over the wave (DPP row shifts + row broadcasts)
+__device__ __forceinline__ uint32_t png_like_scan(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
+
 __global__ void __launch_bounds__(64) k_jpeg_entropy(const uint8_t* __restrict__ files, const int64_t* __restrict__ offs,
                                                      const JpegInfo* __restrict__ infos, int16_t* __restrict__ coef,
                                                      uint32_t blocks_cap, int32_t* __restrict__ status) {
@@ -253,150 +334,252 @@ __global__ void __launch_bounds__(64) k_jpeg_entropy(const uint8_t* __restrict__
         if (lane == 0) status[f] |= BF_JPG_BAD_MARKER;
         return;
     }
+    uint8_t* ring8 = reinterpret_cast<uint8_t*>(L.ring);
+    JST(const uint64_t c0 = __builtin_amdgcn_s_memtime(); const uint64_t r0 = __builtin_amdgcn_s_memrealtime();)
+    JST(uint64_t n_rounds = 0, n_tok = 0, n_slow = 0, n_prod = 0, c_prod = 0, n_blk = 0, c_lanes = 0, c_walk = 0;)
 
-    // producer state: source byte position, bytes produced into the ring, last source byte
+    // ---- producer: source position, bytes in the ring, last source byte, end of the data
     uint32_t sp = 0, prod = 0, prev = 0, real_end = 0xffffffffu;
     bool ended = false;
-    auto produce = [&]() {        // 64 source bytes -> the ring, stuffing and RSTn removed
-        if (ended) {
-            // past the end of the segment: zeros (as libjpeg feeds zeros after a marker)
-            L.ring[(prod + lane) & (JPG_RING - 1)] = 0;
-            prod += 64;
+    auto produce = [&]() {
+        if (ended) {                  // past the segment: zero bits (libjpeg's fill after a marker)
+#pragma unroll
+            for (int j = 0; j < JPG_SUB; ++j) ring8[(prod + j * 64 + lane) & (JPG_RING - 1)] = 0;
+            prod += JPG_SUB * 64;
             return;
         }
-        const uint32_t i = sp + lane;
-        const uint32_t b = i < elen ? ent[i] : 0u;
-        // the shuffles run on all 64 lanes (a lane masked off during one reads back garbage)
-        const uint32_t bu = (uint32_t)__shfl_up((int)b, 1, 64);
-        const uint32_t bp = lane == 0 ? prev : bu;
-        const uint32_t bn = (uint32_t)__shfl_down((int)b, 1, 64);
-        const uint32_t bnext = lane == 63 ? (i + 1 < elen ? ent[i + 1] : 0u) : bn;
-        // drop: the 00 after an FF, an RSTn (FF Dx: both bytes); bytes past the segment end
-        const bool is_rst_ff = b == 0xFF && bnext >= 0xD0 && bnext <= 0xD7 && i + 1 < elen;
-        const bool is_rst_d = bp == 0xFF && b >= 0xD0 && b <= 0xD7 && i < elen && i > 0;
-        const bool keep = i < elen && !(bp == 0xFF && b == 0 && i > 0) && !is_rst_ff && !is_rst_d;
-        const unsigned long long km = __ballot(keep);
-        const uint32_t o = (uint32_t)bf_lanes_below(km);
-        if (keep) L.ring[(prod + o) & (JPG_RING - 1)] = (uint8_t)b;
-        prod += (uint32_t)__popcll(km);
-        prev = jrfl((uint32_t)__shfl((int)b, 63, 64));
-        __builtin_amdgcn_wave_barrier();
-        sp += 64;
-        if (sp >= elen) {
-            ended = true;
-            real_end = prod;                                       // un-stuffed bytes of real data
+        uint32_t b[JPG_SUB];
+#pragma unroll
+        for (int j = 0; j < JPG_SUB; ++j) {
+            const uint32_t i = sp + j * 64 + lane;
+            b[j] = i < elen ? ent[i] : 0u;
         }
-    };
-    while (prod < 1024) produce();
-    JpgBits br{0, 0, 0};
-    auto refill = [&]() {         // keep >= 32 bits in the buffer
-        while (br.nb <= 32) {
-            if (br.rp + 8 > prod) { while (br.rp + 1024 > prod) produce(); }
-            const uint32_t byte = jrfl(L.ring[br.rp & (JPG_RING - 1)]);
-            br.buf |= (uint64_t)byte << (56 - br.nb);
-            br.nb += 8;
-            ++br.rp;
-        }
-    };
-    auto getb = [&](int s) -> uint32_t {        // s <= 16 bits
-        if (s == 0) return 0u;
-        refill();
-        const uint32_t v = (uint32_t)(br.buf >> (64 - s));
-        br.buf <<= s;
-        br.nb -= s;
-        return v;
-    };
-    auto decode = [&](int t, int& err) -> uint32_t {
-        refill();
-        const uint32_t e = jrfl(L.fast[t][(uint32_t)(br.buf >> (64 - JPG_FB))]);
-        if (e) {
-            const int l = (int)(e >> 8);
-            br.buf <<= l;
-            br.nb -= l;
-            return e & 255u;
-        }
-        const uint32_t w = (uint32_t)(br.buf >> 48);                   // 16 bits
-        for (int l = JPG_FB + 1; l <= 16; ++l) {
-            const int code = (int)(w >> (16 - l));
-            const int mc = (int)jrfl((uint32_t)L.maxcode[t][l]);
-            if (code <= mc) {
-                br.buf <<= l;
-                br.nb -= l;
-                return jrfl(L.vals[t][(code + (int)jrfl((uint32_t)L.valoff[t][l])) & 255]);
+        const uint32_t ti = sp + JPG_SUB * 64;
+        const uint32_t tail = jrfl(ti < elen ? (uint32_t)ent[ti] : 0u);
+#pragma unroll
+        for (int j = 0; j < JPG_SUB; ++j) {
+            const uint32_t i = sp + j * 64 + lane;
+            // the shuffles run on all 64 lanes (a lane masked off during one reads back garbage)
+            const uint32_t bu = (uint32_t)__shfl_up((int)b[j], 1, 64);
+            const uint32_t bn = (uint32_t)__shfl_down((int)b[j], 1, 64);
+            const uint32_t first = j == 0 ? prev : jrfl(__builtin_amdgcn_readlane(b[j - 1], 63));
+            const uint32_t after = j + 1 < JPG_SUB ? jrfl(__builtin_amdgcn_readlane(b[j + 1], 0)) : tail;
+            const uint32_t bp = lane == 0 ? first : bu;
+            const uint32_t bx = lane == 63 ? after : bn;
+            const bool valid = i < elen;
+            const bool has_next = i + 1 < elen;
+            const bool rst_next = bx >= 0xD0 && bx <= 0xD7;
+            // a marker other than RSTn (FF xx, xx not 00) ends the entropy-coded segment
+            const unsigned long long tm = __ballot(valid && has_next && b[j] == 0xFF && bx != 0 && !rst_next);
+            const uint32_t lim = tm ? (uint32_t)__builtin_ctzll(tm) : 64u;
+            const bool stuffed = bp == 0xFF && b[j] == 0 && i > 0;
+            const bool rst_ff = b[j] == 0xFF && has_next && rst_next;
+            const bool rst_d = bp == 0xFF && b[j] >= 0xD0 && b[j] <= 0xD7 && i > 0;
+            const bool keep = valid && (uint32_t)lane < lim && !stuffed && !rst_ff && !rst_d;
+            const unsigned long long km = __ballot(keep);
+            if (keep) ring8[(prod + (uint32_t)bf_lanes_below(km)) & (JPG_RING - 1)] = (uint8_t)b[j];
+            prod += (uint32_t)__popcll(km);
+            if (tm || sp + (uint32_t)(j + 1) * 64 >= elen) {   // (uniform: a lane-derived test here makes the whole walk divergent)
+                ended = true;
+                real_end = prod;      // un-stuffed bytes of real data
+                break;
             }
         }
-        err = 1;
-        return 0u;
+        prev = jrfl(__builtin_amdgcn_readlane(b[JPG_SUB - 1], 63));
+        sp += JPG_SUB * 64;
+        __builtin_amdgcn_wave_barrier();
     };
-    int err = 0;
-    int pred[3] = {0, 0, 0};
-    const uint32_t nmcu = I->mcux * I->mcuy, dri = I->dri;
+
+    // ---- scan layout
     uint32_t td[3], ta[3], hh[3], vv[3], bw[3], coff[3];
     for (uint32_t c = 0; c < 3; ++c) {
         const bool in = c < nc;
-        td[c] = in ? I->td[c] : 0; ta[c] = in ? I->ta[c] : 0; hh[c] = in ? I->h[c] : 0; vv[c] = in ? I->v[c] : 0;
-        bw[c] = in ? I->bw[c] : 0; coff[c] = in ? I->coff[c] : 0;
+        td[c] = in ? I->td[c] : 0;
+        ta[c] = in ? I->ta[c] : 0;
+        hh[c] = in ? I->h[c] : 1;
+        vv[c] = in ? I->v[c] : 1;
+        bw[c] = in ? I->bw[c] : 0;
+        coff[c] = in ? I->coff[c] : 0;
     }
-    bool insufficient = false;
-    for (uint32_t mcu = 0; mcu < nmcu && !err; ++mcu) {
-        if (dri && mcu && mcu % dri == 0) {
-            // restart interval: byte-align (the RSTn bytes are gone from the ring), reset predictors
-            const int drop = br.nb & 7;
-            br.buf <<= drop;
-            br.nb -= drop;
-            pred[0] = pred[1] = pred[2] = 0;
-        }
-        // jdhuff.c: once a decode has needed bits past the end of the data, the rest of the MCUs
-        // are left zero (uniform grey), not decoded from the zero fill
-        if ((uint64_t)br.rp * 8 - (uint64_t)br.nb > (uint64_t)real_end * 8) insufficient = true;
-        const uint32_t my = mcu / I->mcux, mx = mcu - my * I->mcux;
-        if (insufficient) {
-            for (uint32_t c = 0; c < nc; ++c)
-                for (uint32_t v = 0; v < vv[c]; ++v)
-                    for (uint32_t h = 0; h < hh[c]; ++h) {
-                        const size_t blk_i = (size_t)coff[c] + (size_t)(my * vv[c] + v) * bw[c] + mx * hh[c] + h;
-                        out[blk_i * 64 + lane] = 0;
+    const bool same12 = nc < 3 || (td[2] == td[1] && ta[2] == ta[1]);
+    const uint32_t mcux = I->mcux, nmcu = mcux * I->mcuy, dri = I->dri;
+    L.zz[lane] = (uint8_t)jpg_zigzag[lane];
+    if (lane < 16) L.zz[64 + lane] = 63;
+    L.blk[lane] = 0;
+
+    // ---- walk state (uniform)
+    uint32_t P = 0;                   // bit position of the next token in the un-stuffed stream
+    uint32_t mcu = 0, mx = 0, my = 0, c = 0, bv = 0, bh = 0, k = 0;   // k == 0: the block's DC is next
+    int pred0 = 0, pred1 = 0, pred2 = 0;
+    bool insufficient = false, err = false;
+    // the block's coefficients (LDS, natural order) -> its slot of the coefficient grid; re-zeroed
+    auto store_block = [&]() {
+        const size_t bi = (size_t)coff[c] + (size_t)(my * vv[c] + bv) * bw[c] + mx * hh[c] + bh;
+        __builtin_amdgcn_wave_barrier();
+        out[bi * 64 + lane] = L.blk[lane];
+        L.blk[lane] = 0;
+        __builtin_amdgcn_wave_barrier();
+    };
+    auto next_block = [&]() -> bool {  // true when a new MCU starts
+        if (++bh < hh[c]) return false;
+        bh = 0;
+        if (++bv < vv[c]) return false;
+        bv = 0;
+        if (++c < nc) return false;
+        c = 0;
+        ++mcu;
+        if (++mx == mcux) { mx = 0; ++my; }
+        return true;
+    };
+    while (prod < 1024) produce();
+    while (mcu < nmcu && !err) {
+        if (insufficient) {           // zero MCU: zero blocks for each block of the MCU
+            do {
+                const size_t bi = (size_t)coff[c] + (size_t)(my * vv[c] + bv) * bw[c] + mx * hh[c] + bh;
+                out[bi * 64 + lane] = 0;
+            } while (!next_block());
+        } else {
+            JST(const uint64_t cp0 = __builtin_amdgcn_s_memtime();)
+            while ((P >> 3) + 96 > prod) {
+                produce();
+                JST(++n_prod;)
+            }
+            JST(c_prod += __builtin_amdgcn_s_memtime() - cp0; ++n_rounds;)
+            // ---- lanes: the token at P + lane with every table of the scan
+            const uint32_t bits = jpg_peek32(L, P + (uint32_t)lane);
+            const uint32_t idx = bits >> (32 - JPG_FB);
+            const uint32_t ed0 = L.fast[td[0]][idx], ea0 = L.fast[4 + ta[0]][idx];
+            uint32_t ed1 = 0, ea1 = 0, ed2 = 0, ea2 = 0;
+            if (nc > 1) {
+                ed1 = L.fast[td[1]][idx];
+                ea1 = L.fast[4 + ta[1]][idx];
+                if (!same12) {
+                    ed2 = L.fast[td[2]][idx];
+                    ea2 = L.fast[4 + ta[2]][idx];
+                }
+            }
+            uint32_t dw0, aw0, av0, dw1 = 0, aw1 = 0, av1 = 0, dw2 = 0, aw2 = 0, av2 = 0;
+            jpg_lane_words(bits, (uint32_t)lane, ed0, ea0, dw0, aw0, av0);
+            if (nc > 1) {
+                jpg_lane_words(bits, (uint32_t)lane, ed1, ea1, dw1, aw1, av1);
+                if (!same12) jpg_lane_words(bits, (uint32_t)lane, ed2, ea2, dw2, aw2, av2);
+                else { dw2 = dw1; aw2 = aw1; av2 = av1; }
+            }
+            JST(const uint64_t cw0 = __builtin_amdgcn_s_memtime(); c_lanes += cw0 - cp0;)
+            // ---- the walk
+            uint32_t at = 0;
+            for (;;) {
+                if (k == 0) {         // the block's DC token
+                    uint32_t inf = jrfl(__builtin_amdgcn_readlane(c == 0 ? dw0 : c == 1 ? dw1 : dw2, (int)at));
+                    JST(++n_tok;)
+                    if (inf & (JT_SLOW | JT_BAD)) {
+                        JST(++n_slow;)
+                        if (inf & JT_SLOW) inf = jrfl(jpg_token_slow(L, (int)td[c], jpg_peek32(L, P + at), true));
+                        if (inf & JT_BAD) { err = true; break; }
                     }
-            continue;
-        }
-        for (uint32_t c = 0; c < nc && !err; ++c) {
-            for (uint32_t v = 0; v < vv[c] && !err; ++v)
-                for (uint32_t h = 0; h < hh[c] && !err; ++h) {
-                    L.blk[lane] = 0;
-                    const uint32_t s = decode(td[c], err);
-                    if (err || s > 11) { err = 1; break; }
-                    uint32_t r = getb((int)s);
-                    int diff = (int)r;
-                    if (s && r < (1u << (s - 1))) diff = (int)r - (1 << s) + 1;
-                    pred[c] += diff;
-                    if (lane == 0) L.blk[0] = (int16_t)pred[c];
-                    for (int k = 1; k < 64;) {
-                        const uint32_t rs = decode(4 + ta[c], err);
-                        if (err) break;
-                        const int run = (int)(rs >> 4), sz = (int)(rs & 15);
-                        if (sz) {
-                            k += run;
-                            if (k > 63) { err = 1; break; }
-                            const uint32_t bits = getb(sz);
-                            int val = (int)bits;
-                            if (bits < (1u << (sz - 1))) val = (int)bits - (1 << sz) + 1;
-                            if (lane == 0) L.blk[jpg_zigzag[k]] = (int16_t)val;
-                            ++k;
-                        } else if (run == 15) {
-                            k += 16;
-                        } else {
-                            break;
-                        }
+                    at += inf & 31u;
+                    int& pr = c == 0 ? pred0 : c == 1 ? pred1 : pred2;
+                    pr += (int)inf >> 16;
+                    if (lane == 0) L.blk[0] = (int16_t)pr;
+                    k = 1;
+                    if (at >= 64) break;
+                }
+                const uint32_t aw = c == 0 ? aw0 : c == 1 ? aw1 : aw2;
+                const uint32_t av = c == 0 ? av0 : c == 1 ? av1 : av2;
+                bool done = false;
+                for (;;) {            // AC segments: chain walks between slow tokens
+                    uint64_t mem = 0;
+                    const uint32_t k0 = k;
+                    uint32_t last, inf;
+                    do {
+                        mem |= 1ull << at;
+                        last = at;
+                        inf = jrfl(__builtin_amdgcn_readlane(aw, (int)at));
+                        k = jrfl(k + (inf >> 8));     // (keeps the walk scalar: the compiler loses it otherwise)
+                        at = inf & 255u;
+                        JST(++n_tok;)
+                    } while (at < 64 && k < 64);
+                    const bool slow = (inf & 255u) == 255u, eob = !slow && (inf & 128u);
+                    if (slow) mem &= ~(1ull << last);
+                    {                 // the chain's coefficients, in parallel: k of each = k0 + prefix
+                        const bool in = (mem >> lane) & 1ull;
+                        const uint32_t kin = in ? (aw >> 8) : 0u;
+                        const uint32_t pos = k0 + png_like_scan(kin) - kin + ((av >> 1) & 15u);
+                        const bool wr = in && (av & 1u);
+                        // (the break stays out of the lane-divergent write: inside it, the compiler
+                        // turns the whole walk into exec-masked vector code)
+                        const bool bad = __ballot(wr && pos > 63) != 0;
+                        if (wr && pos <= 63) L.blk[L.zz[pos]] = (int16_t)((int)av >> 16);
+                        if (bad) err = true;
                     }
                     if (err) break;
-                    const uint32_t by = my * vv[c] + v, bx = mx * hh[c] + h;
-                    const size_t blk_i = (size_t)coff[c] + (size_t)by * bw[c] + bx;
-                    __builtin_amdgcn_wave_barrier();
-                    out[blk_i * 64 + lane] = L.blk[lane];
+                    if (eob) { at = inf & 127u; done = true; break; }
+                    if (slow) {       // a code longer than JPG_FB bits: decoded here, wave-uniform
+                        JST(++n_slow;)
+                        const uint32_t t2 = jrfl(jpg_token_slow(L, 4 + (int)ta[c], jpg_peek32(L, P + last), false));
+                        if (t2 & JT_BAD) { err = true; break; }
+                        at = last + (t2 & 31u);
+                        const uint32_t run = (t2 >> 5) & 15u, sz = (t2 >> 9) & 15u;
+                        if (sz == 0 && run != 15) { done = true; break; }
+                        k += run;
+                        if (k > 63) {
+                            if (sz) err = true;
+                            done = true;
+                            break;
+                        }
+                        if (sz && lane == 0) L.blk[L.zz[k]] = (int16_t)((int)t2 >> 16);
+                        if (++k >= 64) { done = true; break; }
+                        if (at >= 64) break;
+                        continue;
+                    }
+                    if (k >= 64) done = true;
+                    break;
                 }
+                if (err || !done) break;
+                JST(++n_blk;)
+                store_block();
+                k = 0;
+                if (next_block()) {
+                    if (mcu >= nmcu) break;
+                    // a restart interval boundary, or decoding past the data: end the round here
+                    const bool rst = dri && mcu % dri == 0;
+                    const bool past = real_end != 0xffffffffu && P + at > real_end * 8u;
+                    if (rst || past) {
+                        P += at;
+                        at = 0;
+                        if (rst) {
+                            P = (P + 7) & ~7u;   // byte-align; the RSTn bytes are not in the ring
+                            pred0 = pred1 = pred2 = 0;
+                            insufficient = false;
+                        }
+                        // jdhuff.c: once a decode has needed bits past the end of the data, the rest
+                        // of the segment's MCUs are left zero (uniform grey), not decoded from the fill
+                        if (real_end != 0xffffffffu && P > real_end * 8u) insufficient = true;
+                        break;
+                    }
+                }
+                if (at >= 64) break;
+            }
+            JST(c_walk += __builtin_amdgcn_s_memtime() - cw0;)
+            P += at;
+            continue;
+        }
+        // after a zero MCU
+        if (mcu < nmcu && dri && mcu % dri == 0) {
+            P = (P + 7) & ~7u;
+            pred0 = pred1 = pred2 = 0;
+            insufficient = false;
         }
     }
     if (err && lane == 0) status[f] |= BF_JPG_BAD_DATA;
+#ifdef JPG_STATS
+    const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0 && f < 4096) {
+        unsigned long long* o = jpg_stats + f * JPG_NSTAT;
+        o[0] = c1 - c0; o[1] = r1 - r0; o[2] = n_rounds; o[3] = n_tok; o[4] = n_slow; o[5] = n_prod; o[6] = c_prod;
+        o[7] = n_blk; o[8] = c_lanes; o[9] = c_walk;
+    }
+#endif
 }
 
 // ---- IDCT (jidctint.c jpeg_idct_islow) ----------------------------------------------------------
