@@ -505,18 +505,47 @@ def host_png_rate(pool, threads, seconds=3.0):
         return n / (time.perf_counter() - t0)
 
 
-def host_jpeg_rate(threads, seconds=2.0):
-    """PIL decode of a ScanNet-sized colour JPEG (1296 x 968, quality 90: the synthetic scene frame
-    upsampled) on `threads` host threads (frames/s) -- the colour half of cv2.imread
-    (capture_stream.py:194), which stays on the host: only keyframes need their colour image"""
+def keyframe_jpeg():
+    """a ScanNet-sized colour JPEG (1296 x 968, quality 90, 4:2:0: the synthetic scene frame upsampled)"""
     import io
-    from concurrent.futures import ThreadPoolExecutor
     from PIL import Image
     from boxfusion_amd.synthetic import frame_rgbd
     img = Image.fromarray(frame_rgbd(3, 480, 640)[0]).resize((1296, 968), Image.BILINEAR)
     b = io.BytesIO()
     img.save(b, format="JPEG", quality=90)
-    blob = b.getvalue()
+    return b.getvalue()
+
+
+def gpu_jpeg_rate(n=1024, reps=3):
+    """bf_jpeg_decode_rgb over n copies of the keyframe JPEG resident in HBM (one wave per file: n =
+    1024 puts one on every SIMD), frames/s from HIP events (min of reps), and the batch size"""
+    from boxfusion_amd import _lib
+    from boxfusion_amd.capture_stream import upload_files
+    blob = keyframe_jpeg()
+    files, offs, _ = upload_files([blob] * n, "cuda")
+    out = torch.empty((n, 968, 1296, 3), dtype=torch.uint8, device="cuda")
+    work = torch.empty(_lib.jpeg_workspace_bytes(n, 968, 1296), dtype=torch.uint8, device="cuda")
+    _lib.jpeg_decode_rgb(files, offs, 968, 1296, out=out, work=work)
+    best = None
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _lib.jpeg_decode_rgb(files, offs, 968, 1296, out=out, work=work, check=False)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    del out, work, files
+    return n / (best * 1e-3), n
+
+
+def host_jpeg_rate(threads, seconds=2.0):
+    """PIL decode of the keyframe JPEG on `threads` host threads (frames/s) -- the colour half of
+    cv2.imread (capture_stream.py:194): only keyframes need their colour image"""
+    from concurrent.futures import ThreadPoolExecutor
+    from PIL import Image
+    import io
+    blob = keyframe_jpeg()
 
     def dec(_):
         return np.asarray(Image.open(io.BytesIO(blob)).convert("RGB"))
@@ -1107,7 +1136,11 @@ def main(argv=None):
                          "filters, zlib level 6); gpu = one step's files decoded alone (HIP events, mean of "
                          "5); host = PIL on the pool over ~3 s")}
             jr, jb = host_jpeg_rate(thr)
+            gj, gn = gpu_jpeg_rate()
             line["decode"].update(host_jpeg_keyframes_per_s=jr, jpeg_bytes=jb,
+                                  gpu_jpeg_keyframes_per_s=gj, gpu_jpeg_batch=gn,
+                                  jpeg_kernel="bf_jpeg_decode_rgb (k_jpeg_parse + k_jpeg_entropy + k_jpeg_idct "
+                                              "+ k_jpeg_color), bit-exact to libjpeg's defaults",
                                   keyframes_per_s_needed=line["value"] / G)
             line["config"]["depth_input"] = "16-bit PNG bytes in HBM, decoded on the GPU in the timed region"
         if args.breakdown:

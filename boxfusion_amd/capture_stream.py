@@ -7,8 +7,9 @@ depth infos, T_gravity = camera -> gravity rotation, RT = identity) and the `gt`
 camera -> world pose), the frame rotated to the upright orientation first (torch.rot90 on
 whatever device the frame is on).  `make_sample_decoded` / `DecodedFrameStream` take decoded
 colour + 16-bit depth frames and run the rest of the streams' per-frame work on the GPU
-(bf_ingest_rgbd: cvtColor, cv2.resize, depth scaling, rotation); the 16-bit depth PNGs are decoded on the
-GPU too (bf_png_decode_u16), colour images on the host.
+(bf_ingest_rgbd: cvtColor, cv2.resize, depth scaling, rotation); the 16-bit depth PNGs
+(bf_png_decode_u16) and the baseline colour JPEGs (bf_jpeg_decode_rgb) are decoded on the GPU too,
+or on host threads (PIL) when configured so.
 """
 from __future__ import annotations
 
@@ -128,25 +129,60 @@ def decode_depth_pngs(blobs, H, W, device="cuda"):
     return out
 
 
+def decode_color_jpegs(blobs, H, W, device="cuda"):
+    """cv2.imread(color_path) + cvtColor(BGR2RGB) (capture_stream.py:194/:402) for a batch of
+    baseline JPEG files (their bytes), decoded on the GPU (bf_jpeg_decode_rgb) -> u8 [F, H, W, 3]
+    RGB on device; raises if any file does not decode"""
+    from boxfusion_amd import _lib
+    files, offs, _ = upload_files(blobs, device)
+    out, _ = _lib.jpeg_decode_rgb(files, offs, H, W)
+    return out
+
+
+def jpeg_size(blob):
+    """(W, H) from a JPEG's SOFn frame header (file bytes); ValueError if there is none"""
+    if blob[:2] != b"\xff\xd8":
+        raise ValueError("not a JPEG")
+    i = 2
+    while i + 4 <= len(blob):
+        if blob[i] != 0xFF:
+            raise ValueError("JPEG marker expected")
+        m = blob[i + 1]
+        if m == 0xFF:
+            i += 1
+            continue
+        ln = int.from_bytes(blob[i + 2:i + 4], "big")
+        if 0xC0 <= m <= 0xCF and m not in (0xC4, 0xC8, 0xCC):
+            return int.from_bytes(blob[i + 7:i + 9], "big"), int.from_bytes(blob[i + 5:i + 7], "big")
+        i += 2 + ln
+    raise ValueError("JPEG without a frame header")
+
+
 class DecodedFrameStream:
     """a ScanNet / CA-1M style frame directory as demo.py's dataset: colour JPEG / PNG and 16-bit
     depth PNG paths plus camera -> world poses.  Depth PNGs are decoded on the GPU
-    (bf_png_decode_u16, `batch` files per launch); colour images on the host (PIL: cv2 is absent
-    here).  Everything after decode runs in bf_ingest_rgbd on `device`."""
+    (bf_png_decode_u16, `batch` files per launch) or on host threads; colour images on the host
+    (PIL: cv2 is absent here) or, baseline JPEGs, on the GPU (bf_jpeg_decode_rgb).  Everything
+    after decode runs in bf_ingest_rgbd on `device`."""
 
     def __init__(self, color_paths, depth_paths, poses, K, depth_scale, device="cuda", video_id=0, batch=16,
-                 depth_decode="gpu", host_threads=16):
+                 depth_decode="gpu", host_threads=16, color_decode="host"):
         """depth_decode "gpu": bf_png_decode_u16 on `batch` files per launch; "host": PIL on
         `host_threads` threads (the faster choice when a GPU's share of host cores decodes more
-        files per second than the GPU path, DESIGN.md §4 "Depth PNG decode")"""
+        files per second than the GPU path, DESIGN.md §4 "Depth PNG decode").  color_decode "gpu":
+        bf_jpeg_decode_rgb on `batch` baseline JPEGs per launch (a file of another kind raises);
+        "host": PIL, one file at a time"""
         if not (len(color_paths) == len(depth_paths) == len(poses)):
             raise ValueError("one colour image, depth map and pose per frame")
         if depth_decode not in ("gpu", "host"):
             raise ValueError("depth_decode: 'gpu' or 'host'")
+        if color_decode not in ("gpu", "host"):
+            raise ValueError("color_decode: 'gpu' or 'host'")
         self.color, self.depth, self.poses = list(color_paths), list(depth_paths), list(poses)
         self.K, self.scale, self.dev, self.video_id = np.asarray(K, np.float32), float(depth_scale), device, video_id
         self.batch = max(1, int(batch))
         self.depth_decode, self.host_threads = depth_decode, max(1, int(host_threads))
+        self.color_decode = color_decode
 
     def __len__(self):
         return len(self.color)
@@ -174,9 +210,20 @@ class DecodedFrameStream:
                 with ThreadPoolExecutor(self.host_threads) as ex:
                     arrs = list(ex.map(lambda i: np.asarray(Image.open(self.depth[i])).astype(np.uint16), idx))
                 deps = torch.from_numpy(np.stack(arrs).view(np.int16)).to(self.dev).view(torch.uint16)
+            cols = None
+            if self.color_decode == "gpu":
+                blobs = []
+                for i in idx:
+                    with open(self.color[i], "rb") as fh:
+                        blobs.append(fh.read())
+                Wc, Hc = jpeg_size(blobs[0])
+                cols = decode_color_jpegs(blobs, Hc, Wc, self.dev)
             for j, i in enumerate(idx):
-                rgb = np.asarray(Image.open(self.color[i]).convert("RGB"))
-                rgb_t = torch.from_numpy(np.ascontiguousarray(rgb)).to(self.dev, non_blocking=True)
+                if cols is not None:
+                    rgb_t = cols[j]
+                else:
+                    rgb = np.asarray(Image.open(self.color[i]).convert("RGB"))
+                    rgb_t = torch.from_numpy(np.ascontiguousarray(rgb)).to(self.dev, non_blocking=True)
                 yield make_sample_decoded(rgb_t, deps[j].view(torch.int16), self.scale, self.K, self.poses[i],
                                           video_id=self.video_id, index=i, src_bgr=False)
 

@@ -151,3 +151,28 @@ def test_truncated_scan_grey_tail(L):
     grey = (band + 1) * 16 + 1                  # below it: zero blocks, and chroma context from them
     assert grey < 96
     np.testing.assert_array_equal(got[0, grey:], 128)
+
+
+def test_decoded_frame_stream_gpu_colour_equals_host(L, tmp_path):
+    """DecodedFrameStream with color_decode="gpu" (bf_jpeg_decode_rgb, batches of 3) gives the same
+    samples as the host PIL decode: the image after bf_ingest_rgbd's resize / rotation, bit for bit"""
+    from boxfusion_amd.capture_stream import DecodedFrameStream
+    from boxfusion_amd.synthetic import SCANNET_K, frame_rgbd
+    cps, dps = [], []
+    for f in range(5):
+        rgb, d = frame_rgbd(f, 480, 640)
+        big = np.asarray(Image.fromarray(rgb).resize((1296, 968), Image.BILINEAR))
+        cp, dp = tmp_path / f"{f}.jpg", tmp_path / f"{f}.png"
+        Image.fromarray(big).save(cp, quality=90)
+        Image.fromarray(np.clip(d * 1000.0, 0, 65535).astype(np.uint16)).save(dp)
+        cps.append(str(cp))
+        dps.append(str(dp))
+    up = np.eye(4, dtype=np.float32)
+    up[1:3, :3] = [[0, 0, 1], [0, -1, 0]]
+    poses = [up] * 5
+    host = list(DecodedFrameStream(cps, dps, poses, SCANNET_K, 1000.0, device="cuda", batch=3))
+    gpu = list(DecodedFrameStream(cps, dps, poses, SCANNET_K, 1000.0, device="cuda", batch=3, color_decode="gpu"))
+    assert len(host) == len(gpu) == 5
+    for a, b in zip(host, gpu):
+        torch.testing.assert_close(a["wide"]["image"].cpu(), b["wide"]["image"].cpu(), rtol=0, atol=0)
+        torch.testing.assert_close(a["wide"]["depth"].cpu(), b["wide"]["depth"].cpu(), rtol=0, atol=0)

@@ -46,3 +46,11 @@ def test_progressive_is_refused():
     Image.fromarray(np.zeros((16, 16, 3), np.uint8)).save(b, format="JPEG", progressive=True)
     with pytest.raises(J.JpegError):
         J.decode_rgb(b.getvalue())
+
+
+def test_jpeg_size_reads_the_frame_header():
+    from boxfusion_amd.capture_stream import jpeg_size
+    for _, jpg, img in fixtures():
+        assert jpeg_size(jpg) == (img.shape[1], img.shape[0])
+    with pytest.raises(ValueError):
+        jpeg_size(b"\x89PNG\r\n\x1a\n")
