@@ -14,7 +14,7 @@
 //                   (10-bit primary tables in LDS, a 16-bit canonical slow path), each block's
 //                   coefficients gathered in LDS and stored by the 64 lanes (one int16 per lane)
 //   k_jpeg_idct     one thread per 8 x 8 block: dequantise, islow IDCT, post-IDCT range limit
-//   k_jpeg_color    one thread per pixel: fancy upsampling of the chroma planes + ycc -> RGB (u8 HWC)
+//   k_jpeg_color    four pixels per thread: fancy upsampling of the chroma planes + ycc -> RGB (u8 HWC)
 #include "bf_common.h"
 
 #define JPG_FB 10
@@ -286,13 +286,10 @@ __device__ __noinline__ uint32_t jpg_token_slow(const JpegLds& L, int t, uint32_
     return JT_BAD;
 }
 
-// per-lane words of the walk from the 10-bit table entries of one component's DC (ed) / AC (ea) table:
-//   dw  DC token: the jpg_pack word (JT_SLOW when the code is longer than JPG_FB bits)
+// per-lane words of the walk from the 10-bit AC table entry ea of the token at bit P + lane:
 //   aw  AC chain word: next token start (lane + bits, < 128) | (run + 1) << 8; EOB: 128 | next; slow: 255
 //   av  AC coefficient: value << 16 | run << 1 | (size != 0)
-__device__ __forceinline__ void jpg_lane_words(uint32_t bits, uint32_t lane, uint32_t ed, uint32_t ea, uint32_t& dw,
-                                               uint32_t& aw, uint32_t& av) {
-    dw = ed ? jpg_pack(bits, ed >> 8, ed & 255u, true) : JT_SLOW;
+__device__ __forceinline__ void jpg_lane_ac(uint32_t bits, uint32_t lane, uint32_t ea, uint32_t& aw, uint32_t& av) {
     const uint32_t len = ea >> 8, run = (ea >> 4) & 15u, sz = ea & 15u;
     uint32_t val = 0;
     if (sz) {
@@ -401,7 +398,6 @@ __global__ void __launch_bounds__(64) k_jpeg_entropy(const uint8_t* __restrict__
         bw[c] = in ? I->bw[c] : 0;
         coff[c] = in ? I->coff[c] : 0;
     }
-    const bool same12 = nc < 3 || (td[2] == td[1] && ta[2] == ta[1]);
     const uint32_t mcux = I->mcux, nmcu = mcux * I->mcuy, dri = I->dri;
     L.zz[lane] = (uint8_t)jpg_zigzag[lane];
     if (lane < 16) L.zz[64 + lane] = 63;
@@ -445,38 +441,22 @@ __global__ void __launch_bounds__(64) k_jpeg_entropy(const uint8_t* __restrict__
                 JST(++n_prod;)
             }
             JST(c_prod += __builtin_amdgcn_s_memtime() - cp0; ++n_rounds;)
-            // ---- lanes: the token at P + lane with every table of the scan
+            // ---- lanes: the AC token at P + lane with the table of the current block's component
+            // (DC tokens, one per block, are decoded by the walk itself)
+            const uint32_t rta = ta[c];
             const uint32_t bits = jpg_peek32(L, P + (uint32_t)lane);
-            const uint32_t idx = bits >> (32 - JPG_FB);
-            const uint32_t ed0 = L.fast[td[0]][idx], ea0 = L.fast[4 + ta[0]][idx];
-            uint32_t ed1 = 0, ea1 = 0, ed2 = 0, ea2 = 0;
-            if (nc > 1) {
-                ed1 = L.fast[td[1]][idx];
-                ea1 = L.fast[4 + ta[1]][idx];
-                if (!same12) {
-                    ed2 = L.fast[td[2]][idx];
-                    ea2 = L.fast[4 + ta[2]][idx];
-                }
-            }
-            uint32_t dw0, aw0, av0, dw1 = 0, aw1 = 0, av1 = 0, dw2 = 0, aw2 = 0, av2 = 0;
-            jpg_lane_words(bits, (uint32_t)lane, ed0, ea0, dw0, aw0, av0);
-            if (nc > 1) {
-                jpg_lane_words(bits, (uint32_t)lane, ed1, ea1, dw1, aw1, av1);
-                if (!same12) jpg_lane_words(bits, (uint32_t)lane, ed2, ea2, dw2, aw2, av2);
-                else { dw2 = dw1; aw2 = aw1; av2 = av1; }
-            }
+            uint32_t aw, av;
+            jpg_lane_ac(bits, (uint32_t)lane, L.fast[4 + rta][bits >> (32 - JPG_FB)], aw, av);
             JST(const uint64_t cw0 = __builtin_amdgcn_s_memtime(); c_lanes += cw0 - cp0;)
             // ---- the walk
             uint32_t at = 0;
             for (;;) {
-                if (k == 0) {         // the block's DC token
-                    uint32_t inf = jrfl(__builtin_amdgcn_readlane(c == 0 ? dw0 : c == 1 ? dw1 : dw2, (int)at));
+                if (k == 0) {         // the block's DC token, wave-uniform
+                    const uint32_t db = jrfl(jpg_peek32(L, P + at));
+                    const uint32_t de = jrfl(L.fast[td[c]][db >> (32 - JPG_FB)]);
+                    uint32_t inf = de ? jpg_pack(db, de >> 8, de & 255u, true) : jrfl(jpg_token_slow(L, (int)td[c], db, true));
                     JST(++n_tok;)
-                    if (inf & (JT_SLOW | JT_BAD)) {
-                        JST(++n_slow;)
-                        if (inf & JT_SLOW) inf = jrfl(jpg_token_slow(L, (int)td[c], jpg_peek32(L, P + at), true));
-                        if (inf & JT_BAD) { err = true; break; }
-                    }
+                    if (inf & JT_BAD) { err = true; break; }
                     at += inf & 31u;
                     int& pr = c == 0 ? pred0 : c == 1 ? pred1 : pred2;
                     pr += (int)inf >> 16;
@@ -484,8 +464,7 @@ __global__ void __launch_bounds__(64) k_jpeg_entropy(const uint8_t* __restrict__
                     k = 1;
                     if (at >= 64) break;
                 }
-                const uint32_t aw = c == 0 ? aw0 : c == 1 ? aw1 : aw2;
-                const uint32_t av = c == 0 ? av0 : c == 1 ? av1 : av2;
+                if (ta[c] != rta) break;   // another AC table: the next round decodes with it
                 bool done = false;
                 for (;;) {            // AC segments: chain walks between slow tokens
                     uint64_t mem = 0;
@@ -692,39 +671,76 @@ __device__ __forceinline__ int jpg_chroma(const uint8_t* pl, uint32_t pw, int cw
     return c == cw - 1 ? (s * 4 + 7) >> 4 : (s * 3 + colsum(c + 1) + 7) >> 4;
 }
 
+// jdcolor.c ycc_rgb_convert (SCALEBITS 16) of one pixel -> packed 0x00BBGGRR
+__device__ __forceinline__ uint32_t jpg_ycc_rgb(int Y, int cbs, int crs) {
+    const int cb = cbs - 128, cr = crs - 128;
+    const int half = 1 << 15;
+    const int r = Y + ((91881 * cr + half) >> 16);                    // FIX(1.40200) = 91881
+    const int g = Y + (((-22554) * cb + half + (-46802) * cr) >> 16); // FIX(0.34414) = 22554, FIX(0.71414) = 46802
+    const int b = Y + ((116130 * cb + half) >> 16);                   // FIX(1.77200) = 116130
+    return (uint32_t)min(max(r, 0), 255) | ((uint32_t)min(max(g, 0), 255) << 8) | ((uint32_t)min(max(b, 0), 255) << 16);
+}
+
+// four consecutive pixels (row-major over the image) per thread, written as three dwords
 __global__ void __launch_bounds__(256) k_jpeg_color(const JpegInfo* __restrict__ infos, const uint8_t* __restrict__ planes,
                                                     uint32_t blocks_cap, int F, int H, int W, uint8_t* __restrict__ rgb,
                                                     const int32_t* __restrict__ status) {
     const int f = blockIdx.y;
     if (f >= F || status[f]) return;
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= (uint32_t)H * W) return;
-    const int y = (int)(p / W), x = (int)(p - (uint32_t)y * W);
+    const uint32_t HW = (uint32_t)H * (uint32_t)W;
+    const uint32_t p0 = 4u * (blockIdx.x * blockDim.x + threadIdx.x);
+    if (p0 >= HW) return;
     const JpegInfo* I = infos + f;
     const uint8_t* base = planes + (size_t)f * blocks_cap * 64;
-    uint8_t* o = rgb + ((size_t)f * H * W + p) * 3;
-    const int Y = base[(size_t)I->coff[0] * 64 + (size_t)y * (I->bw[0] * 8) + x];
-    if (I->nc == 1) {
-        o[0] = o[1] = o[2] = (uint8_t)Y;
-        return;
-    }
-    int cc[2];
+    const uint8_t* yp = base + (size_t)I->coff[0] * 64;
+    const uint32_t yw = I->bw[0] * 8;
+    const bool grey = I->nc == 1;
+    const uint8_t* cp[2] = {base, base};
+    uint32_t pw[2] = {0, 0};
+    int rx[2] = {1, 1}, ry[2] = {1, 1}, cw[2] = {1, 1}, chh[2] = {1, 1};
+    if (!grey) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const uint32_t c = 1 + k;
-        const int rx = (int)(I->hmax / I->h[c]), ry = (int)(I->vmax / I->v[c]);
-        const int cw = (int)((W * I->h[c] + I->hmax - 1) / I->hmax), ch = (int)((H * I->v[c] + I->vmax - 1) / I->vmax);
-        cc[k] = jpg_chroma(base + (size_t)I->coff[c] * 64, I->bw[c] * 8, cw, ch, rx, ry, x, y);
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t c = 1 + k;
+            rx[k] = (int)(I->hmax / I->h[c]);
+            ry[k] = (int)(I->vmax / I->v[c]);
+            cw[k] = (int)((W * I->h[c] + I->hmax - 1) / I->hmax);
+            chh[k] = (int)((H * I->v[c] + I->vmax - 1) / I->vmax);
+            cp[k] = base + (size_t)I->coff[c] * 64;
+            pw[k] = I->bw[c] * 8;
+        }
     }
-    // jdcolor.c ycc_rgb_convert, SCALEBITS 16
-    const int cb = cc[0] - 128, cr = cc[1] - 128;
-    const int half = 1 << 15;
-    const int r = Y + ((91881 * cr + half) >> 16);                  // FIX(1.40200) = 91881
-    const int g = Y + (((-22554) * cb + half + (-46802) * cr) >> 16); // FIX(0.34414) = 22554, FIX(0.71414) = 46802
-    const int b = Y + ((116130 * cb + half) >> 16);                 // FIX(1.77200) = 116130
-    o[0] = (uint8_t)min(max(r, 0), 255);
-    o[1] = (uint8_t)min(max(g, 0), 255);
-    o[2] = (uint8_t)min(max(b, 0), 255);
+    int y = (int)(p0 / (uint32_t)W), x = (int)(p0 - (uint32_t)y * W);
+    uint32_t px[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint32_t v = 0;
+        if (p0 + j < HW) {
+            const int Y = yp[(size_t)y * yw + x];
+            if (grey) {
+                v = (uint32_t)Y * 0x010101u;
+            } else {
+                const int cb = jpg_chroma(cp[0], pw[0], cw[0], chh[0], rx[0], ry[0], x, y);
+                const int cr = jpg_chroma(cp[1], pw[1], cw[1], chh[1], rx[1], ry[1], x, y);
+                v = jpg_ycc_rgb(Y, cb, cr);
+            }
+        }
+        px[j] = v;
+        if (++x == W) { x = 0; ++y; }
+    }
+    const size_t o = ((size_t)f * HW + p0) * 3;
+    if (p0 + 3 < HW && (o & 3) == 0) {
+        uint32_t* d = reinterpret_cast<uint32_t*>(rgb + o);
+        d[0] = px[0] | (px[1] << 24);
+        d[1] = (px[1] >> 8) | (px[2] << 16);
+        d[2] = (px[2] >> 16) | (px[3] << 8);
+    } else {
+        for (int j = 0; j < 4 && p0 + j < HW; ++j) {
+            rgb[o + 3 * j] = (uint8_t)px[j];
+            rgb[o + 3 * j + 1] = (uint8_t)(px[j] >> 8);
+            rgb[o + 3 * j + 2] = (uint8_t)(px[j] >> 16);
+        }
+    }
 }
 
 BF_API size_t bf_jpeg_workspace_bytes(int F, int H, int W) {
@@ -749,7 +765,7 @@ BF_API int bf_jpeg_decode_rgb(const uint8_t* files, const int64_t* offsets, int 
     hipLaunchKernelGGL(k_jpeg_parse, dim3(F), dim3(64), 0, s, files, offsets, F, H, W, infos, status);
     hipLaunchKernelGGL(k_jpeg_entropy, dim3(F), dim3(64), 0, s, files, offsets, infos, coef, cap, status);
     hipLaunchKernelGGL(k_jpeg_idct, dim3((cap + 255) / 256, F), dim3(256), 0, s, infos, coef, cap, F, planes, status);
-    const unsigned gp = (unsigned)(((size_t)H * W + 255) / 256);
+    const unsigned gp = (unsigned)(((size_t)H * W + 1023) / 1024);
     hipLaunchKernelGGL(k_jpeg_color, dim3(gp, F), dim3(256), 0, s, infos, planes, cap, F, H, W, rgb, status);
     return bf_check_launch();
 }
