@@ -222,8 +222,8 @@ class DecodedFrameStream:
                 if cols is not None:
                     rgb_t = cols[j]
                 else:
-                    rgb = np.asarray(Image.open(self.color[i]).convert("RGB"))
-                    rgb_t = torch.from_numpy(np.ascontiguousarray(rgb)).to(self.dev, non_blocking=True)
+                    rgb = np.array(Image.open(self.color[i]).convert("RGB"))     # (a writable copy)
+                    rgb_t = torch.from_numpy(rgb).to(self.dev, non_blocking=True)
                 yield make_sample_decoded(rgb_t, deps[j].view(torch.int16), self.scale, self.K, self.poses[i],
                                           video_id=self.video_id, index=i, src_bgr=False)
 
