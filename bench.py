@@ -108,7 +108,7 @@ def parse(argv=None):
                    help="objects in the seeded synthetic scene (150: global box sets past the "
                         "one-wave NMS scan's 96, so the 256-thread scan runs)")
     p.add_argument("--gap", type=int, default=1,
-                   help="keyframe gap (demo.py:134 `count % gap == 0`): every step covers batch*gap "
+                   help="keyframe gap (demo.py:134 `count %% gap == 0`): every step covers batch*gap "
                         "frames per GPU; the non-keyframes get demo.py's per-frame preprocessing "
                         "(depth standardisation), the keyframes detect + CLIP + fusion.  Default "
                         "steps at gap > 1: the 1000-frame stream")
@@ -126,11 +126,12 @@ def parse(argv=None):
     p.add_argument("--depth-ratio", type=int, default=1, choices=(1, 2, 4),
                    help="RGB:depth resolution ratio of the stream (--dataset ca1m: 2 / 4 = a lower-"
                         "resolution depth sensor through the CuTR depth grid; not what CA1MDataset streams)")
-    p.add_argument("--png-depth", action="store_true",
+    p.add_argument("--png-depth", "--decode", dest="png_depth", action="store_true",
                    help="every frame's depth arrives as a 16-bit PNG file (bytes resident in HBM) and is "
                         "decoded on the GPU inside the timed region (bf_png_decode_depth: cv2.imread "
                         "IMREAD_UNCHANGED + astype(f32) / depth_scale, capture_stream.py:197-203); the "
-                        "line gains a `decode` object with the host PIL decode rate beside it")
+                        "line gains a `decode` object: the GPU PNG and colour-JPEG decode rates with the "
+                        "host PIL rates beside them")
     p.add_argument("--cpu-rehearsal", action="store_true",
                    help="CPU/gloo rehearsal of the N-rank control flow (no kernels; test harness)")
     return p.parse_args(argv)
