@@ -126,15 +126,24 @@ def parse(argv=None):
     p.add_argument("--depth-ratio", type=int, default=1, choices=(1, 2, 4),
                    help="RGB:depth resolution ratio of the stream (--dataset ca1m: 2 / 4 = a lower-"
                         "resolution depth sensor through the CuTR depth grid; not what CA1MDataset streams)")
-    p.add_argument("--png-depth", "--decode", dest="png_depth", action="store_true",
+    p.add_argument("--png-depth", action="store_true",
                    help="every frame's depth arrives as a 16-bit PNG file (bytes resident in HBM) and is "
                         "decoded on the GPU inside the timed region (bf_png_decode_depth: cv2.imread "
                         "IMREAD_UNCHANGED + astype(f32) / depth_scale, capture_stream.py:197-203); the "
                         "line gains a `decode` object: the GPU PNG and colour-JPEG decode rates with the "
                         "host PIL rates beside them")
+    p.add_argument("--decode", action="store_true",
+                   help="--png-depth, and every keyframe's colour image arrives as a 1296x968 baseline JPEG "
+                        "decoded on the GPU ahead of its detect (bf_jpeg_decode_rgb + cv2.resize, "
+                        "capture_stream.py:194-199)")
+    p.add_argument("--jpeg-ahead", type=int, default=6,
+                   help="--decode: steps per colour-JPEG decode launch (one group, decoded a group ahead of its detects) "
+                        "")
     p.add_argument("--cpu-rehearsal", action="store_true",
                    help="CPU/gloo rehearsal of the N-rank control flow (no kernels; test harness)")
-    return p.parse_args(argv)
+    a = p.parse_args(argv)
+    a.png_depth = a.png_depth or a.decode
+    return a
 
 
 def launch_ranks(argv, n):
@@ -517,6 +526,21 @@ def keyframe_jpeg():
     return b.getvalue()
 
 
+def jpeg_pool(n, H=968, W=1296, quality=90):
+    """n distinct colour JPEGs of the synthetic scene's frames upsampled to ScanNet's colour size
+    (PIL, quality 90, 4:2:0): the kind of file a ScanNet colour directory holds"""
+    import io
+    from PIL import Image
+    from boxfusion_amd.synthetic import frame_rgbd
+    out = []
+    for f in range(n):
+        img = Image.fromarray(frame_rgbd(f * 5, 480, 640)[0]).resize((W, H), Image.BILINEAR)
+        b = io.BytesIO()
+        img.save(b, format="JPEG", quality=quality)
+        out.append(b.getvalue())
+    return out
+
+
 def gpu_jpeg_rate(n=1024, reps=3):
     """bf_jpeg_decode_rgb over n copies of the keyframe JPEG resident in HBM (one wave per file: n =
     1024 puts one on every SIMD), frames/s from HIP events (min of reps), and the batch size"""
@@ -788,6 +812,49 @@ def main(argv=None):
                           for _ in range(n_inflight)]
         png_in["out"] = [torch.empty((nfile, Hd_, Wd_), dtype=torch.float32, device=dev) for _ in range(n_inflight)]
         png_in["bytes_per_frame"] = float(np.mean([len(pool[f % len(pool)]) for f in range(nfile)]))
+    jpg_in = None
+    if args.decode:
+        # every keyframe's colour image as a ScanNet-size 1296 x 968 baseline JPEG (bytes resident in
+        # HBM), decoded on the GPU ahead of its detect on one decode stream, then cv2.resize to the
+        # frame size (capture_stream.py:194-199).  A launch's latency is one wave's Huffman walk over a
+        # whole file (~130 ms) whatever the batch, so the files of D = `jpeg_ahead` steps go in one
+        # launch: group g + 1 is issued at group g's first step (double-buffered slots), and the timed
+        # region carries one group's decode per D steps.  (One stream per step instead oversubscribes
+        # the 4 hardware queues: a long decode then blocks detect launches sharing its queue.)
+        from boxfusion_amd.capture_stream import upload_files
+        D = max(1, args.jpeg_ahead)
+        ngroups = -(-total_steps // D) + 1
+        cpool = jpeg_pool(16)
+        nf = D * Bm
+        jpg_in = {"D": D, "H": 968, "W": 1296, "ready": {}, "used": {},
+                  "groups": [upload_files([cpool[f % len(cpool)] for s_ in range(g * D, (g + 1) * D)
+                                           for f in my_frames(s_)], dev) for g in range(ngroups)],
+                  "work": [torch.empty(_lib.jpeg_workspace_bytes(nf, 968, 1296), dtype=torch.uint8, device=dev)
+                           for _ in range(2)],
+                  "full": [torch.empty((nf, 968, 1296, 3), dtype=torch.uint8, device=dev) for _ in range(2)],
+                  "rgb": [torch.empty((nf, FH, FW, 3), dtype=torch.uint8, device=dev) for _ in range(2)],
+                  "stream": torch.cuda.Stream(device=dev, priority=-1),
+                  "bytes_per_frame": float(np.mean([len(b) for b in cpool]))}
+
+    def jpeg_issue(g):
+        """group g's keyframe JPEGs (steps g*D .. g*D + D - 1) -> RGB at the frame size on the decode
+        stream, into slot g % 2 once the last detect of group g - 2 has copied its input"""
+        st = jpg_in["stream"]
+        with torch.cuda.stream(st):
+            prev = jpg_in["used"].pop(g - 2, None)
+            if prev is not None:
+                st.wait_event(prev)
+            files, offs, _ = jpg_in["groups"][g]
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            _lib.jpeg_decode_rgb(files, offs, jpg_in["H"], jpg_in["W"], out=jpg_in["full"][g % 2],
+                                 work=jpg_in["work"][g % 2], check=False)
+            _lib.cv2_resize_u8(jpg_in["full"][g % 2], FW, FH, out=jpg_in["rgb"][g % 2])
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(st)
+            jpg_in["ready"][g] = ev
+            jpg_in.setdefault("spans", []).append((e0, ev))
+
     poses_all = np.stack([scene.pose(f) for f in all_mine]).astype(np.float32)
     dets_mine = [scene.detections(f, Kf, (FW, FH)) for f in all_mine]
     rec_all = torch.from_numpy(pack_records(dets_mine, poses_all)).to(dev)
@@ -832,8 +899,19 @@ def main(argv=None):
             if nk_depth is not None:          # the step's non-keyframes: per-frame work only
                 _lib.depth_preprocess(dec[Bm:] if png_in is not None else nk_depth[s], nk_K, nk_RT[s], 10.0,
                                       ws=nk_ws[k])
-            det(rgb_all[sl], kf_depth, poses_all[sl], return_instances=False,
+            kf_rgb = rgb_all[sl]
+            if jpg_in is not None:            # colour decoded one group ahead; at a group's first step
+                g, j = divmod(s, jpg_in["D"])  # issue the next group's decode
+                torch.cuda.current_stream().wait_event(jpg_in["ready"][g])
+                if j == 0:                    # (after the wait: a wait issued behind a new decode
+                    jpeg_issue(g + 1)         # launch on that stream would wait for it too)
+                kf_rgb = jpg_in["rgb"][g % 2][j * Bm:(j + 1) * Bm]
+            det(kf_rgb, kf_depth, poses_all[sl], return_instances=False,
                 crop_boxes=crops_all[s * Bm * args.crops:(s + 1) * Bm * args.crops])
+            if jpg_in is not None and j == jpg_in["D"] - 1:   # the group's slot is free after this copy
+                evu = torch.cuda.Event()
+                evu.record()
+                jpg_in["used"][g] = evu
             if args.breakdown:
                 torch.cuda.synchronize()
                 brk["detect"] += time.perf_counter() - tb
@@ -890,6 +968,9 @@ def main(argv=None):
         det_streams = [det_stream] + [_lib.cu_masked_stream(det_cus, local) for _ in range(n_inflight - 1)]
     else:
         det_streams = [det_stream] + [torch.cuda.Stream(device=dev) for _ in range(n_inflight - 1)]
+    if jpg_in is not None and masked and fusion_cus > 0:
+        # --decode with reserved CUs: the colour decode runs on them, out of the detect kernels' way
+        jpg_in["stream"] = _lib.cu_masked_stream(_lib.partition_cus(fusion_cus, local)[1], local)
 
     # capture every DetectStage's graph before the fusion worker exists: a capture must not see
     # another thread's synchronising calls
@@ -903,6 +984,8 @@ def main(argv=None):
         st = FusionStage(CFG, Kf, H=FH, W=FW, device=dev)
         return st if args.sync_fusion else AsyncFusion(st, stream=fus_stream)
 
+    if jpg_in is not None:                     # the first group's colour decode, before the warmup
+        jpeg_issue(0)
     wf = make_fusion()
     run_steps(0, args.warmup, wf)
     if not args.sync_fusion:
@@ -1144,6 +1227,15 @@ def main(argv=None):
                                               "+ k_jpeg_color), bit-exact to libjpeg's defaults",
                                   keyframes_per_s_needed=line["value"] / G)
             line["config"]["depth_input"] = "16-bit PNG bytes in HBM, decoded on the GPU in the timed region"
+            if jpg_in is not None:
+                spans = [a.elapsed_time(b) for a, b in jpg_in["spans"][1:]]
+                line["decode"]["gpu_jpeg_group_ms"] = {"files": jpg_in["D"] * Bm, "mean": float(np.mean(spans)),
+                                                      "max": float(np.max(spans))} if spans else None
+                line["config"]["color_input"] = (f"1296x968 baseline JPEG bytes in HBM (q90 4:2:0, "
+                                                 f"{jpg_in['bytes_per_frame'] / 1e3:.0f} KB), decoded on the GPU "
+                                                 f"one group of {jpg_in['D']} steps ahead on a decode stream "
+                                                 f"(bf_jpeg_decode_rgb + bf_cv2_resize_u8 to {FW}x{FH}) inside the "
+                                                 f"timed region")
         if args.breakdown:
             line["breakdown_ms_per_step"] = {k: 1e3 * v / args.steps for k, v in brk.items()}
         if not args.no_cpu_baseline and N == 1:   # rank 0 at N=1 only
