@@ -801,17 +801,30 @@ def main(argv=None):
         from boxfusion_amd.capture_stream import upload_files
         Hd_, Wd_ = FH // FRAME["r"], FW // FRAME["r"]
         pool = png_pool(16, Hd_, Wd_)
-        png_in = {"pool": pool, "steps": [], "H": Hd_, "W": Wd_}
-        for s_ in range(total_steps):
+        png_in = {"pool": pool, "steps": {}, "H": Hd_, "W": Wd_}
+
+        def step_ids(s_):
             kf = my_frames(s_)
-            ids = list(kf) + [f + o for f in kf for o in range(1, G)]
-            png_in["steps"].append(upload_files([pool[f % len(pool)] for f in ids], dev))
+            return list(kf) + [f + o for f in kf for o in range(1, G)]
+        # --decode: the files go in groups of D steps, decoded a group ahead (below); one step's
+        # files stay for the decode-alone measurement
+        for s_ in ([args.warmup] if args.decode else range(total_steps)):
+            png_in["steps"][s_] = upload_files([pool[f % len(pool)] for f in step_ids(s_)], dev)
         nfile = G * Bm
-        tot = max(int(o[2][-1]) for o in png_in["steps"])
+        tot = max(int(o[2][-1]) for o in png_in["steps"].values())
         png_in["work"] = [torch.empty(_lib.png_workspace_bytes(nfile, Hd_, Wd_, tot), dtype=torch.uint8, device=dev)
                           for _ in range(n_inflight)]
         png_in["out"] = [torch.empty((nfile, Hd_, Wd_), dtype=torch.float32, device=dev) for _ in range(n_inflight)]
         png_in["bytes_per_frame"] = float(np.mean([len(pool[f % len(pool)]) for f in range(nfile)]))
+        if args.decode:
+            D = max(1, args.jpeg_ahead)
+            png_in["groups"] = [upload_files([pool[f % len(pool)] for s_ in range(g * D, (g + 1) * D)
+                                              for f in step_ids(s_)], dev)
+                                for g in range(-(-total_steps // D) + 1)]
+            gt = max(int(o[2][-1]) for o in png_in["groups"])
+            png_in["gwork"] = [torch.empty(_lib.png_workspace_bytes(D * nfile, Hd_, Wd_, gt), dtype=torch.uint8,
+                                           device=dev) for _ in range(2)]
+            png_in["gout"] = [torch.empty((D * nfile, Hd_, Wd_), dtype=torch.float32, device=dev) for _ in range(2)]
     jpg_in = None
     if args.decode:
         # every keyframe's colour image as a ScanNet-size 1296 x 968 baseline JPEG (bytes resident in
@@ -837,16 +850,22 @@ def main(argv=None):
                   "bytes_per_frame": float(np.mean([len(b) for b in cpool]))}
 
     def jpeg_issue(g):
-        """group g's keyframe JPEGs (steps g*D .. g*D + D - 1) -> RGB at the frame size on the decode
-        stream, into slot g % 2 once the last detect of group g - 2 has copied its input"""
+        """group g's depth PNGs and keyframe JPEGs (steps g*D .. g*D + D - 1) -> f32 depth and RGB at the
+        frame size on the decode stream, into slot g % 2 once the last step of group g - 2 has read
+        its inputs"""
         st = jpg_in["stream"]
         with torch.cuda.stream(st):
             prev = jpg_in["used"].pop(g - 2, None)
             if prev is not None:
                 st.wait_event(prev)
-            files, offs, _ = jpg_in["groups"][g]
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record(st)
+            if png_in is not None and "groups" in png_in:     # the group's depth files
+                files, offs, offs_h = png_in["groups"][g]
+                _lib.png_decode_u16(files, offs, png_in["H"], png_in["W"], out=png_in["gout"][g % 2],
+                                    offsets_host=offs_h, depth_scale=CFG["cam"].get("png_depth_scale", 1000.0),
+                                    work=png_in["gwork"][g % 2], check=False)
+            files, offs, _ = jpg_in["groups"][g]
             _lib.jpeg_decode_rgb(files, offs, jpg_in["H"], jpg_in["W"], out=jpg_in["full"][g % 2],
                                  work=jpg_in["work"][g % 2], check=False)
             _lib.cv2_resize_u8(jpg_in["full"][g % 2], FW, FH, out=jpg_in["rgb"][g % 2])
@@ -890,7 +909,16 @@ def main(argv=None):
             st_ctx.__enter__()      # this step's detect, gather and fusion hand-off on its stream
             det = detects[k]
             kf_depth = depth_all[sl]
-            if png_in is not None:            # the step's depth files -> f32 depth (GPU decode)
+            kf_rgb = rgb_all[sl]
+            if jpg_in is not None:            # --decode: colour + depth decoded one group ahead; at a
+                g, j = divmod(s, jpg_in["D"])  # group's first step, issue the next group's decode
+                torch.cuda.current_stream().wait_event(jpg_in["ready"][g])
+                if j == 0:                    # (after the wait: a wait issued behind a new decode
+                    jpeg_issue(g + 1)         # launch on that stream would wait for it too)
+                kf_rgb = jpg_in["rgb"][g % 2][j * Bm:(j + 1) * Bm]
+                dec = png_in["gout"][g % 2][j * G * Bm:(j + 1) * G * Bm]
+                kf_depth = dec[:Bm]
+            elif png_in is not None:          # the step's depth files -> f32 depth (GPU decode, in stream)
                 files, offs, offs_h = png_in["steps"][s]
                 dec = png_in["out"][k]
                 _lib.png_decode_u16(files, offs, png_in["H"], png_in["W"], out=dec, offsets_host=offs_h,
@@ -899,13 +927,6 @@ def main(argv=None):
             if nk_depth is not None:          # the step's non-keyframes: per-frame work only
                 _lib.depth_preprocess(dec[Bm:] if png_in is not None else nk_depth[s], nk_K, nk_RT[s], 10.0,
                                       ws=nk_ws[k])
-            kf_rgb = rgb_all[sl]
-            if jpg_in is not None:            # colour decoded one group ahead; at a group's first step
-                g, j = divmod(s, jpg_in["D"])  # issue the next group's decode
-                torch.cuda.current_stream().wait_event(jpg_in["ready"][g])
-                if j == 0:                    # (after the wait: a wait issued behind a new decode
-                    jpeg_issue(g + 1)         # launch on that stream would wait for it too)
-                kf_rgb = jpg_in["rgb"][g % 2][j * Bm:(j + 1) * Bm]
             det(kf_rgb, kf_depth, poses_all[sl], return_instances=False,
                 crop_boxes=crops_all[s * Bm * args.crops:(s + 1) * Bm * args.crops])
             if jpg_in is not None and j == jpg_in["D"] - 1:   # the group's slot is free after this copy
@@ -1226,7 +1247,9 @@ def main(argv=None):
                                   jpeg_kernel="bf_jpeg_decode_rgb (k_jpeg_parse + k_jpeg_entropy + k_jpeg_idct "
                                               "+ k_jpeg_color), bit-exact to libjpeg's defaults",
                                   keyframes_per_s_needed=line["value"] / G)
-            line["config"]["depth_input"] = "16-bit PNG bytes in HBM, decoded on the GPU in the timed region"
+            line["config"]["depth_input"] = ("16-bit PNG bytes in HBM, decoded on the GPU in the timed region" +
+                                             (f" (one group of {args.jpeg_ahead} steps ahead on a decode stream)"
+                                              if args.decode else " (in the step's stream)"))
             if jpg_in is not None:
                 spans = [a.elapsed_time(b) for a, b in jpg_in["spans"][1:]]
                 line["decode"]["gpu_jpeg_group_ms"] = {"files": jpg_in["D"] * Bm, "mean": float(np.mean(spans)),

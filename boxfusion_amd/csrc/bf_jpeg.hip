@@ -9,7 +9,7 @@
 // Four launches per batch of F files (device bytes back to back + F+1 offsets), all H x W:
 //   k_jpeg_parse    one wave per file: markers (DQT, SOF0/1, DHT, DRI, SOS), the frame and scan
 //                   layout, the entropy-coded segment's extent
-//   k_jpeg_entropy  one wave per file: the lanes un-stuff the entropy bytes (FF 00 -> FF, RSTn
+//   k_jpeg_entropy  one wave per file (four per workgroup): the lanes un-stuff the entropy bytes (FF 00 -> FF, RSTn
 //                   dropped) into an LDS ring 64 bytes per step; the Huffman walk runs wave-uniform
 //                   (10-bit primary tables in LDS, a 16-bit canonical slow path), each block's
 //                   coefficients gathered in LDS and stored by the 64 lanes (one int16 per lane)
@@ -209,10 +209,10 @@ struct JpegLds {
 
 // canonical table (T.81 Annex C / jdhuff.c jpeg_make_d_derived_tbl) from counts + values
 __device__ bool jpg_build(JpegLds& L, int t, const uint8_t* dht) {
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     for (int i = lane; i < (1 << JPG_FB); i += 64) L.fast[t][i] = 0;
     for (int i = lane; i < 256; i += 64) L.vals[t][i] = dht[16 + i];
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();  // (the tables are the wave's own: LDS order within a wave suffices)
     bool ok = true;
     {
         int code = 0;                 // over-subscribed tables (jdhuff.c "Bogus Huffman table") are refused
@@ -244,7 +244,7 @@ __device__ bool jpg_build(JpegLds& L, int t, const uint8_t* dht) {
         }
         L.maxcode[t][17] = 0x7fffffff;
     }
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();
     return ok;
 }
 
@@ -312,13 +312,21 @@ __device__ __forceinline__ uint32_t png_like_scan(uint32_t v) {
     return v;
 }
 
-__global__ void __launch_bounds__(64) k_jpeg_entropy(const uint8_t* __restrict__ files, const int64_t* __restrict__ offs,
-                                                     const JpegInfo* __restrict__ infos, int16_t* __restrict__ coef,
-                                                     uint32_t blocks_cap, int32_t* __restrict__ status) {
-    __shared__ JpegLds L;
-    const int f = blockIdx.x;
-    const int lane = threadIdx.x;
-    if (status[f]) return;
+// JPG_WPB files per workgroup, one wave each with its own LDS: the waves land on the SIMDs of one
+// CU, so a batch occupies F / JPG_WPB CUs instead of F (a full-CU GEMM workgroup cannot co-reside
+// with a decode wave; in the pipeline every CU a decode holds is one the detector loses)
+#define JPG_WPB 4
+__global__ void __launch_bounds__(64 * JPG_WPB) k_jpeg_entropy(const uint8_t* __restrict__ files,
+                                                               const int64_t* __restrict__ offs,
+                                                               const JpegInfo* __restrict__ infos,
+                                                               int16_t* __restrict__ coef, uint32_t blocks_cap,
+                                                               int F, int32_t* __restrict__ status) {
+    __shared__ JpegLds Ls[JPG_WPB];
+    const uint32_t wv = jrfl(threadIdx.x >> 6);     // (wave-uniform; the compiler cannot tell by itself)
+    JpegLds& L = Ls[wv];
+    const int f = (int)(blockIdx.x * JPG_WPB + wv);
+    const int lane = threadIdx.x & 63;
+    if (f >= F || status[f]) return;
     const JpegInfo* I = infos + f;
     const uint8_t* ent = files + offs[f] + I->ent_off;
     const uint32_t elen = I->ent_len;
@@ -763,7 +771,8 @@ BF_API int bf_jpeg_decode_rgb(const uint8_t* files, const int64_t* offsets, int 
     uint8_t* planes = w + jpg_align((size_t)F * sizeof(JpegInfo), 256) + jpg_align((size_t)F * cap * 64 * 2, 256);
     hipStream_t s = bf_stream(stream);
     hipLaunchKernelGGL(k_jpeg_parse, dim3(F), dim3(64), 0, s, files, offsets, F, H, W, infos, status);
-    hipLaunchKernelGGL(k_jpeg_entropy, dim3(F), dim3(64), 0, s, files, offsets, infos, coef, cap, status);
+    hipLaunchKernelGGL(k_jpeg_entropy, dim3((F + JPG_WPB - 1) / JPG_WPB), dim3(64 * JPG_WPB), 0, s, files, offsets,
+                       infos, coef, cap, F, status);
     hipLaunchKernelGGL(k_jpeg_idct, dim3((cap + 255) / 256, F), dim3(256), 0, s, infos, coef, cap, F, planes, status);
     const unsigned gp = (unsigned)(((size_t)H * W + 1023) / 1024);
     hipLaunchKernelGGL(k_jpeg_color, dim3(gp, F), dim3(256), 0, s, infos, planes, cap, F, H, W, rgb, status);

@@ -53,6 +53,32 @@ def main():
     torch.cuda.synchronize()
     print(f"matmul loop alone {alone:.1f} ms; with the decode running {m0.elapsed_time(m1):.1f} ms; "
           f"decode {d0.elapsed_time(d1):.1f} ms; matmul start - decode start {d0.elapsed_time(m0):.1f} ms", flush=True)
+    # a spin kernel of the same residency (12 workgroups x 4 waves spinning) instead of the decode
+    spin = torch.zeros(2 * 4096, dtype=torch.int32, device="cuda")
+    with torch.cuda.stream(sA):
+        s0 = torch.cuda.Event(enable_timing=True)
+        s1 = torch.cuda.Event(enable_timing=True)
+        s0.record()
+        _lib.lib().bf_cu_probe(_lib._ptr(spin), 12, 200_000_000, _lib.c_void_p(sA.cuda_stream))
+        s1.record()
+    m0, m1 = mm_loop()
+    torch.cuda.synchronize()
+    print(f"matmul loop with a 12-workgroup spin kernel running {m0.elapsed_time(m1):.1f} ms "
+          f"(spin {s0.elapsed_time(s1):.1f} ms)", flush=True)
+    # CU-partitioned: the matmul stream masked off the decode's CUs
+    det, res = _lib.partition_cus(16)
+    sB = _lib.cu_masked_stream(det)
+    sA = _lib.cu_masked_stream(res)
+    mm_loop(5)
+    torch.cuda.synchronize()
+    m0, m1 = mm_loop()
+    torch.cuda.synchronize()
+    alone = m0.elapsed_time(m1)
+    d0, d1 = decode()
+    m0, m1 = mm_loop()
+    torch.cuda.synchronize()
+    print(f"masked (matmul on {len(det)} CUs, decode on {len(res)}): matmul alone {alone:.1f} ms, with the decode "
+          f"{m0.elapsed_time(m1):.1f} ms; decode {d0.elapsed_time(d1):.1f} ms", flush=True)
 
 
 if __name__ == "__main__":
