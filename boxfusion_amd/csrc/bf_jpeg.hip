@@ -174,8 +174,8 @@ __global__ void __launch_bounds__(64) k_jpeg_parse(const uint8_t* __restrict__ f
 
 // ---- entropy decode -----------------------------------------------------------------------------
 // One wave per file.  The lanes un-stuff the entropy bytes into an LDS ring (JPG_SUB x 64 source
-// bytes per refill, all loads in flight together; FF 00 -> FF, RSTn dropped, the first other
-// marker ends the segment).  Decoding is speculative, as in the PNG inflate: each round, lane l
+// bytes per refill, all loads in flight together; FF 00 -> FF, RSTn and fill bytes dropped, the
+// first other marker ends the segment).  Decoding is speculative, as in the PNG inflate: each round, lane l
 // decodes the token (Huffman code + its extra bits) that would start at bit P + l, once with each
 // table a component of the scan uses (DC and AC); the scalar walk then follows the chain of real
 // token starts through the per-lane results with v_readlane, across block and MCU boundaries, and
@@ -375,12 +375,15 @@ __global__ void __launch_bounds__(64 * JPG_WPB) k_jpeg_entropy(const uint8_t* __
             const bool has_next = i + 1 < elen;
             const bool rst_next = bx >= 0xD0 && bx <= 0xD7;
             // a marker other than RSTn (FF xx, xx not 00) ends the entropy-coded segment
-            const unsigned long long tm = __ballot(valid && has_next && b[j] == 0xFF && bx != 0 && !rst_next);
+            // (FF FF: a fill byte -- jdhuff.c skips every FF of a run and reads what follows the last)
+            const unsigned long long tm =
+                __ballot(valid && has_next && b[j] == 0xFF && bx != 0 && bx != 0xFF && !rst_next);
             const uint32_t lim = tm ? (uint32_t)__builtin_ctzll(tm) : 64u;
             const bool stuffed = bp == 0xFF && b[j] == 0 && i > 0;
             const bool rst_ff = b[j] == 0xFF && has_next && rst_next;
             const bool rst_d = bp == 0xFF && b[j] >= 0xD0 && b[j] <= 0xD7 && i > 0;
-            const bool keep = valid && (uint32_t)lane < lim && !stuffed && !rst_ff && !rst_d;
+            const bool fill = b[j] == 0xFF && has_next && bx == 0xFF;
+            const bool keep = valid && (uint32_t)lane < lim && !stuffed && !rst_ff && !rst_d && !fill;
             const unsigned long long km = __ballot(keep);
             if (keep) ring8[(prod + (uint32_t)bf_lanes_below(km)) & (JPG_RING - 1)] = (uint8_t)b[j];
             prod += (uint32_t)__popcll(km);

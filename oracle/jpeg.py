@@ -85,7 +85,7 @@ def parse(data: bytes):
             e = pos + 2 + ln
             j = e
             while j + 1 < len(data):
-                if data[j] == 0xFF and data[j + 1] != 0 and not (0xD0 <= data[j + 1] <= 0xD7):
+                if data[j] == 0xFF and data[j + 1] not in (0, 0xFF) and not (0xD0 <= data[j + 1] <= 0xD7):
                     break
                 j += 1
             scans.append((cidx, tabs, data[e:j]))
@@ -121,10 +121,13 @@ class _Bits:
                 v = 0                          # past the end: zeros (libjpeg inserts zeros too)
             else:
                 v = self.b[self.p]
-                if v == 0xFF:
-                    nx = self.b[self.p + 1] if self.p + 1 < len(self.b) else 0
+                if v == 0xFF:                  # jdhuff.c: skip a run of FF (fill bytes), read what follows
+                    q = self.p + 1
+                    while q < len(self.b) and self.b[q] == 0xFF:
+                        q += 1
+                    nx = self.b[q] if q < len(self.b) else 0
                     if nx == 0:
-                        self.p += 1
+                        self.p = q             # FF (FF ...) 00 -> one FF data byte
                     else:                      # a marker: do not consume; feed zeros
                         v = 0
                         self.p -= 1
@@ -142,8 +145,11 @@ class _Bits:
     def restart(self):
         """byte-align and skip an RSTn marker"""
         self.n = 0
-        if self.p + 1 < len(self.b) and self.b[self.p] == 0xFF and 0xD0 <= self.b[self.p + 1] <= 0xD7:
-            self.p += 2
+        q = self.p
+        while q < len(self.b) and self.b[q] == 0xFF:   # fill bytes before the marker
+            q += 1
+        if q > self.p and q < len(self.b) and 0xD0 <= self.b[q] <= 0xD7:
+            self.p = q + 1
 
 
 def _decode(bs, table):

@@ -5,7 +5,7 @@ Run: python tests/golden/make_jpeg_fixtures.py
 
 The files cover what a colour-frame writer can emit: 4:2:0 / 4:2:2 / 4:4:4 chroma, qualities 5 /
 50 / 75 / 95 / 100, optimised Huffman tables, restart markers (every block, every 3 MCUs, every MCU
-row), greyscale, and sizes that are not multiples of the MCU (1 x 1, 17 x 9, 37 x 53, 8 x 23,
+row; fill bytes before them and before a stuffed FF), greyscale, and sizes that are not multiples of the MCU (1 x 1, 17 x 9, 37 x 53, 8 x 23,
 33 x 71).  Data only: key jpg_<i> (u8 file bytes), img_<i> (u8 [H, W, 3] RGB expected), name_<i>.
 """
 from __future__ import annotations
@@ -38,6 +38,27 @@ def pil_jpeg(img, **kw):
     return b.getvalue()
 
 
+def with_fill_bytes(jpg):
+    """the same file with fill bytes (FF FF) before each RSTn marker and before one stuffed FF 00"""
+    i = 2
+    while True:
+        m, ln = jpg[i + 1], int.from_bytes(jpg[i + 2:i + 4], "big")
+        if m == 0xDA:
+            e = i + 2 + ln
+            break
+        i += 2 + ln
+    out, k, stuffed = bytearray(jpg[:e]), e, False
+    while k < len(jpg):
+        if jpg[k] == 0xFF and k + 1 < len(jpg) and (0xD0 <= jpg[k + 1] <= 0xD7 or (jpg[k + 1] == 0 and not stuffed)):
+            stuffed |= jpg[k + 1] == 0
+            out += b"\xff\xff\xff" + bytes([jpg[k + 1]])
+            k += 2
+            continue
+        out.append(jpg[k])
+        k += 1
+    return bytes(out)
+
+
 def cases():
     base = scene(48, 64, 0)
     out = []
@@ -56,6 +77,7 @@ def cases():
                                       restart_marker_blocks=2)))
     for (H, W), ss in (((1, 1), 2), ((17, 9), 2), ((37, 53), 2), ((8, 23), 1), ((33, 71), 0), ((24, 40), 2)):
         out.append((f"odd{H}x{W}_s{ss}", pil_jpeg(scene(H, W, H * W), quality=85, subsampling=ss)))
+    out.append(("s420_rst_fill", with_fill_bytes(pil_jpeg(base, quality=75, restart_marker_blocks=2))))
     flat = np.full((16, 24, 3), (12, 200, 99), np.uint8)          # DC-only blocks, long EOB runs
     out.append(("flat", pil_jpeg(flat, quality=90)))
     sat = np.zeros((16, 16, 3), np.uint8)
