@@ -182,6 +182,9 @@ __global__ void __launch_bounds__(64) k_jpeg_parse(const uint8_t* __restrict__ f
 // ends the round at the first token starting past the 64 lanes.  A block's coefficients build up
 // in one VGPR (lane i = natural index i) and are stored by the 64 lanes at its end.
 #define JPG_SUB 8
+#ifndef JPG_HALVES
+#define JPG_HALVES 2                  // 64-bit halves of the stream decoded per round
+#endif
 
 #ifdef JPG_STATS
 // diagnostic build (scripts/build_var.py jpg_stats -DJPG_STATS=1 bf_jpeg.hip): per file, the entropy
@@ -452,12 +455,22 @@ __global__ void __launch_bounds__(64 * JPG_WPB) k_jpeg_entropy(const uint8_t* __
                 JST(++n_prod;)
             }
             JST(c_prod += __builtin_amdgcn_s_memtime() - cp0; ++n_rounds;)
-            // ---- lanes: the AC token at P + lane with the table of the current block's component
-            // (DC tokens, one per block, are decoded by the walk itself)
+            // ---- lanes: the AC tokens at P + lane (and P + 64 + lane: JPG_HALVES 64-bit halves per
+            // round) with the table of the current block's component (DC tokens, one per block, are
+            // decoded by the walk itself)
             const uint32_t rta = ta[c];
-            const uint32_t bits = jpg_peek32(L, P + (uint32_t)lane);
-            uint32_t aw, av;
-            jpg_lane_ac(bits, (uint32_t)lane, L.fast[4 + rta][bits >> (32 - JPG_FB)], aw, av);
+            const uint32_t bits0 = jpg_peek32(L, P + (uint32_t)lane);
+#if JPG_HALVES > 1
+            const uint32_t bits1 = jpg_peek32(L, P + 64u + (uint32_t)lane);
+            const uint32_t fe1 = L.fast[4 + rta][bits1 >> (32 - JPG_FB)];
+#endif
+            const uint32_t fe0 = L.fast[4 + rta][bits0 >> (32 - JPG_FB)];
+            uint32_t aw0, av0, aw1 = 0, av1 = 0;
+            jpg_lane_ac(bits0, (uint32_t)lane, fe0, aw0, av0);
+#if JPG_HALVES > 1
+            jpg_lane_ac(bits1, (uint32_t)lane, fe1, aw1, av1);
+#endif
+            const uint32_t span = 64u * JPG_HALVES;
             JST(const uint64_t cw0 = __builtin_amdgcn_s_memtime(); c_lanes += cw0 - cp0;)
             // ---- the walk
             uint32_t at = 0;
@@ -473,22 +486,24 @@ __global__ void __launch_bounds__(64 * JPG_WPB) k_jpeg_entropy(const uint8_t* __
                     pr += (int)inf >> 16;
                     if (lane == 0) L.blk[0] = (int16_t)pr;
                     k = 1;
-                    if (at >= 64) break;
+                    if (at >= span) break;
                 }
                 if (ta[c] != rta) break;   // another AC table: the next round decodes with it
                 bool done = false;
-                for (;;) {            // AC segments: chain walks between slow tokens
+                for (;;) {            // AC segments: chain walks within a half, between slow tokens
+                    const uint32_t hb = (JPG_HALVES > 1 && at >= 64) ? 64u : 0u;
+                    const uint32_t aw = hb ? aw1 : aw0, av = hb ? av1 : av0;
                     uint64_t mem = 0;
                     const uint32_t k0 = k;
-                    uint32_t last, inf;
+                    uint32_t a = at - hb, last, inf;
                     do {
-                        mem |= 1ull << at;
-                        last = at;
-                        inf = jrfl(__builtin_amdgcn_readlane(aw, (int)at));
+                        mem |= 1ull << a;
+                        last = a;
+                        inf = jrfl(__builtin_amdgcn_readlane(aw, (int)a));
                         k = jrfl(k + (inf >> 8));     // (keeps the walk scalar: the compiler loses it otherwise)
-                        at = inf & 255u;
+                        a = inf & 255u;
                         JST(++n_tok;)
-                    } while (at < 64 && k < 64);
+                    } while (a < 64 && k < 64);
                     const bool slow = (inf & 255u) == 255u, eob = !slow && (inf & 128u);
                     if (slow) mem &= ~(1ull << last);
                     {                 // the chain's coefficients, in parallel: k of each = k0 + prefix
@@ -503,12 +518,12 @@ __global__ void __launch_bounds__(64 * JPG_WPB) k_jpeg_entropy(const uint8_t* __
                         if (bad) err = true;
                     }
                     if (err) break;
-                    if (eob) { at = inf & 127u; done = true; break; }
+                    if (eob) { at = hb + (inf & 127u); done = true; break; }
                     if (slow) {       // a code longer than JPG_FB bits: decoded here, wave-uniform
                         JST(++n_slow;)
-                        const uint32_t t2 = jrfl(jpg_token_slow(L, 4 + (int)ta[c], jpg_peek32(L, P + last), false));
+                        const uint32_t t2 = jrfl(jpg_token_slow(L, 4 + (int)ta[c], jpg_peek32(L, P + hb + last), false));
                         if (t2 & JT_BAD) { err = true; break; }
-                        at = last + (t2 & 31u);
+                        at = hb + last + (t2 & 31u);
                         const uint32_t run = (t2 >> 5) & 15u, sz = (t2 >> 9) & 15u;
                         if (sz == 0 && run != 15) { done = true; break; }
                         k += run;
@@ -519,12 +534,13 @@ __global__ void __launch_bounds__(64 * JPG_WPB) k_jpeg_entropy(const uint8_t* __
                         }
                         if (sz && lane == 0) L.blk[L.zz[k]] = (int16_t)((int)t2 >> 16);
                         if (++k >= 64) { done = true; break; }
-                        if (at >= 64) break;
+                        if (at >= span) break;
                         continue;
                     }
-                    if (k >= 64) done = true;
-                    break;
-                }
+                    at = hb + a;
+                    if (k >= 64) { done = true; break; }
+                    if (at >= span) break;        // the round ends mid-block
+                }                                 // (else the chain crossed into the next half)
                 if (err || !done) break;
                 JST(++n_blk;)
                 store_block();
@@ -548,7 +564,7 @@ __global__ void __launch_bounds__(64 * JPG_WPB) k_jpeg_entropy(const uint8_t* __
                         break;
                     }
                 }
-                if (at >= 64) break;
+                if (at >= span) break;
             }
             JST(c_walk += __builtin_amdgcn_s_memtime() - cw0;)
             P += at;
