@@ -189,7 +189,7 @@ __global__ void __launch_bounds__(64) k_jpeg_parse(const uint8_t* __restrict__ f
 #ifdef JPG_STATS
 // diagnostic build (scripts/build_var.py jpg_stats -DJPG_STATS=1 bf_jpeg.hip): per file, the entropy
 // kernel's shader-clock and 100-MHz stamps, rounds, tokens, slow tokens, refills, refill cycles, blocks
-#define JPG_NSTAT 10
+#define JPG_NSTAT 12
 __device__ unsigned long long jpg_stats[4096 * JPG_NSTAT];
 BF_API int bf_jpeg_read_stats(unsigned long long* dst, int n) {
     return hipMemcpyFromSymbol(dst, HIP_SYMBOL(jpg_stats), sizeof(unsigned long long) * JPG_NSTAT * n) == hipSuccess
@@ -344,7 +344,7 @@ __global__ void __launch_bounds__(64 * JPG_WPB) k_jpeg_entropy(const uint8_t* __
     }
     uint8_t* ring8 = reinterpret_cast<uint8_t*>(L.ring);
     JST(const uint64_t c0 = __builtin_amdgcn_s_memtime(); const uint64_t r0 = __builtin_amdgcn_s_memrealtime();)
-    JST(uint64_t n_rounds = 0, n_tok = 0, n_slow = 0, n_prod = 0, c_prod = 0, n_blk = 0, c_lanes = 0, c_walk = 0;)
+    JST(uint64_t n_rounds = 0, n_tok = 0, n_slow = 0, n_prod = 0, c_prod = 0, n_blk = 0, c_lanes = 0, c_walk = 0, n_seg = 0, c_post = 0;)
 
     // ---- producer: source position, bytes in the ring, last source byte, end of the data
     uint32_t sp = 0, prod = 0, prev = 0, real_end = 0xffffffffu;
@@ -506,6 +506,7 @@ __global__ void __launch_bounds__(64 * JPG_WPB) k_jpeg_entropy(const uint8_t* __
                     } while (a < 64 && k < 64);
                     const bool slow = (inf & 255u) == 255u, eob = !slow && (inf & 128u);
                     if (slow) mem &= ~(1ull << last);
+                    JST(const uint64_t cq0 = __builtin_amdgcn_s_memtime(); ++n_seg;)
                     {                 // the chain's coefficients, in parallel: k of each = k0 + prefix
                         const bool in = (mem >> lane) & 1ull;
                         const uint32_t kin = in ? (aw >> 8) : 0u;
@@ -517,6 +518,7 @@ __global__ void __launch_bounds__(64 * JPG_WPB) k_jpeg_entropy(const uint8_t* __
                         if (wr && pos <= 63) L.blk[L.zz[pos]] = (int16_t)((int)av >> 16);
                         if (bad) err = true;
                     }
+                    JST(__builtin_amdgcn_s_waitcnt(0); c_post += __builtin_amdgcn_s_memtime() - cq0;)
                     if (err) break;
                     if (eob) { at = hb + (inf & 127u); done = true; break; }
                     if (slow) {       // a code longer than JPG_FB bits: decoded here, wave-uniform
@@ -583,7 +585,7 @@ __global__ void __launch_bounds__(64 * JPG_WPB) k_jpeg_entropy(const uint8_t* __
     if (lane == 0 && f < 4096) {
         unsigned long long* o = jpg_stats + f * JPG_NSTAT;
         o[0] = c1 - c0; o[1] = r1 - r0; o[2] = n_rounds; o[3] = n_tok; o[4] = n_slow; o[5] = n_prod; o[6] = c_prod;
-        o[7] = n_blk; o[8] = c_lanes; o[9] = c_walk;
+        o[7] = n_blk; o[8] = c_lanes; o[9] = c_walk; o[10] = n_seg; o[11] = c_post;
     }
 #endif
 }

@@ -25,9 +25,9 @@ def main():
     for _ in range(2):
         _lib.jpeg_decode_rgb(files, offs, H, W)
         torch.cuda.synchronize()
-    buf = (ctypes.c_ulonglong * (10 * F))()
+    buf = (ctypes.c_ulonglong * (12 * F))()
     assert L.bf_jpeg_read_stats(buf, F) == 0
-    a = np.frombuffer(buf, np.uint64).reshape(F, 10).astype(np.float64)
+    a = np.frombuffer(buf, np.uint64).reshape(F, 12).astype(np.float64)
     cyc, rt = a[:, 0], a[:, 1] * 10.0
     rounds, tok, slow, nprod, cprod, blk = a[:, 2], a[:, 3], a[:, 4], a[:, 5], a[:, 6], a[:, 7]
     print(f"{F} files q{q}, {np.mean([len(b) for b in blobs]) / 1e3:.0f} KB")
@@ -35,7 +35,8 @@ def main():
           f"{rounds.mean():.0f} rounds, {tok.mean():.0f} tokens ({tok.mean() / rounds.mean():.2f}/round), "
           f"{slow.mean():.0f} slow, {blk.mean():.0f} blocks; {cyc.mean() / rounds.mean():.0f} cycles/round, "
           f"{cyc.mean() / tok.mean():.0f} cycles/token; refills {nprod.mean():.0f} taking {cprod.mean() / cyc.mean() * 100:.1f}%; "
-          f"lane tokens {a[:, 8].mean() / rounds.mean():.0f} cycles/round (incl. refills), walk {a[:, 9].mean() / rounds.mean():.0f}")
+          f"lane tokens {a[:, 8].mean() / rounds.mean():.0f} cycles/round (incl. refills), walk {a[:, 9].mean() / rounds.mean():.0f}; "
+          f"{a[:, 10].mean() / rounds.mean():.2f} chain segments/round, placement {a[:, 11].mean() / a[:, 10].mean():.0f} cycles/segment")
 
 
 if __name__ == "__main__":
