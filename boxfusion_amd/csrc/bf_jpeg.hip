@@ -680,24 +680,17 @@ __global__ void __launch_bounds__(256) k_jpeg_idct(const JpegInfo* __restrict__ 
 // chroma sample of the fancy upsampler (jdsample.c h2v2 / h2v1; fullsize copy) at output (x, y)
 __device__ __forceinline__ int jpg_chroma(const uint8_t* pl, uint32_t pw, int cw, int ch, int rx, int ry, int x, int y) {
     if (rx == 1 && ry == 1) return pl[(size_t)y * pw + x];
+    // the triangle filter with the neighbour column (and row) clamped at the plane's edges: at an
+    // edge that reproduces jdsample.c's special cases exactly ((4p + 1) >> 2 = p for h2v1, the
+    // (4s + 8) >> 4 / (4s + 7) >> 4 end columns for h2v2), so no branch is needed
     const int c = x >> 1, e = x & 1;
+    const int cn = e ? min(c + 1, cw - 1) : max(c - 1, 0);
     auto S = [&](int col, int row) -> int { return pl[(size_t)row * pw + col]; };
-    if (ry == 1) {                                      // h2v1_fancy_upsample
-        const int row = y;
-        if (cw == 1) return S(0, row);
-        if (c == 0 && e == 0) return S(0, row);
-        if (c == cw - 1 && e == 1) return S(cw - 1, row);
-        const int m = S(c, row) * 3;
-        return e == 0 ? (m + S(c - 1, row) + 1) >> 2 : (m + S(c + 1, row) + 2) >> 2;
-    }
-    // h2v2_fancy_upsample: column sums with the row above (even output row) or below (odd)
-    const int r = y >> 1, d = y & 1;
-    const int rn = d == 0 ? (r > 0 ? r - 1 : 0) : (r + 1 < ch ? r + 1 : ch - 1);
-    auto colsum = [&](int col) -> int { return S(col, r) * 3 + S(col, rn); };
-    const int s = colsum(c);
-    if (cw == 1) return e == 0 ? (s * 4 + 8) >> 4 : (s * 4 + 7) >> 4;
-    if (e == 0) return c == 0 ? (s * 4 + 8) >> 4 : (s * 3 + colsum(c - 1) + 8) >> 4;
-    return c == cw - 1 ? (s * 4 + 7) >> 4 : (s * 3 + colsum(c + 1) + 7) >> 4;
+    if (ry == 1) return (3 * S(c, y) + S(cn, y) + 1 + e) >> 2;               // h2v1_fancy_upsample
+    const int r = y >> 1;                                                     // h2v2_fancy_upsample:
+    const int rn = (y & 1) ? min(r + 1, ch - 1) : max(r - 1, 0);             // column sums with the row
+    const int sc = 3 * S(c, r) + S(c, rn), sn = 3 * S(cn, r) + S(cn, rn);   // above / below
+    return (3 * sc + sn + 8 - e) >> 4;
 }
 
 // jdcolor.c ycc_rgb_convert (SCALEBITS 16) of one pixel -> packed 0x00BBGGRR
